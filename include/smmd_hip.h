@@ -1,0 +1,251 @@
+/*
+ * smmd_hip.h -- C ABI of libsmmd_hip.so, the MI355X (gfx950) hot path of the
+ * Scaled-MMD-GAN training step.
+ *
+ * Plain pointers and sizes only.  Every device buffer (inputs, outputs and
+ * workspace) is owned by the caller; the library never allocates or frees
+ * device memory and never synchronises the stream.  Every entry point is
+ * stream-ordered on the caller's stream (a hipStream_t passed as void*; NULL
+ * = the legacy default stream) and is safe to capture in a hipGraph.
+ * Reductions use a fixed order, so results are bit-identical run to run for
+ * the same shapes.  No entry point throws or aborts: errors come back as an
+ * smmd_status code.
+ *
+ * Which reference interface each entry point replaces is cited next to it
+ * (paths relative to the playHing/Scaled-MMD-GAN tree).
+ */
+#ifndef SMMD_HIP_H
+#define SMMD_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    SMMD_OK = 0,
+    SMMD_EINVAL = 1,        /* bad argument (shape, range, NULL pointer)      */
+    SMMD_EHIP = 2,          /* a HIP launch / runtime error                   */
+    SMMD_EWORKSPACE = 3,    /* workspace NULL or smaller than *_workspace_bytes */
+    SMMD_EUNSUPPORTED = 4   /* valid request this build does not implement    */
+} smmd_status;
+
+typedef void *smmd_stream_t;   /* hipStream_t */
+
+/* Kernel family of gan/core/mmd.py:18-188, selected in the reference by
+ * getattr(mmd, '_%s_kernel' % config.kernel) (gan/core/smmd.py:11).       */
+typedef enum {
+    SMMD_KIND_RBF = 0,       /* sum_k wt_k exp(-D2 / (2 sigma_k^2))   mmd.py:55-116  */
+    SMMD_KIND_RQ = 1,        /* sum_k wt_k (1 + D2/(2 a_k))^-a_k + add_dot <x,y>   mmd.py:143-188 */
+    SMMD_KIND_DISTANCE = 2,  /* ms(|x|^2)+ms(|y|^2)-ms(raw D2)       mmd.py:18-37   */
+    SMMD_KIND_DOT = 3        /* <x,y>                                mmd.py:44-52   */
+} smmd_kernel_kind;
+
+#define SMMD_MAX_TERMS 8
+
+typedef struct {
+    int32_t kind;                   /* smmd_kernel_kind                          */
+    int32_t n_terms;                /* RBF/RQ mixture size, 1..SMMD_MAX_TERMS    */
+    double param[SMMD_MAX_TERMS];   /* RBF: sigma_k ; RQ: alpha_k                */
+    double wt[SMMD_MAX_TERMS];      /* mixture weights                           */
+    double add_dot;                 /* RQ only (mix_rq_*dot variants)            */
+    int32_t tanh_inputs;            /* tanh_mix_rq / tanh_distance (mmd.py:40,139) */
+    int32_t has_const_diag;         /* 1: subtract m*const_diag; 0: the trace   */
+    double const_diag;              /* mmd.py:82, :116, :188 ("False" -> 0 flag) */
+} smmd_kernel_desc;
+
+const char *smmd_status_string(smmd_status s);
+int smmd_abi_version(void);         /* bumped on any ABI change                  */
+
+/* ---------------------------------------------------------------------------
+ * Fused pairwise MMD^2 (forward + unit gradient).
+ * Replaces mmd.mmd2(mmd._<kind>_kernel(X, Y))  (gan/core/mmd.py:55-82 and
+ * :194-220, called from gan/core/smmd.py:11-15) together with TF's autodiff of
+ * it: the N x N kernel matrices are never materialised.
+ *
+ * X [m, d], Y [n, d]: row-major fp32 feature matrices (critic outputs d_G and
+ * d_images, gan/core/model.py:307-311).  m, n are the GLOBAL batch sizes that
+ * define the estimator's weights.  This call evaluates the rows
+ * [x_begin, x_end) of X and [y_begin, y_end) of Y against all m + n columns
+ * (the whole range for one GPU; a rank's shard in the all-gather mode).
+ *
+ * out_sums[8] (device, fp32), partial over the evaluated rows:
+ *   [0] sum K_XX  [1] sum K_XY  [2] sum K_YY  [3] trace K_XX  [4] trace K_YY
+ *   [5] sum K_YX (only with a gradient request)   [6], [7] zero
+ * out_mmd2 (device, 1 float, may be NULL): the estimator from out_sums; equal
+ *   to the reference's value only when the rows cover everything.
+ * grad_x [x_end-x_begin, d], grad_y [y_end-y_begin, d] (device, may both be
+ *   NULL): d mmd2 / d X[row], d mmd2 / d Y[row] for the evaluated rows, taken
+ *   against ALL columns (TF tie rule of tf.maximum: gradient passes at 0).
+ * ws: zero-filled at allocation, at least smmd_mmd2_workspace_bytes(); the
+ *   library leaves it zero-filled again after every call.
+ * ------------------------------------------------------------------------- */
+size_t smmd_mmd2_workspace_bytes(int m, int n, int d);
+
+smmd_status smmd_mmd2_fwd(const smmd_kernel_desc *desc,
+                          const float *X, int m, const float *Y, int n, int d,
+                          int biased,
+                          int x_begin, int x_end, int y_begin, int y_end,
+                          float *out_sums, float *out_mmd2,
+                          float *grad_x, float *grad_y,
+                          void *ws, size_t ws_bytes, smmd_stream_t stream);
+
+/* The estimator of gan/core/mmd.py:199-220 from (all-reduced) sums:
+ * sums[8] as above -> out_mmd2[1].  Used by the all-gather mode after the
+ * RCCL all_reduce of the per-rank partial sums. */
+smmd_status smmd_mmd2_combine(const smmd_kernel_desc *desc, const float *sums,
+                              int m, int n, int biased, float *out_mmd2,
+                              smmd_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * Witness function of the gradient penalty (gan/core/model.py:336-339):
+ *   w_i = mean_j K(H_i, R_j) - mean_j K(H_i, F_j)   (K_XY_only=True kernels)
+ * out_w [b] (may be NULL), out_dH [b, d] = d(sum_i w_i)/dH (may be NULL).
+ * H [b, d], R [nr, d], F [nf, d].
+ * smmd_witness_bwd: the vector-Jacobian product of out_dH, i.e. given
+ * gdH [b, d] (= dL/d out_dH) it returns dL/dH [b, d], dL/dR [nr, d],
+ * dL/dF [nf, d] -- the second-order term the penalty's parameter gradient
+ * needs (gan/core/model.py:339-345).
+ * ------------------------------------------------------------------------- */
+smmd_status smmd_witness_fwd(const smmd_kernel_desc *desc,
+                             const float *H, int b, const float *R, int nr,
+                             const float *F, int nf, int d,
+                             float *out_w, float *out_dH, smmd_stream_t stream);
+
+smmd_status smmd_witness_bwd(const smmd_kernel_desc *desc,
+                             const float *H, int b, const float *R, int nr,
+                             const float *F, int nf, int d, const float *gdH,
+                             float *gH, float *gR, float *gF,
+                             smmd_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * Scaling regulariser (SMMD / SWGAN).
+ * Replaces ops.squared_norm_jacobian (gan/core/ops.py:228-233),
+ * MMD_GAN.add_scaling (gan/core/model.py:366-403) and the apply_scaling
+ * hooks (gan/core/smmd.py:21-23, :40-42).
+ *
+ * smmd_scaled_loss_fwd: jac [n_cols * b, per_sample]: for each critic output
+ *   column c the gradient d(sum_b D(x_b)_c)/dx of this caller's b samples
+ *   (ops.py:230-232 stacks them column-major over c).  feat [b, dof] (critic
+ *   output; read only when variant == 1 'value_and_grad').
+ *   b_total: the normaliser of the means (global batch in the all-gather
+ *   mode, else b; <= 0 means b).  base_loss [1]: mmd2 (SMMD) or
+ *   mean(images) - mean(G) (SWGAN).
+ *   out (device, 8 floats): [0] g_loss [1] d_loss [2] scale
+ *   [3] J = sum_b ||grad||^2 / b_total  [4] norm_discriminator
+ *   [5] base_loss  [6],[7] zero.
+ *   per_sample [b] (may be NULL): sum_c ||d D_c / d x_b||^2.
+ *   variant: 0 'grad', 1 'value_and_grad' (model.py:387-390).
+ *   sqrt_scale: 0 SMMD (g_loss = base*scale), 1 SWGAN (base*sqrt(scale)).
+ * smmd_scaled_loss_finalize: recompute out[0..2] from out[3..5] (after the
+ *   caller all-reduced out[3], out[4] and replaced out[5]).
+ * smmd_scaled_loss_bwd: given dL/dg_loss (device scalar, NULL = 1) writes
+ *   d_base [1] (may be NULL), gjac [n_cols*b, per_sample] and gfeat [b, dof]
+ *   (only when variant == 1).
+ * ------------------------------------------------------------------------- */
+size_t smmd_scaled_loss_workspace_bytes(int rows, int64_t per_sample);
+
+smmd_status smmd_scaled_loss_fwd(const float *jac, int n_cols, int b, int b_total,
+                                 int64_t per_sample, const float *feat, int dof,
+                                 const float *base_loss, float sc, int variant,
+                                 int sqrt_scale, float *out, float *per_sample_out,
+                                 void *ws, size_t ws_bytes, smmd_stream_t stream);
+
+smmd_status smmd_scaled_loss_finalize(float *out, float sc, int variant, int sqrt_scale,
+                                      smmd_stream_t stream);
+
+smmd_status smmd_scaled_loss_bwd(const float *jac, int n_cols, int b, int b_total,
+                                 int64_t per_sample, const float *feat, int dof,
+                                 const float *fwd_out, float sc, int variant,
+                                 int sqrt_scale, const float *g_loss_grad,
+                                 float *d_base, float *gjac, float *gfeat,
+                                 smmd_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * Spectral normalisation, all layers of a network in one set of launches.
+ * Replaces sn.spectral_normed_weight (gan/core/sn.py:16-59) and the s * W_bar
+ * product of the SN layer wrappers (gan/core/snops.py:82-84, :118-120,
+ * :180-183; gan/core/resnet/ops/conv2d.py:29-33).
+ *
+ * Layout: W is the layer weight flattened to [N = out channels, K] row-major
+ * (a torch conv/linear weight as stored); the reference reshapes to
+ * [K', N] (sn.py:19) with K' a permutation of K, which leaves sigma and u
+ * unchanged and permutes v.
+ * Power iteration (num_iters times, sn.py:24-35):
+ *   v = l2n(W^T u), u' = l2n(W v), l2n(x) = x / (||x|| + eps);
+ *   sigma = (W v) . u'  (sn.py:42);   W_eff = s * (W / sigma)  (snops.py:84).
+ * ------------------------------------------------------------------------- */
+#define SMMD_SN_MAX_LAYERS 32
+
+typedef struct {
+    const float *W;      /* [N, K]                                            */
+    float *W_eff;        /* [N, K] out: s * W / sigma (NULL: not written)     */
+    float *u;            /* [N] in: current u ; out: u' when update_u         */
+    float *v;            /* [K] out: v (normalised)                           */
+    float *sigma;        /* [1] out                                           */
+    const float *s;      /* [1] SN scale (NULL -> 1.0), snops.py:82           */
+    const float *G;      /* bwd: [N, K] dL/dW_eff                             */
+    float *gW;           /* bwd: [N, K] out dL/dW                             */
+    float *gs;           /* bwd: [1] out dL/ds (NULL: not written)            */
+    int32_t N;
+    int32_t K;
+} smmd_sn_layer;
+
+size_t smmd_sn_workspace_bytes(const smmd_sn_layer *layers, int n_layers);
+
+/* update_u = 1 mirrors update_collection=None (u.assign(u'), sn.py:39-46);
+ * 0 mirrors "NO_OPS" (u left untouched). layers[] is a HOST array read during
+ * the call; the pointers in it are device pointers. n_layers <= SMMD_SN_MAX_LAYERS. */
+smmd_status smmd_sn_power_iter(const smmd_sn_layer *layers, int n_layers,
+                               int num_iters, float eps, int update_u,
+                               void *ws, size_t ws_bytes, smmd_stream_t stream);
+
+/* dL/dW = (s/sigma) (G - (<G,W>/sigma) u' v^T),  dL/ds = <G,W>/sigma,
+ * u', v, sigma from the last smmd_sn_power_iter (stop_gradient, sn.py:32-34);
+ * ws must be the workspace that call used (it holds u'). */
+smmd_status smmd_sn_weight_bwd(const smmd_sn_layer *layers, int n_layers,
+                               void *ws, size_t ws_bytes, smmd_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * Materialised kernel matrix K(A, B) [na, nb] (row-major) and its backward
+ * (gA = dL/dA, gB = dL/dB from G = dL/dK; either output may be NULL).
+ * Serves the tuple-returning API of mmd._<kind>_kernel (gan/core/mmd.py:18-188)
+ * and its K_XY_only form; the training loss never calls it.
+ * ------------------------------------------------------------------------- */
+smmd_status smmd_kernel_matrix_fwd(const smmd_kernel_desc *desc, const float *A, int na,
+                                   const float *B, int nb, int d, float *out,
+                                   smmd_stream_t stream);
+
+smmd_status smmd_kernel_matrix_bwd(const smmd_kernel_desc *desc, const float *A, int na,
+                                   const float *B, int nb, int d, const float *G,
+                                   float *gA, float *gB, smmd_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * TF-semantics gradient clip and Adam over the tensors of one flat buffer:
+ * tensor i occupies elements [offsets[i], offsets[i+1]) (offsets: HOST array
+ * of n_tensors + 1 entries).
+ * Replaces clip_by_norm in MMD_GAN.compute_grads (gan/core/model.py:444-456)
+ * and tf.train.AdamOptimizer.apply_gradients (model.py:405-412, :458-468).
+ *  smmd_clip_by_norm_flat: g <- g * clip * min(rsqrt(sum g^2), 1/clip), per
+ *    tensor, in place (the per-tower clip before the tower mean).
+ *  smmd_adam_flat: g' = grad_scale * g, then (clip_norm > 0) the same clip,
+ *    then Eigen's ApplyAdam: m += (g'-m)(1-b1); v += (g'^2-v)(1-b2);
+ *    p -= lr_t m / (sqrt(v) + eps), lr_t = lr sqrt(1-b2^step)/(1-b1^step).
+ * ------------------------------------------------------------------------- */
+size_t smmd_opt_workspace_bytes(const int64_t *offsets, int n_tensors);
+
+smmd_status smmd_clip_by_norm_flat(float *grad, const int64_t *offsets, int n_tensors,
+                                   float clip_norm, void *ws, size_t ws_bytes,
+                                   smmd_stream_t stream);
+
+smmd_status smmd_adam_flat(float *param, const float *grad, float *m, float *v,
+                           const int64_t *offsets, int n_tensors, float grad_scale,
+                           float clip_norm, float lr, float beta1, float beta2, float eps,
+                           int64_t step, void *ws, size_t ws_bytes, smmd_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SMMD_HIP_H */

@@ -1,0 +1,430 @@
+"""CPU oracle for the Scaled-MMD-GAN hot path -- TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline``
+leg may import this module, and only as the checker.  The product path
+(``scaled-mmd-gan_amd/``) never imports it and fails loudly when the HIP
+library is missing.
+
+What it is
+    A float64 NumPy restatement of the reference's TensorFlow-1.x graph for
+    the hot path, op by op, including TF's autodiff tie rules:
+
+    * kernel family          gan/core/mmd.py:12 (mysqrt), :18-188
+    * unbiased/biased MMD^2  gan/core/mmd.py:194-220
+    * safer_norm             gan/core/ops.py:203-206
+    * squared_norm_jacobian  gan/core/ops.py:228-233
+    * scaling regulariser    gan/core/model.py:366-403, gan/core/smmd.py:21-23, :40-42
+    * witness GP             gan/core/model.py:327-350
+    * spectral norm          gan/core/sn.py:12-59, gan/core/snops.py:81-84
+    * clip + average + Adam  gan/core/model.py:233-266, :405-412, :444-456
+                             (tf.clip_by_norm / tf.train.AdamOptimizer semantics)
+
+Parity status: **parity unpinned**.  The reference ships no tests, fixtures or
+golden vectors and imports TensorFlow 1.6 at module
+top (gan/core/mmd.py:8), which is not installed and cannot be installed
+offline, so neither "reference golden vectors" nor "outputs of the reference
+run here" exist.  This oracle is instead pinned by analytic known-answer
+tests and by central finite differences of its own float64 forward
+(tests/test_oracle.py); tests/golden/*.npz are generated from it by
+oracle/gen_golden.py.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+
+EPS = 1.0e-5          # gan/core/mmd.py:6  (_eps)
+SN_EPS = 1.0e-12      # gan/core/sn.py:12  (_l2normalize eps)
+
+
+# --------------------------------------------------------------------------
+# kernel registry: reference kernel name -> parameters
+# --------------------------------------------------------------------------
+@dataclass
+class KernelSpec:
+    """Parameters of one reference kernel (gan/core/mmd.py:18-188).
+
+    kind: 'rbf' (sum of Gaussians), 'rq' (sum of rational quadratics, optional
+    add_dot * <x,y>), 'distance', 'dot'.  const_diag is None when the
+    reference returns ``False`` (trace is used in _mmd2, mmd.py:212-213).
+    """
+    kind: str
+    params: list = field(default_factory=list)   # sigmas (rbf) or alphas (rq)
+    wts: list = field(default_factory=list)
+    add_dot: float = 0.0
+    tanh: bool = False
+    const_diag: float | None = None
+
+
+def kernel_spec(name: str, **kw) -> KernelSpec:
+    """Map ``config.kernel`` (gan/core/smmd.py:11) to a KernelSpec."""
+    if name == 'rbf':                              # mmd.py:55-82
+        sigma = kw.get('sigma', 1.0)
+        wt = kw.get('wt', 1.0)
+        return KernelSpec('rbf', [sigma], [wt], const_diag=wt)
+    if name == 'mix_rbf':                          # mmd.py:85-116
+        sigmas = kw.get('sigmas', [2.0, 5.0, 10.0, 20.0, 40.0, 80.0])
+        wts = kw.get('wts') or [1] * len(sigmas)
+        return KernelSpec('rbf', list(sigmas), list(wts), const_diag=float(sum(wts)))
+    rq_dot = {'mix_rq': 0.0, 'mix_rq_dot': .1, 'mix_rq_1dot': 1., 'mix_rq_10dot': 10.,
+              'mix_rq_01dot': .1, 'mix_rq_001dot': .01, 'tanh_mix_rq': 0.0}
+    if name in rq_dot:                             # mmd.py:119-188
+        alphas = kw.get('alphas', [.1, 1., 10.])
+        wts = kw.get('wts') or [1.] * len(alphas)
+        add_dot = kw.get('add_dot', rq_dot[name])
+        # quirk: const diag = sum(wts) even with add_dot > 0 (mmd.py:182-188)
+        return KernelSpec('rq', list(alphas), list(wts), add_dot=add_dot,
+                          tanh=(name == 'tanh_mix_rq'), const_diag=float(sum(wts)))
+    if name in ('distance', 'tanh_distance'):      # mmd.py:18-41
+        return KernelSpec('distance', tanh=(name == 'tanh_distance'), const_diag=None)
+    if name == 'dot':                              # mmd.py:44-52
+        return KernelSpec('dot', const_diag=None)
+    raise ValueError('unknown kernel %r' % name)
+
+
+KERNEL_NAMES = ['rbf', 'mix_rbf', 'mix_rq', 'mix_rq_dot', 'mix_rq_1dot', 'mix_rq_10dot',
+                'mix_rq_01dot', 'mix_rq_001dot', 'tanh_mix_rq', 'distance',
+                'tanh_distance', 'dot']
+
+
+def _mysqrt(x):
+    """mysqrt = sqrt(max(x + eps, 0))  (gan/core/mmd.py:12)."""
+    return np.sqrt(np.maximum(x + EPS, 0.0))
+
+
+def _mysqrt_grad(x):
+    # d/dx sqrt(max(x+eps,0)); tf.maximum passes the gradient to its first
+    # argument on ties (x+eps >= 0).
+    xe = x + EPS
+    with np.errstate(divide='ignore'):
+        return np.where(xe >= 0, 0.5 / np.sqrt(np.maximum(xe, 0.0)), 0.0)
+
+
+def _block(spec: KernelSpec, A, B, AB, sa, sb):
+    """Kernel block K(A,B) from the Gram pieces, and dK/d(raw), dK/dAB,
+    dK/dsa, dK/dsb as elementwise factors (float64)."""
+    raw = -2.0 * AB + sa[:, None] + sb[None, :]          # mmd.py:67 (pre-clamp)
+    if spec.kind == 'rbf':
+        R = np.maximum(raw, 0.0)                          # mmd.py:67
+        K = np.zeros_like(R)
+        dKdR = np.zeros_like(R)
+        for sigma, wt in zip(spec.params, spec.wts):
+            gamma = 1.0 / (2.0 * sigma ** 2)              # mmd.py:69
+            e = wt * np.exp(-gamma * R)
+            K += e
+            dKdR += -gamma * e
+        dKdraw = dKdR * (raw >= 0)                        # tf.maximum tie rule
+        return K, dKdraw, np.zeros_like(K), None, None
+    if spec.kind == 'rq':
+        R = np.maximum(raw, 0.0)                          # mmd.py:163
+        K = np.zeros_like(R)
+        dKdR = np.zeros_like(R)
+        for alpha, wt in zip(spec.params, spec.wts):
+            q = 1.0 + R / (2.0 * alpha)                   # mmd.py:166
+            e = wt * np.exp(-alpha * np.log(q))           # mmd.py:167
+            K += e
+            dKdR += e * (-alpha) / q / (2.0 * alpha)
+        dKdAB = np.zeros_like(K)
+        if spec.add_dot > 0:                              # mmd.py:168-169
+            K = K + spec.add_dot * AB
+            dKdAB = np.full_like(K, spec.add_dot)
+        dKdraw = dKdR * (raw >= 0)
+        return K, dKdraw, dKdAB, None, None
+    if spec.kind == 'distance':                           # mmd.py:29
+        K = _mysqrt(sa)[:, None] + _mysqrt(sb)[None, :] - _mysqrt(raw)
+        dKdraw = -_mysqrt_grad(raw)
+        dsa = _mysqrt_grad(sa)[:, None] * np.ones_like(K)
+        dsb = _mysqrt_grad(sb)[None, :] * np.ones_like(K)
+        return K, dKdraw, np.zeros_like(K), dsa, dsb
+    if spec.kind == 'dot':                                # mmd.py:45
+        return AB.copy(), np.zeros_like(AB), np.ones_like(AB), None, None
+    raise ValueError(spec.kind)
+
+
+def kernel_matrices(spec: KernelSpec, X, Y, K_XY_only=False):
+    """(K_XX, K_XY, K_YY, const_diag) exactly as mmd._<name>_kernel
+    (gan/core/mmd.py:18-188); const_diag None means the reference's False."""
+    X = np.asarray(X, np.float64)
+    Y = np.asarray(Y, np.float64)
+    if spec.tanh:
+        X, Y = np.tanh(X), np.tanh(Y)
+    XX, XY, YY = X @ X.T, X @ Y.T, Y @ Y.T
+    sx, sy = np.diag(XX).copy(), np.diag(YY).copy()
+    KXY = _block(spec, X, Y, XY, sx, sy)[0]
+    if K_XY_only:
+        return KXY
+    KXX = _block(spec, X, X, XX, sx, sx)[0]
+    KYY = _block(spec, Y, Y, YY, sy, sy)[0]
+    return KXX, KXY, KYY, spec.const_diag
+
+
+def mmd2_from_K(KXX, KXY, KYY, const_diag=None, biased=False):
+    """_mmd2 (gan/core/mmd.py:199-220)."""
+    m, n = KXX.shape[0], KYY.shape[0]
+    if biased:
+        return KXX.sum() / (m * m) + KYY.sum() / (n * n) - 2 * KXY.sum() / (m * n)
+    if const_diag is not None:
+        trX, trY = m * const_diag, n * const_diag
+    else:
+        trX, trY = np.trace(KXX), np.trace(KYY)
+    return ((KXX.sum() - trX) / (m * (m - 1)) + (KYY.sum() - trY) / (n * (n - 1))
+            - 2 * KXY.sum() / (m * n))
+
+
+def mmd2(spec: KernelSpec, X, Y, biased=False):
+    """mmd.mmd2(kernel(X, Y)) (gan/core/mmd.py:194-196)."""
+    KXX, KXY, KYY, c = kernel_matrices(spec, X, Y)
+    return mmd2_from_K(KXX, KXY, KYY, c, biased)
+
+
+def mmd2_sums(spec: KernelSpec, X, Y):
+    """(sum K_XX, sum K_XY, sum K_YY, trace K_XX, trace K_YY) in float64."""
+    KXX, KXY, KYY, _ = kernel_matrices(spec, X, Y)
+    return np.array([KXX.sum(), KXY.sum(), KYY.sum(), np.trace(KXX), np.trace(KYY)])
+
+
+def _block_grads(spec, A, B, AB, sa, sb, G):
+    """TF-autodiff gradient of sum(G * K(A,B)) w.r.t. A and B, where
+    sa = diag(A A^T), sb = diag(B B^T) come from the Gram diagonal
+    (mmd.py:60-61), so d sa_i / d a_i = 2 a_i."""
+    K, dKdraw, dKdAB, dsa, dsb = _block(spec, A, B, AB, sa, sb)
+    Graw = G * dKdraw
+    GAB = -2.0 * Graw + G * dKdAB
+    gsa = Graw.sum(1)
+    gsb = Graw.sum(0)
+    if dsa is not None:
+        gsa = gsa + (G * dsa).sum(1)
+        gsb = gsb + (G * dsb).sum(0)
+    dA = GAB @ B + 2.0 * gsa[:, None] * A
+    dB = GAB.T @ A + 2.0 * gsb[:, None] * B
+    return dA, dB
+
+
+def mmd2_grad(spec: KernelSpec, X, Y, biased=False):
+    """Analytic d mmd2 / dX, d mmd2 / dY following TF autodiff of
+    gan/core/mmd.py:55-220 (tf.maximum ties pass the gradient)."""
+    X0 = np.asarray(X, np.float64)
+    Y0 = np.asarray(Y, np.float64)
+    X1, Y1 = (np.tanh(X0), np.tanh(Y0)) if spec.tanh else (X0, Y0)
+    m, n = X1.shape[0], Y1.shape[0]
+    if biased:
+        gXX = np.full((m, m), 1.0 / (m * m))
+        gYY = np.full((n, n), 1.0 / (n * n))
+    else:
+        gXX = np.full((m, m), 1.0 / (m * (m - 1)))
+        gYY = np.full((n, n), 1.0 / (n * (n - 1)))
+        if spec.const_diag is None:       # trace subtracted -> diag grads cancel
+            np.fill_diagonal(gXX, 0.0)
+            np.fill_diagonal(gYY, 0.0)
+    gXY = np.full((m, n), -2.0 / (m * n))
+    XX, XY, YY = X1 @ X1.T, X1 @ Y1.T, Y1 @ Y1.T
+    sx, sy = np.diag(XX).copy(), np.diag(YY).copy()
+    a, b = _block_grads(spec, X1, X1, XX, sx, sx, gXX)
+    dX = a + b
+    a, b = _block_grads(spec, Y1, Y1, YY, sy, sy, gYY)
+    dY = a + b
+    a, b = _block_grads(spec, X1, Y1, XY, sx, sy, gXY)
+    dX += a
+    dY += b
+    if spec.tanh:
+        dX *= 1.0 - X1 ** 2
+        dY *= 1.0 - Y1 ** 2
+    return dX, dY
+
+
+# --------------------------------------------------------------------------
+# witness (K_XY_only row means), gan/core/model.py:327-350
+# --------------------------------------------------------------------------
+def witness(spec: KernelSpec, H, R, F):
+    """witness_i = mean_j K(h_i, r_j) - mean_j K(h_i, f_j)  (model.py:336-338)."""
+    return (kernel_matrices(spec, H, R, K_XY_only=True).mean(1)
+            - kernel_matrices(spec, H, F, K_XY_only=True).mean(1))
+
+
+def witness_grad_H(spec: KernelSpec, H, R, F):
+    """d sum_i witness_i / d H  (the inner gradient of model.py:339 at the
+    critic-output level), float64 analytic."""
+    H0 = np.asarray(H, np.float64)
+    out = np.zeros_like(H0)
+    for Z, sgn in ((R, 1.0), (F, -1.0)):
+        Z0 = np.asarray(Z, np.float64)
+        H1, Z1 = (np.tanh(H0), np.tanh(Z0)) if spec.tanh else (H0, Z0)
+        G = np.full((H1.shape[0], Z1.shape[0]), sgn / Z1.shape[0])
+        dA, _ = _block_grads(spec, H1, Z1, H1 @ Z1.T, np.diag(H1 @ H1.T).copy(),
+                             np.diag(Z1 @ Z1.T).copy(), G)
+        if spec.tanh:
+            dA *= 1.0 - H1 ** 2
+        out += dA
+    return out
+
+
+def safer_norm(t, axis=None, keep_dims=False, epsilon=EPS):
+    """gan/core/ops.py:203-206."""
+    t = np.asarray(t, np.float64)
+    return np.sqrt(np.sum(t * t, axis=axis, keepdims=keep_dims) + epsilon)
+
+
+def gp_penalty(grad_xhat):
+    """mean((safer_norm(g, axis=1) - 1)^2)  (model.py:341): channel axis only."""
+    return np.mean((safer_norm(grad_xhat, axis=1) - 1.0) ** 2)
+
+
+# --------------------------------------------------------------------------
+# scaling regulariser (gan/core/model.py:366-403, ops.py:228-233)
+# --------------------------------------------------------------------------
+def squared_norm_per_sample(grads):
+    """sum over [1,2,3] of grad^2 per sample (ops.py:231) for one output
+    column's gradient g [b, C, H, W]; ops.py:232 sums these over columns."""
+    g = np.asarray(grads, np.float64)
+    return np.sum(g.reshape(g.shape[0], -1) ** 2, axis=1)
+
+
+def scale_factor(norm2_jac_mean, sc, norm_discriminator=0.0, variant='grad'):
+    """scale = 1/(sc*J + 1) ('grad') or 1/(sc*(J + nD) + 1)  (model.py:387-390)."""
+    if variant == 'grad':
+        return 1.0 / (sc * norm2_jac_mean + 1.0)
+    if variant == 'value_and_grad':
+        return 1.0 / (sc * (norm2_jac_mean + norm_discriminator) + 1.0)
+    raise ValueError(variant)
+
+
+def smmd_loss(mmd2_value, scale):
+    """SMMD.apply_scaling: g_loss = mmd2*scale, d_loss = -g_loss (smmd.py:21-23)."""
+    g = mmd2_value * scale
+    return g, -g
+
+
+def swgan_loss(d_G, d_images, scale):
+    """SWGAN (smmd.py:31-42): d_loss = mean(G) - mean(images), scaled by sqrt(scale)."""
+    d = (np.mean(d_G) - np.mean(d_images)) * math.sqrt(scale)
+    return -d, d
+
+
+# --------------------------------------------------------------------------
+# spectral norm (gan/core/sn.py:12-59)
+# --------------------------------------------------------------------------
+def _l2normalize(v, eps=SN_EPS):
+    """v / (||v|| + eps)   (sn.py:12-13)."""
+    return v / (np.sqrt(np.sum(v ** 2)) + eps)
+
+
+def spectral_normed_weight(W, u, num_iters=1):
+    """Reference layout: W of any shape, reshaped to [-1, W.shape[-1]]
+    (sn.py:18-19); u [1, N].  Returns (W_bar, sigma, u_final, v_final)."""
+    W = np.asarray(W, np.float64)
+    Wr = W.reshape(-1, W.shape[-1])
+    u_i = np.asarray(u, np.float64).reshape(1, -1)
+    v_i = np.zeros((1, Wr.shape[0]))
+    for _ in range(num_iters):                       # sn.py:24-27
+        v_i = _l2normalize(u_i @ Wr.T)
+        u_i = _l2normalize(v_i @ Wr)
+    sigma = (v_i @ Wr @ u_i.T)[0, 0]                  # sn.py:42
+    return (Wr / sigma).reshape(W.shape), sigma, u_i, v_i
+
+
+def spectral_norm_rows(Wt, u, num_iters=1):
+    """Same power iteration on the [N rows = out, K cols] layout this build
+    stores (torch conv/linear weights flattened).  Wt = W_r^T up to a
+    permutation of K, which leaves sigma and u unchanged."""
+    Wt = np.asarray(Wt, np.float64)
+    u_i = np.asarray(u, np.float64).reshape(-1)
+    v_i = np.zeros(Wt.shape[1])
+    for _ in range(num_iters):
+        v_i = _l2normalize(u_i @ Wt)
+        u_i = _l2normalize(Wt @ v_i)
+    sigma = float(v_i @ Wt.T @ u_i)
+    return sigma, u_i, v_i
+
+
+def sn_weight_backward(Wt, s, sigma, u, v, G_eff):
+    """Gradient of L(W_eff), W_eff = s * W / sigma(W) with u, v stopped
+    (sn.py:32-34, :42-43, snops.py:84): returns dL/dW, dL/ds.
+    dsigma/dW = u v^T in the [N, K] layout."""
+    Wt = np.asarray(Wt, np.float64)
+    G = np.asarray(G_eff, np.float64)
+    gWbar = s * G
+    dot = np.sum(gWbar * Wt)
+    gW = gWbar / sigma - (dot / sigma ** 2) * np.outer(u, v)
+    gs = np.sum(G * Wt) / sigma
+    return gW, gs
+
+
+# --------------------------------------------------------------------------
+# clip + average + Adam (gan/core/model.py:233-266, :405-412, :444-468)
+# --------------------------------------------------------------------------
+def clip_by_norm(t, clip_norm=1.0):
+    """tf.clip_by_norm: t * clip_norm / max(||t||_2, clip_norm)."""
+    t = np.asarray(t, np.float64)
+    nrm = np.sqrt(np.sum(t * t))
+    return t * clip_norm / max(nrm, clip_norm)
+
+
+def average_gradients(tower_grads):
+    """mean over towers of each variable's gradient (model.py:245-265)."""
+    return [np.mean(np.stack(gs), axis=0) for gs in zip(*tower_grads)]
+
+
+def adam_step(var, m, v, g, step, lr, beta1=0.5, beta2=0.9, eps=1e-8):
+    """tf.train.AdamOptimizer update (epsilon-hat form); step is 1-based."""
+    lr_t = lr * math.sqrt(1 - beta2 ** step) / (1 - beta1 ** step)
+    m = beta1 * m + (1 - beta1) * g
+    v = beta2 * v + (1 - beta2) * g * g
+    var = var - lr_t * m / (np.sqrt(v) + eps)
+    return var, m, v
+
+
+# --------------------------------------------------------------------------
+# D/G schedule (gan/core/model.py:470-478)
+# --------------------------------------------------------------------------
+class Counters:
+    """Mirror of MMD_GAN.set_counters: 5 D steps then 1 G step; 10 D steps
+    while step < 20 or step % 500 == 0."""
+
+    def __init__(self, dsteps=5, gsteps=1, start_dsteps=10):
+        self.dsteps, self.gsteps, self.start_dsteps = dsteps, gsteps, start_dsteps
+        self.d_counter = 0
+        self.g_counter = 0
+
+    def update(self, step):
+        if self.g_counter == 0:
+            d_steps = self.dsteps
+            if step % 500 == 0 or step < 20:
+                d_steps = self.start_dsteps
+            self.d_counter = (self.d_counter + 1) % (d_steps + 1)
+        if self.d_counter == 0:
+            self.g_counter = (self.g_counter + 1) % self.gsteps
+        return self.d_counter == 0     # True -> generator step
+
+
+# --------------------------------------------------------------------------
+# a tiny differentiable critic for end-to-end loss checks
+# --------------------------------------------------------------------------
+def mlp_critic(x, W1, W2):
+    """h = tanh(x W1); D(x) = h W2.  x [b, P]."""
+    h = np.tanh(np.asarray(x, np.float64) @ W1)
+    return h @ W2, h
+
+
+def mlp_critic_sq_jac(x, W1, W2):
+    """sum_i ||dD_i/dx||^2 per sample for the tanh MLP (analytic)."""
+    _, h = mlp_critic(x, W1, W2)
+    out = np.zeros(x.shape[0])
+    for i in range(W2.shape[1]):
+        # dD_i/dx = W1 diag(1-h^2) W2[:, i]
+        J = ((1 - h ** 2) * W2[:, i][None, :]) @ W1.T      # [b, P]
+        out += np.sum(J ** 2, axis=1)
+    return out
+
+
+def smmd_objective(spec, x_fake, x_real, W1, W2, sc=10.0, variant='grad', biased=False):
+    """Full SMMD generator loss for the tanh-MLP critic (smmd.py:10-19 +
+    model.py:366-403): returns (g_loss, mmd2, scale)."""
+    dG, _ = mlp_critic(x_fake, W1, W2)
+    dI, _ = mlp_critic(x_real, W1, W2)
+    m2 = mmd2(spec, dG, dI, biased)
+    J = float(np.mean(mlp_critic_sq_jac(x_real, W1, W2)))
+    nD = float(np.mean(dI ** 2))
+    sc_ = scale_factor(J, sc, nD, variant)
+    return m2 * sc_, m2, sc_

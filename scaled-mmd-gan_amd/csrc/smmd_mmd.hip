@@ -1,0 +1,865 @@
+// smmd_mmd.hip -- fused pairwise MMD^2 forward + unit gradient, and the
+// witness function of the gradient penalty, for gfx950 (MI355X).
+//
+// Reference being replaced:
+//   gan/core/mmd.py:18-188  kernel family (Gram expansion, clamp, exp/log)
+//   gan/core/mmd.py:194-220 unbiased / biased estimator
+//   gan/core/model.py:327-350 witness (K_XY_only row means) of the GP
+// The TF graph materialises three N x N matrices and runs ~7 elementwise
+// launches per matrix plus the same again for autodiff.  Here one launch
+// sweeps the rows of Z = [X; Y]: each wave owns one row, its 64 lanes stride
+// over all m + n columns, evaluate K and dK together (they share the exp),
+// and the row's gradient d mmd2 / d z_i is complete inside the wave (no
+// cross-block reduction for gradients).  Block sums go to a double-precision
+// slab; the last-arriving block reduces the slab in a fixed order (agent-scope
+// release/acquire, CDNA4 guide G16) and writes the estimator.
+#include "smmd_common.hpp"
+
+namespace smmd {
+
+struct KParams {
+    int n_terms;
+    float c1[SMMD_MAX_TERMS];   // RBF: -gamma_k ; RQ: 2*alpha_k
+    float c2[SMMD_MAX_TERMS];   // RQ: -alpha_k
+    float wt[SMMD_MAX_TERMS];
+    float add_dot;
+};
+
+// d/dz_i K(z_i, z_j) = alpha * z_i + beta * (z_i - z_j)
+template <int KIND>
+struct Kern;
+
+template <>
+struct Kern<SMMD_KIND_RBF> {   // mmd.py:55-116: K = sum wt exp(-gamma max(raw,0))
+    static __device__ __forceinline__ void eval(const KParams &p, float raw, float, float,
+                                                float, float &K, float &al, float &be) {
+        const float R = fmaxf(raw, 0.f);
+        float k = 0.f, dk = 0.f;
+        for (int t = 0; t < p.n_terms; ++t) {
+            const float e = p.wt[t] * expf(p.c1[t] * R);
+            k += e;
+            dk += p.c1[t] * e;
+        }
+        K = k;
+        al = 0.f;
+        be = (raw >= 0.f) ? 2.f * dk : 0.f;   // tf.maximum: ties pass the gradient
+    }
+};
+
+template <>
+struct Kern<SMMD_KIND_RQ> {    // mmd.py:143-188
+    static __device__ __forceinline__ void eval(const KParams &p, float raw, float dot, float,
+                                                float, float &K, float &al, float &be) {
+        const float R = fmaxf(raw, 0.f);
+        float k = 0.f, dk = 0.f;
+        for (int t = 0; t < p.n_terms; ++t) {
+            const float q = 1.f + R / p.c1[t];
+            const float e = p.wt[t] * expf(p.c2[t] * logf(q));
+            k += e;
+            dk += e * p.c2[t] / (q * p.c1[t]);
+        }
+        if (p.add_dot > 0.f) k += p.add_dot * dot;
+        K = k;
+        al = p.add_dot;
+        be = ((raw >= 0.f) ? 2.f * dk : 0.f) - p.add_dot;
+    }
+};
+
+__device__ __forceinline__ float mysqrt(float x) {      // mmd.py:12
+    return sqrtf(fmaxf(x + 1.0e-5f, 0.f));
+}
+__device__ __forceinline__ float mysqrt_grad(float x) {
+    const float xe = x + 1.0e-5f;
+    return (xe >= 0.f) ? 0.5f / sqrtf(xe) : 0.f;
+}
+
+template <>
+struct Kern<SMMD_KIND_DISTANCE> {   // mmd.py:18-37 (no clamp; eps inside sqrt)
+    static __device__ __forceinline__ void eval(const KParams &, float raw, float, float sqr,
+                                                float sqc, float &K, float &al, float &be) {
+        K = (mysqrt(sqr) + mysqrt(sqc)) - mysqrt(raw);
+        al = 2.f * mysqrt_grad(sqr);
+        be = -2.f * mysqrt_grad(raw);
+    }
+};
+
+template <>
+struct Kern<SMMD_KIND_DOT> {   // mmd.py:44-52
+    static __device__ __forceinline__ void eval(const KParams &, float, float dot, float,
+                                                float, float &K, float &al, float &be) {
+        K = dot;
+        al = 1.f;
+        be = -1.f;
+    }
+};
+
+template <int DT>
+__device__ __forceinline__ void load_feat(const float *__restrict__ p, int d, bool tanh_in,
+                                          float (&z)[DT]) {
+#pragma unroll
+    for (int k = 0; k < DT; ++k) z[k] = (k < d) ? p[k] : 0.f;
+    if (tanh_in) {
+#pragma unroll
+        for (int k = 0; k < DT; ++k) z[k] = tanhf(z[k]);
+    }
+}
+
+// <a, b> as a k-ordered fma chain: the same routine produces the Gram entries
+// and the squared norms, so raw D2 is exactly 0 on the diagonal as it is for
+// the reference's diag_part(XX) (mmd.py:60-67).
+template <int DT>
+__device__ __forceinline__ float dotk(const float (&a)[DT], const float (&b)[DT]) {
+    float s = a[0] * b[0];
+#pragma unroll
+    for (int k = 1; k < DT; ++k) s = fmaf(a[k], b[k], s);
+    return s;
+}
+
+struct MmdArgs {
+    const float *X;
+    const float *Y;
+    int m, n, d;
+    int x_begin, x_end, y_begin, y_end;
+    int tanh_in;
+    int trace_mode;      // exclude j == i from the gradient (const_diag False, unbiased)
+    int need_grad;
+    float gw_same_x, gw_same_y, gw_cross;   // gradient weights per block
+    float *grad_x;
+    float *grad_y;
+    double *partials;    // [gridDim.x][8]
+    unsigned *counter;
+    float *out_sums;
+    float *out_mmd2;
+    int biased;
+    int has_const;
+    double const_diag;
+    KParams kp;
+};
+
+__device__ __forceinline__ double estimator(const double *S, double m, double n, int biased,
+                                            int has_const, double c) {
+    // gan/core/mmd.py:199-220
+    if (biased) return S[0] / (m * m) + S[2] / (n * n) - 2.0 * S[1] / (m * n);
+    const double trX = has_const ? m * c : S[3];
+    const double trY = has_const ? n * c : S[4];
+    return (S[0] - trX) / (m * (m - 1.0)) + (S[2] - trY) / (n * (n - 1.0)) -
+           2.0 * S[1] / (m * n);
+}
+
+template <int DT, int KIND>
+__global__ __launch_bounds__(256) void mmd2_fused_kernel(MmdArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int wid = threadIdx.x >> 6;
+    const int nwaves = gridDim.x * 4;
+    const int nxr = a.x_end - a.x_begin;
+    const int nrows = nxr + (a.y_end - a.y_begin);
+    const bool tanh_in = a.tanh_in != 0;
+
+    float s_xx = 0.f, s_xy = 0.f, s_yy = 0.f, s_yx = 0.f, t_xx = 0.f, t_yy = 0.f;
+
+    for (int r = blockIdx.x * 4 + wid; r < nrows; r += nwaves) {
+        const bool isx = r < nxr;
+        const int ri = isx ? a.x_begin + r : a.y_begin + (r - nxr);
+        float zi[DT];
+        load_feat<DT>((isx ? a.X : a.Y) + (size_t)ri * a.d, a.d, tanh_in, zi);
+        const float sqi = dotk<DT>(zi, zi);
+        float acc[DT];
+#pragma unroll
+        for (int k = 0; k < DT; ++k) acc[k] = 0.f;
+        float aacc = 0.f;
+
+        // same-set block: XX for an X row, YY for a Y row
+        {
+            const float *S = isx ? a.X : a.Y;
+            const int ns = isx ? a.m : a.n;
+            const float w = isx ? a.gw_same_x : a.gw_same_y;
+            float sumK = 0.f, trK = 0.f;
+            for (int j = lane; j < ns; j += 64) {
+                float zc[DT];
+                load_feat<DT>(S + (size_t)j * a.d, a.d, tanh_in, zc);
+                const float dot = dotk<DT>(zi, zc);
+                const float sqc = dotk<DT>(zc, zc);
+                const float raw = (-2.f * dot + sqi) + sqc;   // mmd.py:67 order
+                float K, al, be;
+                Kern<KIND>::eval(a.kp, raw, dot, sqi, sqc, K, al, be);
+                sumK += K;
+                const bool diag = (j == ri);
+                if (diag) trK += K;
+                if (a.need_grad && !(diag && a.trace_mode)) {
+                    aacc = fmaf(w, al, aacc);
+                    const float c = w * be;
+#pragma unroll
+                    for (int k = 0; k < DT; ++k) acc[k] = fmaf(c, zi[k] - zc[k], acc[k]);
+                }
+            }
+            if (isx) { s_xx += sumK; t_xx += trK; } else { s_yy += sumK; t_yy += trK; }
+        }
+        // cross-set block: XY for an X row; YX (gradient only) for a Y row
+        if (isx || a.need_grad) {
+            const float *S = isx ? a.Y : a.X;
+            const int ns = isx ? a.n : a.m;
+            const float w = a.gw_cross;
+            float sumK = 0.f;
+            for (int j = lane; j < ns; j += 64) {
+                float zc[DT];
+                load_feat<DT>(S + (size_t)j * a.d, a.d, tanh_in, zc);
+                const float dot = dotk<DT>(zi, zc);
+                const float sqc = dotk<DT>(zc, zc);
+                const float raw = (-2.f * dot + sqi) + sqc;
+                float K, al, be;
+                Kern<KIND>::eval(a.kp, raw, dot, sqi, sqc, K, al, be);
+                sumK += K;
+                if (a.need_grad) {
+                    aacc = fmaf(w, al, aacc);
+                    const float c = w * be;
+#pragma unroll
+                    for (int k = 0; k < DT; ++k) acc[k] = fmaf(c, zi[k] - zc[k], acc[k]);
+                }
+            }
+            if (isx) s_xy += sumK; else s_yx += sumK;
+        }
+        if (a.need_grad) {
+            aacc = wave_sum(aacc);
+#pragma unroll
+            for (int k = 0; k < DT; ++k) acc[k] = wave_sum(acc[k]);
+            if (lane == 0) {
+                float *g = isx ? a.grad_x + (size_t)r * a.d : a.grad_y + (size_t)(r - nxr) * a.d;
+#pragma unroll
+                for (int k = 0; k < DT; ++k) {
+                    if (k < a.d) {
+                        float gk = fmaf(aacc, zi[k], acc[k]);
+                        if (tanh_in) gk *= 1.f - zi[k] * zi[k];
+                        g[k] = gk;
+                    }
+                }
+            }
+        }
+    }
+
+    // ---- block partial sums (fixed order), double precision slab ----------
+    __shared__ double red[4][8];
+    __shared__ int is_last;
+    float v[6] = {s_xx, s_xy, s_yy, t_xx, t_yy, s_yx};
+#pragma unroll
+    for (int k = 0; k < 6; ++k) v[k] = wave_sum(v[k]);
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) red[wid][k] = (double)v[k];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double *slab = a.partials + (size_t)blockIdx.x * 8;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) slab[k] = ((red[0][k] + red[1][k]) + red[2][k]) + red[3][k];
+        // publish: release at agent scope, then the ticket (CDNA4 guide G16)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned prev =
+            __hip_atomic_fetch_add(a.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        is_last = (prev == gridDim.x - 1);
+    }
+    __syncthreads();
+    if (!is_last || wid != 0) return;
+
+    // ---- last arriver: reduce all slabs in block order -------------------
+    if (lane == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    double S[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) S[k] = 0.0;
+    for (int b = lane; b < (int)gridDim.x; b += 64) {
+        const double *slab = a.partials + (size_t)b * 8;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) S[k] += slab[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) S[k] = wave_sum(S[k]);
+    if (lane == 0) {
+        if (a.out_sums) {
+            a.out_sums[0] = (float)S[0];
+            a.out_sums[1] = (float)S[1];
+            a.out_sums[2] = (float)S[2];
+            a.out_sums[3] = (float)S[3];
+            a.out_sums[4] = (float)S[4];
+            a.out_sums[5] = (float)S[5];
+            a.out_sums[6] = 0.f;
+            a.out_sums[7] = 0.f;
+        }
+        if (a.out_mmd2)
+            a.out_mmd2[0] =
+                (float)estimator(S, (double)a.m, (double)a.n, a.biased, a.has_const, a.const_diag);
+        __hip_atomic_store(a.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+__global__ void mmd2_combine_kernel(const float *sums, double m, double n, int biased,
+                                    int has_const, double c, float *out) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        double S[6];
+        for (int k = 0; k < 6; ++k) S[k] = (double)sums[k];
+        out[0] = (float)estimator(S, m, n, biased, has_const, c);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// witness:  w_i = mean_j K(h_i, r_j) - mean_j K(h_i, f_j)   (model.py:336-338)
+// dH_i = d(sum w)/dh_i.  One wave per row of H, lanes stride over R then F.
+// ---------------------------------------------------------------------------
+struct WitArgs {
+    const float *H;
+    const float *R;
+    const float *F;
+    int b, nr, nf, d;
+    int tanh_in;
+    float *out_w;
+    float *out_dH;
+    KParams kp;
+};
+
+template <int DT, int KIND>
+__global__ __launch_bounds__(256) void witness_fwd_kernel(WitArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int nwaves = gridDim.x * 4;
+    const bool tanh_in = a.tanh_in != 0;
+    for (int i = blockIdx.x * 4 + (threadIdx.x >> 6); i < a.b; i += nwaves) {
+        float hi[DT];
+        load_feat<DT>(a.H + (size_t)i * a.d, a.d, tanh_in, hi);
+        const float sqi = dotk<DT>(hi, hi);
+        float acc[DT];
+#pragma unroll
+        for (int k = 0; k < DT; ++k) acc[k] = 0.f;
+        float aacc = 0.f, wsum[2] = {0.f, 0.f};
+#pragma unroll
+        for (int set = 0; set < 2; ++set) {
+            const float *S = set == 0 ? a.R : a.F;
+            const int ns = set == 0 ? a.nr : a.nf;
+            const float w = (set == 0 ? 1.f : -1.f) / (float)ns;
+            for (int j = lane; j < ns; j += 64) {
+                float zc[DT];
+                load_feat<DT>(S + (size_t)j * a.d, a.d, tanh_in, zc);
+                const float dot = dotk<DT>(hi, zc);
+                const float sqc = dotk<DT>(zc, zc);
+                const float raw = (-2.f * dot + sqi) + sqc;
+                float K, al, be;
+                Kern<KIND>::eval(a.kp, raw, dot, sqi, sqc, K, al, be);
+                wsum[set] += K;
+                aacc = fmaf(w, al, aacc);
+                const float c = w * be;
+#pragma unroll
+                for (int k = 0; k < DT; ++k) acc[k] = fmaf(c, hi[k] - zc[k], acc[k]);
+            }
+        }
+        const float sr = wave_sum(wsum[0]), sf = wave_sum(wsum[1]);
+        aacc = wave_sum(aacc);
+#pragma unroll
+        for (int k = 0; k < DT; ++k) acc[k] = wave_sum(acc[k]);
+        if (lane == 0) {
+            // reduce_mean over axis 1 of each K_XY block (model.py:336)
+            if (a.out_w) a.out_w[i] = sr / (float)a.nr - sf / (float)a.nf;
+            if (a.out_dH) {
+#pragma unroll
+                for (int k = 0; k < DT; ++k)
+                    if (k < a.d) {
+                        float g = fmaf(aacc, hi[k], acc[k]);
+                        if (tanh_in) g *= 1.f - hi[k] * hi[k];
+                        a.out_dH[(size_t)i * a.d + k] = g;
+                    }
+            }
+        }
+    }
+}
+
+// Second-order term for the radial kernels (RBF / RQ incl. add_dot):
+//   L = sum_i <g_i, dH_i>,  dH_i = sum_j c_j [al h_i + be_ij (h_i - z_j)],
+//   be_ij = 2 f'(R_ij) [raw >= 0] - add_dot,  al = add_dot.
+//   dL/dh_i = sum_j c_j (al + be_ij) g_i + e_ij (h_i - z_j)
+//   dL/dz_j = sum_i -c_j be_ij g_i - e_ij (h_i - z_j)
+//   e_ij = 4 c_j f''(R_ij) [raw >= 0] <g_i, h_i - z_j>
+template <int KIND>
+__device__ __forceinline__ void radial_d2(const KParams &p, float raw, float &be, float &f2) {
+    const float R = fmaxf(raw, 0.f);
+    float d1 = 0.f, d2 = 0.f;
+    if (KIND == SMMD_KIND_RBF) {
+        for (int t = 0; t < p.n_terms; ++t) {
+            const float e = p.wt[t] * expf(p.c1[t] * R);
+            d1 += p.c1[t] * e;
+            d2 += p.c1[t] * p.c1[t] * e;
+        }
+    } else {
+        for (int t = 0; t < p.n_terms; ++t) {
+            const float q = 1.f + R / p.c1[t];
+            const float e = p.wt[t] * expf(p.c2[t] * logf(q));
+            const float dq = 1.f / p.c1[t];
+            const float g1 = e * p.c2[t] / q * dq;                     // de/dR
+            d1 += g1;
+            d2 += g1 * (p.c2[t] - 1.f) / q * dq;                       // d2e/dR2
+        }
+    }
+    const bool pass = raw >= 0.f;
+    be = (pass ? 2.f * d1 : 0.f) - (KIND == SMMD_KIND_RQ ? p.add_dot : 0.f);
+    f2 = pass ? d2 : 0.f;
+}
+
+struct WitBwdArgs {
+    const float *H;
+    const float *R;
+    const float *F;
+    const float *gdH;
+    int b, nr, nf, d;
+    float *gH;
+    float *gR;
+    float *gF;
+    KParams kp;
+};
+
+// rows of H: dL/dh_i
+template <int DT, int KIND>
+__global__ __launch_bounds__(256) void witness_bwd_h_kernel(WitBwdArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int nwaves = gridDim.x * 4;
+    const float al = (KIND == SMMD_KIND_RQ) ? a.kp.add_dot : 0.f;
+    for (int i = blockIdx.x * 4 + (threadIdx.x >> 6); i < a.b; i += nwaves) {
+        float hi[DT], gi[DT], acc[DT];
+        load_feat<DT>(a.H + (size_t)i * a.d, a.d, false, hi);
+        load_feat<DT>(a.gdH + (size_t)i * a.d, a.d, false, gi);
+        const float sqi = dotk<DT>(hi, hi);
+#pragma unroll
+        for (int k = 0; k < DT; ++k) acc[k] = 0.f;
+        float gcoef = 0.f;
+#pragma unroll
+        for (int set = 0; set < 2; ++set) {
+            const float *S = set == 0 ? a.R : a.F;
+            const int ns = set == 0 ? a.nr : a.nf;
+            const float c = (set == 0 ? 1.f : -1.f) / (float)ns;
+            for (int j = lane; j < ns; j += 64) {
+                float zc[DT], df[DT];
+                load_feat<DT>(S + (size_t)j * a.d, a.d, false, zc);
+                const float raw = (-2.f * dotk<DT>(hi, zc) + sqi) + dotk<DT>(zc, zc);
+                float be, f2;
+                radial_d2<KIND>(a.kp, raw, be, f2);
+#pragma unroll
+                for (int k = 0; k < DT; ++k) df[k] = hi[k] - zc[k];
+                const float e = 4.f * c * f2 * dotk<DT>(gi, df);
+                gcoef = fmaf(c, al + be, gcoef);
+#pragma unroll
+                for (int k = 0; k < DT; ++k) acc[k] = fmaf(e, df[k], acc[k]);
+            }
+        }
+        gcoef = wave_sum(gcoef);
+#pragma unroll
+        for (int k = 0; k < DT; ++k) acc[k] = wave_sum(acc[k]);
+        if (lane == 0) {
+#pragma unroll
+            for (int k = 0; k < DT; ++k)
+                if (k < a.d) a.gH[(size_t)i * a.d + k] = fmaf(gcoef, gi[k], acc[k]);
+        }
+    }
+}
+
+// rows of R then F: dL/dz_j (a sweep over H per column point)
+template <int DT, int KIND>
+__global__ __launch_bounds__(256) void witness_bwd_z_kernel(WitBwdArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int nwaves = gridDim.x * 4;
+    const int nz = a.nr + a.nf;
+    for (int r = blockIdx.x * 4 + (threadIdx.x >> 6); r < nz; r += nwaves) {
+        const bool isr = r < a.nr;
+        const int j = isr ? r : r - a.nr;
+        const float c = (isr ? 1.f : -1.f) / (float)(isr ? a.nr : a.nf);
+        float zj[DT], acc[DT];
+        load_feat<DT>((isr ? a.R : a.F) + (size_t)j * a.d, a.d, false, zj);
+        const float sqj = dotk<DT>(zj, zj);
+#pragma unroll
+        for (int k = 0; k < DT; ++k) acc[k] = 0.f;
+        for (int i = lane; i < a.b; i += 64) {
+            float hi[DT], gi[DT], df[DT];
+            load_feat<DT>(a.H + (size_t)i * a.d, a.d, false, hi);
+            load_feat<DT>(a.gdH + (size_t)i * a.d, a.d, false, gi);
+            // raw in the forward's order: row = h_i, column = z_j
+            const float raw = (-2.f * dotk<DT>(hi, zj) + dotk<DT>(hi, hi)) + sqj;
+            float be, f2;
+            radial_d2<KIND>(a.kp, raw, be, f2);
+#pragma unroll
+            for (int k = 0; k < DT; ++k) df[k] = hi[k] - zj[k];
+            const float e = 4.f * c * f2 * dotk<DT>(gi, df);
+#pragma unroll
+            for (int k = 0; k < DT; ++k) acc[k] = acc[k] - c * be * gi[k] - e * df[k];
+        }
+#pragma unroll
+        for (int k = 0; k < DT; ++k) acc[k] = wave_sum(acc[k]);
+        if (lane == 0) {
+            float *out = isr ? a.gR : a.gF;
+#pragma unroll
+            for (int k = 0; k < DT; ++k)
+                if (k < a.d) out[(size_t)j * a.d + k] = acc[k];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+static bool make_kparams(const smmd_kernel_desc *desc, KParams &kp) {
+    memset(&kp, 0, sizeof(kp));
+    if (desc->kind == SMMD_KIND_RBF || desc->kind == SMMD_KIND_RQ) {
+        if (desc->n_terms < 1 || desc->n_terms > SMMD_MAX_TERMS) return false;
+        kp.n_terms = desc->n_terms;
+        for (int t = 0; t < desc->n_terms; ++t) {
+            const double s = desc->param[t];
+            if (desc->kind == SMMD_KIND_RBF) {
+                if (!(s > 0)) return false;
+                kp.c1[t] = (float)(-(1.0 / (2.0 * s * s)));   // -gamma, mmd.py:69-70
+            } else {
+                if (!(s > 0)) return false;
+                kp.c1[t] = (float)(2.0 * s);                   // 2.*alpha, mmd.py:166
+                kp.c2[t] = (float)(-s);                        // -alpha, mmd.py:167
+            }
+            kp.wt[t] = (float)desc->wt[t];
+        }
+        kp.add_dot = (desc->kind == SMMD_KIND_RQ) ? (float)desc->add_dot : 0.f;
+        return true;
+    }
+    return desc->kind == SMMD_KIND_DISTANCE || desc->kind == SMMD_KIND_DOT;
+}
+
+static int pick_dt(int d) {
+    if (d <= 1) return 1;
+    if (d <= 2) return 2;
+    if (d <= 4) return 4;
+    if (d <= 8) return 8;
+    if (d <= 16) return 16;
+    if (d <= 32) return 32;
+    return 0;
+}
+
+static int mmd2_grid(int rows) {
+    int g = (rows + 3) / 4;
+    if (g > 2048) g = 2048;
+    if (g < 1) g = 1;
+    return g;
+}
+
+template <int DT, int KIND>
+static void launch_mmd2(const MmdArgs &a, int grid, hipStream_t s) {
+    hipLaunchKernelGGL((mmd2_fused_kernel<DT, KIND>), dim3(grid), dim3(256), 0, s, a);
+}
+
+template <int KIND>
+static bool dispatch_mmd2_dt(int dt, const MmdArgs &a, int grid, hipStream_t s) {
+    switch (dt) {
+        case 1: launch_mmd2<1, KIND>(a, grid, s); return true;
+        case 2: launch_mmd2<2, KIND>(a, grid, s); return true;
+        case 4: launch_mmd2<4, KIND>(a, grid, s); return true;
+        case 8: launch_mmd2<8, KIND>(a, grid, s); return true;
+        case 16: launch_mmd2<16, KIND>(a, grid, s); return true;
+        case 32: launch_mmd2<32, KIND>(a, grid, s); return true;
+    }
+    return false;
+}
+
+// ---------------------------------------------------------------------------
+// materialised kernel matrix K(A, B) [na, nb] and its backward -- the tuple API
+// of mmd._<kind>_kernel (mmd.py:18-188) for callers that index the matrices.
+// ---------------------------------------------------------------------------
+struct KmArgs {
+    const float *A;
+    const float *B;
+    const float *G;
+    int na, nb, d;
+    int tanh_in;
+    float *out;
+    float *gA;
+    float *gB;
+    KParams kp;
+};
+
+template <int DT, int KIND>
+__global__ __launch_bounds__(256) void kmat_fwd_kernel(KmArgs a) {
+    const int j = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int i = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (i >= a.na || j >= a.nb) return;
+    const bool t = a.tanh_in != 0;
+    float zi[DT], zc[DT];
+    load_feat<DT>(a.A + (size_t)i * a.d, a.d, t, zi);
+    load_feat<DT>(a.B + (size_t)j * a.d, a.d, t, zc);
+    const float dot = dotk<DT>(zi, zc);
+    const float sqi = dotk<DT>(zi, zi), sqc = dotk<DT>(zc, zc);
+    const float raw = (-2.f * dot + sqi) + sqc;
+    float K, al, be;
+    Kern<KIND>::eval(a.kp, raw, dot, sqi, sqc, K, al, be);
+    a.out[(size_t)i * a.nb + j] = K;
+}
+
+// one wave per output row; SIDE 0: rows of A (lanes over j), SIDE 1: rows of B
+template <int DT, int KIND, int SIDE>
+__global__ __launch_bounds__(256) void kmat_bwd_kernel(KmArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int nwaves = gridDim.x * 4;
+    const int nrows = SIDE == 0 ? a.na : a.nb;
+    const int ncols = SIDE == 0 ? a.nb : a.na;
+    const bool t = a.tanh_in != 0;
+    for (int r = blockIdx.x * 4 + (threadIdx.x >> 6); r < nrows; r += nwaves) {
+        float zr[DT], acc[DT];
+        load_feat<DT>((SIDE == 0 ? a.A : a.B) + (size_t)r * a.d, a.d, t, zr);
+        const float sqr = dotk<DT>(zr, zr);
+#pragma unroll
+        for (int k = 0; k < DT; ++k) acc[k] = 0.f;
+        float aacc = 0.f;
+        for (int c = lane; c < ncols; c += 64) {
+            float zc[DT];
+            load_feat<DT>((SIDE == 0 ? a.B : a.A) + (size_t)c * a.d, a.d, t, zc);
+            const float dot = dotk<DT>(zr, zc);
+            const float sqc = dotk<DT>(zc, zc);
+            // raw in the forward's orientation (row of A first)
+            const float raw = SIDE == 0 ? (-2.f * dot + sqr) + sqc : (-2.f * dot + sqc) + sqr;
+            float K, al, be;
+            Kern<KIND>::eval(a.kp, raw, dot, sqr, sqc, K, al, be);
+            const float g = SIDE == 0 ? a.G[(size_t)r * a.nb + c] : a.G[(size_t)c * a.nb + r];
+            aacc = fmaf(g, al, aacc);
+            const float cb = g * be;
+#pragma unroll
+            for (int k = 0; k < DT; ++k) acc[k] = fmaf(cb, zr[k] - zc[k], acc[k]);
+        }
+        aacc = wave_sum(aacc);
+#pragma unroll
+        for (int k = 0; k < DT; ++k) acc[k] = wave_sum(acc[k]);
+        if (lane == 0) {
+            float *o = (SIDE == 0 ? a.gA : a.gB) + (size_t)r * a.d;
+#pragma unroll
+            for (int k = 0; k < DT; ++k)
+                if (k < a.d) {
+                    float gk = fmaf(aacc, zr[k], acc[k]);
+                    if (t) gk *= 1.f - zr[k] * zr[k];
+                    o[k] = gk;
+                }
+        }
+    }
+}
+
+}  // namespace smmd
+
+using namespace smmd;
+
+extern "C" {
+
+const char *smmd_status_string(smmd_status s) {
+    switch (s) {
+        case SMMD_OK: return "SMMD_OK";
+        case SMMD_EINVAL: return "SMMD_EINVAL: invalid argument";
+        case SMMD_EHIP: return "SMMD_EHIP: HIP runtime/launch error";
+        case SMMD_EWORKSPACE: return "SMMD_EWORKSPACE: workspace missing or too small";
+        case SMMD_EUNSUPPORTED: return "SMMD_EUNSUPPORTED: not implemented in this build";
+    }
+    return "SMMD_?: unknown status";
+}
+
+int smmd_abi_version(void) { return 1; }
+
+size_t smmd_mmd2_workspace_bytes(int m, int n, int d) {
+    (void)d;
+    const int rows = (m > 0 ? m : 0) + (n > 0 ? n : 0);
+    return 256 + align_up((size_t)mmd2_grid(rows) * 8 * sizeof(double), 256);
+}
+
+smmd_status smmd_mmd2_fwd(const smmd_kernel_desc *desc, const float *X, int m, const float *Y,
+                          int n, int d, int biased, int x_begin, int x_end, int y_begin,
+                          int y_end, float *out_sums, float *out_mmd2, float *grad_x,
+                          float *grad_y, void *ws, size_t ws_bytes, smmd_stream_t stream) {
+    if (!desc || !X || !Y || m < 1 || n < 1 || d < 1) return SMMD_EINVAL;
+    if (x_begin < 0 || x_end < x_begin || x_end > m) return SMMD_EINVAL;
+    if (y_begin < 0 || y_end < y_begin || y_end > n) return SMMD_EINVAL;
+    const int need_grad = (grad_x != nullptr) || (grad_y != nullptr);
+    if (need_grad && (!grad_x || !grad_y)) return SMMD_EINVAL;
+    KParams kp;
+    if (!make_kparams(desc, kp)) return SMMD_EINVAL;
+    const int dt = pick_dt(d);
+    if (dt == 0) return SMMD_EUNSUPPORTED;
+    const int rows = (x_end - x_begin) + (y_end - y_begin);
+    const int grid = mmd2_grid(rows);
+    if (!ws || ws_bytes < smmd_mmd2_workspace_bytes(m, n, d)) return SMMD_EWORKSPACE;
+    if (rows == 0) return SMMD_EINVAL;
+
+    MmdArgs a;
+    memset(&a, 0, sizeof(a));
+    a.X = X;
+    a.Y = Y;
+    a.m = m;
+    a.n = n;
+    a.d = d;
+    a.x_begin = x_begin;
+    a.x_end = x_end;
+    a.y_begin = y_begin;
+    a.y_end = y_end;
+    a.tanh_in = desc->tanh_inputs ? 1 : 0;
+    a.biased = biased ? 1 : 0;
+    a.has_const = desc->has_const_diag ? 1 : 0;
+    a.const_diag = desc->const_diag;
+    a.trace_mode = (!a.biased && !a.has_const) ? 1 : 0;
+    a.need_grad = need_grad;
+    const double md = m, nd = n;
+    const double wxx = a.biased ? 1.0 / (md * md) : 1.0 / (md * (md - 1.0));
+    const double wyy = a.biased ? 1.0 / (nd * nd) : 1.0 / (nd * (nd - 1.0));
+    a.gw_same_x = (float)(2.0 * wxx);
+    a.gw_same_y = (float)(2.0 * wyy);
+    a.gw_cross = (float)(-2.0 / (md * nd));
+    a.grad_x = grad_x;
+    a.grad_y = grad_y;
+    a.counter = (unsigned *)ws;
+    a.partials = (double *)((char *)ws + 256);
+    a.out_sums = out_sums;
+    a.out_mmd2 = out_mmd2;
+    a.kp = kp;
+
+    hipStream_t s = (hipStream_t)stream;
+    bool ok = false;
+    switch (desc->kind) {
+        case SMMD_KIND_RBF: ok = dispatch_mmd2_dt<SMMD_KIND_RBF>(dt, a, grid, s); break;
+        case SMMD_KIND_RQ: ok = dispatch_mmd2_dt<SMMD_KIND_RQ>(dt, a, grid, s); break;
+        case SMMD_KIND_DISTANCE: ok = dispatch_mmd2_dt<SMMD_KIND_DISTANCE>(dt, a, grid, s); break;
+        case SMMD_KIND_DOT: ok = dispatch_mmd2_dt<SMMD_KIND_DOT>(dt, a, grid, s); break;
+    }
+    if (!ok) return SMMD_EINVAL;
+    return last_launch_status();
+}
+
+smmd_status smmd_mmd2_combine(const smmd_kernel_desc *desc, const float *sums, int m, int n,
+                              int biased, float *out_mmd2, smmd_stream_t stream) {
+    if (!desc || !sums || !out_mmd2 || m < 1 || n < 1) return SMMD_EINVAL;
+    hipLaunchKernelGGL(mmd2_combine_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, sums,
+                       (double)m, (double)n, biased ? 1 : 0, desc->has_const_diag ? 1 : 0,
+                       desc->const_diag, out_mmd2);
+    return last_launch_status();
+}
+
+smmd_status smmd_witness_fwd(const smmd_kernel_desc *desc, const float *H, int b, const float *R,
+                             int nr, const float *F, int nf, int d, float *out_w, float *out_dH,
+                             smmd_stream_t stream) {
+    if (!desc || !H || !R || !F || b < 1 || nr < 1 || nf < 1 || d < 1) return SMMD_EINVAL;
+    KParams kp;
+    if (!make_kparams(desc, kp)) return SMMD_EINVAL;
+    const int dt = pick_dt(d);
+    if (dt == 0) return SMMD_EUNSUPPORTED;
+    WitArgs a;
+    memset(&a, 0, sizeof(a));
+    a.H = H; a.R = R; a.F = F; a.b = b; a.nr = nr; a.nf = nf; a.d = d;
+    a.tanh_in = desc->tanh_inputs ? 1 : 0;
+    a.out_w = out_w; a.out_dH = out_dH; a.kp = kp;
+    const int grid = mmd2_grid(b);
+    hipStream_t s = (hipStream_t)stream;
+#define SMMD_WIT(DT_)                                                                          \
+    case DT_:                                                                                  \
+        switch (desc->kind) {                                                                  \
+            case SMMD_KIND_RBF: hipLaunchKernelGGL((witness_fwd_kernel<DT_, SMMD_KIND_RBF>), dim3(grid), dim3(256), 0, s, a); break; \
+            case SMMD_KIND_RQ: hipLaunchKernelGGL((witness_fwd_kernel<DT_, SMMD_KIND_RQ>), dim3(grid), dim3(256), 0, s, a); break; \
+            case SMMD_KIND_DISTANCE: hipLaunchKernelGGL((witness_fwd_kernel<DT_, SMMD_KIND_DISTANCE>), dim3(grid), dim3(256), 0, s, a); break; \
+            case SMMD_KIND_DOT: hipLaunchKernelGGL((witness_fwd_kernel<DT_, SMMD_KIND_DOT>), dim3(grid), dim3(256), 0, s, a); break; \
+            default: return SMMD_EINVAL;                                                        \
+        }                                                                                      \
+        break;
+    switch (dt) {
+        SMMD_WIT(1) SMMD_WIT(2) SMMD_WIT(4) SMMD_WIT(8) SMMD_WIT(16) SMMD_WIT(32)
+        default: return SMMD_EUNSUPPORTED;
+    }
+#undef SMMD_WIT
+    return last_launch_status();
+}
+
+smmd_status smmd_witness_bwd(const smmd_kernel_desc *desc, const float *H, int b, const float *R,
+                             int nr, const float *F, int nf, int d, const float *gdH, float *gH,
+                             float *gR, float *gF, smmd_stream_t stream) {
+    if (!desc || !H || !R || !F || !gdH || !gH || !gR || !gF) return SMMD_EINVAL;
+    if (b < 1 || nr < 1 || nf < 1 || d < 1) return SMMD_EINVAL;
+    KParams kp;
+    if (!make_kparams(desc, kp)) return SMMD_EINVAL;
+    // second derivatives implemented for the radial families on raw inputs
+    if (desc->tanh_inputs) return SMMD_EUNSUPPORTED;
+    if (desc->kind != SMMD_KIND_RBF && desc->kind != SMMD_KIND_RQ) return SMMD_EUNSUPPORTED;
+    const int dt = pick_dt(d);
+    if (dt == 0) return SMMD_EUNSUPPORTED;
+    WitBwdArgs a;
+    memset(&a, 0, sizeof(a));
+    a.H = H; a.R = R; a.F = F; a.gdH = gdH; a.b = b; a.nr = nr; a.nf = nf; a.d = d;
+    a.gH = gH; a.gR = gR; a.gF = gF; a.kp = kp;
+    hipStream_t s = (hipStream_t)stream;
+    const int gh = mmd2_grid(b), gz = mmd2_grid(nr + nf);
+#define SMMD_WB(DT_)                                                                           \
+    case DT_:                                                                                  \
+        if (desc->kind == SMMD_KIND_RBF) {                                                     \
+            hipLaunchKernelGGL((witness_bwd_h_kernel<DT_, SMMD_KIND_RBF>), dim3(gh), dim3(256), 0, s, a); \
+            hipLaunchKernelGGL((witness_bwd_z_kernel<DT_, SMMD_KIND_RBF>), dim3(gz), dim3(256), 0, s, a); \
+        } else {                                                                               \
+            hipLaunchKernelGGL((witness_bwd_h_kernel<DT_, SMMD_KIND_RQ>), dim3(gh), dim3(256), 0, s, a); \
+            hipLaunchKernelGGL((witness_bwd_z_kernel<DT_, SMMD_KIND_RQ>), dim3(gz), dim3(256), 0, s, a); \
+        }                                                                                      \
+        break;
+    switch (dt) {
+        SMMD_WB(1) SMMD_WB(2) SMMD_WB(4) SMMD_WB(8) SMMD_WB(16) SMMD_WB(32)
+        default: return SMMD_EUNSUPPORTED;
+    }
+#undef SMMD_WB
+    return last_launch_status();
+}
+
+#define SMMD_KM_SWITCH(DT_, BODY)                                                             \
+    case DT_:                                                                                  \
+        switch (desc->kind) {                                                                  \
+            case SMMD_KIND_RBF: { constexpr int KIND_ = SMMD_KIND_RBF; BODY; } break;          \
+            case SMMD_KIND_RQ: { constexpr int KIND_ = SMMD_KIND_RQ; BODY; } break;            \
+            case SMMD_KIND_DISTANCE: { constexpr int KIND_ = SMMD_KIND_DISTANCE; BODY; } break; \
+            case SMMD_KIND_DOT: { constexpr int KIND_ = SMMD_KIND_DOT; BODY; } break;          \
+            default: return SMMD_EINVAL;                                                        \
+        }                                                                                      \
+        break;
+
+smmd_status smmd_kernel_matrix_fwd(const smmd_kernel_desc *desc, const float *A, int na,
+                                   const float *B, int nb, int d, float *out,
+                                   smmd_stream_t stream) {
+    if (!desc || !A || !B || !out || na < 1 || nb < 1 || d < 1) return SMMD_EINVAL;
+    KParams kp;
+    if (!make_kparams(desc, kp)) return SMMD_EINVAL;
+    const int dt = pick_dt(d);
+    KmArgs a;
+    memset(&a, 0, sizeof(a));
+    a.A = A; a.B = B; a.na = na; a.nb = nb; a.d = d; a.tanh_in = desc->tanh_inputs ? 1 : 0;
+    a.out = out; a.kp = kp;
+    const dim3 grid((nb + 63) / 64, (na + 3) / 4);
+    hipStream_t s = (hipStream_t)stream;
+    switch (dt) {
+        SMMD_KM_SWITCH(1, hipLaunchKernelGGL((kmat_fwd_kernel<1, KIND_>), grid, dim3(256), 0, s, a))
+        SMMD_KM_SWITCH(2, hipLaunchKernelGGL((kmat_fwd_kernel<2, KIND_>), grid, dim3(256), 0, s, a))
+        SMMD_KM_SWITCH(4, hipLaunchKernelGGL((kmat_fwd_kernel<4, KIND_>), grid, dim3(256), 0, s, a))
+        SMMD_KM_SWITCH(8, hipLaunchKernelGGL((kmat_fwd_kernel<8, KIND_>), grid, dim3(256), 0, s, a))
+        SMMD_KM_SWITCH(16, hipLaunchKernelGGL((kmat_fwd_kernel<16, KIND_>), grid, dim3(256), 0, s, a))
+        SMMD_KM_SWITCH(32, hipLaunchKernelGGL((kmat_fwd_kernel<32, KIND_>), grid, dim3(256), 0, s, a))
+        default: return SMMD_EUNSUPPORTED;
+    }
+    return last_launch_status();
+}
+
+smmd_status smmd_kernel_matrix_bwd(const smmd_kernel_desc *desc, const float *A, int na,
+                                   const float *B, int nb, int d, const float *G, float *gA,
+                                   float *gB, smmd_stream_t stream) {
+    if (!desc || !A || !B || !G || na < 1 || nb < 1 || d < 1) return SMMD_EINVAL;
+    KParams kp;
+    if (!make_kparams(desc, kp)) return SMMD_EINVAL;
+    const int dt = pick_dt(d);
+    KmArgs a;
+    memset(&a, 0, sizeof(a));
+    a.A = A; a.B = B; a.G = G; a.na = na; a.nb = nb; a.d = d;
+    a.tanh_in = desc->tanh_inputs ? 1 : 0; a.gA = gA; a.gB = gB; a.kp = kp;
+    hipStream_t s = (hipStream_t)stream;
+    const int ga = mmd2_grid(na), gb = mmd2_grid(nb);
+#define SMMD_KMB(DT_)                                                                          \
+    SMMD_KM_SWITCH(DT_, {                                                                      \
+        if (gA) hipLaunchKernelGGL((kmat_bwd_kernel<DT_, KIND_, 0>), dim3(ga), dim3(256), 0, s, a); \
+        if (gB) hipLaunchKernelGGL((kmat_bwd_kernel<DT_, KIND_, 1>), dim3(gb), dim3(256), 0, s, a); \
+    })
+    switch (dt) {
+        SMMD_KMB(1) SMMD_KMB(2) SMMD_KMB(4) SMMD_KMB(8) SMMD_KMB(16) SMMD_KMB(32)
+        default: return SMMD_EUNSUPPORTED;
+    }
+#undef SMMD_KMB
+    return last_launch_status();
+}
+
+}  // extern "C"

@@ -1,0 +1,356 @@
+// smmd_scale.hip -- scaling regulariser of the SMMD/SWGAN loss and the
+// TF-semantics clip + Adam update, gfx950 (MI355X).  All HBM-bound.
+//
+// Reference: gan/core/ops.py:228-233 (squared_norm_jacobian),
+// gan/core/model.py:366-403 (add_scaling), gan/core/smmd.py:21-23, :40-42
+// (apply_scaling), gan/core/model.py:444-468 (clip_by_norm + Adam).
+#include "smmd_common.hpp"
+
+namespace smmd {
+
+constexpr int SQ_CHUNK = 4096;   // floats per block of the squared-norm pass
+
+// ---- per-(row, chunk) partial sum of squares -------------------------------
+__global__ __launch_bounds__(256) void sqnorm_partial_kernel(const float *__restrict__ jac,
+                                                             int64_t per_sample, int nchunk,
+                                                             int vec, double *__restrict__ part) {
+    const int row = blockIdx.x / nchunk, ch = blockIdx.x % nchunk;
+    const float *p = jac + (size_t)row * per_sample;
+    const int64_t b0 = (int64_t)ch * SQ_CHUNK;
+    const int64_t e0 = (b0 + SQ_CHUNK < per_sample) ? b0 + SQ_CHUNK : per_sample;
+    float acc = 0.f;
+    if (vec) {
+        for (int64_t i = b0 + threadIdx.x * 4; i < e0; i += 1024) {
+            const float4 x = *reinterpret_cast<const float4 *>(p + i);
+            acc = fmaf(x.x, x.x, acc);
+            acc = fmaf(x.y, x.y, acc);
+            acc = fmaf(x.z, x.z, acc);
+            acc = fmaf(x.w, x.w, acc);
+        }
+    } else {
+        for (int64_t i = b0 + threadIdx.x; i < e0; i += 256) acc = fmaf(p[i], p[i], acc);
+    }
+    __shared__ double red[4];
+    const double s = block_sum<4>((double)acc, red);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+// ---- finalize: per-sample norms, J, nD, scale, losses (one block) ----------
+__global__ __launch_bounds__(256) void scaled_loss_final_kernel(
+    const double *__restrict__ part, int n_cols, int b, int b_total, int nchunk,
+    const float *feat, int dof, const float *base_loss, float sc, int variant, int sqrt_scale,
+    float *out, float *per_sample_out) {
+    __shared__ double red[4];
+    double jsum = 0.0;
+    for (int s = threadIdx.x; s < b; s += 256) {
+        double ps = 0.0;
+        for (int c = 0; c < n_cols; ++c) {          // ops.py:232 sum over columns
+            const double *q = part + ((size_t)c * b + s) * nchunk;
+            double t = 0.0;
+            for (int k = 0; k < nchunk; ++k) t += q[k];
+            ps += t;
+        }
+        if (per_sample_out) per_sample_out[s] = (float)ps;
+        jsum += ps;
+    }
+    jsum = block_sum<4>(jsum, red);
+    double nd = 0.0;
+    if (variant == 1 && feat) {
+        double a = 0.0;
+        for (int i = threadIdx.x; i < b * dof; i += 256) a += (double)feat[i] * (double)feat[i];
+        a = block_sum<4>(a, red);
+        nd = a / ((double)b_total * dof);               // model.py:385
+    }
+    if (threadIdx.x == 0) {
+        const float J = (float)(jsum / (double)b_total); // model.py:384
+        const float nD = (float)nd;
+        const float q = (variant == 1) ? (J + nD) : J;  // model.py:387-390
+        const float scale = 1.f / (sc * q + 1.f);
+        const float base = base_loss ? base_loss[0] : 0.f;
+        const float f = sqrt_scale ? sqrtf(scale) : scale;   // smmd.py:22 / :41
+        const float g = base * f;
+        out[0] = g;
+        out[1] = -g;
+        out[2] = scale;
+        out[3] = J;
+        out[4] = nD;
+        out[5] = base;
+        out[6] = 0.f;
+        out[7] = 0.f;
+    }
+}
+
+// ---- backward: d base, d jac, d feat ---------------------------------------
+__global__ void scaled_loss_finalize_kernel(float *out, float sc, int variant, int sqrt_scale) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        const float q = (variant == 1) ? (out[3] + out[4]) : out[3];
+        const float scale = 1.f / (sc * q + 1.f);
+        const float g = out[5] * (sqrt_scale ? sqrtf(scale) : scale);
+        out[0] = g;
+        out[1] = -g;
+        out[2] = scale;
+    }
+}
+
+__global__ __launch_bounds__(256) void scaled_loss_bwd_kernel(
+    const float *__restrict__ jac, int64_t n_jac, int b, const float *__restrict__ feat,
+    int64_t n_feat, int dof, const float *fwd_out, float sc, int variant, int sqrt_scale,
+    const float *g_loss_grad, float *d_base, float *__restrict__ gjac, float *__restrict__ gfeat,
+    int vec) {
+    const float go = g_loss_grad ? g_loss_grad[0] : 1.f;
+    const float scale = fwd_out[2];
+    const float base = fwd_out[5];
+    const float f = sqrt_scale ? sqrtf(scale) : scale;
+    const float fp = sqrt_scale ? 0.5f / sqrtf(scale) : 1.f;
+    const float coefq = go * base * fp * (-sc * scale * scale);   // dL/dQ
+    const float cj = coefq * (2.f / (float)b);
+    const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t nth = (size_t)gridDim.x * blockDim.x;
+    if (tid == 0 && d_base) d_base[0] = go * f;
+    if (vec) {
+        const int64_t n4 = n_jac / 4;
+        for (size_t i = tid; i < (size_t)n4; i += nth) {
+            const float4 x = reinterpret_cast<const float4 *>(jac)[i];
+            float4 o;
+            o.x = cj * x.x; o.y = cj * x.y; o.z = cj * x.z; o.w = cj * x.w;
+            reinterpret_cast<float4 *>(gjac)[i] = o;
+        }
+        for (size_t i = (size_t)n4 * 4 + tid; i < (size_t)n_jac; i += nth) gjac[i] = cj * jac[i];
+    } else {
+        for (size_t i = tid; i < (size_t)n_jac; i += nth) gjac[i] = cj * jac[i];
+    }
+    if (gfeat && feat) {
+        const float cf = (variant == 1) ? coefq * (2.f / ((float)b * (float)dof)) : 0.f;
+        for (size_t i = tid; i < (size_t)n_feat; i += nth) gfeat[i] = cf * feat[i];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// flat multi-tensor clip / Adam.  Tensors are [off[i], off[i+1]) of one flat
+// buffer; each tensor is cut into OPT_CHUNK-element blocks.
+// ---------------------------------------------------------------------------
+constexpr int OPT_CHUNK = 16384;
+constexpr int OPT_MAX = 96;     // tensors per launch set (kernel-arg budget)
+
+struct OptTable {
+    int n;
+    int total_blocks;
+    int64_t off[OPT_MAX + 1];
+    int blk[OPT_MAX + 1];        // first block of each tensor
+};
+
+__device__ __forceinline__ int opt_find(const OptTable &t, int b) {
+    int lo = 0, hi = t.n - 1;
+    while (lo < hi) {                 // last i with blk[i] <= b
+        const int mid = (lo + hi + 1) >> 1;
+        if (t.blk[mid] <= b) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(256) void opt_sqsum_kernel(OptTable t, const float *__restrict__ g,
+                                                        float gscale, double *__restrict__ part) {
+    const int ti = opt_find(t, blockIdx.x);
+    const int64_t lo = t.off[ti] + (int64_t)(blockIdx.x - t.blk[ti]) * OPT_CHUNK;
+    const int64_t hi = (lo + OPT_CHUNK < t.off[ti + 1]) ? lo + OPT_CHUNK : t.off[ti + 1];
+    float acc = 0.f;
+    for (int64_t i = lo + threadIdx.x; i < hi; i += 256) {
+        const float x = g[i] * gscale;
+        acc = fmaf(x, x, acc);
+    }
+    __shared__ double red[4];
+    const double s = block_sum<4>((double)acc, red);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+// clip factor of tf.clip_by_norm (TF 1.x form): clip * min(rsqrt(ss), 1/clip)
+__device__ __forceinline__ float clip_factor(const OptTable &t, int ti, const double *part,
+                                             float clip, float *sh) {
+    if (threadIdx.x < 64) {
+        double s = 0.0;
+        for (int b = t.blk[ti] + (int)threadIdx.x; b < t.blk[ti + 1]; b += 64) s += part[b];
+        s = wave_sum(s);
+        if (threadIdx.x == 0) {
+            const float ss = (float)s;
+            const float inv = (ss > 0.f) ? rsqrtf(ss) : INFINITY;
+            sh[0] = clip * fminf(inv, 1.f / clip);
+        }
+    }
+    __syncthreads();
+    return sh[0];
+}
+
+__global__ __launch_bounds__(256) void opt_clip_kernel(OptTable t, float *__restrict__ g,
+                                                       const double *__restrict__ part, float clip) {
+    const int ti = opt_find(t, blockIdx.x);
+    __shared__ float sh[1];
+    const float f = clip_factor(t, ti, part, clip, sh);
+    const int64_t lo = t.off[ti] + (int64_t)(blockIdx.x - t.blk[ti]) * OPT_CHUNK;
+    const int64_t hi = (lo + OPT_CHUNK < t.off[ti + 1]) ? lo + OPT_CHUNK : t.off[ti + 1];
+    for (int64_t i = lo + threadIdx.x; i < hi; i += 256) g[i] = g[i] * f;
+}
+
+__global__ __launch_bounds__(256) void opt_adam_kernel(OptTable t, float *__restrict__ p,
+                                                       const float *__restrict__ g,
+                                                       float *__restrict__ m,
+                                                       float *__restrict__ v,
+                                                       const double *__restrict__ part,
+                                                       float gscale, float clip, float lr_t,
+                                                       float b1, float b2, float eps) {
+    const int ti = opt_find(t, blockIdx.x);
+    __shared__ float sh[1];
+    const float f = (clip > 0.f) ? clip_factor(t, ti, part, clip, sh) : 1.f;
+    const int64_t lo = t.off[ti] + (int64_t)(blockIdx.x - t.blk[ti]) * OPT_CHUNK;
+    const int64_t hi = (lo + OPT_CHUNK < t.off[ti + 1]) ? lo + OPT_CHUNK : t.off[ti + 1];
+    for (int64_t i = lo + threadIdx.x; i < hi; i += 256) {
+        float gi = g[i] * gscale;
+        if (clip > 0.f) gi = gi * f;
+        // Eigen ApplyAdam: m += (g - m)(1-b1); v += (g^2 - v)(1-b2);
+        //                  var -= lr_t m / (sqrt(v) + eps)
+        float mi = m[i], vi = v[i];
+        mi += (gi - mi) * (1.f - b1);
+        vi += (gi * gi - vi) * (1.f - b2);
+        m[i] = mi;
+        v[i] = vi;
+        p[i] -= (mi * lr_t) / (sqrtf(vi) + eps);
+    }
+}
+
+static bool build_opt(const int64_t *off, int first, int count, OptTable &t) {
+    memset(&t, 0, sizeof(t));
+    t.n = count;
+    int blocks = 0;
+    for (int i = 0; i <= count; ++i) {
+        t.off[i] = off[first + i];
+        if (i > 0 && t.off[i] < t.off[i - 1]) return false;
+    }
+    for (int i = 0; i < count; ++i) {
+        t.blk[i] = blocks;
+        const int64_t n = t.off[i + 1] - t.off[i];
+        blocks += (int)((n + OPT_CHUNK - 1) / OPT_CHUNK);
+        if (n == 0) blocks += 1;   // keep blk strictly increasing
+    }
+    t.blk[count] = blocks;
+    t.total_blocks = blocks;
+    return true;
+}
+
+}  // namespace smmd
+
+using namespace smmd;
+
+extern "C" {
+
+size_t smmd_scaled_loss_workspace_bytes(int rows, int64_t per_sample) {
+    if (rows < 1 || per_sample < 1) return 0;
+    const int64_t nchunk = (per_sample + SQ_CHUNK - 1) / SQ_CHUNK;
+    return align_up((size_t)rows * nchunk * sizeof(double), 256);
+}
+
+smmd_status smmd_scaled_loss_fwd(const float *jac, int n_cols, int b, int b_total,
+                                 int64_t per_sample, const float *feat, int dof,
+                                 const float *base_loss, float sc,
+                                 int variant, int sqrt_scale, float *out, float *per_sample_out,
+                                 void *ws, size_t ws_bytes, smmd_stream_t stream) {
+    if (!jac || !out || n_cols < 1 || b < 1 || per_sample < 1) return SMMD_EINVAL;
+    if (b_total < 1) b_total = b;
+    if (variant != 0 && variant != 1) return SMMD_EINVAL;
+    if (variant == 1 && (!feat || dof < 1)) return SMMD_EINVAL;
+    const int rows = n_cols * b;
+    if (!ws || ws_bytes < smmd_scaled_loss_workspace_bytes(rows, per_sample)) return SMMD_EWORKSPACE;
+    const int nchunk = (int)((per_sample + SQ_CHUNK - 1) / SQ_CHUNK);
+    const int vec = (per_sample % 4 == 0) && ((uintptr_t)jac % 16 == 0);
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(sqnorm_partial_kernel, dim3(rows * nchunk), dim3(256), 0, s, jac,
+                       per_sample, nchunk, vec, (double *)ws);
+    hipLaunchKernelGGL(scaled_loss_final_kernel, dim3(1), dim3(256), 0, s, (const double *)ws,
+                       n_cols, b, b_total, nchunk, feat, dof, base_loss, sc, variant, sqrt_scale,
+                       out, per_sample_out);
+    return last_launch_status();
+}
+
+smmd_status smmd_scaled_loss_finalize(float *out, float sc, int variant, int sqrt_scale,
+                                      smmd_stream_t stream) {
+    if (!out || (variant != 0 && variant != 1)) return SMMD_EINVAL;
+    hipLaunchKernelGGL(scaled_loss_finalize_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream,
+                       out, sc, variant, sqrt_scale);
+    return last_launch_status();
+}
+
+smmd_status smmd_scaled_loss_bwd(const float *jac, int n_cols, int b, int b_total,
+                                 int64_t per_sample, const float *feat, int dof,
+                                 const float *fwd_out, float sc,
+                                 int variant, int sqrt_scale, const float *g_loss_grad,
+                                 float *d_base, float *gjac, float *gfeat, smmd_stream_t stream) {
+    if (!jac || !fwd_out || !gjac || n_cols < 1 || b < 1 || per_sample < 1) return SMMD_EINVAL;
+    if (variant == 1 && (!feat || !gfeat || dof < 1)) return SMMD_EINVAL;
+    if (b_total < 1) b_total = b;
+    const int64_t n_jac = (int64_t)n_cols * b * per_sample;
+    const int vec = ((uintptr_t)jac % 16 == 0) && ((uintptr_t)gjac % 16 == 0);
+    int64_t blocks = (n_jac / 4 + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(scaled_loss_bwd_kernel, dim3((unsigned)blocks), dim3(256), 0,
+                       (hipStream_t)stream, jac, n_jac, b_total, feat, (int64_t)b * (dof > 0 ? dof : 0),
+                       dof, fwd_out, sc, variant, sqrt_scale, g_loss_grad, d_base, gjac, gfeat, vec);
+    return last_launch_status();
+}
+
+size_t smmd_opt_workspace_bytes(const int64_t *offsets, int n_tensors) {
+    if (!offsets || n_tensors < 1) return 0;
+    int64_t blocks = 0;
+    for (int i = 0; i < n_tensors; ++i) {
+        const int64_t n = offsets[i + 1] - offsets[i];
+        blocks += (n + OPT_CHUNK - 1) / OPT_CHUNK + (n == 0 ? 1 : 0);
+    }
+    return align_up((size_t)blocks * sizeof(double) + 256, 256);
+}
+
+smmd_status smmd_clip_by_norm_flat(float *grad, const int64_t *offsets, int n_tensors,
+                                   float clip_norm, void *ws, size_t ws_bytes,
+                                   smmd_stream_t stream) {
+    if (!grad || !offsets || n_tensors < 1 || !(clip_norm > 0.f)) return SMMD_EINVAL;
+    if (!ws || ws_bytes < smmd_opt_workspace_bytes(offsets, n_tensors)) return SMMD_EWORKSPACE;
+    hipStream_t s = (hipStream_t)stream;
+    for (int first = 0; first < n_tensors; first += OPT_MAX) {
+        const int count = (n_tensors - first < OPT_MAX) ? n_tensors - first : OPT_MAX;
+        OptTable t;
+        if (!build_opt(offsets, first, count, t)) return SMMD_EINVAL;
+        hipLaunchKernelGGL(opt_sqsum_kernel, dim3(t.total_blocks), dim3(256), 0, s, t,
+                           (const float *)grad, 1.f, (double *)ws);
+        hipLaunchKernelGGL(opt_clip_kernel, dim3(t.total_blocks), dim3(256), 0, s, t, grad,
+                           (const double *)ws, clip_norm);
+        smmd_status st = last_launch_status();
+        if (st != SMMD_OK) return st;
+    }
+    return SMMD_OK;
+}
+
+smmd_status smmd_adam_flat(float *param, const float *grad, float *m, float *v,
+                           const int64_t *offsets, int n_tensors, float grad_scale,
+                           float clip_norm, float lr, float beta1, float beta2, float eps,
+                           int64_t step, void *ws, size_t ws_bytes, smmd_stream_t stream) {
+    if (!param || !grad || !m || !v || !offsets || n_tensors < 1 || step < 1) return SMMD_EINVAL;
+    if (clip_norm > 0.f && (!ws || ws_bytes < smmd_opt_workspace_bytes(offsets, n_tensors)))
+        return SMMD_EWORKSPACE;
+    // tf.train.AdamOptimizer: lr_t = lr * sqrt(1 - b2^t) / (1 - b1^t)
+    const double lr_t = (double)lr * sqrt(1.0 - pow((double)beta2, (double)step)) /
+                        (1.0 - pow((double)beta1, (double)step));
+    hipStream_t s = (hipStream_t)stream;
+    for (int first = 0; first < n_tensors; first += OPT_MAX) {
+        const int count = (n_tensors - first < OPT_MAX) ? n_tensors - first : OPT_MAX;
+        OptTable t;
+        if (!build_opt(offsets, first, count, t)) return SMMD_EINVAL;
+        if (clip_norm > 0.f)
+            hipLaunchKernelGGL(opt_sqsum_kernel, dim3(t.total_blocks), dim3(256), 0, s, t, grad,
+                               grad_scale, (double *)ws);
+        hipLaunchKernelGGL(opt_adam_kernel, dim3(t.total_blocks), dim3(256), 0, s, t, param, grad,
+                           m, v, (const double *)ws, grad_scale, clip_norm, (float)lr_t, beta1,
+                           beta2, eps);
+        smmd_status st = last_launch_status();
+        if (st != SMMD_OK) return st;
+    }
+    return SMMD_OK;
+}
+
+}  // extern "C"

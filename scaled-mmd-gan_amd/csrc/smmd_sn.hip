@@ -1,0 +1,438 @@
+// smmd_sn.hip -- spectral normalisation of every SN layer of a network in one
+// set of launches (gfx950 / MI355X).
+//
+// Reference: gan/core/sn.py:12-59 (power iteration, sigma, W_bar = W/sigma),
+// gan/core/snops.py:82-84 (W_eff = s * W_bar), their TF autodiff (backward).
+// The TF graph runs ~8 small ops per layer per discriminator call (2 GEMV,
+// 2 norms, sigma, RealDiv, Mul, assign).  Here all layers are cut into
+// 64 x 256 fp32 tiles (64 KiB) and one launch walks every tile of every layer:
+//
+//   P1  tile -> partial column sums  sum_rows u_n W[n, k]     (HBM pass 1)
+//   P2  tile -> v_raw for its 256 columns from the P1 slab, then partial row
+//       dots sum_cols v_raw_k W[n, k]                          (HBM pass 2,
+//       usually served by the Infinity Cache: the net fits in 256 MiB)
+//   R2  one block per layer: ||v_raw||, v, u_raw, ||u_raw||, u', sigma
+//   P3  tile -> W_eff = (W / sigma) * s                        (read + write)
+//
+// Lanes own 4 consecutive columns (16-byte loads), waves own 16 rows, so a
+// wave-instruction reads 1 KiB of one row.  All reductions have a fixed order.
+#include "smmd_common.hpp"
+
+namespace smmd {
+
+constexpr int SN_TR = 64;      // tile rows
+constexpr int SN_TC = 256;     // tile cols (64 lanes x 4)
+constexpr int SN_RPW = SN_TR / 4;   // rows per wave
+constexpr int SN_CHUNK = 16;   // layers per launch set
+
+struct SnLayerDev {
+    const float *W;
+    float *W_eff;
+    float *u;        // user u (read at iteration 0, written when update_u)
+    float *v;
+    float *sigma;
+    const float *s;
+    const float *G;
+    float *gW;
+    float *gs;
+    float *p1;       // ws [nrt][K]
+    float *vraw;     // ws [K]
+    float *q2;       // ws [nct][N]
+    float *ucur;     // ws [N]  u' of the last iteration
+    float *dotp;     // ws [ntiles] backward partial <G, W>
+    int N, K, nrt, nct;
+    int tile_begin;
+    int vec;         // K % 4 == 0 and 16-byte aligned rows
+};
+
+struct SnTable {
+    int n_layers;
+    int total_tiles;
+    int iter;        // current power iteration (0 -> read layer.u)
+    int last_iter;
+    int update_u;
+    float eps;
+    SnLayerDev L[SN_CHUNK];
+};
+
+__device__ __forceinline__ int find_layer(const SnTable &t, int tile) {
+    int l = 0;
+    for (int i = 1; i < t.n_layers; ++i)
+        if (tile >= t.L[i].tile_begin) l = i;
+    return l;
+}
+
+// load the 16 rows x 4 cols this thread owns (zero outside the matrix)
+__device__ __forceinline__ void load_tile(const SnLayerDev &L, const float *__restrict__ base,
+                                          int r0, int c0, float4 (&w)[SN_RPW]) {
+    const bool full_cols = (c0 + 3 < L.K);
+#pragma unroll
+    for (int i = 0; i < SN_RPW; ++i) {
+        const int r = r0 + i;
+        float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (r < L.N) {
+            const float *p = base + (size_t)r * L.K + c0;
+            if (L.vec && full_cols) {
+                x = *reinterpret_cast<const float4 *>(p);
+            } else {
+                if (c0 + 0 < L.K) x.x = p[0];
+                if (c0 + 1 < L.K) x.y = p[1];
+                if (c0 + 2 < L.K) x.z = p[2];
+                if (c0 + 3 < L.K) x.w = p[3];
+            }
+        }
+        w[i] = x;
+    }
+}
+
+__global__ __launch_bounds__(256) void sn_p1_kernel(SnTable t) {
+    const int tile = blockIdx.x;
+    const SnLayerDev &L = t.L[find_layer(t, tile)];
+    const int lt = tile - L.tile_begin;
+    const int rt = lt / L.nct, ct = lt % L.nct;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int r0 = rt * SN_TR + w * SN_RPW;
+    const int c0 = ct * SN_TC + lane * 4;
+    const float *uin = (t.iter == 0) ? L.u : L.ucur;
+
+    float4 wt[SN_RPW];
+    load_tile(L, L.W, r0, c0, wt);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int i = 0; i < SN_RPW; ++i) {
+        const float un = (r0 + i < L.N) ? uin[r0 + i] : 0.f;
+        acc.x = fmaf(un, wt[i].x, acc.x);
+        acc.y = fmaf(un, wt[i].y, acc.y);
+        acc.z = fmaf(un, wt[i].z, acc.z);
+        acc.w = fmaf(un, wt[i].w, acc.w);
+    }
+    __shared__ float4 red[4][64];
+    red[w][lane] = acc;
+    __syncthreads();
+    if (w == 0) {
+        float4 s = red[0][lane];
+#pragma unroll
+        for (int i = 1; i < 4; ++i) {
+            s.x += red[i][lane].x; s.y += red[i][lane].y;
+            s.z += red[i][lane].z; s.w += red[i][lane].w;
+        }
+        float *dst = L.p1 + (size_t)rt * L.K;
+        const float sv[4] = {s.x, s.y, s.z, s.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (c0 + k < L.K) dst[c0 + k] = sv[k];
+    }
+}
+
+__global__ __launch_bounds__(256) void sn_p2_kernel(SnTable t) {
+    const int tile = blockIdx.x;
+    const SnLayerDev &L = t.L[find_layer(t, tile)];
+    const int lt = tile - L.tile_begin;
+    const int rt = lt / L.nct, ct = lt % L.nct;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int r0 = rt * SN_TR + w * SN_RPW;
+    const int c0 = ct * SN_TC + lane * 4;
+
+    float4 wt[SN_RPW];
+    load_tile(L, L.W, r0, c0, wt);   // issue the tile loads first
+
+    // v_raw for this tile's columns: fixed-order sum over row tiles of P1
+    __shared__ float vr[SN_TC];
+    {
+        const int c = ct * SN_TC + threadIdx.x;
+        float s = 0.f;
+        if (c < L.K)
+            for (int r = 0; r < L.nrt; ++r) s += L.p1[(size_t)r * L.K + c];
+        vr[threadIdx.x] = s;
+        if (rt == 0 && c < L.K) L.vraw[c] = s;
+    }
+    __syncthreads();
+    const float v0 = vr[lane * 4 + 0], v1 = vr[lane * 4 + 1];
+    const float v2 = vr[lane * 4 + 2], v3 = vr[lane * 4 + 3];
+    float part[SN_RPW];
+#pragma unroll
+    for (int i = 0; i < SN_RPW; ++i)
+        part[i] = fmaf(v3, wt[i].w, fmaf(v2, wt[i].z, fmaf(v1, wt[i].y, v0 * wt[i].x)));
+#pragma unroll
+    for (int i = 0; i < SN_RPW; ++i) part[i] = wave_sum(part[i]);
+    if (lane == 0) {
+        float *dst = L.q2 + (size_t)ct * L.N;
+#pragma unroll
+        for (int i = 0; i < SN_RPW; ++i)
+            if (r0 + i < L.N) dst[r0 + i] = part[i];
+    }
+}
+
+// one block (256 threads) per layer
+__global__ __launch_bounds__(256) void sn_r2_kernel(SnTable t) {
+    const SnLayerDev &L = t.L[blockIdx.x];
+    __shared__ double red[4];
+    __shared__ float sh_nv, sh_nu;
+    const int tid = threadIdx.x;
+    // ||v_raw||
+    double a = 0.0;
+    for (int k = tid; k < L.K; k += 256) a += (double)L.vraw[k] * (double)L.vraw[k];
+    a = block_sum<4>(a, red);
+    if (tid == 0) sh_nv = (float)sqrt(a) + t.eps;            // sn.py:13
+    __syncthreads();
+    const float nv = sh_nv;
+    for (int k = tid; k < L.K; k += 256) L.v[k] = L.vraw[k] / nv;
+    // u_raw = W v = (W v_raw) / nv ; ||u_raw||
+    double b = 0.0;
+    for (int n = tid; n < L.N; n += 256) {
+        float s = 0.f;
+        for (int c = 0; c < L.nct; ++c) s += L.q2[(size_t)c * L.N + n];
+        s = s / nv;
+        L.ucur[n] = s;                       // temporarily u_raw
+        b += (double)s * (double)s;
+    }
+    b = block_sum<4>(b, red);
+    if (tid == 0) sh_nu = (float)sqrt(b) + t.eps;
+    __syncthreads();
+    const float nu = sh_nu;
+    double sg = 0.0;
+    for (int n = tid; n < L.N; n += 256) {
+        const float ur = L.ucur[n];
+        const float un = ur / nu;            // u' = l2n(v W)
+        sg += (double)ur * (double)un;       // sigma = (v W) . u'   sn.py:42
+        L.ucur[n] = un;
+        if (t.update_u && t.last_iter) L.u[n] = un;
+    }
+    sg = block_sum<4>(sg, red);
+    if (tid == 0 && t.last_iter) L.sigma[0] = (float)sg;
+}
+
+__global__ __launch_bounds__(256) void sn_p3_kernel(SnTable t) {
+    const int tile = blockIdx.x;
+    const SnLayerDev &L = t.L[find_layer(t, tile)];
+    if (!L.W_eff) return;
+    const int lt = tile - L.tile_begin;
+    const int rt = lt / L.nct, ct = lt % L.nct;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int r0 = rt * SN_TR + w * SN_RPW;
+    const int c0 = ct * SN_TC + lane * 4;
+    const float sigma = L.sigma[0];
+    const float s = L.s ? L.s[0] : 1.f;
+    float4 wt[SN_RPW];
+    load_tile(L, L.W, r0, c0, wt);
+    const bool full_cols = (c0 + 3 < L.K);
+#pragma unroll
+    for (int i = 0; i < SN_RPW; ++i) {
+        const int r = r0 + i;
+        if (r >= L.N) break;
+        // W_bar = W / sigma (sn.py:43), then s * W_bar (snops.py:84)
+        float4 o;
+        o.x = (wt[i].x / sigma) * s;
+        o.y = (wt[i].y / sigma) * s;
+        o.z = (wt[i].z / sigma) * s;
+        o.w = (wt[i].w / sigma) * s;
+        float *p = L.W_eff + (size_t)r * L.K + c0;
+        if (L.vec && full_cols) {
+            *reinterpret_cast<float4 *>(p) = o;
+        } else {
+            if (c0 + 0 < L.K) p[0] = o.x;
+            if (c0 + 1 < L.K) p[1] = o.y;
+            if (c0 + 2 < L.K) p[2] = o.z;
+            if (c0 + 3 < L.K) p[3] = o.w;
+        }
+    }
+}
+
+// backward A: partial <G, W> per tile
+__global__ __launch_bounds__(256) void sn_bwd_a_kernel(SnTable t) {
+    const int tile = blockIdx.x;
+    const SnLayerDev &L = t.L[find_layer(t, tile)];
+    const int lt = tile - L.tile_begin;
+    const int rt = lt / L.nct, ct = lt % L.nct;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int r0 = rt * SN_TR + w * SN_RPW;
+    const int c0 = ct * SN_TC + lane * 4;
+    float4 wt[SN_RPW], gt[SN_RPW];
+    load_tile(L, L.W, r0, c0, wt);
+    load_tile(L, L.G, r0, c0, gt);
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < SN_RPW; ++i) {
+        acc = fmaf(gt[i].x, wt[i].x, acc);
+        acc = fmaf(gt[i].y, wt[i].y, acc);
+        acc = fmaf(gt[i].z, wt[i].z, acc);
+        acc = fmaf(gt[i].w, wt[i].w, acc);
+    }
+    __shared__ float red[4];
+    acc = block_sum<4>(acc, red);
+    if (threadIdx.x == 0) L.dotp[lt] = acc;
+}
+
+// backward B: gW = (s G)/sigma - (s <G,W> / sigma^2) u' v^T ; gs = <G,W>/sigma
+__global__ __launch_bounds__(256) void sn_bwd_b_kernel(SnTable t) {
+    const int tile = blockIdx.x;
+    const SnLayerDev &L = t.L[find_layer(t, tile)];
+    const int lt = tile - L.tile_begin;
+    const int rt = lt / L.nct, ct = lt % L.nct;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int r0 = rt * SN_TR + w * SN_RPW;
+    const int c0 = ct * SN_TC + lane * 4;
+    float4 gt[SN_RPW];
+    load_tile(L, L.G, r0, c0, gt);
+    __shared__ float sh_d;
+    if (w == 0) {
+        const int nt = L.nrt * L.nct;
+        double d = 0.0;
+        for (int i = lane; i < nt; i += 64) d += (double)L.dotp[i];
+        d = wave_sum(d);
+        if (lane == 0) sh_d = (float)d;
+    }
+    __syncthreads();
+    const float d = sh_d;                         // <G, W>
+    const float sigma = L.sigma[0];
+    const float s = L.s ? L.s[0] : 1.f;
+    if (lt == 0 && threadIdx.x == 0 && L.gs) L.gs[0] = d / sigma;
+    const float coef = (s * d) / (sigma * sigma);  // -dsigma factor
+    float vv[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) vv[k] = (c0 + k < L.K) ? L.v[c0 + k] : 0.f;
+    const bool full_cols = (c0 + 3 < L.K);
+#pragma unroll
+    for (int i = 0; i < SN_RPW; ++i) {
+        const int r = r0 + i;
+        if (r >= L.N) break;
+        const float cu = coef * L.ucur[r];
+        float4 o;
+        o.x = (s * gt[i].x) / sigma - cu * vv[0];
+        o.y = (s * gt[i].y) / sigma - cu * vv[1];
+        o.z = (s * gt[i].z) / sigma - cu * vv[2];
+        o.w = (s * gt[i].w) / sigma - cu * vv[3];
+        float *p = L.gW + (size_t)r * L.K + c0;
+        if (L.vec && full_cols) {
+            *reinterpret_cast<float4 *>(p) = o;
+        } else {
+            if (c0 + 0 < L.K) p[0] = o.x;
+            if (c0 + 1 < L.K) p[1] = o.y;
+            if (c0 + 2 < L.K) p[2] = o.z;
+            if (c0 + 3 < L.K) p[3] = o.w;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host side: workspace carve and launch sets
+// ---------------------------------------------------------------------------
+static int ceil_div(int a, int b) { return (a + b - 1) / b; }
+
+static size_t layer_ws_bytes(int N, int K) {
+    const int nrt = ceil_div(N, SN_TR), nct = ceil_div(K, SN_TC);
+    size_t b = 0;
+    b += align_up((size_t)nrt * K * 4, 256);   // p1
+    b += align_up((size_t)K * 4, 256);         // vraw
+    b += align_up((size_t)nct * N * 4, 256);   // q2
+    b += align_up((size_t)N * 4, 256);         // ucur
+    b += align_up((size_t)nrt * nct * 4, 256); // dotp
+    return b;
+}
+
+static bool build_table(const smmd_sn_layer *layers, int first, int count, char *ws,
+                        SnTable &t) {
+    memset(&t, 0, sizeof(t));
+    t.n_layers = count;
+    int tiles = 0;
+    // every chunk gets the workspace region of its layers (by global index)
+    size_t off = 0;
+    for (int i = 0; i < first; ++i) off += layer_ws_bytes(layers[i].N, layers[i].K);
+    for (int i = 0; i < count; ++i) {
+        const smmd_sn_layer &src = layers[first + i];
+        if (!src.W || src.N < 1 || src.K < 1) return false;
+        SnLayerDev &L = t.L[i];
+        L.W = src.W;
+        L.W_eff = src.W_eff;
+        L.u = src.u;
+        L.v = src.v;
+        L.sigma = src.sigma;
+        L.s = src.s;
+        L.G = src.G;
+        L.gW = src.gW;
+        L.gs = src.gs;
+        L.N = src.N;
+        L.K = src.K;
+        L.nrt = ceil_div(src.N, SN_TR);
+        L.nct = ceil_div(src.K, SN_TC);
+        L.tile_begin = tiles;
+        tiles += L.nrt * L.nct;
+        const uintptr_t al = (uintptr_t)src.W | (uintptr_t)(src.W_eff ? src.W_eff : src.W) |
+                             (uintptr_t)(src.G ? src.G : src.W) | (uintptr_t)(src.gW ? src.gW : src.W);
+        L.vec = (src.K % 4 == 0) && (al % 16 == 0);
+        char *p = ws + off;
+        L.p1 = (float *)p;   p += align_up((size_t)L.nrt * L.K * 4, 256);
+        L.vraw = (float *)p; p += align_up((size_t)L.K * 4, 256);
+        L.q2 = (float *)p;   p += align_up((size_t)L.nct * L.N * 4, 256);
+        L.ucur = (float *)p; p += align_up((size_t)L.N * 4, 256);
+        L.dotp = (float *)p; p += align_up((size_t)L.nrt * L.nct * 4, 256);
+        off += layer_ws_bytes(L.N, L.K);
+    }
+    t.total_tiles = tiles;
+    return true;
+}
+
+}  // namespace smmd
+
+using namespace smmd;
+
+extern "C" {
+
+size_t smmd_sn_workspace_bytes(const smmd_sn_layer *layers, int n_layers) {
+    if (!layers || n_layers < 1) return 0;
+    size_t b = 256;
+    for (int i = 0; i < n_layers; ++i) b += layer_ws_bytes(layers[i].N, layers[i].K);
+    return b;
+}
+
+smmd_status smmd_sn_power_iter(const smmd_sn_layer *layers, int n_layers, int num_iters,
+                               float eps, int update_u, void *ws, size_t ws_bytes,
+                               smmd_stream_t stream) {
+    if (!layers || n_layers < 1 || n_layers > SMMD_SN_MAX_LAYERS || num_iters < 1)
+        return SMMD_EINVAL;
+    for (int i = 0; i < n_layers; ++i)
+        if (!layers[i].u || !layers[i].v || !layers[i].sigma) return SMMD_EINVAL;
+    if (!ws || ws_bytes < smmd_sn_workspace_bytes(layers, n_layers)) return SMMD_EWORKSPACE;
+    hipStream_t s = (hipStream_t)stream;
+    for (int first = 0; first < n_layers; first += SN_CHUNK) {
+        const int count = (n_layers - first < SN_CHUNK) ? n_layers - first : SN_CHUNK;
+        SnTable t;
+        if (!build_table(layers, first, count, (char *)ws + 256, t)) return SMMD_EINVAL;
+        t.eps = eps;
+        t.update_u = update_u ? 1 : 0;
+        for (int it = 0; it < num_iters; ++it) {
+            t.iter = it;
+            t.last_iter = (it == num_iters - 1);
+            hipLaunchKernelGGL(sn_p1_kernel, dim3(t.total_tiles), dim3(256), 0, s, t);
+            hipLaunchKernelGGL(sn_p2_kernel, dim3(t.total_tiles), dim3(256), 0, s, t);
+            hipLaunchKernelGGL(sn_r2_kernel, dim3(t.n_layers), dim3(256), 0, s, t);
+        }
+        bool any_eff = false;
+        for (int i = 0; i < count; ++i) any_eff |= (t.L[i].W_eff != nullptr);
+        if (any_eff) hipLaunchKernelGGL(sn_p3_kernel, dim3(t.total_tiles), dim3(256), 0, s, t);
+        smmd_status st = last_launch_status();
+        if (st != SMMD_OK) return st;
+    }
+    return SMMD_OK;
+}
+
+smmd_status smmd_sn_weight_bwd(const smmd_sn_layer *layers, int n_layers, void *ws,
+                               size_t ws_bytes, smmd_stream_t stream) {
+    if (!layers || n_layers < 1 || n_layers > SMMD_SN_MAX_LAYERS) return SMMD_EINVAL;
+    for (int i = 0; i < n_layers; ++i)
+        if (!layers[i].G || !layers[i].gW || !layers[i].v || !layers[i].sigma) return SMMD_EINVAL;
+    if (!ws || ws_bytes < smmd_sn_workspace_bytes(layers, n_layers)) return SMMD_EWORKSPACE;
+    hipStream_t s = (hipStream_t)stream;
+    for (int first = 0; first < n_layers; first += SN_CHUNK) {
+        const int count = (n_layers - first < SN_CHUNK) ? n_layers - first : SN_CHUNK;
+        SnTable t;
+        if (!build_table(layers, first, count, (char *)ws + 256, t)) return SMMD_EINVAL;
+        hipLaunchKernelGGL(sn_bwd_a_kernel, dim3(t.total_tiles), dim3(256), 0, s, t);
+        hipLaunchKernelGGL(sn_bwd_b_kernel, dim3(t.total_tiles), dim3(256), 0, s, t);
+        smmd_status st = last_launch_status();
+        if (st != SMMD_OK) return st;
+    }
+    return SMMD_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,170 @@
+"""ctypes binding of libsmmd_hip.so (the C ABI in include/smmd_hip.h).
+
+The library is the only compute path for the hot ops: there is no CPU or
+eager-PyTorch fallback.  Importing this module does not touch the GPU;
+``lib()`` loads the shared object on first use and raises ``SmmdLibraryError``
+when it is missing, so a box without the build fails loudly.
+
+Device buffers are torch tensors (PyTorch is the allocator and the stream
+owner); every call is issued on ``torch.cuda.current_stream()``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must be imported before the .so: shares HIP runtime)
+
+_PKG_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+LIB_PATH = os.environ.get('SMMD_HIP_LIB', os.path.join(_PKG_ROOT, 'lib', 'libsmmd_hip.so'))
+
+SMMD_MAX_TERMS = 8
+SMMD_SN_MAX_LAYERS = 32
+ABI_VERSION = 1
+
+KIND_RBF, KIND_RQ, KIND_DISTANCE, KIND_DOT = 0, 1, 2, 3
+
+
+class SmmdLibraryError(RuntimeError):
+    """libsmmd_hip.so is missing or failed to load."""
+
+
+class SmmdError(RuntimeError):
+    """A libsmmd_hip.so entry point returned a non-OK smmd_status."""
+
+
+class KernelDesc(ctypes.Structure):
+    _fields_ = [('kind', ctypes.c_int32),
+                ('n_terms', ctypes.c_int32),
+                ('param', ctypes.c_double * SMMD_MAX_TERMS),
+                ('wt', ctypes.c_double * SMMD_MAX_TERMS),
+                ('add_dot', ctypes.c_double),
+                ('tanh_inputs', ctypes.c_int32),
+                ('has_const_diag', ctypes.c_int32),
+                ('const_diag', ctypes.c_double)]
+
+
+class SnLayer(ctypes.Structure):
+    _fields_ = [('W', ctypes.c_void_p),
+                ('W_eff', ctypes.c_void_p),
+                ('u', ctypes.c_void_p),
+                ('v', ctypes.c_void_p),
+                ('sigma', ctypes.c_void_p),
+                ('s', ctypes.c_void_p),
+                ('G', ctypes.c_void_p),
+                ('gW', ctypes.c_void_p),
+                ('gs', ctypes.c_void_p),
+                ('N', ctypes.c_int32),
+                ('K', ctypes.c_int32)]
+
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_I64 = ctypes.c_int64
+_F = ctypes.c_float
+_SZ = ctypes.c_size_t
+
+# name -> (restype, argtypes)
+_SIGS = {
+    'smmd_status_string': (ctypes.c_char_p, [_I]),
+    'smmd_abi_version': (_I, []),
+    'smmd_mmd2_workspace_bytes': (_SZ, [_I, _I, _I]),
+    'smmd_mmd2_fwd': (_I, [ctypes.POINTER(KernelDesc), _P, _I, _P, _I, _I, _I, _I, _I, _I, _I,
+                           _P, _P, _P, _P, _P, _SZ, _P]),
+    'smmd_mmd2_combine': (_I, [ctypes.POINTER(KernelDesc), _P, _I, _I, _I, _P, _P]),
+    'smmd_witness_fwd': (_I, [ctypes.POINTER(KernelDesc), _P, _I, _P, _I, _P, _I, _I, _P, _P, _P]),
+    'smmd_witness_bwd': (_I, [ctypes.POINTER(KernelDesc), _P, _I, _P, _I, _P, _I, _I, _P, _P, _P,
+                              _P, _P]),
+    'smmd_kernel_matrix_fwd': (_I, [ctypes.POINTER(KernelDesc), _P, _I, _P, _I, _I, _P, _P]),
+    'smmd_kernel_matrix_bwd': (_I, [ctypes.POINTER(KernelDesc), _P, _I, _P, _I, _I, _P, _P, _P,
+                                    _P]),
+    'smmd_scaled_loss_workspace_bytes': (_SZ, [_I, _I64]),
+    'smmd_scaled_loss_fwd': (_I, [_P, _I, _I, _I, _I64, _P, _I, _P, _F, _I, _I, _P, _P, _P, _SZ,
+                                  _P]),
+    'smmd_scaled_loss_finalize': (_I, [_P, _F, _I, _I, _P]),
+    'smmd_scaled_loss_bwd': (_I, [_P, _I, _I, _I, _I64, _P, _I, _P, _F, _I, _I, _P, _P, _P, _P,
+                                  _P]),
+    'smmd_sn_workspace_bytes': (_SZ, [ctypes.POINTER(SnLayer), _I]),
+    'smmd_sn_power_iter': (_I, [ctypes.POINTER(SnLayer), _I, _I, _F, _I, _P, _SZ, _P]),
+    'smmd_sn_weight_bwd': (_I, [ctypes.POINTER(SnLayer), _I, _P, _SZ, _P]),
+    'smmd_opt_workspace_bytes': (_SZ, [ctypes.POINTER(ctypes.c_int64), _I]),
+    'smmd_clip_by_norm_flat': (_I, [_P, ctypes.POINTER(ctypes.c_int64), _I, _F, _P, _SZ, _P]),
+    'smmd_adam_flat': (_I, [_P, _P, _P, _P, ctypes.POINTER(ctypes.c_int64), _I, _F, _F, _F, _F,
+                            _F, _F, _I64, _P, _SZ, _P]),
+}
+
+EXPORTED_SYMBOLS = tuple(_SIGS)
+
+_lock = threading.Lock()
+_lib = None
+
+
+def lib():
+    """Load libsmmd_hip.so once (raises SmmdLibraryError if absent)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise SmmdLibraryError(
+                    'libsmmd_hip.so not found at %s -- build it with '
+                    '`python -c "import __graft_entry__ as g; g.build()"` or '
+                    '`make -C scaled-mmd-gan_amd/csrc`' % LIB_PATH)
+            try:
+                handle = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+            except OSError as e:
+                raise SmmdLibraryError('failed to load %s: %s' % (LIB_PATH, e)) from e
+            for name, (res, args) in _SIGS.items():
+                fn = getattr(handle, name)
+                fn.restype = res
+                fn.argtypes = args
+            if handle.smmd_abi_version() != ABI_VERSION:
+                raise SmmdLibraryError('ABI version mismatch')
+            _lib = handle
+    return _lib
+
+
+def check(status: int, what: str):
+    if status != 0:
+        msg = lib().smmd_status_string(status).decode()
+        raise SmmdError('%s failed: %s' % (what, msg))
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_handle(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def require_cuda(*tensors):
+    for t in tensors:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise SmmdError('libsmmd_hip needs device tensors (got %s on %s): there is no CPU '
+                            'path' % (tuple(t.shape), t.device))
+        if t.dtype != torch.float32:
+            raise SmmdError('libsmmd_hip computes in fp32 (got %s)' % t.dtype)
+
+
+# ---------------------------------------------------------------------------
+# workspaces: zero-filled at allocation, owned per (device, stream, tag)
+# ---------------------------------------------------------------------------
+_ws_cache = {}
+
+
+def workspace(tag: str, nbytes: int, device: torch.device):
+    key = (device.index, torch.cuda.current_stream(device).cuda_stream, tag)
+    buf = _ws_cache.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.zeros(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+        _ws_cache[key] = buf
+    return buf
+
+
+def clear_workspaces():
+    _ws_cache.clear()

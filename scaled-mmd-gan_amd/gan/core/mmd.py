@@ -1,0 +1,373 @@
+"""MMD kernels and the MMD^2 estimator on the MI355X hot path.
+
+Drop-in for the reference's ``gan/core/mmd.py`` (names, signatures, default
+parameters and the ``(K_XX, K_XY, K_YY, const_diagonal)`` contract of
+``_<kind>_kernel``), re-implemented on ``libsmmd_hip.so``:
+
+* ``mmd2(_rbf_kernel(X, Y))`` -- the loss of ``SMMD.set_loss``
+  (gan/core/smmd.py:11-15) -- runs as ONE fused HIP launch that never
+  materialises the N x N matrices and produces d mmd2 / dX, dY in the same
+  sweep (``smmd_mmd2_fwd``).
+* The kernel functions return a lazy :class:`KernelMatrices`; its elements are
+  materialised (by ``smmd_kernel_matrix_fwd``) only when a caller indexes or
+  unpacks it, exactly like the reference tuple.
+* ``K_XY_only=True`` returns the materialised K_XY (gan/core/mmd.py:72-73).
+
+All arithmetic is fp32 on the GPU.  There is no CPU path: tensors must live on
+a ROCm device and the library must be built (see ``_lib``).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import torch
+import torch.distributed as dist
+
+from . import _lib
+
+_eps = 1.0e-5   # gan/core/mmd.py:6
+
+
+def mysqrt(x):
+    """sqrt(max(x + eps, 0))  (gan/core/mmd.py:12)."""
+    return torch.sqrt(torch.clamp(x + _eps, min=0.0))
+
+
+# ---------------------------------------------------------------------------
+# kernel specification
+# ---------------------------------------------------------------------------
+@dataclass(frozen=True)
+class KernelSpec:
+    """One member of the kernel family (gan/core/mmd.py:18-188).
+
+    const_diag is None where the reference returns ``False`` (the estimator
+    then subtracts the trace, mmd.py:212-213)."""
+    name: str
+    kind: int
+    params: tuple = ()
+    wts: tuple = ()
+    add_dot: float = 0.0
+    tanh: bool = False
+    const_diag: float | None = None
+    _desc: object = field(default=None, compare=False, repr=False)
+
+    def desc(self):
+        d = _lib.KernelDesc()
+        d.kind = self.kind
+        d.n_terms = len(self.params)
+        for i, (p, w) in enumerate(zip(self.params, self.wts)):
+            d.param[i] = float(p)
+            d.wt[i] = float(w)
+        d.add_dot = float(self.add_dot)
+        d.tanh_inputs = 1 if self.tanh else 0
+        d.has_const_diag = 0 if self.const_diag is None else 1
+        d.const_diag = 0.0 if self.const_diag is None else float(self.const_diag)
+        return d
+
+
+_RQ_DOT = {'mix_rq': 0.0, 'mix_rq_dot': .1, 'mix_rq_1dot': 1., 'mix_rq_10dot': 10.,
+           'mix_rq_01dot': .1, 'mix_rq_001dot': .01, 'tanh_mix_rq': 0.0}
+
+KERNEL_NAMES = ('rbf', 'mix_rbf', 'mix_rq', 'mix_rq_dot', 'mix_rq_1dot', 'mix_rq_10dot',
+                'mix_rq_01dot', 'mix_rq_001dot', 'tanh_mix_rq', 'distance', 'tanh_distance',
+                'dot')
+
+
+def get_kernel_spec(name: str, **kw) -> KernelSpec:
+    """``config.kernel`` string -> KernelSpec with the reference defaults."""
+    if name == 'rbf':                                           # mmd.py:55
+        sigma, wt = kw.get('sigma', 1.), kw.get('wt', 1.)
+        return KernelSpec('rbf', _lib.KIND_RBF, (sigma,), (wt,), const_diag=float(wt))
+    if name == 'mix_rbf':                                       # mmd.py:85-87
+        sigmas = tuple(kw.get('sigmas', (2.0, 5.0, 10.0, 20.0, 40.0, 80.0)))
+        wts = tuple(kw.get('wts') or [1] * len(sigmas))
+        return KernelSpec('mix_rbf', _lib.KIND_RBF, sigmas, wts, const_diag=float(sum(wts)))
+    if name in _RQ_DOT:                                         # mmd.py:119-188
+        alphas = tuple(kw.get('alphas', (.1, 1., 10.)))
+        wts = tuple(kw.get('wts') or [1.] * len(alphas))
+        add_dot = float(kw.get('add_dot', _RQ_DOT[name]))
+        # quirk kept: const diagonal = sum(wts) even when add_dot > 0 (mmd.py:182-188)
+        return KernelSpec(name, _lib.KIND_RQ, alphas, wts, add_dot=add_dot,
+                          tanh=(name == 'tanh_mix_rq'), const_diag=float(sum(wts)))
+    if name in ('distance', 'tanh_distance'):                   # mmd.py:18-41
+        return KernelSpec(name, _lib.KIND_DISTANCE, tanh=(name == 'tanh_distance'))
+    if name == 'dot':                                           # mmd.py:44-52
+        return KernelSpec('dot', _lib.KIND_DOT)
+    raise ValueError('unknown kernel %r (known: %s)' % (name, ', '.join(KERNEL_NAMES)))
+
+
+def _as_spec(kernel, **kw) -> KernelSpec:
+    if isinstance(kernel, KernelSpec):
+        return kernel
+    return get_kernel_spec(kernel, **kw)
+
+
+def _features(t):
+    if t.dim() == 1:
+        t = t.unsqueeze(1)
+    if t.dim() != 2:
+        raise ValueError('critic features must be [batch, dof] (got %s)' % (tuple(t.shape),))
+    _lib.require_cuda(t)
+    return t.contiguous()
+
+
+# ---------------------------------------------------------------------------
+# fused MMD^2 (forward + unit gradient in one launch)
+# ---------------------------------------------------------------------------
+class _MMD2Fused(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, X, Y, spec, biased, group):
+        X = _features(X)
+        Y = _features(Y)
+        if X.shape[1] != Y.shape[1]:
+            raise ValueError('X and Y feature dims differ: %d vs %d' % (X.shape[1], Y.shape[1]))
+        dev = X.device
+        L = _lib.lib()
+        need_grad = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
+        d = X.shape[1]
+        if group is not None and dist.get_world_size(group) > 1:
+            world, rank = dist.get_world_size(group), dist.get_rank(group)
+            ml, nl = X.shape[0], Y.shape[0]
+            Xa = torch.empty((world * ml, d), device=dev, dtype=torch.float32)
+            Ya = torch.empty((world * nl, d), device=dev, dtype=torch.float32)
+            dist.all_gather_into_tensor(Xa, X, group=group)
+            dist.all_gather_into_tensor(Ya, Y, group=group)
+            rows = (rank * ml, (rank + 1) * ml, rank * nl, (rank + 1) * nl)
+        else:
+            group = None
+            Xa, Ya = X, Y
+            rows = (0, X.shape[0], 0, Y.shape[0])
+        m, n = Xa.shape[0], Ya.shape[0]
+        sums = torch.empty(8, device=dev, dtype=torch.float32)
+        out = torch.empty(1, device=dev, dtype=torch.float32)
+        gx = torch.empty_like(X) if need_grad else None
+        gy = torch.empty_like(Y) if need_grad else None
+        nbytes = L.smmd_mmd2_workspace_bytes(m, n, d)
+        ws = _lib.workspace('mmd2', nbytes, dev)
+        desc = spec.desc()
+        _lib.check(L.smmd_mmd2_fwd(desc, _lib.ptr(Xa), m, _lib.ptr(Ya), n, d, 1 if biased else 0,
+                                   *rows, _lib.ptr(sums), _lib.ptr(out), _lib.ptr(gx),
+                                   _lib.ptr(gy), _lib.ptr(ws), ws.numel(),
+                                   _lib.stream_handle(dev)), 'smmd_mmd2_fwd')
+        if group is not None:
+            dist.all_reduce(sums, group=group)
+            _lib.check(L.smmd_mmd2_combine(desc, _lib.ptr(sums), m, n, 1 if biased else 0,
+                                           _lib.ptr(out), _lib.stream_handle(dev)),
+                       'smmd_mmd2_combine')
+        ctx.save_for_backward(gx, gy)
+        ctx.mark_non_differentiable(sums)
+        return out.view(()), sums
+
+    @staticmethod
+    def backward(ctx, g_mmd2, g_sums):
+        gx, gy = ctx.saved_tensors
+        dX = dY = None
+        if gx is not None:
+            dX = gx * g_mmd2
+            dY = gy * g_mmd2
+        return dX, dY, None, None, None
+
+
+def mmd2_fused(X, Y, kernel='rbf', biased=False, process_group=None, return_sums=False, **kw):
+    """mmd.mmd2(mmd._<kernel>_kernel(X, Y), biased) as one HIP launch.
+
+    ``process_group`` (a torch.distributed group with >1 ranks) selects the
+    all-gather mode: every rank contributes its local rows of X and Y, sees
+    the full (world * batch) pairwise kernel, and gets the same estimator
+    (one all_gather per input + one all_reduce of 8 floats)."""
+    spec = _as_spec(kernel, **kw)
+    val, sums = _MMD2Fused.apply(X, Y, spec, bool(biased), process_group)
+    return (val, sums) if return_sums else val
+
+
+# ---------------------------------------------------------------------------
+# materialised kernel matrices (tuple API)
+# ---------------------------------------------------------------------------
+class _KernelMatrix(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, A, B, spec):
+        A = _features(A)
+        B = _features(B)
+        L = _lib.lib()
+        out = torch.empty((A.shape[0], B.shape[0]), device=A.device, dtype=torch.float32)
+        _lib.check(L.smmd_kernel_matrix_fwd(spec.desc(), _lib.ptr(A), A.shape[0], _lib.ptr(B),
+                                            B.shape[0], A.shape[1], _lib.ptr(out),
+                                            _lib.stream_handle(A.device)),
+                   'smmd_kernel_matrix_fwd')
+        ctx.save_for_backward(A, B)
+        ctx.spec = spec
+        return out
+
+    @staticmethod
+    def backward(ctx, G):
+        A, B = ctx.saved_tensors
+        G = G.contiguous()
+        gA = torch.empty_like(A) if ctx.needs_input_grad[0] else None
+        gB = torch.empty_like(B) if ctx.needs_input_grad[1] else None
+        _lib.check(_lib.lib().smmd_kernel_matrix_bwd(
+            ctx.spec.desc(), _lib.ptr(A), A.shape[0], _lib.ptr(B), B.shape[0], A.shape[1],
+            _lib.ptr(G), _lib.ptr(gA), _lib.ptr(gB), _lib.stream_handle(A.device)),
+            'smmd_kernel_matrix_bwd')
+        return gA, gB, None
+
+
+def kernel_matrix(A, B, kernel='rbf', **kw):
+    """K(A, B) [na, nb] materialised (differentiable)."""
+    return _KernelMatrix.apply(A, B, _as_spec(kernel, **kw))
+
+
+class KernelMatrices:
+    """The value of ``mmd._<kind>_kernel(X, Y)``: behaves as the reference
+    tuple ``(K_XX, K_XY, K_YY, const_diagonal)`` (mmd.py:82, :116, :188, :37,
+    :52), materialising on first element access, while ``mmd2`` consumes it
+    without materialising anything."""
+
+    def __init__(self, spec: KernelSpec, X, Y):
+        self.spec, self.X, self.Y = spec, X, Y
+        self._mats = None
+
+    def _materialise(self):
+        if self._mats is None:
+            X, Y = self.X, self.Y
+            self._mats = (kernel_matrix(X, X, self.spec), kernel_matrix(X, Y, self.spec),
+                          kernel_matrix(Y, Y, self.spec),
+                          False if self.spec.const_diag is None else self.spec.const_diag)
+        return self._mats
+
+    def __len__(self):
+        return 4
+
+    def __iter__(self):
+        return iter(self._materialise())
+
+    def __getitem__(self, i):
+        return self._materialise()[i]
+
+
+def _make(name, X, Y, K_XY_only, **kw):
+    spec = get_kernel_spec(name, **kw)
+    if K_XY_only:
+        return kernel_matrix(X, Y, spec)
+    return KernelMatrices(spec, X, Y)
+
+
+def _distance_kernel(X, Y, K_XY_only=False):
+    return _make('distance', X, Y, K_XY_only)
+
+
+def _tanh_distance_kernel(X, Y, K_XY_only=False):
+    return _make('tanh_distance', X, Y, K_XY_only)
+
+
+def _dot_kernel(X, Y, K_XY_only=False):
+    return _make('dot', X, Y, K_XY_only)
+
+
+def _rbf_kernel(X, Y, sigma=1., wt=1., K_XY_only=False):
+    return _make('rbf', X, Y, K_XY_only, sigma=sigma, wt=wt)
+
+
+def _mix_rbf_kernel(X, Y, sigmas=(2.0, 5.0, 10.0, 20.0, 40.0, 80.0), wts=None, K_XY_only=False):
+    return _make('mix_rbf', X, Y, K_XY_only, sigmas=sigmas, wts=wts)
+
+
+def _mix_rq_kernel(X, Y, alphas=(.1, 1., 10.), wts=None, K_XY_only=False, add_dot=.0):
+    return _make('mix_rq', X, Y, K_XY_only, alphas=alphas, wts=wts, add_dot=add_dot)
+
+
+def _mix_rq_dot_kernel(X, Y, alphas=(.1, 1., 10.), wts=None, K_XY_only=False):
+    return _make('mix_rq_dot', X, Y, K_XY_only, alphas=alphas, wts=wts)
+
+
+def _mix_rq_1dot_kernel(X, Y, alphas=(.1, 1., 10.), wts=None, K_XY_only=False):
+    return _make('mix_rq_1dot', X, Y, K_XY_only, alphas=alphas, wts=wts)
+
+
+def _mix_rq_10dot_kernel(X, Y, alphas=(.1, 1., 10.), wts=None, K_XY_only=False):
+    return _make('mix_rq_10dot', X, Y, K_XY_only, alphas=alphas, wts=wts)
+
+
+def _mix_rq_01dot_kernel(X, Y, alphas=(.1, 1., 10.), wts=None, K_XY_only=False):
+    return _make('mix_rq_01dot', X, Y, K_XY_only, alphas=alphas, wts=wts)
+
+
+def _mix_rq_001dot_kernel(X, Y, alphas=(.1, 1., 10.), wts=None, K_XY_only=False):
+    return _make('mix_rq_001dot', X, Y, K_XY_only, alphas=alphas, wts=wts)
+
+
+def _tanh_mix_rq_kernel(X, Y, K_XY_only=False):
+    return _make('tanh_mix_rq', X, Y, K_XY_only)
+
+
+def get_kernel(name):
+    """getattr(mmd, '_%s_kernel' % name) as the reference does (smmd.py:11)."""
+    fn = globals().get('_%s_kernel' % name)
+    if fn is None:
+        raise ValueError('unknown kernel %r' % name)
+    return fn
+
+
+# ---------------------------------------------------------------------------
+# estimator
+# ---------------------------------------------------------------------------
+def mmd2(K, biased=False):
+    """gan/core/mmd.py:194-196.  A KernelMatrices argument takes the fused
+    path; an explicit 4-tuple of matrices is reduced as given."""
+    if isinstance(K, KernelMatrices):
+        return mmd2_fused(K.X, K.Y, K.spec, biased)
+    K_XX, K_XY, K_YY, const_diagonal = K
+    return _mmd2(K_XX, K_XY, K_YY, const_diagonal, biased)
+
+
+def _mmd2(K_XX, K_XY, K_YY, const_diagonal=False, biased=False):
+    """gan/core/mmd.py:199-220 on explicit matrices."""
+    m = float(K_XX.shape[0])
+    n = float(K_YY.shape[0])
+    if biased:
+        return (K_XX.sum() / (m * m) + K_YY.sum() / (n * n) - 2 * K_XY.sum() / (m * n))
+    if const_diagonal is not False:
+        trace_X = m * float(const_diagonal)
+        trace_Y = n * float(const_diagonal)
+    else:
+        trace_X = torch.diagonal(K_XX).sum()
+        trace_Y = torch.diagonal(K_YY).sum()
+    return ((K_XX.sum() - trace_X) / (m * (m - 1)) + (K_YY.sum() - trace_Y) / (n * (n - 1))
+            - 2 * K_XY.sum() / (m * n))
+
+
+# ---------------------------------------------------------------------------
+# witness function of the gradient penalty (gan/core/model.py:336-339)
+# ---------------------------------------------------------------------------
+class _WitnessGrad(torch.autograd.Function):
+    """dH = d(sum_i witness_i)/dH with a HIP second-order backward."""
+
+    @staticmethod
+    def forward(ctx, H, R, F, spec):
+        H, R, F = _features(H), _features(R), _features(F)
+        dH = torch.empty_like(H)
+        w = torch.empty(H.shape[0], device=H.device, dtype=torch.float32)
+        _lib.check(_lib.lib().smmd_witness_fwd(
+            spec.desc(), _lib.ptr(H), H.shape[0], _lib.ptr(R), R.shape[0], _lib.ptr(F),
+            F.shape[0], H.shape[1], _lib.ptr(w), _lib.ptr(dH), _lib.stream_handle(H.device)),
+            'smmd_witness_fwd')
+        ctx.save_for_backward(H, R, F)
+        ctx.spec = spec
+        ctx.mark_non_differentiable(w)
+        return dH, w
+
+    @staticmethod
+    def backward(ctx, gdH, gw):
+        H, R, F = ctx.saved_tensors
+        gdH = gdH.contiguous()
+        gH, gR, gF = torch.empty_like(H), torch.empty_like(R), torch.empty_like(F)
+        _lib.check(_lib.lib().smmd_witness_bwd(
+            ctx.spec.desc(), _lib.ptr(H), H.shape[0], _lib.ptr(R), R.shape[0], _lib.ptr(F),
+            F.shape[0], H.shape[1], _lib.ptr(gdH), _lib.ptr(gH), _lib.ptr(gR), _lib.ptr(gF),
+            _lib.stream_handle(H.device)), 'smmd_witness_bwd')
+        return gH, gR, gF, None
+
+
+def witness_and_grad(H, R, F, kernel='rbf', **kw):
+    """(d sum_i w_i / dH, w) with w_i = mean_j K(H_i,R_j) - mean_j K(H_i,F_j)."""
+    dH, w = _WitnessGrad.apply(H, R, F, _as_spec(kernel, **kw))
+    return dH, w

@@ -1,0 +1,96 @@
+"""Flat-buffer TF-semantics Adam with per-tensor clip_by_norm (libsmmd_hip).
+
+Replaces the per-variable ``tf.clip_by_norm(g, 1.)`` of MMD_GAN.compute_grads
+(gan/core/model.py:444-456) and ``tf.train.AdamOptimizer`` (model.py:405-412,
+:458-468).  Every parameter of a network is re-pointed into ONE contiguous
+fp32 buffer, and so is its gradient, so
+
+* the data-parallel gradient exchange is a single RCCL all_reduce over
+  ``flat_grad`` (one bucket of ~40 MB for the SNResNet critic), and
+* clip + Adam for all tensors is one ``smmd_adam_flat`` launch set.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+
+
+class FlatAdam:
+    def __init__(self, params, lr, beta1=0.5, beta2=0.9, eps=1e-8, clip_norm=1.0):
+        self.params = [p for p in params]
+        if not self.params:
+            raise ValueError('no parameters')
+        dev = self.params[0].device
+        _lib.require_cuda(*self.params)
+        self.lr, self.beta1, self.beta2, self.eps = lr, beta1, beta2, eps
+        self.clip_norm = clip_norm if clip_norm else 0.0
+        sizes = [p.numel() for p in self.params]
+        offs = [0]
+        for s in sizes:
+            offs.append(offs[-1] + s)
+        self.numel = offs[-1]
+        self.offsets = (ctypes.c_int64 * len(offs))(*offs)
+        self.flat_param = torch.empty(self.numel, device=dev, dtype=torch.float32)
+        self.flat_grad = torch.zeros(self.numel, device=dev, dtype=torch.float32)
+        self.m = torch.zeros(self.numel, device=dev, dtype=torch.float32)
+        self.v = torch.zeros(self.numel, device=dev, dtype=torch.float32)
+        with torch.no_grad():
+            for p, o, s in zip(self.params, offs, sizes):
+                view = self.flat_param[o:o + s].view_as(p)
+                view.copy_(p)
+                p.data = view
+                p.grad = self.flat_grad[o:o + s].view_as(p)
+        self.step_count = 0
+        nbytes = _lib.lib().smmd_opt_workspace_bytes(self.offsets, len(self.params))
+        self.ws = torch.zeros(max(nbytes, 256), dtype=torch.uint8, device=dev)
+
+    def zero_grad(self, set_to_none=False):
+        self.flat_grad.zero_()
+        # re-attach views in case autograd replaced a .grad tensor
+        o = 0
+        for p in self.params:
+            n = p.numel()
+            if n and (p.grad is None or p.grad.data_ptr() != self.flat_grad[o:o + n].data_ptr()):
+                p.grad = self.flat_grad[o:o + n].view_as(p)
+            o += n
+
+    def _check_grads(self):
+        o = 0
+        for p in self.params:
+            n = p.numel()
+            if n and (p.grad is None or p.grad.data_ptr() != self.flat_grad[o:o + n].data_ptr()):
+                raise RuntimeError('a parameter gradient was re-allocated outside flat_grad; '
+                                   'call zero_grad() before backward()')
+            o += n
+
+    def clip_(self, clip_norm=None):
+        """Per-tensor clip_by_norm in place (the per-tower clip)."""
+        c = self.clip_norm if clip_norm is None else clip_norm
+        _lib.check(_lib.lib().smmd_clip_by_norm_flat(
+            _lib.ptr(self.flat_grad), self.offsets, len(self.params), float(c),
+            _lib.ptr(self.ws), self.ws.numel(), _lib.stream_handle(self.flat_grad.device)),
+            'smmd_clip_by_norm_flat')
+
+    def step(self, grad_scale=1.0, clip=True, lr=None):
+        self._check_grads()
+        self.step_count += 1
+        c = float(self.clip_norm) if clip else 0.0
+        _lib.check(_lib.lib().smmd_adam_flat(
+            _lib.ptr(self.flat_param), _lib.ptr(self.flat_grad), _lib.ptr(self.m),
+            _lib.ptr(self.v), self.offsets, len(self.params), float(grad_scale), c,
+            float(self.lr if lr is None else lr), float(self.beta1), float(self.beta2),
+            float(self.eps), self.step_count, _lib.ptr(self.ws), self.ws.numel(),
+            _lib.stream_handle(self.flat_grad.device)), 'smmd_adam_flat')
+
+    def state_dict(self):
+        return {'m': self.m.clone(), 'v': self.v.clone(), 'step': self.step_count,
+                'lr': self.lr}
+
+    def load_state_dict(self, sd):
+        self.m.copy_(sd['m'])
+        self.v.copy_(sd['v'])
+        self.step_count = int(sd['step'])
+        self.lr = float(sd['lr'])

@@ -1,0 +1,217 @@
+"""Spectral normalisation on the MI355X hot path.
+
+Drop-in for gan/core/sn.py (``spectral_normed_weight``, ``NO_OPS``) plus the
+batched form the networks use: :class:`SpectralNormBank` runs the power
+iteration, sigma and ``W_eff = s * W / sigma`` for EVERY SN layer of a network
+in one set of HIP launches (``smmd_sn_power_iter``) and the matching backward
+in another (``smmd_sn_weight_bwd``).
+
+Layout note: weights are kept as PyTorch stores them, flattened to
+[N = out channels, K].  The reference reshapes its [kh, kw, Cin, Cout] weight
+to [kh*kw*Cin, Cout] (sn.py:18-19); that is the transpose of ours up to a
+permutation of K, which leaves sigma and u unchanged (v is permuted).
+"""
+from __future__ import annotations
+
+import warnings
+
+import torch
+
+from . import _lib
+
+NO_OPS = 'NO_OPS'         # gan/core/sn.py:9
+SN_EPS = 1e-12            # gan/core/sn.py:12
+
+
+def truncated_normal_(t, std=1.0):
+    """tf.truncated_normal_initializer: normal re-drawn outside 2 std."""
+    with torch.no_grad():
+        torch.nn.init.trunc_normal_(t, mean=0.0, std=std, a=-2 * std, b=2 * std)
+    return t
+
+
+class _SNBatch(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, bank, update_u, *tensors):
+        n = len(bank.entries)
+        Ws, ss = tensors[:n], tensors[n:]
+        outs = []
+        arr = (_lib.SnLayer * n)()
+        for i, (e, W, s) in enumerate(zip(bank.entries, Ws, ss)):
+            W2 = W.detach().reshape(e.N, e.K)
+            if not W2.is_contiguous():
+                raise ValueError('SN weight %d is not contiguous' % i)
+            W_eff = torch.empty_like(W)
+            outs.append(W_eff)
+            L = arr[i]
+            L.W = W2.data_ptr()
+            L.W_eff = W_eff.data_ptr()
+            L.u = e.u.data_ptr()
+            L.v = e.v.data_ptr()
+            L.sigma = e.sigma.data_ptr()
+            L.s = s.data_ptr() if s is not None and s.numel() > 0 else None
+            L.N, L.K = e.N, e.K
+        dev = Ws[0].device
+        lib = _lib.lib()
+        _lib.check(lib.smmd_sn_power_iter(arr, n, bank.num_iters, SN_EPS, 1 if update_u else 0,
+                                          _lib.ptr(bank.ws), bank.ws.numel(),
+                                          _lib.stream_handle(dev)), 'smmd_sn_power_iter')
+        ctx.bank = bank
+        ctx.save_for_backward(*Ws, *ss)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        bank = ctx.bank
+        n = len(bank.entries)
+        saved = ctx.saved_tensors
+        Ws, ss = saved[:n], saved[n:]
+        arr = (_lib.SnLayer * n)()
+        gWs, gss, keep = [], [], []
+        for i, (e, W, s, G) in enumerate(zip(bank.entries, Ws, ss, grads)):
+            if G is None:
+                G = torch.zeros_like(W)
+            G = G.contiguous()
+            keep.append(G)
+            gW = torch.empty_like(W)
+            gs = torch.empty(1, device=W.device, dtype=torch.float32)
+            gWs.append(gW)
+            gss.append(gs if (s is not None and s.numel() > 0) else None)
+            L = arr[i]
+            L.W = W.data_ptr()
+            L.u = e.u.data_ptr()
+            L.v = e.v.data_ptr()
+            L.sigma = e.sigma.data_ptr()
+            L.s = s.data_ptr() if s is not None and s.numel() > 0 else None
+            L.G = G.data_ptr()
+            L.gW = gW.data_ptr()
+            L.gs = gs.data_ptr()
+            L.N, L.K = e.N, e.K
+        _lib.check(_lib.lib().smmd_sn_weight_bwd(arr, n, _lib.ptr(bank.ws), bank.ws.numel(),
+                                                 _lib.stream_handle(Ws[0].device)),
+                   'smmd_sn_weight_bwd')
+        gs_out = []
+        for s, gs in zip(ss, gss):
+            if gs is None:
+                gs_out.append(None)
+            else:
+                gs_out.append(gs.view_as(s))
+        return (None, None, *gWs, *gs_out)
+
+
+class SNEntry:
+    """State of one SN layer: u [N] (truncated normal, sn.py:20-21), v [K],
+    sigma [1]; the weight and scale parameters live in the layer module."""
+
+    def __init__(self, module, weight_name='weight', scale_name='sn_scale'):
+        self.module = module
+        self.weight_name = weight_name
+        self.scale_name = scale_name
+        W = getattr(module, weight_name)
+        self.N = W.shape[0]
+        self.K = W[0].numel()
+        dev = W.device
+        self.u = truncated_normal_(torch.empty(self.N, device=dev, dtype=torch.float32))
+        self.v = torch.zeros(self.K, device=dev, dtype=torch.float32)
+        self.sigma = torch.ones(1, device=dev, dtype=torch.float32)
+
+    @property
+    def weight(self):
+        return getattr(self.module, self.weight_name)
+
+    @property
+    def scale(self):
+        return getattr(self.module, self.scale_name, None)
+
+    def to(self, device):
+        self.u = self.u.to(device)
+        self.v = self.v.to(device)
+        self.sigma = self.sigma.to(device)
+
+
+class SpectralNormBank:
+    """All SN layers of one network, normalised together once per step.
+
+    ``refresh(update_u)`` computes W_eff for every layer (one HIP launch set)
+    and stores it on each module as ``module.w_eff``; it is reused by every
+    critic call of the step (real, fake, GP), which also removes the
+    reference's u read/assign race."""
+
+    def __init__(self, modules, num_iters=1):
+        self.entries = [SNEntry(m) for m in modules]
+        self.num_iters = num_iters
+        self.ws = None
+        self._alloc_ws()
+
+    def _alloc_ws(self):
+        if not self.entries:
+            return
+        arr = (_lib.SnLayer * len(self.entries))()
+        for i, e in enumerate(self.entries):
+            arr[i].N, arr[i].K = e.N, e.K
+        nbytes = _lib.lib().smmd_sn_workspace_bytes(arr, len(self.entries))
+        dev = self.entries[0].weight.device
+        self.ws = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
+
+    def to(self, device):
+        for e in self.entries:
+            e.to(device)
+        self._alloc_ws()
+
+    def refresh(self, update_u=True):
+        if not self.entries:
+            return []
+        Ws = [e.weight for e in self.entries]
+        ss = [e.scale if e.scale is not None else torch.empty(0, device=Ws[0].device)
+              for e in self.entries]
+        _lib.require_cuda(*Ws)
+        outs = _SNBatch.apply(self, bool(update_u), *Ws, *ss)
+        for e, w in zip(self.entries, outs):
+            e.module.w_eff = w
+        return list(outs)
+
+    def sigmas(self):
+        return torch.cat([e.sigma for e in self.entries])
+
+    def state_dict(self):
+        return {'u': [e.u.clone() for e in self.entries]}
+
+    def load_state_dict(self, sd):
+        for e, u in zip(self.entries, sd['u']):
+            e.u.copy_(u)
+
+
+def spectral_normed_weight(W, u=None, num_iters=1, update_collection=None, with_sigma=False,
+                           stop_grad=True):
+    """gan/core/sn.py:16-59 for one weight in the REFERENCE layout
+    (last dim = out).  ``u`` [1, N] is updated in place when
+    ``update_collection is None`` (sn.py:39-46); any other value leaves it
+    (NO_OPS semantics: the reference only queues the assign)."""
+    if not stop_grad:
+        raise NotImplementedError('stop_grad=False is not supported (the reference default '
+                                  'and every caller use stop_grad=True, sn.py:16, :32-34)')
+    N = W.shape[-1]
+    if u is None:
+        warnings.warn('spectral_normed_weight: no u given; a fresh truncated-normal u is used '
+                      '(pass u to keep the power-iteration state)')
+        u = truncated_normal_(torch.empty(1, N, device=W.device, dtype=torch.float32))
+    Wt = W.reshape(-1, N).t().contiguous()          # [N, K]
+    holder = torch.nn.Module()
+    holder.weight = Wt
+    bank = SpectralNormBank.__new__(SpectralNormBank)
+    e = SNEntry.__new__(SNEntry)
+    e.module, e.weight_name, e.scale_name = holder, 'weight', 'sn_scale'
+    e.N, e.K = N, Wt.shape[1]
+    e.u = u.reshape(N).detach().clone().contiguous()
+    e.v = torch.zeros(e.K, device=W.device, dtype=torch.float32)
+    e.sigma = torch.ones(1, device=W.device, dtype=torch.float32)
+    bank.entries, bank.num_iters, bank.ws = [e], num_iters, None
+    bank._alloc_ws()
+    W_eff_t, = _SNBatch.apply(bank, True, Wt, torch.empty(0, device=W.device))
+    if update_collection is None:
+        with torch.no_grad():
+            u.copy_(e.u.view_as(u))
+    W_bar = W_eff_t.t().reshape(W.shape)
+    if with_sigma:
+        return W_bar, e.sigma[0]
+    return W_bar

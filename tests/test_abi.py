@@ -1,0 +1,83 @@
+"""The C-ABI library loads and exports every symbol include/smmd_hip.h
+declares; host-only entry points (workspace sizing, argument validation,
+status strings) behave without a GPU."""
+import ctypes
+import os
+import re
+
+import pytest
+
+torch = pytest.importorskip('torch')
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, 'include', 'smmd_hip.h')
+
+
+def _declared():
+    src = open(HEADER).read()
+    src = re.sub(r'/\*.*?\*/', '', src, flags=re.S)
+    return sorted(set(re.findall(r'\b(smmd_[a-z0-9_]+)\s*\(', src)))
+
+
+@pytest.fixture(scope='module')
+def L():
+    from gan.core import _lib
+    return _lib.lib()
+
+
+def test_header_and_binding_agree():
+    from gan.core import _lib
+    assert _declared() == sorted(_lib.EXPORTED_SYMBOLS)
+
+
+def test_every_declared_symbol_is_exported(L):
+    for name in _declared():
+        assert hasattr(L, name), name
+
+
+def test_status_strings(L):
+    assert L.smmd_status_string(0) == b'SMMD_OK'
+    assert b'EINVAL' in L.smmd_status_string(1)
+    assert L.smmd_abi_version() == 1
+
+
+def test_workspace_sizing(L):
+    from gan.core import _lib
+    assert L.smmd_mmd2_workspace_bytes(64, 64, 1) >= 256 + 32 * 8 * 8
+    assert L.smmd_scaled_loss_workspace_bytes(64, 3 * 64 * 64) >= 64 * 3 * 8
+    arr = (_lib.SnLayer * 2)()
+    arr[0].N, arr[0].K, arr[1].N, arr[1].K = 64, 27, 1024, 4608
+    assert L.smmd_sn_workspace_bytes(arr, 2) > 16 * 4608 * 4
+    offs = (ctypes.c_int64 * 3)(0, 10, 70000)
+    assert L.smmd_opt_workspace_bytes(offs, 2) >= 8 * 6
+
+
+def test_argument_validation_without_gpu(L):
+    from gan.core import _lib
+    d = _lib.KernelDesc()
+    d.kind, d.n_terms, d.param[0], d.wt[0] = 0, 1, 1.0, 1.0
+    # NULL inputs / bad ranges are rejected before any launch
+    assert L.smmd_mmd2_fwd(d, None, 4, None, 4, 1, 0, 0, 4, 0, 4, None, None, None, None, None,
+                           0, None) == 1
+    bad = _lib.KernelDesc()
+    bad.kind, bad.n_terms = 0, 0
+    x = ctypes.c_void_p(16)
+    assert L.smmd_mmd2_fwd(bad, x, 4, x, 4, 1, 0, 0, 4, 0, 4, None, None, None, None, x, 1 << 20,
+                           None) == 1
+    assert L.smmd_mmd2_fwd(d, x, 4, x, 4, 1, 0, 0, 5, 0, 4, None, None, None, None, x, 1 << 20,
+                           None) == 1
+    assert L.smmd_mmd2_fwd(d, x, 4, x, 4, 1, 0, 0, 4, 0, 4, None, None, None, None, x, 8,
+                           None) == 3          # EWORKSPACE
+    assert L.smmd_mmd2_fwd(d, x, 4, x, 4, 64, 0, 0, 4, 0, 4, None, None, None, None, x, 1 << 20,
+                           None) == 4          # EUNSUPPORTED (d > 32 this round)
+    assert L.smmd_sn_power_iter(None, 0, 1, 1e-12, 1, None, 0, None) == 1
+    assert L.smmd_witness_bwd(d, x, 4, x, 4, x, 4, 1, None, x, x, x, None) == 1
+
+
+def test_product_never_imports_oracle():
+    pkg = os.path.join(ROOT, 'scaled-mmd-gan_amd')
+    for dp, _, fs in os.walk(pkg):
+        for f in fs:
+            if f.endswith('.py'):
+                src = open(os.path.join(dp, f)).read()
+                assert 'oracle' not in re.findall(r'^\s*(?:from|import)\s+(\w+)', src, re.M), f

@@ -1,0 +1,311 @@
+"""GPU parity: libsmmd_hip (through the C ABI, via the gan.core API) against the
+float64 CPU oracle (oracle/smmd_oracle.py) on the same seeded inputs.
+
+Tolerances (fp32 kernels vs float64 oracle on identical fp32 inputs):
+  mmd2 / sums / kernel values:  |d| <= 1e-5 + 1e-4 |ref|
+  gradients:                     |d| <= 1e-4 max|ref| + 1e-3 |ref|   (elementwise)
+  spectral norm sigma, u, v:     rtol 1e-4 ; W_eff, dW: rtol 1e-4, atol 1e-6 max|ref|
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip('torch')
+
+from oracle import smmd_oracle as O  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(got, ref, atol, rtol, what):
+    got = np.asarray(got, np.float64)
+    ref = np.asarray(ref, np.float64)
+    err = np.abs(got - ref)
+    lim = atol + rtol * np.abs(ref)
+    bad = err > lim
+    assert not bad.any(), '%s: max err %.3e (worst at %s: got %r ref %r)' % (
+        what, err.max(), np.argmax(err - lim), got.flat[np.argmax(err - lim)],
+        ref.flat[np.argmax(err - lim)])
+
+
+def _grad_close(got, ref, what):
+    ref = np.asarray(ref, np.float64)
+    scale = max(np.abs(ref).max(), 1e-12)
+    _close(got, ref, 1e-4 * scale, 1e-3, what)
+
+
+def _feats(m, n, d, seed, scale=1.0):
+    rng = np.random.default_rng(seed)
+    X = (rng.standard_normal((m, d)) * scale).astype(np.float32)
+    Y = (rng.standard_normal((n, d)) * scale + 0.3).astype(np.float32)
+    return X, Y
+
+
+SHAPES = [(4, 4, 1), (32, 32, 1), (64, 64, 1), (256, 256, 1), (64, 48, 3), (33, 70, 16),
+          (17, 9, 32), (130, 127, 2)]
+
+
+@pytest.mark.parametrize('name', O.KERNEL_NAMES)
+@pytest.mark.parametrize('shape', SHAPES)
+@pytest.mark.parametrize('biased', [False, True])
+def test_mmd2_fused_vs_oracle(dev, name, shape, biased):
+    from gan.core import mmd
+    m, n, d = shape
+    X, Y = _feats(m, n, d, seed=hash((name, shape)) % 2**31)
+    spec = O.kernel_spec(name)
+    ref = O.mmd2(spec, X, Y, biased)
+    rdx, rdy = O.mmd2_grad(spec, X, Y, biased)
+    Xt = torch.tensor(X, device=dev, requires_grad=True)
+    Yt = torch.tensor(Y, device=dev, requires_grad=True)
+    val, sums = mmd.mmd2_fused(Xt, Yt, name, biased=biased, return_sums=True)
+    val.backward()
+    _close(val.item(), ref, 1e-5, 1e-4, 'mmd2 %s %s' % (name, shape))
+    rs = O.mmd2_sums(spec, X, Y)
+    _close(sums[:5].cpu().numpy(), rs, 1e-4, 1e-4, 'sums')
+    _grad_close(Xt.grad.cpu().numpy(), rdx, 'dX %s %s' % (name, shape))
+    _grad_close(Yt.grad.cpu().numpy(), rdy, 'dY %s %s' % (name, shape))
+
+
+def test_mmd2_reference_api_path(dev):
+    """mmd.mmd2(mmd._rbf_kernel(X, Y)) -- the exact call of SMMD.set_loss."""
+    from gan.core import mmd
+    X, Y = _feats(64, 64, 1, seed=7)
+    Xt, Yt = torch.tensor(X, device=dev), torch.tensor(Y, device=dev)
+    got = mmd.mmd2(mmd._rbf_kernel(Xt, Yt)).item()
+    _close(got, O.mmd2(O.kernel_spec('rbf'), X, Y), 1e-5, 1e-4, 'api')
+    # materialised tuple then the explicit-matrix estimator
+    K = mmd._mix_rq_kernel(Xt, Yt)
+    KXX, KXY, KYY, c = K
+    rK = O.kernel_matrices(O.kernel_spec('mix_rq'), X, Y)
+    for a, b in zip((KXX, KXY, KYY), rK[:3]):
+        _close(a.cpu().numpy(), b, 1e-5, 1e-4, 'kmat')
+    assert c == 3.0
+    _close(mmd.mmd2((KXX, KXY, KYY, c)).item(), O.mmd2_from_K(*rK), 1e-5, 1e-4, 'tuple')
+
+
+def test_mmd2_deterministic(dev):
+    from gan.core import mmd
+    X, Y = _feats(256, 256, 4, seed=3)
+    Xt, Yt = torch.tensor(X, device=dev), torch.tensor(Y, device=dev)
+    a = [mmd.mmd2_fused(Xt, Yt, 'mix_rbf').item() for _ in range(5)]
+    assert len(set(a)) == 1
+
+
+@pytest.mark.parametrize('name', ['rbf', 'mix_rq_dot', 'distance', 'dot', 'tanh_mix_rq'])
+def test_kernel_matrix_backward(dev, name):
+    from gan.core import mmd
+    A, B = _feats(19, 70, 3, seed=11)
+    spec = O.kernel_spec(name)
+    rng = np.random.default_rng(5)
+    G = rng.standard_normal((19, 70))
+    At = torch.tensor(A, device=dev, requires_grad=True)
+    Bt = torch.tensor(B, device=dev, requires_grad=True)
+    K = mmd.kernel_matrix(At, Bt, name)
+    (K * torch.tensor(G, device=dev, dtype=torch.float32)).sum().backward()
+    A1, B1 = (np.tanh(A.astype(np.float64)), np.tanh(B.astype(np.float64))) if spec.tanh else (A, B)
+    A1, B1 = np.asarray(A1, np.float64), np.asarray(B1, np.float64)
+    rdA, rdB = O._block_grads(spec, A1, B1, A1 @ B1.T, np.sum(A1 * A1, 1), np.sum(B1 * B1, 1), G)
+    if spec.tanh:
+        rdA = rdA * (1 - A1 ** 2)
+        rdB = rdB * (1 - B1 ** 2)
+    _close(K.detach().cpu().numpy(), O.kernel_matrices(spec, A, B, K_XY_only=True), 1e-5, 1e-4,
+           'K')
+    _grad_close(At.grad.cpu().numpy(), rdA, 'gA')
+    _grad_close(Bt.grad.cpu().numpy(), rdB, 'gB')
+
+
+@pytest.mark.parametrize('name', O.KERNEL_NAMES)
+def test_witness_forward(dev, name):
+    from gan.core import mmd
+    rng = np.random.default_rng(21)
+    H = rng.standard_normal((40, 2)).astype(np.float32)
+    R = rng.standard_normal((40, 2)).astype(np.float32)
+    F = (rng.standard_normal((40, 2)) + 0.5).astype(np.float32)
+    spec = O.kernel_spec(name)
+    dH, w = mmd.witness_and_grad(*(torch.tensor(a, device=dev) for a in (H, R, F)), kernel=name)
+    _close(w.cpu().numpy(), O.witness(spec, H, R, F), 1e-5, 1e-4, 'witness')
+    _grad_close(dH.cpu().numpy(), O.witness_grad_H(spec, H, R, F), 'dH')
+
+
+@pytest.mark.parametrize('name', ['rbf', 'mix_rbf', 'mix_rq', 'mix_rq_dot'])
+def test_witness_second_order(dev, name):
+    """d <g, dH>/d(H, R, F) against central differences of the float64 oracle."""
+    from gan.core import mmd
+    rng = np.random.default_rng(4)
+    H = rng.standard_normal((12, 2))
+    R = rng.standard_normal((10, 2))
+    F = rng.standard_normal((9, 2)) + 0.5
+    g = rng.standard_normal((12, 2))
+    spec = O.kernel_spec(name)
+    ts = [torch.tensor(a, device=dev, dtype=torch.float32, requires_grad=True) for a in (H, R, F)]
+    dH, _ = mmd.witness_and_grad(*ts, kernel=name)
+    (dH * torch.tensor(g, device=dev, dtype=torch.float32)).sum().backward()
+    H32, R32, F32 = (np.asarray(a, np.float32).astype(np.float64) for a in (H, R, F))
+
+    def f(Hh, Rr, Ff):
+        return np.sum(O.witness_grad_H(spec, Hh, Rr, Ff) * g)
+
+    for idx, arr in enumerate((H32, R32, F32)):
+        num = np.zeros_like(arr)
+        for k in np.ndindex(arr.shape):
+            e = 1e-5
+            ap, am = arr.copy(), arr.copy()
+            ap[k] += e
+            am[k] -= e
+            args_p = [H32, R32, F32]
+            args_m = [H32, R32, F32]
+            args_p[idx], args_m[idx] = ap, am
+            num[k] = (f(*args_p) - f(*args_m)) / (2 * e)
+        _close(ts[idx].grad.cpu().numpy(), num, 2e-3 * max(np.abs(num).max(), 1e-6), 2e-3,
+               'witness 2nd order arg %d' % idx)
+
+
+SN_SHAPES = [(64, 27), (128, 576), (256, 1152), (1, 1024), (1024, 4608), (7, 13), (130, 300)]
+
+
+def test_sn_bank_vs_oracle(dev):
+    from gan.core import sn
+    rng = np.random.default_rng(2)
+    mods = []
+    for N, K in SN_SHAPES:
+        m = torch.nn.Module()
+        m.weight = torch.nn.Parameter(torch.tensor(rng.standard_normal((N, K)) * 0.05,
+                                                   dtype=torch.float32, device=dev))
+        m.sn_scale = torch.nn.Parameter(torch.tensor([1.3], device=dev))
+        mods.append(m)
+    bank = sn.SpectralNormBank(mods)
+    u0 = [e.u.cpu().numpy().astype(np.float64) for e in bank.entries]
+    outs = bank.refresh(update_u=True)
+    Gs = [rng.standard_normal((N, K)) for N, K in SN_SHAPES]
+    loss = sum((o * torch.tensor(G, device=dev, dtype=torch.float32)).sum()
+               for o, G in zip(outs, Gs))
+    loss.backward()
+    for i, (m, e) in enumerate(zip(mods, bank.entries)):
+        W = m.weight.detach().cpu().numpy().astype(np.float64)
+        sigma, u1, v1 = O.spectral_norm_rows(W, u0[i])
+        _close(e.sigma.item(), sigma, 0, 1e-4, 'sigma %d' % i)
+        _close(e.u.cpu().numpy(), u1, 1e-6, 1e-4, 'u %d' % i)
+        _close(e.v.cpu().numpy(), v1, 1e-6, 1e-4, 'v %d' % i)
+        weff = W / sigma * 1.3
+        _close(outs[i].detach().cpu().numpy(), weff, 1e-6 * np.abs(weff).max(), 1e-4, 'Weff')
+        gW, gs = O.sn_weight_backward(W, 1.3, sigma, u1, v1, Gs[i])
+        _close(m.weight.grad.cpu().numpy(), gW, 1e-4 * np.abs(gW).max(), 1e-3, 'gW %d' % i)
+        _close(m.sn_scale.grad.item(), gs, 1e-4 * abs(gs), 1e-3, 'gs %d' % i)
+
+
+def test_sn_reference_layout(dev):
+    """spectral_normed_weight on a TF-layout conv weight [kh, kw, Cin, Cout]."""
+    from gan.core import sn
+    rng = np.random.default_rng(9)
+    W = rng.standard_normal((3, 3, 16, 32)).astype(np.float32)
+    u = O.np.asarray(rng.standard_normal((1, 32)), np.float32)
+    Wb, sigma, u1, _ = O.spectral_normed_weight(W, u)
+    ut = torch.tensor(u, device=dev)
+    got, s = sn.spectral_normed_weight(torch.tensor(W, device=dev), u=ut, with_sigma=True)
+    _close(s.item(), sigma, 0, 1e-4, 'sigma')
+    _close(got.cpu().numpy(), Wb, 1e-6, 1e-4, 'W_bar')
+    _close(ut.cpu().numpy(), u1, 1e-6, 1e-4, 'u assign')
+
+
+@pytest.mark.parametrize('variant', ['grad', 'value_and_grad'])
+@pytest.mark.parametrize('sqrt_scale', [False, True])
+def test_scaled_loss_vs_oracle(dev, variant, sqrt_scale):
+    from gan.core import ops
+    rng = np.random.default_rng(13)
+    b = 24
+    jac = rng.standard_normal((2, b, 3, 9, 7)).astype(np.float32) * 0.1
+    feat = rng.standard_normal((b, 2)).astype(np.float32)
+    base = np.float32(0.37)
+    jt = torch.tensor(jac, device=dev, requires_grad=True)
+    ft = torch.tensor(feat, device=dev, requires_grad=True)
+    bt = torch.tensor(base, device=dev, requires_grad=True)
+    g, aux = ops.scaled_loss(bt, jt, ft, sc=10.0, variant=variant, sqrt_scale=sqrt_scale)
+    J = np.mean(sum(O.squared_norm_per_sample(jac[c]) for c in range(2)))
+    nD = np.mean(feat.astype(np.float64) ** 2)
+    sc_ = O.scale_factor(J, 10.0, nD, variant)
+    f = np.sqrt(sc_) if sqrt_scale else sc_
+    _close(aux[3].item(), J, 0, 1e-5, 'J')
+    _close(aux[2].item(), sc_, 0, 1e-5, 'scale')
+    _close(g.item(), base * f, 0, 1e-5, 'g_loss')
+    g.backward()
+    fp = 0.5 / np.sqrt(sc_) if sqrt_scale else 1.0
+    coefq = base * fp * (-10.0 * sc_ ** 2)
+    _close(bt.grad.item(), f, 0, 1e-5, 'd base')
+    _grad_close(jt.grad.cpu().numpy(), coefq * 2.0 / b * jac.astype(np.float64), 'd jac')
+    if variant == 'value_and_grad':
+        _grad_close(ft.grad.cpu().numpy(), coefq * 2.0 / (b * 2) * feat.astype(np.float64),
+                    'd feat')
+
+
+def test_smmd_objective_end_to_end(dev):
+    """SMMD generator loss through a tanh-MLP critic: value vs the oracle and
+    d loss / d critic params (double backward through jac) vs central
+    differences of the float64 oracle."""
+    from gan.core import mmd, ops
+    rng = np.random.default_rng(17)
+    P, Hd = 12, 6
+    xf = rng.uniform(0, 1, (16, P))
+    xr = rng.uniform(0, 1, (16, P))
+    W1 = rng.standard_normal((P, Hd)) * 0.5
+    W2 = rng.standard_normal((Hd, 1)) * 0.5
+    ref, _, _ = O.smmd_objective(O.kernel_spec('rbf'), xf.astype(np.float32),
+                                 xr.astype(np.float32), W1.astype(np.float32),
+                                 W2.astype(np.float32))
+    t = lambda a, g=False: torch.tensor(a, device=dev, dtype=torch.float32, requires_grad=g)
+    W1t, W2t = t(W1, True), t(W2, True)
+    xft, xrt = t(xf), t(xr, True)
+    dG = torch.tanh(xft @ W1t) @ W2t
+    dI = torch.tanh(xrt @ W1t) @ W2t
+    m2 = mmd.mmd2(mmd._rbf_kernel(dG, dI))
+    jac = ops.jacobian_columns(dI, xrt)
+    g_loss, aux = ops.scaled_loss(m2, jac, None, sc=10.0)
+    _close(g_loss.item(), ref, 1e-6, 1e-4, 'smmd g_loss')
+    g_loss.backward()
+    W1_32, W2_32 = W1.astype(np.float32).astype(np.float64), W2.astype(np.float32).astype(np.float64)
+    xf32, xr32 = xf.astype(np.float32).astype(np.float64), xr.astype(np.float32).astype(np.float64)
+    for which, arr, got in ((0, W1_32, W1t.grad), (1, W2_32, W2t.grad)):
+        num = np.zeros_like(arr)
+        for k in np.ndindex(arr.shape):
+            e = 1e-6
+            ap, am = arr.copy(), arr.copy()
+            ap[k] += e
+            am[k] -= e
+            if which == 0:
+                fp = O.smmd_objective(O.kernel_spec('rbf'), xf32, xr32, ap, W2_32)[0]
+                fm = O.smmd_objective(O.kernel_spec('rbf'), xf32, xr32, am, W2_32)[0]
+            else:
+                fp = O.smmd_objective(O.kernel_spec('rbf'), xf32, xr32, W1_32, ap)[0]
+                fm = O.smmd_objective(O.kernel_spec('rbf'), xf32, xr32, W1_32, am)[0]
+            num[k] = (fp - fm) / (2 * e)
+        _close(got.cpu().numpy(), num, 2e-3 * np.abs(num).max(), 2e-3, 'dparam %d' % which)
+
+
+def test_clip_adam_vs_oracle(dev):
+    from gan.core import optim
+    rng = np.random.default_rng(23)
+    sizes = [5, 70000, 1, 33000, 0, 128]
+    shapes = [(s,) for s in sizes]
+    params = [torch.nn.Parameter(torch.tensor(rng.standard_normal(s), dtype=torch.float32,
+                                              device=dev)) for s in shapes]
+    opt = optim.FlatAdam(params, lr=2e-4, beta1=0.5, beta2=0.9, clip_norm=1.0)
+    ref_p = [p.detach().cpu().numpy().astype(np.float64) for p in params]
+    ref_m = [np.zeros_like(p) for p in ref_p]
+    ref_v = [np.zeros_like(p) for p in ref_p]
+    for step in range(1, 4):
+        grads = [rng.standard_normal(s).astype(np.float32) * (3.0 if i % 2 else 0.1)
+                 for i, s in enumerate(shapes)]
+        opt.zero_grad()
+        for p, g in zip(params, grads):
+            p.grad.copy_(torch.tensor(g, device=dev))
+        opt.step()
+        for i, g in enumerate(grads):
+            gc = O.clip_by_norm(g, 1.0) if g.size else g.astype(np.float64)
+            ref_p[i], ref_m[i], ref_v[i] = O.adam_step(ref_p[i], ref_m[i], ref_v[i], gc, step,
+                                                       2e-4)
+    for p, r in zip(params, ref_p):
+        _close(p.detach().cpu().numpy(), r, 1e-6, 1e-5, 'adam param')
+
+
+def test_missing_inputs_fail_loudly(dev):
+    from gan.core import mmd, _lib
+    with pytest.raises(_lib.SmmdError):
+        mmd.mmd2_fused(torch.zeros(4, 1), torch.zeros(4, 1))   # CPU tensors: no CPU path
