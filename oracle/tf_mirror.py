@@ -1,0 +1,111 @@
+"""Op-by-op CPU mirror of the reference TF-1.x training step -- TEST / BASELINE
+INFRASTRUCTURE ONLY (bench.py's cpu_baseline leg and tests).
+
+TensorFlow 1.6 cannot run in this pipeline (BASELINE.md
+section 2), so the CPU baseline is this restatement in torch-CPU fp32, which
+materialises everything the TF graph materialises:
+
+* per SN layer: W_r reshape in the reference layout, 2 GEMVs, 2 l2-norms,
+  sigma, W_bar = W_r / sigma, s * W_bar   (gan/core/sn.py:16-59, snops.py:84)
+* K_XX, K_XY, K_YY via 3 matmuls + diag + clamp + exp, then 3 full sums
+  (gan/core/mmd.py:55-82, :199-220)
+* tf.gradients of the critic w.r.t. its input, sum of squares, mean, scale
+  (gan/core/ops.py:228-233, gan/core/model.py:382-390, smmd.py:21-23)
+* per-variable tf.clip_by_norm and the TF Adam update (model.py:444-468)
+
+The convolution stack itself is the same PyTorch module graph the product
+uses (gan.core.architecture, pure torch); only its SN weights are produced
+here instead of by the HIP bank.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import smmd_oracle as O
+
+
+def _l2n(v, eps=O.SN_EPS):
+    return v / (torch.sqrt(torch.sum(v * v)) + eps)
+
+
+def sn_weight_tf(W_torch, u, s, ref_layout_perm):
+    """W_torch: module weight; ref_layout_perm maps it to the TF layout
+    [kh, kw, Cin, Cout] (or [in, out] for linear).  Returns the effective
+    weight in torch layout and the new u (sn.py:24-46)."""
+    W_ref = W_torch.permute(*ref_layout_perm)
+    Wr = W_ref.reshape(-1, W_ref.shape[-1])
+    with torch.no_grad():
+        v = _l2n(u @ Wr.t())
+        u_new = _l2n(v @ Wr)
+    sigma = (v @ Wr @ u_new.t())[0, 0]
+    W_bar = (Wr / sigma).reshape(W_ref.shape)
+    if s is not None:
+        W_bar = s * W_bar
+    inv = [0] * len(ref_layout_perm)
+    for i, p in enumerate(ref_layout_perm):
+        inv[p] = i
+    return W_bar.permute(*inv), u_new
+
+
+def rbf_mmd2_tf(X, Y, sigma=1.0, wt=1.0):
+    XX, XY, YY = X @ X.t(), X @ Y.t(), Y @ Y.t()
+    sx, sy = torch.diagonal(XX), torch.diagonal(YY)
+    gamma = 1.0 / (2 * sigma ** 2)
+    KXY = wt * torch.exp(-gamma * torch.clamp(-2 * XY + sx[:, None] + sy[None, :], min=0.0))
+    KXX = wt * torch.exp(-gamma * torch.clamp(-2 * XX + sx[:, None] + sx[None, :], min=0.0))
+    KYY = wt * torch.exp(-gamma * torch.clamp(-2 * YY + sy[:, None] + sy[None, :], min=0.0))
+    m, n = float(X.shape[0]), float(Y.shape[0])
+    return ((KXX.sum() - m * wt) / (m * (m - 1)) + (KYY.sum() - n * wt) / (n * (n - 1))
+            - 2 * KXY.sum() / (m * n))
+
+
+class TFMirrorStep:
+    """One critic (D) update of SMMD exactly as the TF graph computes it."""
+
+    def __init__(self, G, D, sn_layers, lr=2e-4, beta1=0.5, beta2=0.9, sc=10.0, z_dim=128):
+        self.G, self.D, self.sn_layers = G, D, sn_layers
+        self.lr, self.b1, self.b2, self.sc, self.z_dim = lr, beta1, beta2, sc, z_dim
+        self.us = [torch.randn(1, m.weight.shape[0]) for m in sn_layers]
+        self.params = [p for p in D.parameters() if p.requires_grad]
+        self.m = [torch.zeros_like(p) for p in self.params]
+        self.v = [torch.zeros_like(p) for p in self.params]
+        self.t = 0
+
+    @staticmethod
+    def _perm(m):
+        return (2, 3, 1, 0) if m.weight.dim() == 4 and not hasattr(m, 'cout_first') else (1, 0)
+
+    def _sn(self):
+        for i, m in enumerate(self.sn_layers):
+            if m.weight.dim() == 4:
+                perm = (2, 3, 1, 0)          # [Cout, Cin, kh, kw] -> [kh, kw, Cin, Cout]
+            else:
+                perm = (1, 0)                # [out, in] -> [in, out]
+            s = m.sn_scale if hasattr(m, 'sn_scale') else None
+            m.w_eff, self.us[i] = sn_weight_tf(m.weight, self.us[i], s, perm)
+
+    def step(self, images):
+        self._sn()
+        with torch.no_grad():
+            fake = self.G(torch.empty(images.shape[0], self.z_dim).uniform_(-1, 1))
+        x = images.detach().requires_grad_(True)
+        d_images = self.D(x)
+        d_G = self.D(fake)
+        mmd2 = rbf_mmd2_tf(d_G, d_images)
+        g, = torch.autograd.grad(d_images[:, 0].sum(), x, create_graph=True)
+        J = torch.sum(g * g, dim=(1, 2, 3)).mean()
+        scale = 1.0 / (self.sc * J + 1.0)
+        d_loss = -(mmd2 * scale)
+        grads = torch.autograd.grad(d_loss, self.params)
+        self.t += 1
+        lr_t = self.lr * math.sqrt(1 - self.b2 ** self.t) / (1 - self.b1 ** self.t)
+        with torch.no_grad():
+            for p, gr, m, v in zip(self.params, grads, self.m, self.v):
+                inv = torch.rsqrt(torch.sum(gr * gr))
+                gr = gr * 1.0 * torch.clamp(inv, max=1.0)       # tf.clip_by_norm(g, 1.)
+                m += (gr - m) * (1 - self.b1)
+                v += (gr * gr - v) * (1 - self.b2)
+                p -= lr_t * m / (torch.sqrt(v) + 1e-8)
+        return float(d_loss.detach())

@@ -1,0 +1,342 @@
+"""Generators / critics of the BASELINE configs (gan/core/architecture.py),
+on PyTorch-ROCm, NCHW fp32.
+
+Built: sngan (SNGANGenerator + SNGANDiscriminator, cifar10_smmd.yml),
+snresnet (SNResNetGenerator + SNResNetDiscriminator, imagenet_smmd.yml),
+g-resnet5 (ResNetGenerator + DCGAN5Discriminator, celebA_smmd.yml), plus the
+plain dcgan / dcgan5 / sngan-dcgan5 / resnet5 variants.  The conditional
+(label) networks are out of scope.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .snops import Conv2d, Deconv2d, Linear, batch_norm, lrelu
+
+
+def conv_sizes(size, layers, stride=2):
+    """gan/utils/misc.py:228-232."""
+    s = [int(size)]
+    for _ in range(layers):
+        s.append(int(-(-s[-1] // stride)))
+    return tuple(s)
+
+
+class _Identity(nn.Module):
+    def forward(self, x):
+        return x
+
+
+def _bn_or_id(use, c):
+    return batch_norm(c) if use else _Identity()
+
+
+# ---------------------------------------------------------------------------
+# ResNet blocks (gan/core/resnet/block.py:9-86)
+# ---------------------------------------------------------------------------
+class _Up(nn.Module):
+    """UpsampleConv (block.py:53-60): concat x4 + depth_to_space(2) = nearest x2."""
+
+    def __init__(self, cin, cout, k, bias, **sn):
+        super().__init__()
+        self.conv = Conv2d(cin, cout, k, 1, bias=bias, init='glorot_uniform', **sn)
+
+    def forward(self, x):
+        return self.conv(F.interpolate(x, scale_factor=2, mode='nearest'))
+
+
+class _ConvMeanPool(nn.Module):
+    """block.py:63-66."""
+
+    def __init__(self, cin, cout, k, bias, **sn):
+        super().__init__()
+        self.conv = Conv2d(cin, cout, k, 1, bias=bias, init='glorot_uniform', **sn)
+
+    def forward(self, x):
+        return F.avg_pool2d(self.conv(x), 2)
+
+
+class _MeanPoolConv(nn.Module):
+    """block.py:69-73."""
+
+    def __init__(self, cin, cout, k, bias, **sn):
+        super().__init__()
+        self.conv = Conv2d(cin, cout, k, 1, bias=bias, init='glorot_uniform', **sn)
+
+    def forward(self, x):
+        return self.conv(F.avg_pool2d(x, 2))
+
+
+class ResidualBlock(nn.Module):
+    """block.py:9-50: shortcut + conv_2(relu(norm(conv_1(relu(norm(x))))))."""
+
+    def __init__(self, cin, cout, k=3, resample=None, mode='', with_sn=False,
+                 with_learnable_sn_scale=False):
+        super().__init__()
+        sn = dict(with_sn=with_sn, with_learnable_sn_scale=with_learnable_sn_scale)
+        if resample == 'down':
+            short = _MeanPoolConv
+            self.conv_1 = Conv2d(cin, cin, k, 1, bias=False, init='glorot_uniform', **sn)
+            self.conv_2 = _ConvMeanPool(cin, cout, k, True, **sn)
+            n1, n2 = cin, cin
+        elif resample == 'up':
+            short = _Up
+            self.conv_1 = _Up(cin, cout, k, False, **sn)
+            self.conv_2 = Conv2d(cout, cout, k, 1, bias=True, init='glorot_uniform', **sn)
+            n1, n2 = cin, cout
+        elif resample is None:
+            short = None
+            self.conv_1 = Conv2d(cin, cin, k, 1, bias=False, init='glorot_uniform', **sn)
+            self.conv_2 = Conv2d(cin, cout, k, 1, bias=True, init='glorot_uniform', **sn)
+            n1, n2 = cin, cin
+        else:
+            raise ValueError('invalid resample value')
+        if cin == cout and resample is None:
+            self.shortcut = None
+        elif short is None:
+            self.shortcut = Conv2d(cin, cout, 1, 1, bias=True, init='glorot_uniform', **sn)
+        else:
+            self.shortcut = short(cin, cout, 1, True, **sn)
+        use_bn = mode == 'batchnorm'                     # Normalize, block.py:76-86
+        self.bn1 = _bn_or_id(use_bn, n1)
+        self.bn2 = _bn_or_id(use_bn, n2)
+
+    def forward(self, x):
+        s = x if self.shortcut is None else self.shortcut(x)
+        h = self.conv_1(F.relu(self.bn1(x)))
+        h = self.conv_2(F.relu(self.bn2(h)))
+        return s + h
+
+
+# ---------------------------------------------------------------------------
+# generators
+# ---------------------------------------------------------------------------
+class SNGANGenerator(nn.Module):
+    """architecture.py:211-230."""
+
+    def __init__(self, dim, c_dim, output_size, use_batch_norm, z_dim=128):
+        super().__init__()
+        s1, s2, s4, s8, _ = conv_sizes(output_size, 4)
+        self.dim, self.s8 = dim, s8
+        self.h0_lin = Linear(z_dim, dim * 8 * s8 * s8)
+        self.bn0 = _bn_or_id(use_batch_norm, dim * 8)
+        self.h1 = Deconv2d(dim * 8, dim * 4)
+        self.bn1 = _bn_or_id(use_batch_norm, dim * 4)
+        self.h2 = Deconv2d(dim * 4, dim * 2)
+        self.bn2 = _bn_or_id(use_batch_norm, dim * 2)
+        self.h3 = Deconv2d(dim * 2, dim)
+        self.bn3 = _bn_or_id(use_batch_norm, dim)
+        self.h4 = Deconv2d(dim, c_dim, 3, 1)
+
+    def forward(self, z):
+        h = self.h0_lin(z).view(-1, self.dim * 8, self.s8, self.s8)
+        h = F.relu(self.bn0(h))
+        h = F.relu(self.bn1(self.h1(h)))
+        h = F.relu(self.bn2(self.h2(h)))
+        h = F.relu(self.bn3(self.h3(h)))
+        return torch.sigmoid(self.h4(h))
+
+
+class DCGANGenerator(nn.Module):
+    """architecture.py:103-124 (layers=4) and DCGAN5Generator :127-149 (layers=5)."""
+
+    def __init__(self, dim, c_dim, output_size, use_batch_norm, z_dim=128, layers=4):
+        super().__init__()
+        s = conv_sizes(output_size, layers)
+        mult = 8 if layers == 4 else 16
+        self.top, self.s0 = dim * mult, s[-1]
+        self.h0_lin = Linear(z_dim, self.top * s[-1] * s[-1])
+        self.bn0 = _bn_or_id(use_batch_norm, self.top)
+        chans = [self.top // (2 ** i) for i in range(layers)] + [c_dim]
+        self.deconvs = nn.ModuleList(Deconv2d(chans[i], chans[i + 1]) for i in range(layers))
+        self.bns = nn.ModuleList(_bn_or_id(use_batch_norm, chans[i + 1])
+                                 for i in range(layers - 1))
+
+    def forward(self, z):
+        h = F.relu(self.bn0(self.h0_lin(z).view(-1, self.top, self.s0, self.s0)))
+        for i, dc in enumerate(self.deconvs):
+            h = dc(h)
+            if i < len(self.bns):
+                h = F.relu(self.bns[i](h))
+        return torch.sigmoid(h)
+
+
+class ResNetGenerator(nn.Module):
+    """architecture.py:152-175 (g-resnet5): blocks with mode='' (no BN), final
+    Batchnorm + relu + deconv 5x5/2 + sigmoid."""
+
+    def __init__(self, dim, c_dim, output_size, use_batch_norm, z_dim=128):
+        super().__init__()
+        s = conv_sizes(output_size, 5)
+        self.dim, self.s32 = dim, s[5]
+        self.h0_lin = Linear(z_dim, dim * 16 * s[5] * s[5])
+        self.res = nn.Sequential(ResidualBlock(16 * dim, 8 * dim, 3, 'up'),
+                                 ResidualBlock(8 * dim, 4 * dim, 3, 'up'),
+                                 ResidualBlock(4 * dim, 2 * dim, 3, 'up'),
+                                 ResidualBlock(2 * dim, dim, 3, 'up'))
+        self.bn4 = batch_norm(dim)
+        self.h5 = Deconv2d(dim, c_dim)
+
+    def forward(self, z):
+        h = self.h0_lin(z).view(-1, self.dim * 16, self.s32, self.s32)
+        h = F.relu(self.bn4(self.res(h)))
+        return torch.sigmoid(self.h5(h))
+
+
+class SNResNetGenerator(nn.Module):
+    """architecture.py:178-208: mode='batchnorm' blocks; 64 px starts at 4x4."""
+
+    def __init__(self, dim, c_dim, output_size, use_batch_norm, z_dim=128):
+        super().__init__()
+        s = conv_sizes(output_size, 5)
+        s32 = 4 if output_size == 64 else s[5]
+        self.dim, self.s32 = dim, s32
+        self.h0_lin = Linear(z_dim, dim * 16 * s32 * s32)
+        blocks = []
+        if output_size != 64:
+            blocks.append(ResidualBlock(16 * dim, 16 * dim, 3, 'up', 'batchnorm'))
+        blocks += [ResidualBlock(16 * dim, 8 * dim, 3, 'up', 'batchnorm'),
+                   ResidualBlock(8 * dim, 4 * dim, 3, 'up', 'batchnorm'),
+                   ResidualBlock(4 * dim, 2 * dim, 3, 'up', 'batchnorm'),
+                   ResidualBlock(2 * dim, dim, 3, 'up', 'batchnorm')]
+        self.res = nn.Sequential(*blocks)
+        self.bn4 = batch_norm(dim)
+        self.h5 = Deconv2d(dim, c_dim, 3, 1)
+
+    def forward(self, z):
+        h = self.h0_lin(z).view(-1, self.dim * 16, self.s32, self.s32)
+        h = F.relu(self.bn4(self.res(h)))
+        return torch.sigmoid(self.h5(h))
+
+
+# ---------------------------------------------------------------------------
+# critics
+# ---------------------------------------------------------------------------
+class SNGANDiscriminator(nn.Module):
+    """architecture.py:395-407 (final linear is always SN, :406)."""
+
+    def __init__(self, dim, o_dim, use_batch_norm, with_sn=False, with_learnable_sn_scale=False,
+                 input_size=32):
+        super().__init__()
+        sn = dict(with_sn=with_sn, with_learnable_sn_scale=with_learnable_sn_scale)
+        spec = [(3, 64, 3, 1), (64, 128, 4, 2), (128, 128, 3, 1), (128, 256, 4, 2),
+                (256, 256, 3, 1), (256, 512, 4, 2), (512, 512, 3, 1)]
+        self.convs = nn.ModuleList(Conv2d(ci, co, k, s, stddev=0.02, **sn) for ci, co, k, s in spec)
+        final = input_size // 8
+        self.l4 = Linear(512 * final * final, o_dim, with_sn=True, stddev=0.02)
+
+    def forward(self, x, return_layers=False):
+        layers = {}
+        h = x
+        for i, c in enumerate(self.convs):
+            h = lrelu(c(h))
+            layers['h%d' % i] = h
+        hF = self.l4(h.reshape(h.shape[0], -1))
+        layers['hF'] = hF
+        return layers if return_layers else hF
+
+
+class DCGANDiscriminator(nn.Module):
+    """architecture.py:323-343 (DCGAN: 4 convs, DCGAN5: 5 convs), 5x5/2 SAME."""
+
+    def __init__(self, dim, o_dim, use_batch_norm, with_sn=False, with_learnable_sn_scale=False,
+                 input_size=64, layers=4):
+        super().__init__()
+        sn = dict(with_sn=with_sn, with_learnable_sn_scale=with_learnable_sn_scale)
+        chans = [3] + [dim * (2 ** i) for i in range(layers)]
+        self.convs = nn.ModuleList(Conv2d(chans[i], chans[i + 1], 5, 2, **sn)
+                                   for i in range(layers))
+        self.bns = nn.ModuleList(_bn_or_id(use_batch_norm and i > 0, chans[i + 1])
+                                 for i in range(layers))
+        final = conv_sizes(input_size, layers)[-1]
+        o = o_dim if o_dim > 0 else chans[-1]
+        self.lin = Linear(chans[-1] * final * final, o, **sn)
+
+    def forward(self, x, return_layers=False):
+        layers = {}
+        h = x
+        for i, (c, bn) in enumerate(zip(self.convs, self.bns)):
+            h = lrelu(bn(c(h)))
+            layers['h%d' % i] = h
+        hF = self.lin(h.reshape(h.shape[0], -1))
+        layers['hF'] = hF
+        return layers if return_layers else hF
+
+
+class SNResNetDiscriminator(nn.Module):
+    """architecture.py:410-434."""
+
+    def __init__(self, dim, o_dim, use_batch_norm, with_sn=False, with_learnable_sn_scale=False,
+                 input_size=64):
+        super().__init__()
+        sn = dict(with_sn=with_sn, with_learnable_sn_scale=with_learnable_sn_scale)
+        self.h0 = Conv2d(3, dim, 3, 1, init='glorot_uniform', **sn)
+        blocks = [ResidualBlock(dim, 2 * dim, 3, 'down', **sn),
+                  ResidualBlock(2 * dim, 4 * dim, 3, 'down', **sn),
+                  ResidualBlock(4 * dim, 8 * dim, 3, 'down', **sn),
+                  ResidualBlock(8 * dim, 16 * dim, 3, 'down', **sn)]
+        if input_size != 64:
+            blocks.append(ResidualBlock(16 * dim, 16 * dim, 3, None, **sn))
+        self.res = nn.ModuleList(blocks)
+        self.h5_lin = Linear(16 * dim, o_dim, **sn)
+
+    def forward(self, x, return_layers=False):
+        layers = {}
+        h = lrelu(self.h0(x))
+        layers['h0'] = h
+        for i, b in enumerate(self.res):
+            h = b(h)
+            layers['h%d' % (i + 1)] = h
+        h = lrelu(h).sum(dim=(2, 3))
+        hF = self.h5_lin(h)
+        layers['hF'] = hF
+        return layers if return_layers else hF
+
+
+class ResNetDiscriminator(nn.Module):
+    """architecture.py:358-375 (no SN)."""
+
+    def __init__(self, dim, o_dim, use_batch_norm, with_sn=False, with_learnable_sn_scale=False,
+                 input_size=64):
+        super().__init__()
+        self.h0 = Conv2d(3, dim, 3, 1, init='glorot_uniform')
+        self.res = nn.ModuleList([ResidualBlock(dim, 2 * dim, 3, 'down'),
+                                  ResidualBlock(2 * dim, 4 * dim, 3, 'down'),
+                                  ResidualBlock(4 * dim, 8 * dim, 3, 'down'),
+                                  ResidualBlock(8 * dim, 8 * dim, 3, 'down')])
+        self.h5_lin = Linear(4 * 4 * 8 * dim, o_dim)
+
+    def forward(self, x, return_layers=False):
+        layers = {}
+        h = lrelu(self.h0(x))
+        layers['h0'] = h
+        for i, b in enumerate(self.res):
+            h = b(h)
+            layers['h%d' % (i + 1)] = h
+        hF = self.h5_lin(h.reshape(h.shape[0], -1))
+        layers['hF'] = hF
+        return layers if return_layers else hF
+
+
+def get_networks(architecture):
+    """architecture.py:437-459 -> (Generator factory, Discriminator factory)."""
+    gd = {
+        'dcgan': (lambda *a, **k: DCGANGenerator(*a, layers=4, **k),
+                  lambda *a, **k: DCGANDiscriminator(*a, layers=4, **k)),
+        'dcgan5': (lambda *a, **k: DCGANGenerator(*a, layers=5, **k),
+                   lambda *a, **k: DCGANDiscriminator(*a, layers=5, **k)),
+        'sngan': (SNGANGenerator, SNGANDiscriminator),
+        'sngan-dcgan5': (SNGANGenerator, lambda *a, **k: DCGANDiscriminator(*a, layers=5, **k)),
+        'snresnet': (SNResNetGenerator, SNResNetDiscriminator),
+        'resnet5': (ResNetGenerator, ResNetDiscriminator),
+    }
+    if architecture in gd:
+        return gd[architecture]
+    if 'g-resnet5' in architecture:
+        return ResNetGenerator, lambda *a, **k: DCGANDiscriminator(*a, layers=5, **k)
+    if architecture in ('cond_snresnet', 'd-fullconv5', 'dc64', 'dcgan64', 'dc128'):
+        raise NotImplementedError('architecture %r is outside this build (SURVEY.md section 2)'
+                                  % architecture)
+    raise ValueError('Wrong architecture: "%s"' % architecture)

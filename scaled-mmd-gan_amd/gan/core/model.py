@@ -1,0 +1,283 @@
+"""MMD-GAN trainer (gan/core/model.py, MMD_GAN) on PyTorch-ROCm + libsmmd_hip.
+
+One process per GPU.  A training step (one optimizer update, model.py:507-546):
+
+  D step:  SN bank refresh (all critic layers, 1 HIP launch set)
+           -> G(z) (no grad) -> critic(real), critic(fake)
+           -> fused MMD^2 (1 HIP launch, gradient in the same sweep)
+           -> jac = d critic(real) / d real   (PyTorch, create_graph)
+           -> scaled loss (HIP) -> backward (PyTorch double backward + HIP ops)
+           -> [RCCL all_reduce of one flat gradient buffer]
+           -> clip_by_norm + TF-Adam over all critic tensors (1 HIP launch set)
+  G step:  same forward with G in the graph; the scale is a constant for G
+           (it depends on the critic only), so no double backward.
+
+Data-parallel modes:
+  'tower'  -- the reference's towers (model.py:187-266): local MMD^2 and scale
+              per rank, per-rank clip_by_norm, all_reduce(SUM)/world, Adam.
+  'global' -- the north-star mode: critic features all-gathered so each rank
+              evaluates the full (world*batch) pairwise kernel; one scalar
+              all_reduce; parameter gradients all_reduce(SUM); clip; Adam.
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import mmd, ops
+from .architecture import get_networks
+from .optim import FlatAdam
+from .sn import SpectralNormBank
+from .snops import sn_modules
+
+
+class Timer:
+    """gan/utils/timer.py: '[%8d][%s] msg' every `limit` steps and the first 10."""
+
+    def __init__(self, start_time=None, limit=100):
+        self.start_time = time.time() if start_time is None else start_time
+        self.limit = limit
+
+    def __call__(self, step, mess='', prints=True):
+        if prints and (step % self.limit != 0) and (step > 10):
+            return None
+        t = int(time.time() - self.start_time)
+        m, s = t // 60, t % 60
+        h, m = m // 60, m % 60
+        hms = '%2dh%02dm%02ds' % (h, m, s) if h else ('%5dm%02ds' % (m, s) if m else '%8ds' % s)
+        msg = '[%8d][%s] %s' % (step, hms, mess)
+        if prints:
+            print(msg)
+            return None
+        return msg
+
+
+class MMD_GAN:
+    """Base model: loss = mmd2 of the configured kernel (model.py:313-325),
+    optional witness gradient penalty (:327-350) and L2 critic penalty
+    (:352-364)."""
+
+    def __init__(self, config, device=None, process_group=None, dp_mode='tower',
+                 batch_size=None, output_size=None, c_dim=3):
+        c = config
+        if getattr(c, 'learning_rate_D', -1) < 0:               # model.py:18-19
+            c.learning_rate_D = c.learning_rate
+        if getattr(c, 'real_batch_size', -1) == -1:             # model.py:42-43
+            c.real_batch_size = c.batch_size
+        self.config = c
+        self.device = device or torch.device('cuda', torch.cuda.current_device())
+        self.group = process_group
+        self.world = dist.get_world_size(process_group) if (
+            process_group is not None or (dist.is_available() and dist.is_initialized())) else 1
+        if dp_mode not in ('tower', 'global'):
+            raise ValueError(dp_mode)
+        self.dp_mode = dp_mode
+        self.batch_size = batch_size or c.batch_size
+        self.real_batch_size = c.real_batch_size
+        self.output_size = output_size or c.output_size
+        self.c_dim = c_dim
+        self.z_dim = c.z_dim
+        self.timer = Timer()
+        G_cls, D_cls = get_networks(c.architecture)
+        dbn = bool(c.batch_norm) and (c.gradient_penalty <= 0)   # model.py:270
+        self.generator = G_cls(c.gf_dim, c_dim, self.output_size, c.batch_norm,
+                               z_dim=c.z_dim).to(self.device)
+        self.discriminator = D_cls(c.df_dim, c.dof_dim, dbn, with_sn=c.with_sn,
+                                   with_learnable_sn_scale=c.with_learnable_sn_scale,
+                                   input_size=self.output_size).to(self.device)
+        self.sn_D = SpectralNormBank(sn_modules(self.discriminator))
+        self.sn_G = SpectralNormBank(sn_modules(self.generator))
+        self.spec = mmd.get_kernel_spec(c.kernel) if c.kernel else None
+        self.g_vars = [p for p in self.generator.parameters() if p.requires_grad]
+        self.d_vars = [p for p in self.discriminator.parameters() if p.requires_grad]
+        clip = 1.0 if c.clip_grad else 0.0
+        self.g_optim = FlatAdam(self.g_vars, c.learning_rate, c.beta1, c.beta2, clip_norm=clip)
+        self.d_optim = FlatAdam(self.d_vars, c.learning_rate_D, c.beta1, c.beta2, clip_norm=clip)
+        self.lr = float(c.learning_rate)
+        self.sc = float(c.scaling_coeff) if c.with_scaling else None
+        self.gp = float(c.gradient_penalty)
+        self.step = 0
+        self.d_counter = 0
+        self.g_counter = 0
+        self.optim_name = 'kernel_loss'
+        self.last = {}
+        if self.world > 1:
+            self._broadcast_params()
+
+    # ------------------------------------------------------------------
+    def _dist_group(self):
+        return self.group if self.world > 1 else None
+
+    def _broadcast_params(self):
+        for opt in (self.g_optim, self.d_optim):
+            dist.broadcast(opt.flat_param, 0, group=self.group)
+        for bank in (self.sn_D, self.sn_G):
+            for e in bank.entries:
+                dist.broadcast(e.u, 0, group=self.group)
+
+    def set_counters(self, step):
+        """model.py:470-478."""
+        c = self.config
+        if self.g_counter == 0:
+            d_steps = c.dsteps
+            if (step % 500 == 0) or (step < 20):
+                d_steps = c.start_dsteps
+            self.d_counter = (self.d_counter + 1) % (d_steps + 1)
+        if self.d_counter == 0:
+            self.g_counter = (self.g_counter + 1) % c.gsteps
+
+    def sample_z(self, n):
+        return torch.empty(n, self.z_dim, device=self.device).uniform_(-1.0, 1.0)  # model.py:271
+
+    # ------------------------------------------------------------------
+    # losses (overridden by SMMD / SWGAN)
+    # ------------------------------------------------------------------
+    def base_loss(self, d_G, d_images):
+        """mmd2 of the configured kernel (model.py:314-318)."""
+        grp = self._dist_group() if self.dp_mode == 'global' else None
+        return mmd.mmd2_fused(d_G, d_images, self.spec, process_group=grp)
+
+    def apply_scaling(self, base, jac, d_images):
+        return ops.scaled_loss(base, jac, d_images, sc=self.sc, variant=self.config.scaling_variant,
+                               sqrt_scale=False,
+                               process_group=self._dist_group() if self.dp_mode == 'global'
+                               else None)
+
+    def uses_scaling(self):
+        return False
+
+    # ------------------------------------------------------------------
+    def _critic_losses(self, images, fake, need_critic_grad):
+        """Returns (g_loss, d_loss, aux).  need_critic_grad: build the graph
+        for d_loss w.r.t. the critic (including the Jacobian double backward)."""
+        D = self.discriminator
+        scaling = self.uses_scaling()
+        if scaling:
+            images = images.detach().requires_grad_(True)
+        d_images = D(images)
+        d_G = D(fake)
+        base = self.base_loss(d_G, d_images)
+        aux = None
+        if scaling:
+            jac = ops.jacobian_columns(d_images, images, create_graph=need_critic_grad)
+            if not need_critic_grad:
+                jac = jac.detach()
+            g_loss, aux = self.apply_scaling(base, jac, d_images)
+        else:
+            g_loss = base
+        d_loss = -g_loss
+        if need_critic_grad and self.gp > 0:
+            d_loss = d_loss + self.gp * self.gradient_penalty(images, fake, d_images, d_G)
+        if need_critic_grad and self.config.L2_discriminator_penalty > 0:
+            raise NotImplementedError('L2_discriminator_penalty is outside this build')
+        return g_loss, d_loss, aux
+
+    def gradient_penalty(self, images, fake, d_images, d_G):
+        """Witness GP (model.py:327-350): x_hat = (1-a) real + a fake; the
+        witness gradient at the critic output comes from the HIP witness op
+        (with its own second-order backward); the input gradient and the
+        penalty (norm over the CHANNEL axis only, model.py:341) are PyTorch."""
+        bs = min(self.batch_size, self.real_batch_size)
+        alpha = torch.rand(bs, 1, 1, 1, device=self.device)
+        x_hat = ((1.0 - alpha) * images[:bs].detach() + alpha * fake[:bs].detach())
+        x_hat.requires_grad_(True)
+        h = self.discriminator(x_hat)
+        dH, _ = mmd.witness_and_grad(h, d_images[:bs], d_G[:bs], self.spec)
+        g, = torch.autograd.grad(h, x_hat, grad_outputs=dH, create_graph=True)
+        return torch.mean((ops.safer_norm(g, axis=1) - 1.0) ** 2)
+
+    # ------------------------------------------------------------------
+    def _exchange(self, opt):
+        if self.world == 1:
+            opt.step()
+            return
+        if self.dp_mode == 'tower':
+            # per-tower clip (model.py:449,455), then the tower mean (:257-258)
+            if opt.clip_norm > 0:
+                opt.clip_()
+            dist.all_reduce(opt.flat_grad, group=self.group)
+            opt.step(grad_scale=1.0 / self.world, clip=False)
+        else:
+            dist.all_reduce(opt.flat_grad, group=self.group)
+            opt.step()
+
+    def d_step(self, images):
+        self.sn_D.refresh(update_u=True)
+        if self.sn_G.entries:
+            self.sn_G.refresh(update_u=True)
+        with torch.no_grad():
+            fake = self.generator(self.sample_z(self.batch_size))
+        for p in self.d_vars:
+            p.requires_grad_(True)
+        self.d_optim.zero_grad()
+        g_loss, d_loss, aux = self._critic_losses(images, fake, need_critic_grad=True)
+        d_loss.backward()
+        self._exchange(self.d_optim)
+        return g_loss, d_loss, aux
+
+    def g_step(self, images):
+        self.sn_D.refresh(update_u=True)
+        if self.sn_G.entries:
+            self.sn_G.refresh(update_u=True)
+        for p in self.d_vars:
+            p.requires_grad_(False)
+        try:
+            self.g_optim.zero_grad()
+            fake = self.generator(self.sample_z(self.batch_size))
+            g_loss, d_loss, aux = self._critic_losses(images, fake, need_critic_grad=False)
+            g_loss.backward()
+            self._exchange(self.g_optim)
+        finally:
+            for p in self.d_vars:
+                p.requires_grad_(True)
+        return g_loss, d_loss, aux
+
+    def train_step(self, images):
+        """model.py:507-546 (lean: only the gradient set being applied)."""
+        step = self.step
+        self.set_counters(step)
+        if self.d_counter == 0:
+            g_loss, d_loss, aux = self.g_step(images)
+            self.step += 1                                   # global_step (model.py:460-463)
+        else:
+            g_loss, d_loss, aux = self.d_step(images)
+        self.last = {'g_loss': g_loss.detach(), 'd_loss': d_loss.detach(), 'aux': aux}
+        return g_loss, d_loss, step
+
+    def check_finite(self):
+        """NaN asserts of model.py:537-538 (forces a host sync)."""
+        g = float(self.last['g_loss'])
+        d = float(self.last['d_loss'])
+        assert not np.isnan(g), 'NaN g_loss'
+        assert not np.isnan(d), 'NaN d_loss'
+        return g, d
+
+    def decay_ops(self):
+        """lr *= decay_rate (min 1e-6) and sc *= sc_decay_rate (model.py:162, :173, :493-496)."""
+        c = self.config
+        self.lr = max(self.lr * c.decay_rate, 1e-6)
+        self.g_optim.lr = self.lr
+        self.d_optim.lr = self.lr * c.learning_rate_D / c.learning_rate
+        if self.sc is not None:
+            self.sc *= c.sc_decay_rate
+
+    # checkpoint: torch state (the TF Saver format is out of scope)
+    def state_dict(self):
+        return {'G': self.generator.state_dict(), 'D': self.discriminator.state_dict(),
+                'sn_D': self.sn_D.state_dict(), 'sn_G': self.sn_G.state_dict(),
+                'g_optim': self.g_optim.state_dict(), 'd_optim': self.d_optim.state_dict(),
+                'step': self.step, 'lr': self.lr, 'sc': self.sc,
+                'counters': (self.d_counter, self.g_counter)}
+
+    def load_state_dict(self, sd):
+        self.generator.load_state_dict(sd['G'])
+        self.discriminator.load_state_dict(sd['D'])
+        self.sn_D.load_state_dict(sd['sn_D'])
+        self.sn_G.load_state_dict(sd['sn_G'])
+        self.g_optim.load_state_dict(sd['g_optim'])
+        self.d_optim.load_state_dict(sd['d_optim'])
+        self.step, self.lr, self.sc = sd['step'], sd['lr'], sd['sc']
+        self.d_counter, self.g_counter = sd['counters']

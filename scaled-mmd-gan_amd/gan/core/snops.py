@@ -1,0 +1,135 @@
+"""SN-aware layers (gan/core/snops.py, gan/core/resnet/ops/conv2d.py) on
+PyTorch-ROCm.
+
+The conv / matmul math runs on MIOpen / hipBLASLt; the spectral
+normalisation is NOT done per layer: each SN layer registers with its
+network's :class:`~gan.core.sn.SpectralNormBank`, which writes ``w_eff``
+(= s * W / sigma, snops.py:82-84) for every layer in one HIP launch set
+before the critic runs.  TF 'SAME' padding is reproduced exactly
+(asymmetric padding where TF pads more on the bottom/right).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+def same_pad(n_in, k, s):
+    """TF 'SAME': total = max((ceil(n/s) - 1) s + k - n, 0), before = total // 2."""
+    n_out = -(-n_in // s)
+    total = max((n_out - 1) * s + k - n_in, 0)
+    return total // 2, total - total // 2
+
+
+def _trunc_normal_(t, std):
+    nn.init.trunc_normal_(t, mean=0.0, std=std, a=-2 * std, b=2 * std)
+
+
+def _glorot_uniform_(t, fan_in, fan_out):
+    lim = math.sqrt(6.0 / (fan_in + fan_out))
+    nn.init.uniform_(t, -lim, lim)
+
+
+class _SNMixin:
+    """with_sn: forward uses self.w_eff (set by the bank); with_learnable_sn_scale
+    makes ``sn_scale`` trainable (snops.py:82)."""
+
+    def _init_sn(self, with_sn, with_learnable_sn_scale, scale):
+        self.with_sn = with_sn
+        if with_sn:
+            self.sn_scale = nn.Parameter(torch.full((1,), float(scale)),
+                                         requires_grad=with_learnable_sn_scale)
+        self.w_eff = None
+
+    def effective_weight(self):
+        if not self.with_sn:
+            return self.weight
+        if self.w_eff is None:
+            raise RuntimeError('SN layer used before its SpectralNormBank.refresh()')
+        return self.w_eff
+
+
+class Conv2d(nn.Module, _SNMixin):
+    """snops.conv2d / resnet Conv2D: NCHW conv with TF SAME padding.
+    init: 'truncated_normal' (snops.py:77-78) or 'glorot_uniform'
+    (resnet/ops/conv2d.py:26-27)."""
+
+    def __init__(self, cin, cout, k=5, stride=2, bias=True, with_sn=False,
+                 with_learnable_sn_scale=False, scale=1.0, init='truncated_normal', stddev=0.02):
+        super().__init__()
+        self.cin, self.cout, self.k, self.stride = cin, cout, k, stride
+        self.weight = nn.Parameter(torch.empty(cout, cin, k, k))
+        if init == 'glorot_uniform':
+            _glorot_uniform_(self.weight, k * k * cin, k * k * cout)
+        else:
+            _trunc_normal_(self.weight, stddev)
+        self.bias = nn.Parameter(torch.zeros(cout)) if bias else None
+        self._init_sn(with_sn, with_learnable_sn_scale, scale)
+
+    def forward(self, x):
+        w = self.effective_weight()
+        ph = same_pad(x.shape[2], self.k, self.stride)
+        pw = same_pad(x.shape[3], self.k, self.stride)
+        if ph[0] == ph[1] and pw[0] == pw[1]:
+            return F.conv2d(x, w, self.bias, self.stride, (ph[0], pw[0]))
+        x = F.pad(x, (pw[0], pw[1], ph[0], ph[1]))
+        return F.conv2d(x, w, self.bias, self.stride)
+
+
+class Deconv2d(nn.Module, _SNMixin):
+    """snops.deconv2d: tf.nn.conv2d_transpose with SAME padding, output = in * s.
+    Weight kept as torch stores it, [cin, cout, k, k]; its SN rows are the
+    input channels, matching the reference reshape [kh*kw*cout, cin]
+    (snops.py:114-117)."""
+
+    def __init__(self, cin, cout, k=5, stride=2, bias=True, with_sn=False,
+                 with_learnable_sn_scale=False, scale=1.0, stddev=0.02):
+        super().__init__()
+        self.cin, self.cout, self.k, self.stride = cin, cout, k, stride
+        self.weight = nn.Parameter(torch.empty(cin, cout, k, k))
+        nn.init.normal_(self.weight, 0.0, stddev)
+        self.bias = nn.Parameter(torch.zeros(cout)) if bias else None
+        self._init_sn(with_sn, with_learnable_sn_scale, scale)
+
+    def forward(self, x):
+        w = self.effective_weight()
+        h, wd = x.shape[2] * self.stride, x.shape[3] * self.stride
+        before, _ = same_pad(h, self.k, self.stride)
+        y = F.conv_transpose2d(x, w, self.bias, self.stride, before)
+        if y.shape[2] != h or y.shape[3] != wd:
+            y = y[:, :, :h, :wd]
+        return y
+
+
+class Linear(nn.Module, _SNMixin):
+    """snops.linear: weight [out, in] (reference Matrix [in, out]),
+    random-normal init (snops.py:175-176)."""
+
+    def __init__(self, cin, cout, bias=True, with_sn=False, with_learnable_sn_scale=False,
+                 scale=1.0, stddev=0.01, bias_start=0.0):
+        super().__init__()
+        self.weight = nn.Parameter(torch.empty(cout, cin))
+        nn.init.normal_(self.weight, 0.0, stddev)
+        self.bias = nn.Parameter(torch.full((cout,), float(bias_start))) if bias else None
+        self._init_sn(with_sn, with_learnable_sn_scale, scale)
+
+    def forward(self, x):
+        return F.linear(x, self.effective_weight(), self.bias)
+
+
+def batch_norm(c):
+    """tf.layers.batch_normalization(momentum=.9, eps=1e-5, training=True)
+    (snops.py:31-40, resnet/ops/batchnorm.py:10-18)."""
+    return nn.BatchNorm2d(c, eps=1e-5, momentum=0.1)
+
+
+def lrelu(x, leak=0.2):
+    """max(x, leak * x)  (snops.py:165-166)."""
+    return F.leaky_relu(x, leak)
+
+
+def sn_modules(module):
+    return [m for m in module.modules() if isinstance(m, _SNMixin) and m.with_sn]

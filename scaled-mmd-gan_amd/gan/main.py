@@ -1,0 +1,157 @@
+"""Drop-in CLI of gan/main.py: same single-dash flags, same defaults, and the
+same YAML-overrides-CLI rule (gan/main.py:18-25), dispatching to the MI355X
+trainer.
+
+    python scaled-mmd-gan_amd/gan/main.py -config_file configs/imagenet_smmd.yml
+    torchrun --nproc-per-node 8 scaled-mmd-gan_amd/gan/main.py -config_file ... -dp_mode global
+
+Data: datasets are not shipped (no network); ``-dataset synthetic`` (or any
+dataset whose files are absent, with a warning) feeds U[0,1] images of the
+configured size, matching the reference pipeline's value range
+(gan/core/pipeline.py:201, :403).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_PKG = os.path.dirname(_HERE)
+if _PKG not in sys.path:
+    sys.path.insert(0, _PKG)
+
+
+def str2bool(v):
+    """gan/main.py:9-15."""
+    if isinstance(v, bool):
+        return v
+    if v.lower() in ('yes', 'true', 't', 'y', '1'):
+        return True
+    if v.lower() in ('no', 'false', 'f', 'n', '0'):
+        return False
+    raise argparse.ArgumentTypeError('Boolean value expected.')
+
+
+# (flag, default, type) -- gan/main.py:32-121
+_FLAGS = [
+    ('max_iteration', 150000, int), ('beta1', 0.5, float), ('beta2', 0.9, float),
+    ('learning_rate', 0.0001, float), ('learning_rate_D', -1, float), ('dsteps', 5, int),
+    ('gsteps', 1, int), ('start_dsteps', 10, int), ('clip_grad', True, str2bool),
+    ('batch_norm', False, str2bool), ('init', 0.02, float), ('batch_size', 64, int),
+    ('real_batch_size', -1, int), ('output_size', 128, int), ('c_dim', 3, int),
+    ('z_dim', 128, int), ('df_dim', 64, int), ('dof_dim', 1, int), ('gf_dim', 64, int),
+    ('dataset', 'cifar10', str), ('name', '', str), ('checkpoint_dir', 'checkpoint', str),
+    ('sample_dir', 'sample', str), ('log_dir', 'log', str), ('data_dir', './data', str),
+    ('out_dir', './out', str), ('config_file', '', str), ('architecture', 'dcgan', str),
+    ('kernel', '', str), ('model', 'smmd', str), ('is_train', True, str2bool),
+    ('visualize', False, str2bool), ('is_demo', False, str2bool), ('log', True, str2bool),
+    ('compute_scores', True, str2bool), ('print_pca', False, str2bool), ('suffix', '', str),
+    ('gpu_mem', .9, float), ('no_of_samples', 100000, int), ('save_layer_outputs', 0, int),
+    ('ckpt_name', '', str), ('decay_rate', .8, float), ('gp_decay_rate', .8, float),
+    ('sc_decay_rate', 1., float), ('restart_lr', False, str2bool),
+    ('restart_sc', False, str2bool), ('MMD_lr_scheduler', True, str2bool),
+    ('MMD_sdlr_past_sample', 10, int), ('MMD_sdlr_num_test', 3, int),
+    ('MMD_sdlr_freq', 2000, int), ('gradient_penalty', 0.0, float),
+    ('L2_discriminator_penalty', 0.0, float), ('with_scaling', False, str2bool),
+    ('scaling_coeff', 10., float), ('scaling_variant', 'grad', str),
+    ('with_sn', False, str2bool), ('with_learnable_sn_scale', False, str2bool),
+    ('multi_gpu', False, str2bool), ('num_gpus', 1, int), ('with_labels', False, str2bool),
+    ('use_gaussian_noise', False, str2bool),
+    # this build: data-parallel mode of the all-gather extension
+    ('dp_mode', 'tower', str),
+]
+_DOUBLE_DASH = [('use-incomplete-cho', True, str2bool), ('incho-eta', 1e-3, float),
+                ('incho-max-steps', 1000, int)]
+
+
+def build_parser():
+    p = argparse.ArgumentParser()
+    for name, default, typ in _FLAGS:
+        p.add_argument('-' + name, default=default, type=typ)
+    for name, default, typ in _DOUBLE_DASH:
+        p.add_argument('--' + name, default=default, type=typ)
+    return p
+
+
+def default_flags():
+    return vars(build_parser().parse_args([]))
+
+
+def load_yaml(path):
+    import yaml
+    with open(path) as f:
+        return yaml.safe_load(f) or {}
+
+
+def make_flags(parser=None, argv=None):
+    """YAML keys REPLACE parsed values (gan/main.py:18-25)."""
+    parser = parser or build_parser()
+    flags = parser.parse_args(argv)
+    if flags.config_file:
+        config = load_yaml(flags.config_file)
+        dic = vars(flags)
+        for k in config:
+            dic.pop(k, None)
+        dic.update(config)
+    return flags
+
+
+def num_gpus_from_env():
+    """gan/main.py:126 reads CUDA_VISIBLE_DEVICES (KeyError when unset); here
+    the process-group world size or the visible HIP devices."""
+    ws = os.environ.get('WORLD_SIZE')
+    if ws:
+        return int(ws)
+    vis = os.environ.get('HIP_VISIBLE_DEVICES') or os.environ.get('CUDA_VISIBLE_DEVICES')
+    return len(vis.split(',')) if vis else 1
+
+
+def output_size_for(flags):
+    """gan/main.py:159-167 (cifar10 forces 32, mnist 28)."""
+    if flags.dataset == 'cifar10':
+        return 32, 3
+    if flags.dataset == 'mnist':
+        return 28, 1
+    return flags.output_size, flags.c_dim
+
+
+def main(argv=None):
+    import torch
+    import torch.distributed as dist
+    from gan.core.smmd import get_model
+
+    flags = make_flags(argv=argv)
+    flags.num_gpus = num_gpus_from_env()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+    if world > 1:
+        dist.init_process_group('nccl', device_id=dev)
+    rank = dist.get_rank() if world > 1 else 0
+    if rank == 0:
+        import pprint
+        pprint.PrettyPrinter().pprint(vars(flags))
+    size, c_dim = output_size_for(flags)
+    Model = get_model(flags.model)
+    torch.manual_seed(rank)
+    gan = Model(flags, device=dev, process_group=dist.group.WORLD if world > 1 else None,
+                dp_mode=flags.dp_mode, output_size=size, c_dim=c_dim)
+    if flags.is_train:
+        gen = torch.Generator(device=dev).manual_seed(rank)
+        step = 0
+        while step <= flags.max_iteration:
+            images = torch.rand(flags.real_batch_size, c_dim, size, size, device=dev,
+                                generator=gen)
+            _, _, step = gan.train_step(images)
+            if gan.d_counter == 0 and (step % 100 == 0 or step <= 10):
+                g, d = gan.check_finite()
+                if rank == 0:
+                    gan.timer(step, '%s, G: %.8f, D: %.8f' % (gan.optim_name, g, d))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()
