@@ -73,10 +73,6 @@ class TFMirrorStep:
         self.v = [torch.zeros_like(p) for p in self.params]
         self.t = 0
 
-    @staticmethod
-    def _perm(m):
-        return (2, 3, 1, 0) if m.weight.dim() == 4 and not hasattr(m, 'cout_first') else (1, 0)
-
     def _sn(self):
         for i, m in enumerate(self.sn_layers):
             if m.weight.dim() == 4:
@@ -86,10 +82,14 @@ class TFMirrorStep:
             s = m.sn_scale if hasattr(m, 'sn_scale') else None
             m.w_eff, self.us[i] = sn_weight_tf(m.weight, self.us[i], s, perm)
 
-    def step(self, images):
+    def grads(self, images, z=None):
+        """(d_loss, [dL/dp for p in D params] before clipping) of one critic
+        update; advances u (update_collection=None on the real-image call)."""
         self._sn()
+        if z is None:
+            z = torch.empty(images.shape[0], self.z_dim).uniform_(-1, 1)
         with torch.no_grad():
-            fake = self.G(torch.empty(images.shape[0], self.z_dim).uniform_(-1, 1))
+            fake = self.G(z)
         x = images.detach().requires_grad_(True)
         d_images = self.D(x)
         d_G = self.D(fake)
@@ -99,6 +99,10 @@ class TFMirrorStep:
         scale = 1.0 / (self.sc * J + 1.0)
         d_loss = -(mmd2 * scale)
         grads = torch.autograd.grad(d_loss, self.params)
+        return d_loss.detach(), grads
+
+    def step(self, images, z=None):
+        d_loss, grads = self.grads(images, z)
         self.t += 1
         lr_t = self.lr * math.sqrt(1 - self.b2 ** self.t) / (1 - self.b1 ** self.t)
         with torch.no_grad():

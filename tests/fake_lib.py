@@ -1,0 +1,158 @@
+"""TEST-ONLY stand-in for libsmmd_hip.so that runs the oracle on CPU memory,
+so the multi-process (gloo) tests can exercise the data-parallel plumbing of
+gan.core (all_gather rows, partial sums, all_reduce, row-local gradients,
+tower/global gradient exchange) without a GPU.  Never used by the product."""
+import ctypes
+
+import numpy as np
+
+from oracle import smmd_oracle as O
+
+
+def _arr(p, n, dtype=np.float32):
+    if p is None:
+        return None
+    addr = p.value if isinstance(p, ctypes.c_void_p) else int(p)
+    if not addr:
+        return None
+    ct = {np.float32: ctypes.c_float, np.float64: ctypes.c_double,
+          np.int64: ctypes.c_int64}[dtype]
+    return np.ctypeslib.as_array((ct * n).from_address(addr))
+
+
+def _spec(desc):
+    kinds = {0: 'rbf', 1: 'rq', 2: 'distance', 3: 'dot'}
+    k = kinds[desc.kind]
+    params = [desc.param[i] for i in range(desc.n_terms)]
+    wts = [desc.wt[i] for i in range(desc.n_terms)]
+    return O.KernelSpec(k, params, wts, add_dot=desc.add_dot, tanh=bool(desc.tanh_inputs),
+                        const_diag=desc.const_diag if desc.has_const_diag else None)
+
+
+class FakeLib:
+    def smmd_mmd2_workspace_bytes(self, m, n, d):
+        return 256
+
+    def smmd_mmd2_fwd(self, desc, X, m, Y, n, d, biased, xb, xe, yb, ye, sums, out, gx, gy, ws,
+                      wsb, stream):
+        spec = _spec(desc)
+        Xa = _arr(X, m * d).reshape(m, d).astype(np.float64)
+        Ya = _arr(Y, n * d).reshape(n, d).astype(np.float64)
+        KXX, KXY, KYY, _ = O.kernel_matrices(spec, Xa, Ya)
+        S = np.zeros(8)
+        S[0] = KXX[xb:xe].sum()
+        S[1] = KXY[xb:xe].sum()
+        S[2] = KYY[yb:ye].sum()
+        S[3] = np.trace(KXX[xb:xe, xb:xe]) if xe > xb else 0.0
+        S[4] = np.trace(KYY[yb:ye, yb:ye]) if ye > yb else 0.0
+        S[5] = KXY[:, yb:ye].sum()
+        _arr(sums, 8)[:] = S
+        if out is not None and _arr(out, 1) is not None:
+            _arr(out, 1)[0] = O.mmd2_from_K(KXX, KXY, KYY, spec.const_diag, bool(biased)) \
+                if (xe - xb == m and ye - yb == n) else 0.0
+        if _arr(gx, 1) is not None:
+            dX, dY = O.mmd2_grad(spec, Xa, Ya, bool(biased))
+            _arr(gx, (xe - xb) * d)[:] = dX[xb:xe].ravel()
+            _arr(gy, (ye - yb) * d)[:] = dY[yb:ye].ravel()
+        return 0
+
+    def smmd_mmd2_combine(self, desc, sums, m, n, biased, out, stream):
+        S = _arr(sums, 8).astype(np.float64)
+        spec = _spec(desc)
+        if biased:
+            v = S[0] / m ** 2 + S[2] / n ** 2 - 2 * S[1] / (m * n)
+        else:
+            trX = m * spec.const_diag if spec.const_diag is not None else S[3]
+            trY = n * spec.const_diag if spec.const_diag is not None else S[4]
+            v = (S[0] - trX) / (m * (m - 1)) + (S[2] - trY) / (n * (n - 1)) - 2 * S[1] / (m * n)
+        _arr(out, 1)[0] = v
+        return 0
+
+    def smmd_scaled_loss_workspace_bytes(self, rows, per):
+        return 256
+
+    def smmd_scaled_loss_fwd(self, jac, n_cols, b, b_total, per, feat, dof, base, sc, variant,
+                             sqrt_scale, out, per_sample, ws, wsb, stream):
+        J = _arr(jac, n_cols * b * per).reshape(n_cols, b, per).astype(np.float64)
+        ps = (J ** 2).sum(axis=(0, 2))
+        if _arr(per_sample, 1) is not None:
+            _arr(per_sample, b)[:] = ps
+        o = _arr(out, 8)
+        Jm = ps.sum() / b_total
+        nD = 0.0
+        if variant == 1:
+            f = _arr(feat, b * dof).astype(np.float64)
+            nD = (f ** 2).sum() / (b_total * dof)
+        bl = float(_arr(base, 1)[0]) if _arr(base, 1) is not None else 0.0
+        o[3], o[4], o[5] = Jm, nD, bl
+        return self.smmd_scaled_loss_finalize(out, sc, variant, sqrt_scale, stream)
+
+    def smmd_scaled_loss_finalize(self, out, sc, variant, sqrt_scale, stream):
+        o = _arr(out, 8)
+        q = o[3] + o[4] if variant == 1 else o[3]
+        scale = 1.0 / (sc * q + 1.0)
+        g = o[5] * (np.sqrt(scale) if sqrt_scale else scale)
+        o[0], o[1], o[2] = g, -g, scale
+        return 0
+
+    def smmd_scaled_loss_bwd(self, jac, n_cols, b, b_total, per, feat, dof, fwd, sc, variant,
+                             sqrt_scale, go, d_base, gjac, gfeat, stream):
+        o = _arr(fwd, 8).astype(np.float64)
+        g = float(_arr(go, 1)[0]) if _arr(go, 1) is not None else 1.0
+        scale, base = o[2], o[5]
+        f = np.sqrt(scale) if sqrt_scale else scale
+        fp = 0.5 / np.sqrt(scale) if sqrt_scale else 1.0
+        cq = g * base * fp * (-sc * scale * scale)
+        if _arr(d_base, 1) is not None:
+            _arr(d_base, 1)[0] = g * f
+        n = n_cols * b * per
+        _arr(gjac, n)[:] = cq * 2.0 / b_total * _arr(jac, n)
+        if variant == 1 and _arr(gfeat, 1) is not None:
+            _arr(gfeat, b * dof)[:] = cq * 2.0 / (b_total * dof) * _arr(feat, b * dof)
+        return 0
+
+    def smmd_opt_workspace_bytes(self, offs, n):
+        return 256
+
+    def _tensors(self, offs, n):
+        return [(offs[i], offs[i + 1]) for i in range(n)]
+
+    def smmd_clip_by_norm_flat(self, grad, offs, n, clip, ws, wsb, stream):
+        tot = offs[n]
+        g = _arr(grad, tot)
+        for a, b in self._tensors(offs, n):
+            if b > a:
+                g[a:b] = O.clip_by_norm(g[a:b], clip)
+        return 0
+
+    def smmd_adam_flat(self, param, grad, m, v, offs, n, gscale, clip, lr, b1, b2, eps, step, ws,
+                       wsb, stream):
+        tot = offs[n]
+        P, G, M, V = (_arr(x, tot) for x in (param, grad, m, v))
+        for a, b in self._tensors(offs, n):
+            if b == a:
+                continue
+            g = G[a:b].astype(np.float64) * gscale
+            if clip > 0:
+                g = O.clip_by_norm(g, clip)
+            p, mm, vv = O.adam_step(P[a:b].astype(np.float64), M[a:b].astype(np.float64),
+                                    V[a:b].astype(np.float64), g, step, lr, b1, b2, eps)
+            P[a:b], M[a:b], V[a:b] = p, mm, vv
+        return 0
+
+    def smmd_status_string(self, s):
+        return b'fake'
+
+
+def install(monkeypatch=None):
+    """Route gan.core._lib to the fake (CPU tensors allowed)."""
+    import torch
+    from gan.core import _lib
+    fake = FakeLib()
+    _lib._lib = fake
+    _lib.lib = lambda: fake
+    _lib.require_cuda = lambda *t: None
+    _lib.stream_handle = lambda device=None: None
+    _lib.workspace = lambda tag, nbytes, device: torch.zeros(max(int(nbytes), 256),
+                                                             dtype=torch.uint8)
+    return fake

@@ -1,0 +1,154 @@
+"""End-to-end training-step checks on the GPU.
+
+The critic update of SMMD (SN bank -> critic -> fused MMD^2 -> Jacobian ->
+scaled loss -> double backward -> HIP SN backward) is compared with the
+oracle's CPU op-by-op mirror of the TF graph (oracle/tf_mirror.py) from the
+same weights, u vectors, images and z.  Tolerances (MIOpen fp32 convs vs CPU
+fp32 convs, same graph): d_loss rtol 1e-3; per-tensor gradients
+|d| <= max(2e-3 max|ref|, 1e-5 max over all tensors) + 2e-3 |ref|.
+"""
+import argparse
+import copy
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip('torch')
+
+pytestmark = pytest.mark.gpu
+
+
+def _cfg(**kw):
+    from gan.main import default_flags
+    c = default_flags()
+    c.update(dict(batch_size=8, output_size=32, architecture='sngan', kernel='rbf', model='smmd',
+                  batch_norm=True, with_sn=True, with_learnable_sn_scale=True, with_scaling=True,
+                  dof_dim=1, learning_rate=1e-4, dataset='cifar10'))
+    c.update(kw)
+    return argparse.Namespace(**c)
+
+
+def _mirror_from(model):
+    from gan.core.snops import sn_modules
+    from oracle.tf_mirror import TFMirrorStep
+    G = copy.deepcopy(model.generator).cpu()
+    D = copy.deepcopy(model.discriminator).cpu()
+    for m in sn_modules(D):
+        m.w_eff = None
+    st = TFMirrorStep(G, D, sn_modules(D), lr=model.config.learning_rate, sc=model.sc)
+    st.us = [e.u.detach().cpu().view(1, -1).clone() for e in model.sn_D.entries]
+    return st
+
+
+@pytest.mark.parametrize('arch,size', [('sngan', 32), ('snresnet', 64)])
+def test_critic_step_matches_tf_mirror(dev, arch, size):
+    from gan.core.smmd import SMMD
+    torch.manual_seed(0)
+    cfg = _cfg(architecture=arch, output_size=size, df_dim=16 if arch == 'snresnet' else 64,
+               gf_dim=16 if arch == 'snresnet' else 64)
+    model = SMMD(cfg, device=dev)
+    mirror = _mirror_from(model)
+    g = torch.Generator().manual_seed(1)
+    images = torch.rand(8, 3, size, size, generator=g)
+    z = torch.empty(8, 128).uniform_(-1, 1, generator=g)
+    ref_loss, ref_grads = mirror.grads(images, z)
+
+    model.sample_z = lambda n: z.to(dev)
+    captured = {}
+    orig = model.d_optim.step
+
+    def cap(*a, **k):
+        captured['g'] = model.d_optim.flat_grad.detach().cpu().clone()
+        return orig(*a, **k)
+    model.d_optim.step = cap
+    model.step = 25
+    model.d_counter, model.g_counter = 0, 0
+    _, d_loss, aux = model.d_step(images.to(dev))
+    assert float(d_loss.detach()) == pytest.approx(float(ref_loss), rel=1e-3, abs=1e-6)
+    flat = captured['g']
+    gmax = max(float(rg.abs().max()) for rg in ref_grads)
+    o = 0
+    for p, rg in zip(model.d_vars, ref_grads):
+        n = p.numel()
+        got = flat[o:o + n].view_as(rg).numpy().astype(np.float64)
+        ref = rg.numpy().astype(np.float64)
+        # exact zeros (e.g. the output bias: RBF-MMD is translation invariant) are
+        # rounding noise in both: absolute floor 1e-5 of the largest gradient
+        tol = max(2e-3 * np.abs(ref).max(), 1e-5 * gmax) + 2e-3 * np.abs(ref)
+        assert (np.abs(got - ref) <= tol + 1e-12).all(), (p.shape, np.abs(got - ref).max(),
+                                                           np.abs(ref).max())
+        o += n
+    # u advanced exactly as the reference's u.assign(u') (sn.py:39-46)
+    for e, u in zip(model.sn_D.entries, mirror.us):
+        np.testing.assert_allclose(e.u.cpu().numpy(), u.numpy()[0], rtol=1e-4, atol=1e-6)
+
+
+def test_generator_step_updates_only_G(dev):
+    from gan.core.smmd import SMMD
+    torch.manual_seed(0)
+    model = SMMD(_cfg(), device=dev)
+    d_before = model.d_optim.flat_param.clone()
+    g_before = model.g_optim.flat_param.clone()
+    images = torch.rand(8, 3, 32, 32, device=dev)
+    g_loss, d_loss, _ = model.g_step(images)
+    assert torch.isfinite(g_loss)
+    assert torch.equal(d_before, model.d_optim.flat_param)
+    assert not torch.equal(g_before, model.g_optim.flat_param)
+    assert all(p.requires_grad for p in model.d_vars)
+
+
+def test_schedule_and_losses_finite(dev):
+    from gan.core.smmd import SMMD
+    torch.manual_seed(0)
+    model = SMMD(_cfg(), device=dev)
+    images = torch.rand(8, 3, 32, 32, device=dev)
+    kinds = []
+    for _ in range(13):
+        before = model.step
+        model.train_step(images)
+        kinds.append('G' if model.step != before else 'D')
+    assert ''.join(kinds) == 'DDDDDDDDDDGDD'      # steps < 20: 10 critic updates per G
+    g, d = model.check_finite()
+    assert g == pytest.approx(-d)
+
+
+@pytest.mark.parametrize('model_name,extra', [
+    ('swgan', {}),
+    ('mmd', {'gradient_penalty': 1.0, 'kernel': 'mix_rq', 'with_scaling': False}),
+    ('smmd', {'kernel': 'mix_rbf', 'scaling_variant': 'value_and_grad'}),
+    ('smmd', {'architecture': 'g-resnet5', 'output_size': 64, 'batch_norm': False}),
+])
+def test_other_models_step(dev, model_name, extra):
+    from gan.core.smmd import get_model
+    torch.manual_seed(0)
+    cfg = _cfg(model=model_name, **extra)
+    size = cfg.output_size
+    model = get_model(model_name)(cfg, device=dev)
+    images = torch.rand(8, 3, size, size, device=dev)
+    for _ in range(3):
+        model.train_step(images)
+    g, d = model.check_finite()
+    assert np.isfinite(g) and np.isfinite(d)
+
+
+def test_tower_and_global_agree_on_one_gpu(dev):
+    """Same critic gradient in both modes at world size 1 (compared before Adam:
+    its first step maps rounding noise on zero-gradient tensors to +-lr)."""
+    from gan.core.smmd import SMMD
+    outs = []
+    for mode in ('tower', 'global'):
+        torch.manual_seed(0)
+        model = SMMD(_cfg(), device=dev, dp_mode=mode)
+        cap = {}
+        orig = model.d_optim.step
+
+        def step(*a, _o=orig, _c=cap, _m=model, **k):
+            _c['g'] = _m.d_optim.flat_grad.clone()
+            return _o(*a, **k)
+        model.d_optim.step = step
+        torch.manual_seed(5)
+        images = torch.rand(8, 3, 32, 32, device=dev)
+        model.train_step(images)
+        outs.append(cap['g'])
+    scale = float(outs[0].abs().max())
+    assert torch.allclose(outs[0], outs[1], rtol=1e-4, atol=1e-5 * scale)
