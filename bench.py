@@ -46,28 +46,6 @@ def imagenet_config():
     return argparse.Namespace(**c)
 
 
-class EventTimer:
-    """HIP events on the current (compute) stream around one library call."""
-
-    def __init__(self):
-        self.pairs = []
-
-    def __enter__(self):
-        self.s = torch.cuda.Event(enable_timing=True)
-        self.e = torch.cuda.Event(enable_timing=True)
-        self.s.record()
-        return self
-
-    def __exit__(self, *a):
-        self.e.record()
-        self.pairs.append((self.s, self.e))
-
-    def mean_ms(self):
-        if not self.pairs:
-            return float('nan')
-        return sum(s.elapsed_time(e) for s, e in self.pairs) / len(self.pairs)
-
-
 def cpu_baseline(cfg, seconds_budget=20.0):
     """Oracle mirror of the TF graph on the host CPU (bounded sample)."""
     from gan.core.architecture import get_networks
@@ -105,9 +83,18 @@ def main():
     ap.add_argument('--warmup', type=int, default=12)
     ap.add_argument('--dp-mode', default='global', choices=['global', 'tower'])
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--channels-last', type=int, default=0)
+    ap.add_argument('--miopen-winograd', type=int, default=1,
+                    help='0: disable MIOpen Winograd solvers (immediate mode then picks '
+                         'the MFMA implicit-GEMM ones)')
     ap.add_argument('--cpu-seconds', type=float, default=20.0)
     args = ap.parse_args()
 
+    if not args.miopen_winograd:      # read by MIOpen at its first solver query
+        for k in ('MIOPEN_DEBUG_AMD_WINOGRAD_RXS_F2X3', 'MIOPEN_DEBUG_AMD_WINOGRAD_RXS_F3X2',
+                  'MIOPEN_DEBUG_AMD_WINOGRAD_3X3', 'MIOPEN_DEBUG_AMD_WINOGRAD_RXS',
+                  'MIOPEN_DEBUG_AMD_FUSED_WINOGRAD'):
+            os.environ[k] = '0'
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
@@ -123,32 +110,12 @@ def main():
     cfg = imagenet_config()
     torch.manual_seed(2 + rank)
     model = SMMD(cfg, device=dev, process_group=dist.group.WORLD if world > 1 else None,
-                 dp_mode=args.dp_mode)
+                 dp_mode=args.dp_mode, channels_last=bool(args.channels_last))
     gen = torch.Generator(device=dev).manual_seed(0 + rank)
     images = [torch.rand(BATCH, 3, 64, 64, device=dev, generator=gen) for _ in range(4)]
     model.step = 21          # steady-state 5D+1G schedule (model.py:474-475)
 
-    # instrument the dominant launch set and the fused MMD kernel
-    adam_t, mmd_t = EventTimer(), EventTimer()
-    from gan.core import mmd as mmd_mod
-    orig_step = model.d_optim.step
-    orig_fused = mmd_mod._MMD2Fused.forward
-    timing = {'on': False}
-
-    def timed_step(*a, **k):
-        if timing['on']:
-            with adam_t:
-                return orig_step(*a, **k)
-        return orig_step(*a, **k)
-
-    def timed_fused(ctx, *a, **k):
-        if timing['on']:
-            with mmd_t:
-                return orig_fused(ctx, *a, **k)
-        return orig_fused(ctx, *a, **k)
-
-    model.d_optim.step = timed_step
-    mmd_mod._MMD2Fused.forward = staticmethod(timed_fused)
+    from gan.core import _lib
 
     tw = time.perf_counter()
     for i in range(args.warmup):
@@ -162,7 +129,8 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    timing['on'] = True
+    _lib.reset_timing()
+    _lib.enable_timing(True)
     t0 = time.perf_counter()
     for i in range(args.steps):
         model.train_step(images[i % len(images)])
@@ -171,24 +139,45 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    timing['on'] = False
+    _lib.enable_timing(False)
     g_loss, d_loss = model.check_finite()
     if world > 1:
         t = torch.tensor([dt], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t)
 
-    # dominant HIP launch set: critic clip + TF-Adam over the flat buffer
-    n_d = model.d_optim.numel
-    n_tensors = len(model.d_optim.params)
-    adam_ms = adam_t.mean_ms()
-    # algorithmic bytes: sqsum pass reads g; update pass reads g, p, m, v and writes p, m, v
-    adam_bytes = n_d * 4 * (1 + 4 + 3)
-    achieved = adam_bytes / (adam_ms * 1e-3) / 1e9
-    mmd_ms = mmd_t.mean_ms()
+    # every libsmmd_hip entry point of the timed region: HIP-event time on the
+    # compute stream and its algorithmic HBM bytes per call
+    tm = _lib.timing_ms()
     m_all = BATCH * world
-    mmd_bytes = (2 * m_all * 1 * 4) + 2 * BATCH * 4 + 8 * 4   # X,Y read; dX,dY written; sums
-    pairs = (2 * m_all) * (2 * m_all)                     # rows x columns swept per D step
+    sn_kn = sum(e.N * e.K for e in model.sn_D.entries)
+    per_img = 3 * 64 * 64
+    alg = {
+        # sqsum pass reads g; update pass reads g, p, m, v and writes p, m, v
+        'smmd_adam_flat[D]': model.d_optim.numel * 4 * 8,
+        'smmd_adam_flat[G]': model.g_optim.numel * 4 * 8,
+        # P1 read W, P2 read W, P3 read W + write W_eff
+        'smmd_sn_power_iter': sn_kn * 4 * 4,
+        # A read G, W; B read G, write gW
+        'smmd_sn_weight_bwd': sn_kn * 4 * 4,
+        # X, Y rows read, unit gradients written, sums
+        'smmd_mmd2_fwd': 2 * m_all * 4 + 2 * BATCH * 4 + 8 * 4,
+        'smmd_scaled_loss_fwd': BATCH * per_img * 4,
+        'smmd_scaled_loss_bwd': 2 * BATCH * per_img * 4,
+    }
+    kernels = {}
+    for name, (calls, ms) in tm.items():
+        b = alg.get(name)
+        row = {'calls': calls, 'avg_ms': round(ms, 5), 'ms_per_step': round(ms * calls /
+                                                                           args.steps, 5)}
+        if b:
+            row.update(bytes=b, GB_s=round(b / (ms * 1e-3) / 1e9, 1),
+                       frac=round(b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
+        kernels[name] = row
+    dom = max((k for k in kernels if 'GB_s' in kernels[k] and k != 'smmd_mmd2_fwd'),
+              key=lambda k: kernels[k]['ms_per_step'])
+    mk = kernels.get('smmd_mmd2_fwd', {})
+    pairs = (2 * m_all) * (2 * m_all)                     # rows x columns swept per critic step
 
     result = {
         'metric': 'images/sec/step (64x64 SMMD, batch 64) + MMD-kernel GB/s at 1/2/4/8 GPU',
@@ -206,17 +195,18 @@ def main():
         'config': {'workload': 'imagenet_smmd 64x64 SNResNet G/D, rbf kernel, scaling, SN, '
                                'batch 64/GPU, 5D+1G schedule',
                    'model': 'snresnet', 'global_batch': BATCH * world, 'seq_len': None,
-                   'parallelism': 'dp%d' % world, 'dp_mode': args.dp_mode},
-        'roofline': {'bound': 'hbm', 'kernel': 'smmd_adam_flat (opt_sqsum + opt_adam, critic '
-                                                '%d tensors, %.2fM params)' % (n_tensors,
-                                                                                n_d / 1e6),
-                     'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                     'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': None,
-                     'avg_ms': round(adam_ms, 5), 'algorithmic_bytes': adam_bytes},
-        'mmd_kernel': {'kernel': 'mmd2_fused_kernel<1,RBF>', 'avg_ms': round(mmd_ms, 5),
-                       'GB_s': round(mmd_bytes / (mmd_ms * 1e-3) / 1e9, 4),
-                       'pair_evals_per_s': round(pairs / (mmd_ms * 1e-3), 1),
-                       'bound': 'latency (D=1: %d B algorithmic)' % mmd_bytes},
+                   'parallelism': 'dp%d' % world, 'dp_mode': args.dp_mode,
+                   'memory_format': 'channels_last' if args.channels_last else 'nchw',
+                   'miopen_winograd': bool(args.miopen_winograd)},
+        'roofline': {'bound': 'hbm', 'kernel': dom, 'achieved': kernels[dom]['GB_s'],
+                     'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': kernels[dom]['frac'],
+                     'traffic': None, 'avg_ms': kernels[dom]['avg_ms'],
+                     'algorithmic_bytes': kernels[dom]['bytes']},
+        'mmd_kernel': {'kernel': 'smmd_mmd2_fwd (mmd2_fused_kernel<1,RBF>)',
+                       'avg_ms': mk.get('avg_ms'), 'GB_s': mk.get('GB_s'),
+                       'pair_evals_per_s': round(pairs / (mk['avg_ms'] * 1e-3), 1) if mk else None,
+                       'bound': 'latency (D=1: %s B algorithmic per call)' % mk.get('bytes')},
+        'hip_kernels': kernels,
         'losses': {'g_loss': g_loss, 'd_loss': d_loss},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

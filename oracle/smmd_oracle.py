@@ -102,10 +102,13 @@ def _mysqrt_grad(x):
         return np.where(xe >= 0, 0.5 / np.sqrt(np.maximum(xe, 0.0)), 0.0)
 
 
-def _block(spec: KernelSpec, A, B, AB, sa, sb):
+def _block(spec: KernelSpec, A, B, AB, sa, sb, gram32=False):
     """Kernel block K(A,B) from the Gram pieces, and dK/d(raw), dK/dAB,
     dK/dsa, dK/dsb as elementwise factors (float64)."""
-    raw = -2.0 * AB + sa[:, None] + sb[None, :]          # mmd.py:67 (pre-clamp)
+    if gram32:
+        raw = _raw32(AB, sa, sb)
+    else:
+        raw = -2.0 * AB + sa[:, None] + sb[None, :]      # mmd.py:67 (pre-clamp)
     if spec.kind == 'rbf':
         R = np.maximum(raw, 0.0)                          # mmd.py:67
         K = np.zeros_like(R)
@@ -143,20 +146,46 @@ def _block(spec: KernelSpec, A, B, AB, sa, sb):
     raise ValueError(spec.kind)
 
 
-def kernel_matrices(spec: KernelSpec, X, Y, K_XY_only=False):
+def _gram(A, B, gram32):
+    """A B^T, diag(A A^T), diag(B B^T).  gram32=True forms them in float32 the
+    way the reference's fp32 graph does (tf.matmul + diag_part, mmd.py:57-61),
+    then widens: the Gram expansion -2ab + |a|^2 + |b|^2 loses the same bits
+    as in TF, which matters for the ill-conditioned distance kernel."""
+    if not gram32:
+        return A @ B.T, np.sum(A * A, 1), np.sum(B * B, 1)
+    A32, B32 = A.astype(np.float32), B.astype(np.float32)
+    AB = (A32 @ B32.T).astype(np.float32)
+    sa = np.sum(A32 * A32, 1, dtype=np.float32)
+    sb = np.sum(B32 * B32, 1, dtype=np.float32)
+    return AB.astype(np.float64), sa.astype(np.float64), sb.astype(np.float64)
+
+
+def _raw32(AB, sa, sb):
+    """(-2 AB + sa) + sb evaluated in float32 (mmd.py:67 operation order)."""
+    r = (np.float32(-2.0) * AB.astype(np.float32) + sa.astype(np.float32)[:, None])
+    return (r + sb.astype(np.float32)[None, :]).astype(np.float64)
+
+
+def kernel_matrices(spec: KernelSpec, X, Y, K_XY_only=False, gram32=False):
     """(K_XX, K_XY, K_YY, const_diag) exactly as mmd._<name>_kernel
     (gan/core/mmd.py:18-188); const_diag None means the reference's False."""
     X = np.asarray(X, np.float64)
     Y = np.asarray(Y, np.float64)
     if spec.tanh:
         X, Y = np.tanh(X), np.tanh(Y)
-    XX, XY, YY = X @ X.T, X @ Y.T, Y @ Y.T
-    sx, sy = np.diag(XX).copy(), np.diag(YY).copy()
-    KXY = _block(spec, X, Y, XY, sx, sy)[0]
+    XY, sx, sy = _gram(X, Y, gram32)
+    XX, _, _ = _gram(X, X, gram32)
+    YY, _, _ = _gram(Y, Y, gram32)
+    if gram32:
+        np.fill_diagonal(XX, sx)
+        np.fill_diagonal(YY, sy)
+    else:
+        sx, sy = np.diag(XX).copy(), np.diag(YY).copy()
+    KXY = _block(spec, X, Y, XY, sx, sy, gram32)[0]
     if K_XY_only:
         return KXY
-    KXX = _block(spec, X, X, XX, sx, sx)[0]
-    KYY = _block(spec, Y, Y, YY, sy, sy)[0]
+    KXX = _block(spec, X, X, XX, sx, sx, gram32)[0]
+    KYY = _block(spec, Y, Y, YY, sy, sy, gram32)[0]
     return KXX, KXY, KYY, spec.const_diag
 
 
@@ -173,23 +202,23 @@ def mmd2_from_K(KXX, KXY, KYY, const_diag=None, biased=False):
             - 2 * KXY.sum() / (m * n))
 
 
-def mmd2(spec: KernelSpec, X, Y, biased=False):
+def mmd2(spec: KernelSpec, X, Y, biased=False, gram32=False):
     """mmd.mmd2(kernel(X, Y)) (gan/core/mmd.py:194-196)."""
-    KXX, KXY, KYY, c = kernel_matrices(spec, X, Y)
+    KXX, KXY, KYY, c = kernel_matrices(spec, X, Y, gram32=gram32)
     return mmd2_from_K(KXX, KXY, KYY, c, biased)
 
 
-def mmd2_sums(spec: KernelSpec, X, Y):
+def mmd2_sums(spec: KernelSpec, X, Y, gram32=False):
     """(sum K_XX, sum K_XY, sum K_YY, trace K_XX, trace K_YY) in float64."""
-    KXX, KXY, KYY, _ = kernel_matrices(spec, X, Y)
+    KXX, KXY, KYY, _ = kernel_matrices(spec, X, Y, gram32=gram32)
     return np.array([KXX.sum(), KXY.sum(), KYY.sum(), np.trace(KXX), np.trace(KYY)])
 
 
-def _block_grads(spec, A, B, AB, sa, sb, G):
+def _block_grads(spec, A, B, AB, sa, sb, G, gram32=False):
     """TF-autodiff gradient of sum(G * K(A,B)) w.r.t. A and B, where
     sa = diag(A A^T), sb = diag(B B^T) come from the Gram diagonal
     (mmd.py:60-61), so d sa_i / d a_i = 2 a_i."""
-    K, dKdraw, dKdAB, dsa, dsb = _block(spec, A, B, AB, sa, sb)
+    K, dKdraw, dKdAB, dsa, dsb = _block(spec, A, B, AB, sa, sb, gram32)
     Graw = G * dKdraw
     GAB = -2.0 * Graw + G * dKdAB
     gsa = Graw.sum(1)
@@ -202,7 +231,7 @@ def _block_grads(spec, A, B, AB, sa, sb, G):
     return dA, dB
 
 
-def mmd2_grad(spec: KernelSpec, X, Y, biased=False):
+def mmd2_grad(spec: KernelSpec, X, Y, biased=False, gram32=False):
     """Analytic d mmd2 / dX, d mmd2 / dY following TF autodiff of
     gan/core/mmd.py:55-220 (tf.maximum ties pass the gradient)."""
     X0 = np.asarray(X, np.float64)
@@ -219,13 +248,19 @@ def mmd2_grad(spec: KernelSpec, X, Y, biased=False):
             np.fill_diagonal(gXX, 0.0)
             np.fill_diagonal(gYY, 0.0)
     gXY = np.full((m, n), -2.0 / (m * n))
-    XX, XY, YY = X1 @ X1.T, X1 @ Y1.T, Y1 @ Y1.T
-    sx, sy = np.diag(XX).copy(), np.diag(YY).copy()
-    a, b = _block_grads(spec, X1, X1, XX, sx, sx, gXX)
+    XY, sx, sy = _gram(X1, Y1, gram32)
+    XX, _, _ = _gram(X1, X1, gram32)
+    YY, _, _ = _gram(Y1, Y1, gram32)
+    if gram32:
+        np.fill_diagonal(XX, sx)
+        np.fill_diagonal(YY, sy)
+    else:
+        sx, sy = np.diag(XX).copy(), np.diag(YY).copy()
+    a, b = _block_grads(spec, X1, X1, XX, sx, sx, gXX, gram32)
     dX = a + b
-    a, b = _block_grads(spec, Y1, Y1, YY, sy, sy, gYY)
+    a, b = _block_grads(spec, Y1, Y1, YY, sy, sy, gYY, gram32)
     dY = a + b
-    a, b = _block_grads(spec, X1, Y1, XY, sx, sy, gXY)
+    a, b = _block_grads(spec, X1, Y1, XY, sx, sy, gXY, gram32)
     dX += a
     dY += b
     if spec.tanh:
@@ -237,13 +272,13 @@ def mmd2_grad(spec: KernelSpec, X, Y, biased=False):
 # --------------------------------------------------------------------------
 # witness (K_XY_only row means), gan/core/model.py:327-350
 # --------------------------------------------------------------------------
-def witness(spec: KernelSpec, H, R, F):
+def witness(spec: KernelSpec, H, R, F, gram32=False):
     """witness_i = mean_j K(h_i, r_j) - mean_j K(h_i, f_j)  (model.py:336-338)."""
-    return (kernel_matrices(spec, H, R, K_XY_only=True).mean(1)
-            - kernel_matrices(spec, H, F, K_XY_only=True).mean(1))
+    return (kernel_matrices(spec, H, R, K_XY_only=True, gram32=gram32).mean(1)
+            - kernel_matrices(spec, H, F, K_XY_only=True, gram32=gram32).mean(1))
 
 
-def witness_grad_H(spec: KernelSpec, H, R, F):
+def witness_grad_H(spec: KernelSpec, H, R, F, gram32=False):
     """d sum_i witness_i / d H  (the inner gradient of model.py:339 at the
     critic-output level), float64 analytic."""
     H0 = np.asarray(H, np.float64)
@@ -252,8 +287,8 @@ def witness_grad_H(spec: KernelSpec, H, R, F):
         Z0 = np.asarray(Z, np.float64)
         H1, Z1 = (np.tanh(H0), np.tanh(Z0)) if spec.tanh else (H0, Z0)
         G = np.full((H1.shape[0], Z1.shape[0]), sgn / Z1.shape[0])
-        dA, _ = _block_grads(spec, H1, Z1, H1 @ Z1.T, np.diag(H1 @ H1.T).copy(),
-                             np.diag(Z1 @ Z1.T).copy(), G)
+        HZ, sh, sz = _gram(H1, Z1, gram32)
+        dA, _ = _block_grads(spec, H1, Z1, HZ, sh, sz, G, gram32)
         if spec.tanh:
             dA *= 1.0 - H1 ** 2
         out += dA

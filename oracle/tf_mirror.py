@@ -13,15 +13,18 @@ materialises everything the TF graph materialises:
   (gan/core/ops.py:228-233, gan/core/model.py:382-390, smmd.py:21-23)
 * per-variable tf.clip_by_norm and the TF Adam update (model.py:444-468)
 
-The convolution stack itself is the same PyTorch module graph the product
-uses (gan.core.architecture, pure torch); only its SN weights are produced
-here instead of by the HIP bank.
+The convolution stack is the product's PyTorch module graph
+(gan.core.architecture) with its convolutions and mean pools swapped back to
+stock F.conv2d / F.avg_pool2d while the mirror runs (plain autograd, as the
+TF graph is), and its SN weights produced here instead of by the HIP bank.
 """
 from __future__ import annotations
 
+import contextlib
 import math
 
 import torch
+import torch.nn.functional as F
 
 from . import smmd_oracle as O
 
@@ -61,6 +64,19 @@ def rbf_mmd2_tf(X, Y, sigma=1.0, wt=1.0):
             - 2 * KXY.sum() / (m * n))
 
 
+@contextlib.contextmanager
+def stock_torch_ops():
+    """Run the product modules with stock PyTorch conv / pool autograd."""
+    from gan.core import architecture, snops
+    saved = snops.conv2d, architecture.mean_pool2
+    snops.conv2d = lambda x, w, b=None, stride=1, padding=0: F.conv2d(x, w, b, stride, padding)
+    architecture.mean_pool2 = lambda x: F.avg_pool2d(x, 2)
+    try:
+        yield
+    finally:
+        snops.conv2d, architecture.mean_pool2 = saved
+
+
 class TFMirrorStep:
     """One critic (D) update of SMMD exactly as the TF graph computes it."""
 
@@ -85,6 +101,10 @@ class TFMirrorStep:
     def grads(self, images, z=None):
         """(d_loss, [dL/dp for p in D params] before clipping) of one critic
         update; advances u (update_collection=None on the real-image call)."""
+        with stock_torch_ops():
+            return self._grads(images, z)
+
+    def _grads(self, images, z=None):
         self._sn()
         if z is None:
             z = torch.empty(images.shape[0], self.z_dim).uniform_(-1, 1)

@@ -146,23 +146,80 @@ __device__ __forceinline__ double estimator(const double *S, double m, double n,
            2.0 * S[1] / (m * n);
 }
 
-template <int DT, int KIND>
-__global__ __launch_bounds__(256) void mmd2_fused_kernel(MmdArgs a) {
+// NW waves per block.  A one-block launch (small batches: the configs' 64+64
+// rows) reduces in LDS and writes the outputs directly; larger launches use
+// the slab + last-arriver path.  STAGED: the block first copies every feature
+// row of Z = [X; Y] (tanh applied) and its squared norm into LDS, so the row
+// and column sweeps read LDS instead of issuing dependent global loads.
+template <int DT, bool STAGED>
+struct Feats {
+    const float *X, *Y;
+    const float *lds;      // [(m+n)][DT] features, then [(m+n)] squared norms
+    int m, n, d;
+    bool tanh_in;
+    __device__ __forceinline__ void get(bool isx, int i, float (&z)[DT], float &sq) const {
+        if (STAGED) {
+            const int r = isx ? i : m + i;
+#pragma unroll
+            for (int k = 0; k < DT; ++k) z[k] = lds[r * DT + k];
+            sq = lds[(m + n) * DT + r];
+        } else {
+            load_feat<DT>((isx ? X : Y) + (size_t)i * d, d, tanh_in, z);
+            sq = dotk<DT>(z, z);
+        }
+    }
+};
+
+// Lane layout: a wave owns 8 rows; row slot = lane >> 3 and the 8 lanes of a
+// slot stride over the columns (j = lane & 7, +8, ...).  The row's kernel sums
+// and gradient are reduced over those 8 lanes only (3 xor-shuffle steps), so
+// the per-row overhead is shared by 8 rows.
+constexpr int MMD_RPW = 8;    // rows per wave
+constexpr int MMD_LPR = 8;    // lanes per row
+
+__device__ __forceinline__ float group8_sum(float x) {
+    x += __shfl_xor(x, 4, SMMD_WAVE);
+    x += __shfl_xor(x, 2, SMMD_WAVE);
+    x += __shfl_xor(x, 1, SMMD_WAVE);
+    return x;
+}
+
+template <int DT, int KIND, int NW, bool STAGED>
+__global__ __launch_bounds__(NW * 64) void mmd2_fused_kernel(MmdArgs a) {
+    extern __shared__ float smem[];
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
-    const int nwaves = gridDim.x * 4;
+    const int slot = lane >> 3, l8 = lane & 7;
+    const int nwaves = gridDim.x * NW;
     const int nxr = a.x_end - a.x_begin;
     const int nrows = nxr + (a.y_end - a.y_begin);
     const bool tanh_in = a.tanh_in != 0;
+    Feats<DT, STAGED> F{a.X, a.Y, smem, a.m, a.n, a.d, tanh_in};
+
+    if (STAGED) {
+        const int tot = a.m + a.n;
+        for (int r = threadIdx.x; r < tot; r += NW * 64) {
+            float z[DT];
+            const bool isx = r < a.m;
+            load_feat<DT>((isx ? a.X : a.Y) + (size_t)(isx ? r : r - a.m) * a.d, a.d, tanh_in, z);
+#pragma unroll
+            for (int k = 0; k < DT; ++k) smem[r * DT + k] = z[k];
+            smem[tot * DT + r] = dotk<DT>(z, z);
+        }
+        __syncthreads();
+    }
 
     float s_xx = 0.f, s_xy = 0.f, s_yy = 0.f, s_yx = 0.f, t_xx = 0.f, t_yy = 0.f;
 
-    for (int r = blockIdx.x * 4 + wid; r < nrows; r += nwaves) {
+    for (int g = blockIdx.x * NW + wid; g * MMD_RPW < nrows; g += nwaves) {
+        const int r = g * MMD_RPW + slot;
+        const bool active = r < nrows;
         const bool isx = r < nxr;
         const int ri = isx ? a.x_begin + r : a.y_begin + (r - nxr);
-        float zi[DT];
-        load_feat<DT>((isx ? a.X : a.Y) + (size_t)ri * a.d, a.d, tanh_in, zi);
-        const float sqi = dotk<DT>(zi, zi);
+        float zi[DT], sqi = 0.f;
+#pragma unroll
+        for (int k = 0; k < DT; ++k) zi[k] = 0.f;
+        if (active) F.get(isx, ri, zi, sqi);
         float acc[DT];
 #pragma unroll
         for (int k = 0; k < DT; ++k) acc[k] = 0.f;
@@ -170,15 +227,13 @@ __global__ __launch_bounds__(256) void mmd2_fused_kernel(MmdArgs a) {
 
         // same-set block: XX for an X row, YY for a Y row
         {
-            const float *S = isx ? a.X : a.Y;
-            const int ns = isx ? a.m : a.n;
+            const int ns = active ? (isx ? a.m : a.n) : 0;
             const float w = isx ? a.gw_same_x : a.gw_same_y;
             float sumK = 0.f, trK = 0.f;
-            for (int j = lane; j < ns; j += 64) {
-                float zc[DT];
-                load_feat<DT>(S + (size_t)j * a.d, a.d, tanh_in, zc);
+            for (int j = l8; j < ns; j += MMD_LPR) {
+                float zc[DT], sqc;
+                F.get(isx, j, zc, sqc);
                 const float dot = dotk<DT>(zi, zc);
-                const float sqc = dotk<DT>(zc, zc);
                 const float raw = (-2.f * dot + sqi) + sqc;   // mmd.py:67 order
                 float K, al, be;
                 Kern<KIND>::eval(a.kp, raw, dot, sqi, sqc, K, al, be);
@@ -195,16 +250,14 @@ __global__ __launch_bounds__(256) void mmd2_fused_kernel(MmdArgs a) {
             if (isx) { s_xx += sumK; t_xx += trK; } else { s_yy += sumK; t_yy += trK; }
         }
         // cross-set block: XY for an X row; YX (gradient only) for a Y row
-        if (isx || a.need_grad) {
-            const float *S = isx ? a.Y : a.X;
-            const int ns = isx ? a.n : a.m;
+        {
+            const int ns = (active && (isx || a.need_grad)) ? (isx ? a.n : a.m) : 0;
             const float w = a.gw_cross;
             float sumK = 0.f;
-            for (int j = lane; j < ns; j += 64) {
-                float zc[DT];
-                load_feat<DT>(S + (size_t)j * a.d, a.d, tanh_in, zc);
+            for (int j = l8; j < ns; j += MMD_LPR) {
+                float zc[DT], sqc;
+                F.get(!isx, j, zc, sqc);
                 const float dot = dotk<DT>(zi, zc);
-                const float sqc = dotk<DT>(zc, zc);
                 const float raw = (-2.f * dot + sqi) + sqc;
                 float K, al, be;
                 Kern<KIND>::eval(a.kp, raw, dot, sqi, sqc, K, al, be);
@@ -219,25 +272,25 @@ __global__ __launch_bounds__(256) void mmd2_fused_kernel(MmdArgs a) {
             if (isx) s_xy += sumK; else s_yx += sumK;
         }
         if (a.need_grad) {
-            aacc = wave_sum(aacc);
+            aacc = group8_sum(aacc);
 #pragma unroll
-            for (int k = 0; k < DT; ++k) acc[k] = wave_sum(acc[k]);
-            if (lane == 0) {
-                float *g = isx ? a.grad_x + (size_t)r * a.d : a.grad_y + (size_t)(r - nxr) * a.d;
+            for (int k = 0; k < DT; ++k) acc[k] = group8_sum(acc[k]);
+            if (active && l8 == 0) {
+                float *gp = isx ? a.grad_x + (size_t)r * a.d : a.grad_y + (size_t)(r - nxr) * a.d;
 #pragma unroll
                 for (int k = 0; k < DT; ++k) {
                     if (k < a.d) {
                         float gk = fmaf(aacc, zi[k], acc[k]);
                         if (tanh_in) gk *= 1.f - zi[k] * zi[k];
-                        g[k] = gk;
+                        gp[k] = gk;
                     }
                 }
             }
         }
     }
 
-    // ---- block partial sums (fixed order), double precision slab ----------
-    __shared__ double red[4][8];
+    // ---- block partial sums (fixed order), double precision ---------------
+    __shared__ double red[NW][8];
     __shared__ int is_last;
     float v[6] = {s_xx, s_xy, s_yy, t_xx, t_yy, s_yx};
 #pragma unroll
@@ -247,10 +300,35 @@ __global__ __launch_bounds__(256) void mmd2_fused_kernel(MmdArgs a) {
         for (int k = 0; k < 6; ++k) red[wid][k] = (double)v[k];
     }
     __syncthreads();
+    if (gridDim.x == 1) {                       // one block: no slab, no ticket
+        if (threadIdx.x == 0) {
+            double S[6];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                double t = 0.0;
+                for (int w = 0; w < NW; ++w) t += red[w][k];
+                S[k] = t;
+            }
+            if (a.out_sums) {
+#pragma unroll
+                for (int k = 0; k < 6; ++k) a.out_sums[k] = (float)S[k];
+                a.out_sums[6] = 0.f;
+                a.out_sums[7] = 0.f;
+            }
+            if (a.out_mmd2)
+                a.out_mmd2[0] = (float)estimator(S, (double)a.m, (double)a.n, a.biased,
+                                                 a.has_const, a.const_diag);
+        }
+        return;
+    }
     if (threadIdx.x == 0) {
         double *slab = a.partials + (size_t)blockIdx.x * 8;
 #pragma unroll
-        for (int k = 0; k < 6; ++k) slab[k] = ((red[0][k] + red[1][k]) + red[2][k]) + red[3][k];
+        for (int k = 0; k < 6; ++k) {
+            double t = 0.0;
+            for (int w = 0; w < NW; ++w) t += red[w][k];
+            slab[k] = t;
+        }
         // publish: release at agent scope, then the ticket (CDNA4 guide G16)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -532,16 +610,45 @@ static int pick_dt(int d) {
     return 0;
 }
 
-static int mmd2_grid(int rows) {
+// one wave per row, 4 waves per 256-thread block (witness / kernel-matrix sweeps)
+static int wave_grid(int rows) {
     int g = (rows + 3) / 4;
     if (g > 2048) g = 2048;
-    if (g < 1) g = 1;
-    return g;
+    return g < 1 ? 1 : g;
 }
+
+// rows are handed out 8 per wave.  One block (16 waves for DT <= 8, else 4:
+// register budget) covers small problems without any cross-block reduction;
+// beyond that one-wave blocks, ceil(rows / 8) of them (capped, grid-stride)
+static int single_waves(int dt) { return dt <= 8 ? 16 : 4; }
+
+static int mmd2_grid(int rows, int dt) {
+    if (rows <= 8 * single_waves(dt)) return 1;
+    int g = (rows + 7) / 8;
+    if (g > 4096) g = 4096;
+    return g < 1 ? 1 : g;
+}
+
+constexpr size_t MMD_STAGE_MAX_LDS = 64 * 1024;
 
 template <int DT, int KIND>
 static void launch_mmd2(const MmdArgs &a, int grid, hipStream_t s) {
-    hipLaunchKernelGGL((mmd2_fused_kernel<DT, KIND>), dim3(grid), dim3(256), 0, s, a);
+    const size_t lds = (size_t)(a.m + a.n) * (DT + 1) * sizeof(float);
+    const bool staged = lds <= MMD_STAGE_MAX_LDS;
+    if (grid == 1) {           // one block, 8 rows per wave
+        constexpr int NW1 = DT <= 8 ? 16 : 4;
+        if (staged)
+            hipLaunchKernelGGL((mmd2_fused_kernel<DT, KIND, NW1, true>), dim3(1), dim3(NW1 * 64), lds,
+                               s, a);
+        else
+            hipLaunchKernelGGL((mmd2_fused_kernel<DT, KIND, NW1, false>), dim3(1), dim3(NW1 * 64), 0,
+                               s, a);
+    } else {                   // one wave (8 rows) per block
+        if (staged)
+            hipLaunchKernelGGL((mmd2_fused_kernel<DT, KIND, 1, true>), dim3(grid), dim3(64), lds, s, a);
+        else
+            hipLaunchKernelGGL((mmd2_fused_kernel<DT, KIND, 1, false>), dim3(grid), dim3(64), 0, s, a);
+    }
 }
 
 template <int KIND>
@@ -658,7 +765,7 @@ int smmd_abi_version(void) { return 1; }
 size_t smmd_mmd2_workspace_bytes(int m, int n, int d) {
     (void)d;
     const int rows = (m > 0 ? m : 0) + (n > 0 ? n : 0);
-    return 256 + align_up((size_t)mmd2_grid(rows) * 8 * sizeof(double), 256);
+    return 256 + align_up((size_t)mmd2_grid(rows, pick_dt(d)) * 8 * sizeof(double), 256);
 }
 
 smmd_status smmd_mmd2_fwd(const smmd_kernel_desc *desc, const float *X, int m, const float *Y,
@@ -675,7 +782,7 @@ smmd_status smmd_mmd2_fwd(const smmd_kernel_desc *desc, const float *X, int m, c
     const int dt = pick_dt(d);
     if (dt == 0) return SMMD_EUNSUPPORTED;
     const int rows = (x_end - x_begin) + (y_end - y_begin);
-    const int grid = mmd2_grid(rows);
+    const int grid = mmd2_grid(rows, dt);
     if (!ws || ws_bytes < smmd_mmd2_workspace_bytes(m, n, d)) return SMMD_EWORKSPACE;
     if (rows == 0) return SMMD_EINVAL;
 
@@ -744,7 +851,7 @@ smmd_status smmd_witness_fwd(const smmd_kernel_desc *desc, const float *H, int b
     a.H = H; a.R = R; a.F = F; a.b = b; a.nr = nr; a.nf = nf; a.d = d;
     a.tanh_in = desc->tanh_inputs ? 1 : 0;
     a.out_w = out_w; a.out_dH = out_dH; a.kp = kp;
-    const int grid = mmd2_grid(b);
+    const int grid = wave_grid(b);
     hipStream_t s = (hipStream_t)stream;
 #define SMMD_WIT(DT_)                                                                          \
     case DT_:                                                                                  \
@@ -781,7 +888,7 @@ smmd_status smmd_witness_bwd(const smmd_kernel_desc *desc, const float *H, int b
     a.H = H; a.R = R; a.F = F; a.gdH = gdH; a.b = b; a.nr = nr; a.nf = nf; a.d = d;
     a.gH = gH; a.gR = gR; a.gF = gF; a.kp = kp;
     hipStream_t s = (hipStream_t)stream;
-    const int gh = mmd2_grid(b), gz = mmd2_grid(nr + nf);
+    const int gh = wave_grid(b), gz = wave_grid(nr + nf);
 #define SMMD_WB(DT_)                                                                           \
     case DT_:                                                                                  \
         if (desc->kind == SMMD_KIND_RBF) {                                                     \
@@ -848,7 +955,7 @@ smmd_status smmd_kernel_matrix_bwd(const smmd_kernel_desc *desc, const float *A,
     a.A = A; a.B = B; a.G = G; a.na = na; a.nb = nb; a.d = d;
     a.tanh_in = desc->tanh_inputs ? 1 : 0; a.gA = gA; a.gB = gB; a.kp = kp;
     hipStream_t s = (hipStream_t)stream;
-    const int ga = mmd2_grid(na), gb = mmd2_grid(nb);
+    const int ga = wave_grid(na), gb = wave_grid(nb);
 #define SMMD_KMB(DT_)                                                                          \
     SMMD_KM_SWITCH(DT_, {                                                                      \
         if (gA) hipLaunchKernelGGL((kmat_bwd_kernel<DT_, KIND_, 0>), dim3(ga), dim3(256), 0, s, a); \

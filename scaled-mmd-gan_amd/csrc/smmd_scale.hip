@@ -148,18 +148,33 @@ __device__ __forceinline__ int opt_find(const OptTable &t, int b) {
     return lo;
 }
 
+// every tensor range [off[i], off[i+1]) of the flat buffer is walked as float4
+// when all offsets are multiples of 4 and the buffers 16-byte aligned (vec);
+// FlatAdam pads its tensors to that.
 __global__ __launch_bounds__(256) void opt_sqsum_kernel(OptTable t, const float *__restrict__ g,
-                                                        float gscale, double *__restrict__ part) {
+                                                        float gscale, int vec,
+                                                        double *__restrict__ part) {
     const int ti = opt_find(t, blockIdx.x);
     const int64_t lo = t.off[ti] + (int64_t)(blockIdx.x - t.blk[ti]) * OPT_CHUNK;
     const int64_t hi = (lo + OPT_CHUNK < t.off[ti + 1]) ? lo + OPT_CHUNK : t.off[ti + 1];
-    float acc = 0.f;
-    for (int64_t i = lo + threadIdx.x; i < hi; i += 256) {
-        const float x = g[i] * gscale;
-        acc = fmaf(x, x, acc);
+    float acc0 = 0.f, acc1 = 0.f;
+    if (vec) {
+        const float4 *g4 = reinterpret_cast<const float4 *>(g);
+        for (int64_t i = lo / 4 + threadIdx.x; i < hi / 4; i += 256) {
+            const float4 x = g4[i];
+            acc0 = fmaf(x.x * gscale, x.x * gscale, acc0);
+            acc1 = fmaf(x.y * gscale, x.y * gscale, acc1);
+            acc0 = fmaf(x.z * gscale, x.z * gscale, acc0);
+            acc1 = fmaf(x.w * gscale, x.w * gscale, acc1);
+        }
+    } else {
+        for (int64_t i = lo + threadIdx.x; i < hi; i += 256) {
+            const float x = g[i] * gscale;
+            acc0 = fmaf(x, x, acc0);
+        }
     }
     __shared__ double red[4];
-    const double s = block_sum<4>((double)acc, red);
+    const double s = block_sum<4>((double)acc0 + (double)acc1, red);
     if (threadIdx.x == 0) part[blockIdx.x] = s;
 }
 
@@ -181,14 +196,36 @@ __device__ __forceinline__ float clip_factor(const OptTable &t, int ti, const do
 }
 
 __global__ __launch_bounds__(256) void opt_clip_kernel(OptTable t, float *__restrict__ g,
-                                                       const double *__restrict__ part, float clip) {
+                                                       const double *__restrict__ part, float clip,
+                                                       int vec) {
     const int ti = opt_find(t, blockIdx.x);
     __shared__ float sh[1];
     const float f = clip_factor(t, ti, part, clip, sh);
     const int64_t lo = t.off[ti] + (int64_t)(blockIdx.x - t.blk[ti]) * OPT_CHUNK;
     const int64_t hi = (lo + OPT_CHUNK < t.off[ti + 1]) ? lo + OPT_CHUNK : t.off[ti + 1];
-    for (int64_t i = lo + threadIdx.x; i < hi; i += 256) g[i] = g[i] * f;
+    if (vec) {
+        float4 *g4 = reinterpret_cast<float4 *>(g);
+        for (int64_t i = lo / 4 + threadIdx.x; i < hi / 4; i += 256) {
+            float4 x = g4[i];
+            x.x *= f; x.y *= f; x.z *= f; x.w *= f;
+            g4[i] = x;
+        }
+    } else {
+        for (int64_t i = lo + threadIdx.x; i < hi; i += 256) g[i] = g[i] * f;
+    }
 }
+
+struct AdamK {
+    float gscale, f, lr_t, b1c, b2c, eps;   // b1c = 1 - b1, b2c = 1 - b2
+    __device__ __forceinline__ void upd(float &p, float g, float &m, float &v) const {
+        // Eigen ApplyAdam: m += (g - m)(1-b1); v += (g^2 - v)(1-b2);
+        //                  var -= lr_t m / (sqrt(v) + eps)
+        g = (g * gscale) * f;
+        m += (g - m) * b1c;
+        v += (g * g - v) * b2c;
+        p -= (m * lr_t) / (sqrtf(v) + eps);
+    }
+};
 
 __global__ __launch_bounds__(256) void opt_adam_kernel(OptTable t, float *__restrict__ p,
                                                        const float *__restrict__ g,
@@ -196,24 +233,51 @@ __global__ __launch_bounds__(256) void opt_adam_kernel(OptTable t, float *__rest
                                                        float *__restrict__ v,
                                                        const double *__restrict__ part,
                                                        float gscale, float clip, float lr_t,
-                                                       float b1, float b2, float eps) {
+                                                       float b1, float b2, float eps, int vec) {
     const int ti = opt_find(t, blockIdx.x);
     __shared__ float sh[1];
-    const float f = (clip > 0.f) ? clip_factor(t, ti, part, clip, sh) : 1.f;
+    AdamK k;
+    k.gscale = gscale;
+    k.f = (clip > 0.f) ? clip_factor(t, ti, part, clip, sh) : 1.f;
+    k.lr_t = lr_t;
+    k.b1c = 1.f - b1;
+    k.b2c = 1.f - b2;
+    k.eps = eps;
     const int64_t lo = t.off[ti] + (int64_t)(blockIdx.x - t.blk[ti]) * OPT_CHUNK;
     const int64_t hi = (lo + OPT_CHUNK < t.off[ti + 1]) ? lo + OPT_CHUNK : t.off[ti + 1];
-    for (int64_t i = lo + threadIdx.x; i < hi; i += 256) {
-        float gi = g[i] * gscale;
-        if (clip > 0.f) gi = gi * f;
-        // Eigen ApplyAdam: m += (g - m)(1-b1); v += (g^2 - v)(1-b2);
-        //                  var -= lr_t m / (sqrt(v) + eps)
-        float mi = m[i], vi = v[i];
-        mi += (gi - mi) * (1.f - b1);
-        vi += (gi * gi - vi) * (1.f - b2);
-        m[i] = mi;
-        v[i] = vi;
-        p[i] -= (mi * lr_t) / (sqrtf(vi) + eps);
+    if (vec) {
+        float4 *p4 = reinterpret_cast<float4 *>(p);
+        const float4 *g4 = reinterpret_cast<const float4 *>(g);
+        float4 *m4 = reinterpret_cast<float4 *>(m);
+        float4 *v4 = reinterpret_cast<float4 *>(v);
+        for (int64_t i = lo / 4 + threadIdx.x; i < hi / 4; i += 256) {
+            float4 pp = p4[i], mm = m4[i], vv = v4[i];
+            const float4 gg = g4[i];
+            k.upd(pp.x, gg.x, mm.x, vv.x);
+            k.upd(pp.y, gg.y, mm.y, vv.y);
+            k.upd(pp.z, gg.z, mm.z, vv.z);
+            k.upd(pp.w, gg.w, mm.w, vv.w);
+            p4[i] = pp;
+            m4[i] = mm;
+            v4[i] = vv;
+        }
+    } else {
+        for (int64_t i = lo + threadIdx.x; i < hi; i += 256) {
+            float pp = p[i], mm = m[i], vv = v[i];
+            k.upd(pp, g[i], mm, vv);
+            p[i] = pp;
+            m[i] = mm;
+            v[i] = vv;
+        }
     }
+}
+
+static int opt_vec(const int64_t *off, int n, const void *a, const void *b, const void *c,
+                   const void *d) {
+    for (int i = 0; i <= n; ++i)
+        if (off[i] % 4) return 0;
+    const uintptr_t al = (uintptr_t)a | (uintptr_t)b | (uintptr_t)c | (uintptr_t)d;
+    return (al % 16) == 0;
 }
 
 static bool build_opt(const int64_t *off, int first, int count, OptTable &t) {
@@ -316,10 +380,11 @@ smmd_status smmd_clip_by_norm_flat(float *grad, const int64_t *offsets, int n_te
         const int count = (n_tensors - first < OPT_MAX) ? n_tensors - first : OPT_MAX;
         OptTable t;
         if (!build_opt(offsets, first, count, t)) return SMMD_EINVAL;
+        const int vec = opt_vec(offsets + first, count, grad, grad, grad, grad);
         hipLaunchKernelGGL(opt_sqsum_kernel, dim3(t.total_blocks), dim3(256), 0, s, t,
-                           (const float *)grad, 1.f, (double *)ws);
+                           (const float *)grad, 1.f, vec, (double *)ws);
         hipLaunchKernelGGL(opt_clip_kernel, dim3(t.total_blocks), dim3(256), 0, s, t, grad,
-                           (const double *)ws, clip_norm);
+                           (const double *)ws, clip_norm, vec);
         smmd_status st = last_launch_status();
         if (st != SMMD_OK) return st;
     }
@@ -341,12 +406,13 @@ smmd_status smmd_adam_flat(float *param, const float *grad, float *m, float *v,
         const int count = (n_tensors - first < OPT_MAX) ? n_tensors - first : OPT_MAX;
         OptTable t;
         if (!build_opt(offsets, first, count, t)) return SMMD_EINVAL;
+        const int vec = opt_vec(offsets + first, count, param, grad, m, v);
         if (clip_norm > 0.f)
             hipLaunchKernelGGL(opt_sqsum_kernel, dim3(t.total_blocks), dim3(256), 0, s, t, grad,
-                               grad_scale, (double *)ws);
+                               grad_scale, vec, (double *)ws);
         hipLaunchKernelGGL(opt_adam_kernel, dim3(t.total_blocks), dim3(256), 0, s, t, param, grad,
                            m, v, (const double *)ws, grad_scale, clip_norm, (float)lr_t, beta1,
-                           beta2, eps);
+                           beta2, eps, vec);
         smmd_status st = last_launch_status();
         if (st != SMMD_OK) return st;
     }

@@ -55,31 +55,39 @@ struct SnTable {
     SnLayerDev L[SN_CHUNK];
 };
 
+// Layer of a tile: static-index scan of the (monotone) tile_begin fields, then
+// readfirstlane so the index is provably wave-uniform and the descriptor is
+// read with scalar loads instead of a dependent chain of vector loads.
 __device__ __forceinline__ int find_layer(const SnTable &t, int tile) {
     int l = 0;
-    for (int i = 1; i < t.n_layers; ++i)
-        if (tile >= t.L[i].tile_begin) l = i;
-    return l;
+#pragma unroll
+    for (int i = 1; i < SN_CHUNK; ++i)
+        l += (i < t.n_layers && tile >= t.L[i].tile_begin) ? 1 : 0;
+    return __builtin_amdgcn_readfirstlane(l);
 }
 
-// load the 16 rows x 4 cols this thread owns (zero outside the matrix)
-__device__ __forceinline__ void load_tile(const SnLayerDev &L, const float *__restrict__ base,
+// load the 16 rows x 4 cols this thread owns (zero outside the matrix).
+// Interior tiles of 16-B aligned layers take one branch-free path: 16
+// independent float4 loads issued back to back.
+__device__ __forceinline__ void load_tile(const float *__restrict__ base, int N, int K, int vec,
                                           int r0, int c0, float4 (&w)[SN_RPW]) {
-    const bool full_cols = (c0 + 3 < L.K);
+    if (vec && r0 + SN_RPW <= N && c0 + 3 < K) {
+        const float4 *p = reinterpret_cast<const float4 *>(base + (size_t)r0 * K + c0);
+        const int stride4 = K / 4;
+#pragma unroll
+        for (int i = 0; i < SN_RPW; ++i) w[i] = p[(size_t)i * stride4];
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < SN_RPW; ++i) {
         const int r = r0 + i;
         float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (r < L.N) {
-            const float *p = base + (size_t)r * L.K + c0;
-            if (L.vec && full_cols) {
-                x = *reinterpret_cast<const float4 *>(p);
-            } else {
-                if (c0 + 0 < L.K) x.x = p[0];
-                if (c0 + 1 < L.K) x.y = p[1];
-                if (c0 + 2 < L.K) x.z = p[2];
-                if (c0 + 3 < L.K) x.w = p[3];
-            }
+        if (r < N) {
+            const float *p = base + (size_t)r * K + c0;
+            if (c0 + 0 < K) x.x = p[0];
+            if (c0 + 1 < K) x.y = p[1];
+            if (c0 + 2 < K) x.z = p[2];
+            if (c0 + 3 < K) x.w = p[3];
         }
         w[i] = x;
     }
@@ -87,7 +95,7 @@ __device__ __forceinline__ void load_tile(const SnLayerDev &L, const float *__re
 
 __global__ __launch_bounds__(256) void sn_p1_kernel(SnTable t) {
     const int tile = blockIdx.x;
-    const SnLayerDev &L = t.L[find_layer(t, tile)];
+    const SnLayerDev L = t.L[find_layer(t, tile)];
     const int lt = tile - L.tile_begin;
     const int rt = lt / L.nct, ct = lt % L.nct;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -96,7 +104,7 @@ __global__ __launch_bounds__(256) void sn_p1_kernel(SnTable t) {
     const float *uin = (t.iter == 0) ? L.u : L.ucur;
 
     float4 wt[SN_RPW];
-    load_tile(L, L.W, r0, c0, wt);
+    load_tile(L.W, L.N, L.K, L.vec, r0, c0, wt);
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int i = 0; i < SN_RPW; ++i) {
@@ -126,7 +134,7 @@ __global__ __launch_bounds__(256) void sn_p1_kernel(SnTable t) {
 
 __global__ __launch_bounds__(256) void sn_p2_kernel(SnTable t) {
     const int tile = blockIdx.x;
-    const SnLayerDev &L = t.L[find_layer(t, tile)];
+    const SnLayerDev L = t.L[find_layer(t, tile)];
     const int lt = tile - L.tile_begin;
     const int rt = lt / L.nct, ct = lt % L.nct;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -134,15 +142,17 @@ __global__ __launch_bounds__(256) void sn_p2_kernel(SnTable t) {
     const int c0 = ct * SN_TC + lane * 4;
 
     float4 wt[SN_RPW];
-    load_tile(L, L.W, r0, c0, wt);   // issue the tile loads first
+    load_tile(L.W, L.N, L.K, L.vec, r0, c0, wt);   // issue the tile loads first
 
     // v_raw for this tile's columns: fixed-order sum over row tiles of P1
     __shared__ float vr[SN_TC];
     {
         const int c = ct * SN_TC + threadIdx.x;
         float s = 0.f;
-        if (c < L.K)
+        if (c < L.K) {
+#pragma unroll 4
             for (int r = 0; r < L.nrt; ++r) s += L.p1[(size_t)r * L.K + c];
+        }
         vr[threadIdx.x] = s;
         if (rt == 0 && c < L.K) L.vraw[c] = s;
     }
@@ -163,48 +173,73 @@ __global__ __launch_bounds__(256) void sn_p2_kernel(SnTable t) {
     }
 }
 
-// one block (256 threads) per layer
-__global__ __launch_bounds__(256) void sn_r2_kernel(SnTable t) {
+// one block (1024 threads) per layer: norms, v, u', sigma.  Every loop body
+// issues independent loads (unrolled) so the block is not a latency chain.
+__global__ __launch_bounds__(1024) void sn_r2_kernel(SnTable t) {
     const SnLayerDev &L = t.L[blockIdx.x];
-    __shared__ double red[4];
-    __shared__ float sh_nv, sh_nu;
+    __shared__ double red[16];
     const int tid = threadIdx.x;
     // ||v_raw||
     double a = 0.0;
-    for (int k = tid; k < L.K; k += 256) a += (double)L.vraw[k] * (double)L.vraw[k];
-    a = block_sum<4>(a, red);
-    if (tid == 0) sh_nv = (float)sqrt(a) + t.eps;            // sn.py:13
-    __syncthreads();
-    const float nv = sh_nv;
-    for (int k = tid; k < L.K; k += 256) L.v[k] = L.vraw[k] / nv;
-    // u_raw = W v = (W v_raw) / nv ; ||u_raw||
-    double b = 0.0;
-    for (int n = tid; n < L.N; n += 256) {
-        float s = 0.f;
-        for (int c = 0; c < L.nct; ++c) s += L.q2[(size_t)c * L.N + n];
-        s = s / nv;
-        L.ucur[n] = s;                       // temporarily u_raw
-        b += (double)s * (double)s;
+#pragma unroll 4
+    for (int k = tid; k < L.K; k += 1024) {
+        const double x = (double)L.vraw[k];
+        a += x * x;
     }
-    b = block_sum<4>(b, red);
-    if (tid == 0) sh_nu = (float)sqrt(b) + t.eps;
-    __syncthreads();
-    const float nu = sh_nu;
+    const float nv = (float)sqrt(block_sum<16>(a, red)) + t.eps;     // sn.py:13
+#pragma unroll 4
+    for (int k = tid; k < L.K; k += 1024) L.v[k] = L.vraw[k] / nv;
+    // u_raw = W v = (W v_raw) / nv, summed over column tiles in fixed order
+    float ur[2] = {0.f, 0.f};
+    double b = 0.0;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int n = tid + j * 1024;
+        if (n < L.N) {
+            float s0 = 0.f, s1 = 0.f;
+            int c = 0;
+            for (; c + 1 < L.nct; c += 2) {
+                s0 += L.q2[(size_t)c * L.N + n];
+                s1 += L.q2[(size_t)(c + 1) * L.N + n];
+            }
+            if (c < L.nct) s0 += L.q2[(size_t)c * L.N + n];
+            ur[j] = (s0 + s1) / nv;
+            b += (double)ur[j] * (double)ur[j];
+        }
+    }
+    for (int n = tid + 2048; n < L.N; n += 1024) {          // N > 2048: rare, simple path
+        float s0 = 0.f;
+        for (int c = 0; c < L.nct; ++c) s0 += L.q2[(size_t)c * L.N + n];
+        s0 /= nv;
+        L.ucur[n] = s0;
+        b += (double)s0 * (double)s0;
+    }
+    const float nu = (float)sqrt(block_sum<16>(b, red)) + t.eps;
     double sg = 0.0;
-    for (int n = tid; n < L.N; n += 256) {
-        const float ur = L.ucur[n];
-        const float un = ur / nu;            // u' = l2n(v W)
-        sg += (double)ur * (double)un;       // sigma = (v W) . u'   sn.py:42
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int n = tid + j * 1024;
+        if (n < L.N) {
+            const float un = ur[j] / nu;                    // u' = l2n(v W)
+            sg += (double)ur[j] * (double)un;               // sigma = (v W) . u'  sn.py:42
+            L.ucur[n] = un;
+            if (t.update_u && t.last_iter) L.u[n] = un;
+        }
+    }
+    for (int n = tid + 2048; n < L.N; n += 1024) {
+        const float r = L.ucur[n];
+        const float un = r / nu;
+        sg += (double)r * (double)un;
         L.ucur[n] = un;
         if (t.update_u && t.last_iter) L.u[n] = un;
     }
-    sg = block_sum<4>(sg, red);
+    sg = block_sum<16>(sg, red);
     if (tid == 0 && t.last_iter) L.sigma[0] = (float)sg;
 }
 
 __global__ __launch_bounds__(256) void sn_p3_kernel(SnTable t) {
     const int tile = blockIdx.x;
-    const SnLayerDev &L = t.L[find_layer(t, tile)];
+    const SnLayerDev L = t.L[find_layer(t, tile)];
     if (!L.W_eff) return;
     const int lt = tile - L.tile_begin;
     const int rt = lt / L.nct, ct = lt % L.nct;
@@ -214,7 +249,7 @@ __global__ __launch_bounds__(256) void sn_p3_kernel(SnTable t) {
     const float sigma = L.sigma[0];
     const float s = L.s ? L.s[0] : 1.f;
     float4 wt[SN_RPW];
-    load_tile(L, L.W, r0, c0, wt);
+    load_tile(L.W, L.N, L.K, L.vec, r0, c0, wt);
     const bool full_cols = (c0 + 3 < L.K);
 #pragma unroll
     for (int i = 0; i < SN_RPW; ++i) {
@@ -241,15 +276,15 @@ __global__ __launch_bounds__(256) void sn_p3_kernel(SnTable t) {
 // backward A: partial <G, W> per tile
 __global__ __launch_bounds__(256) void sn_bwd_a_kernel(SnTable t) {
     const int tile = blockIdx.x;
-    const SnLayerDev &L = t.L[find_layer(t, tile)];
+    const SnLayerDev L = t.L[find_layer(t, tile)];
     const int lt = tile - L.tile_begin;
     const int rt = lt / L.nct, ct = lt % L.nct;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int r0 = rt * SN_TR + w * SN_RPW;
     const int c0 = ct * SN_TC + lane * 4;
     float4 wt[SN_RPW], gt[SN_RPW];
-    load_tile(L, L.W, r0, c0, wt);
-    load_tile(L, L.G, r0, c0, gt);
+    load_tile(L.W, L.N, L.K, L.vec, r0, c0, wt);
+    load_tile(L.G, L.N, L.K, L.vec, r0, c0, gt);
     float acc = 0.f;
 #pragma unroll
     for (int i = 0; i < SN_RPW; ++i) {
@@ -266,14 +301,14 @@ __global__ __launch_bounds__(256) void sn_bwd_a_kernel(SnTable t) {
 // backward B: gW = (s G)/sigma - (s <G,W> / sigma^2) u' v^T ; gs = <G,W>/sigma
 __global__ __launch_bounds__(256) void sn_bwd_b_kernel(SnTable t) {
     const int tile = blockIdx.x;
-    const SnLayerDev &L = t.L[find_layer(t, tile)];
+    const SnLayerDev L = t.L[find_layer(t, tile)];
     const int lt = tile - L.tile_begin;
     const int rt = lt / L.nct, ct = lt % L.nct;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int r0 = rt * SN_TR + w * SN_RPW;
     const int c0 = ct * SN_TC + lane * 4;
     float4 gt[SN_RPW];
-    load_tile(L, L.G, r0, c0, gt);
+    load_tile(L.G, L.N, L.K, L.vec, r0, c0, gt);
     __shared__ float sh_d;
     if (w == 0) {
         const int nt = L.nrt * L.nct;
@@ -405,7 +440,7 @@ smmd_status smmd_sn_power_iter(const smmd_sn_layer *layers, int n_layers, int nu
             t.last_iter = (it == num_iters - 1);
             hipLaunchKernelGGL(sn_p1_kernel, dim3(t.total_tiles), dim3(256), 0, s, t);
             hipLaunchKernelGGL(sn_p2_kernel, dim3(t.total_tiles), dim3(256), 0, s, t);
-            hipLaunchKernelGGL(sn_r2_kernel, dim3(t.n_layers), dim3(256), 0, s, t);
+            hipLaunchKernelGGL(sn_r2_kernel, dim3(t.n_layers), dim3(1024), 0, s, t);
         }
         bool any_eff = false;
         for (int i = 0; i < count; ++i) any_eff |= (t.L[i].W_eff != nullptr);

@@ -152,6 +152,62 @@ def require_cuda(*tensors):
 
 
 # ---------------------------------------------------------------------------
+# optional per-entry-point timing with HIP events on the current stream
+# (used by bench.py; a no-op unless enabled)
+# ---------------------------------------------------------------------------
+class _Timing:
+    enabled = False
+    records = {}
+
+
+class _NullCtx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+_NULL = _NullCtx()
+
+
+class _EventCtx:
+    def __init__(self, name):
+        self.name = name
+
+    def __enter__(self):
+        self.s = torch.cuda.Event(enable_timing=True)
+        self.e = torch.cuda.Event(enable_timing=True)
+        self.s.record()
+        return self
+
+    def __exit__(self, *a):
+        self.e.record()
+        _Timing.records.setdefault(self.name, []).append((self.s, self.e))
+        return False
+
+
+def timed(name):
+    """Context manager bracketing one library call with HIP events."""
+    return _EventCtx(name) if _Timing.enabled else _NULL
+
+
+def enable_timing(on=True):
+    _Timing.enabled = on
+
+
+def timing_ms():
+    """{entry point: (calls, mean ms)} over the recorded events (syncs)."""
+    torch.cuda.synchronize()
+    return {k: (len(v), sum(s.elapsed_time(e) for s, e in v) / len(v))
+            for k, v in _Timing.records.items() if v}
+
+
+def reset_timing():
+    _Timing.records = {}
+
+
+# ---------------------------------------------------------------------------
 # workspaces: zero-filled at allocation, owned per (device, stream, tag)
 # ---------------------------------------------------------------------------
 _ws_cache = {}

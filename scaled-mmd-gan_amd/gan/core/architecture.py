@@ -13,6 +13,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .convops import mean_pool2
 from .snops import Conv2d, Deconv2d, Linear, batch_norm, lrelu
 
 
@@ -55,7 +56,7 @@ class _ConvMeanPool(nn.Module):
         self.conv = Conv2d(cin, cout, k, 1, bias=bias, init='glorot_uniform', **sn)
 
     def forward(self, x):
-        return F.avg_pool2d(self.conv(x), 2)
+        return mean_pool2(self.conv(x))
 
 
 class _MeanPoolConv(nn.Module):
@@ -66,7 +67,7 @@ class _MeanPoolConv(nn.Module):
         self.conv = Conv2d(cin, cout, k, 1, bias=bias, init='glorot_uniform', **sn)
 
     def forward(self, x):
-        return self.conv(F.avg_pool2d(x, 2))
+        return self.conv(mean_pool2(x))
 
 
 class ResidualBlock(nn.Module):

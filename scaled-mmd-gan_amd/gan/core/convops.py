@@ -1,0 +1,151 @@
+"""Convolution with an explicit second-order rule (PyTorch-ROCm / MIOpen).
+
+The SMMD critic update differentiates THROUGH the critic's input gradient
+(the scaling regulariser, gan/core/ops.py:228-233 + model.py:382-390), so
+every critic convolution is differentiated twice.  PyTorch's generic
+double-backward computes the weight term of that second pass as a FORWARD
+convolution of batch/channel-transposed tensors whose "filter" is a whole
+activation map (e.g. MIOpen problem ``-n 512 -c 64 -H 8 -W 8 -k 512 -y 8 -x 8``),
+which MIOpen runs at 2-4 ms a call on MI355X.  Here the pass is spelled out
+with the three standard primitives on the layer's own shapes:
+
+  y = conv(x, w)            gx = Dx(gy, w)          gw = Dw(x, gy)
+  second order, given ggx (and ggw):
+    d/dgy = conv(ggx, w) + conv(x, ggw)
+    d/dw  = Dw(ggx, gy)
+    d/dx  = Dx(gy, ggw)
+
+so it uses MIOpen's forward, backward-data and backward-weights kernels.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+_aten = torch.ops.aten
+
+# >0 while an autograd.grad call that needs input gradients ONLY is running
+# (the critic Jacobian of the scaling regulariser).  A custom Function cannot
+# see which edges the engine needs, so without this every conv of that pass
+# would also run a weight-gradient kernel whose result is discarded.
+_input_only = [0]
+
+
+class input_grad_only:
+    def __enter__(self):
+        _input_only[0] += 1
+
+    def __exit__(self, *a):
+        _input_only[0] -= 1
+
+
+def _bwd(gy, x, w, stride, padding, mask):
+    """(Dx, Dw) of conv(x, w) at upstream gy via the native backward kernels."""
+    gx, gw, _ = _aten.convolution_backward(gy, x, w, None, stride, padding, [1, 1], False,
+                                           [0, 0], 1, [mask[0], mask[1], False])
+    return gx, gw
+
+
+class _ConvBackward(torch.autograd.Function):
+    """(gx, gw) = backward of conv(x, w); differentiable once more."""
+
+    @staticmethod
+    def forward(ctx, x, w, gy, stride, padding, want_w):
+        ctx.save_for_backward(x, w, gy)
+        ctx.cfg = (stride, padding)
+        gx, gw = _bwd(gy, x, w, stride, padding, (True, want_w))
+        if gw is None:          # placeholder, discarded by the caller: no allocation
+            gw = w.new_zeros(()).expand_as(w)
+            ctx.mark_non_differentiable(gw)
+        return gx, gw
+
+    @staticmethod
+    def backward(ctx, ggx, ggw):
+        x, w, gy = ctx.saved_tensors
+        stride, padding = ctx.cfg
+        need_x, need_w, need_gy = ctx.needs_input_grad[:3]
+        g_x = g_w = g_gy = None
+        if ggx is not None:
+            ggx = ggx.contiguous(memory_format=_fmt(x))
+            if need_gy:
+                g_gy = F.conv2d(ggx, w, None, stride, padding)
+            if need_w:
+                _, g_w = _bwd(gy, ggx, w, stride, padding, (False, True))
+        if ggw is not None:
+            if need_gy:
+                t = F.conv2d(x, ggw, None, stride, padding)
+                g_gy = t if g_gy is None else g_gy + t
+            if need_x:
+                g_x, _ = _bwd(gy, x, ggw, stride, padding, (True, False))
+        return g_x, g_w, g_gy, None, None, None
+
+
+def _fmt(t):
+    if t.dim() == 4 and not t.is_contiguous() and t.is_contiguous(
+            memory_format=torch.channels_last):
+        return torch.channels_last
+    return torch.contiguous_format
+
+
+class _Conv2d(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, stride, padding):
+        ctx.save_for_backward(x, w)
+        ctx.cfg = (stride, padding, b is not None)
+        return F.conv2d(x, w, b, stride, padding)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        stride, padding, has_b = ctx.cfg
+        gy = gy.contiguous(memory_format=_fmt(x))
+        want_w = ctx.needs_input_grad[1] and _input_only[0] == 0
+        if torch.is_grad_enabled():          # create_graph: keep it differentiable
+            gx, gw = _ConvBackward.apply(x, w, gy, stride, padding, want_w)
+            if not want_w:
+                gw = None
+        else:
+            gx, gw = _bwd(gy, x, w, stride, padding, (ctx.needs_input_grad[0], want_w))
+        gb = (gy.sum(dim=(0, 2, 3)) if (has_b and ctx.needs_input_grad[2] and _input_only[0] == 0)
+              else None)
+        return gx, gw, gb, None, None
+
+
+def conv2d(x, w, b=None, stride=1, padding=0):
+    """F.conv2d with the MIOpen-friendly second-order rule above."""
+    s = (stride, stride) if isinstance(stride, int) else tuple(stride)
+    p = (padding, padding) if isinstance(padding, int) else tuple(padding)
+    return _Conv2d.apply(x, w, b, list(s), list(p))
+
+
+class _Up2Quarter(torch.autograd.Function):
+    """g -> nearest-upsample(g / 4): the adjoint of the 2x2 mean pool."""
+
+    @staticmethod
+    def forward(ctx, g):
+        return F.interpolate(g * 0.25, scale_factor=2, mode='nearest')
+
+    @staticmethod
+    def backward(ctx, gg):
+        return _MeanPool2.apply(gg)
+
+
+class _MeanPool2(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        return F.avg_pool2d(x, 2)
+
+    @staticmethod
+    def backward(ctx, g):
+        return _Up2Quarter.apply(g.contiguous())
+
+
+def mean_pool2(x):
+    """2x2 mean pool, the reference's add_n of the four strided slices / 4
+    (gan/core/resnet/block.py:65, :71), as a linear op whose backward is one
+    nearest-upsample of g/4 (and whose double backward is the pool again),
+    instead of four strided-slice backwards (zero fill + copy each)."""
+    if x.shape[2] % 2 or x.shape[3] % 2:
+        return (x[:, :, ::2, ::2] + x[:, :, 1::2, ::2] + x[:, :, ::2, 1::2]
+                + x[:, :, 1::2, 1::2]) / 4.
+    return _MeanPool2.apply(x)

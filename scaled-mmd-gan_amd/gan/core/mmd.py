@@ -145,10 +145,12 @@ class _MMD2Fused(torch.autograd.Function):
         nbytes = L.smmd_mmd2_workspace_bytes(m, n, d)
         ws = _lib.workspace('mmd2', nbytes, dev)
         desc = spec.desc()
-        _lib.check(L.smmd_mmd2_fwd(desc, _lib.ptr(Xa), m, _lib.ptr(Ya), n, d, 1 if biased else 0,
-                                   *rows, _lib.ptr(sums), _lib.ptr(out), _lib.ptr(gx),
-                                   _lib.ptr(gy), _lib.ptr(ws), ws.numel(),
-                                   _lib.stream_handle(dev)), 'smmd_mmd2_fwd')
+        args = (desc, _lib.ptr(Xa), m, _lib.ptr(Ya), n, d, 1 if biased else 0, *rows,
+                _lib.ptr(sums), _lib.ptr(out), _lib.ptr(gx), _lib.ptr(gy), _lib.ptr(ws),
+                ws.numel(), _lib.stream_handle(dev))
+        with _lib.timed('smmd_mmd2_fwd'):
+            st = L.smmd_mmd2_fwd(*args)
+        _lib.check(st, 'smmd_mmd2_fwd')
         if group is not None:
             dist.all_reduce(sums, group=group)
             _lib.check(L.smmd_mmd2_combine(desc, _lib.ptr(sums), m, n, 1 if biased else 0,

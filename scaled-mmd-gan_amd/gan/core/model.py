@@ -61,7 +61,7 @@ class MMD_GAN:
     (:352-364)."""
 
     def __init__(self, config, device=None, process_group=None, dp_mode='tower',
-                 batch_size=None, output_size=None, c_dim=3):
+                 batch_size=None, output_size=None, c_dim=3, channels_last=False):
         c = config
         if getattr(c, 'learning_rate_D', -1) < 0:               # model.py:18-19
             c.learning_rate_D = c.learning_rate
@@ -88,14 +88,20 @@ class MMD_GAN:
         self.discriminator = D_cls(c.df_dim, c.dof_dim, dbn, with_sn=c.with_sn,
                                    with_learnable_sn_scale=c.with_learnable_sn_scale,
                                    input_size=self.output_size).to(self.device)
+        self.memory_format = torch.channels_last if channels_last else torch.contiguous_format
+        if channels_last:               # NHWC activations and conv weights (MIOpen NHWC solvers)
+            self.generator.to(memory_format=torch.channels_last)
+            self.discriminator.to(memory_format=torch.channels_last)
         self.sn_D = SpectralNormBank(sn_modules(self.discriminator))
         self.sn_G = SpectralNormBank(sn_modules(self.generator))
         self.spec = mmd.get_kernel_spec(c.kernel) if c.kernel else None
         self.g_vars = [p for p in self.generator.parameters() if p.requires_grad]
         self.d_vars = [p for p in self.discriminator.parameters() if p.requires_grad]
         clip = 1.0 if c.clip_grad else 0.0
-        self.g_optim = FlatAdam(self.g_vars, c.learning_rate, c.beta1, c.beta2, clip_norm=clip)
-        self.d_optim = FlatAdam(self.d_vars, c.learning_rate_D, c.beta1, c.beta2, clip_norm=clip)
+        self.g_optim = FlatAdam(self.g_vars, c.learning_rate, c.beta1, c.beta2, clip_norm=clip,
+                                name='G')
+        self.d_optim = FlatAdam(self.d_vars, c.learning_rate_D, c.beta1, c.beta2, clip_norm=clip,
+                                name='D')
         self.lr = float(c.learning_rate)
         self.sc = float(c.scaling_coeff) if c.with_scaling else None
         self.gp = float(c.gradient_penalty)
@@ -155,6 +161,8 @@ class MMD_GAN:
         for d_loss w.r.t. the critic (including the Jacobian double backward)."""
         D = self.discriminator
         scaling = self.uses_scaling()
+        if images.dim() == 4:
+            images = images.contiguous(memory_format=self.memory_format)
         if scaling:
             images = images.detach().requires_grad_(True)
         d_images = D(images)

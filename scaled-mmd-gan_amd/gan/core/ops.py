@@ -14,6 +14,7 @@ import torch
 import torch.distributed as dist
 
 from . import _lib
+from .convops import input_grad_only
 from .mmd import _eps
 
 
@@ -47,8 +48,9 @@ def jacobian_columns(y, x, create_graph=True):
     d = y.shape[1]
     cols = []
     for i in range(d):
-        g, = torch.autograd.grad(y[:, i].sum(), x, create_graph=create_graph,
-                                 retain_graph=True)
+        with input_grad_only():       # no weight-gradient kernels in this pass
+            g, = torch.autograd.grad(y[:, i].sum(), x, create_graph=create_graph,
+                                     retain_graph=True)
         cols.append(g)
     return torch.stack(cols, 0) if d > 1 else cols[0].unsqueeze(0)
 
@@ -74,10 +76,12 @@ class _ScaledLoss(torch.autograd.Function):
         nbytes = L.smmd_scaled_loss_workspace_bytes(n_cols * b, per)
         ws = _lib.workspace('scaled_loss', nbytes, dev)
         s = _lib.stream_handle(dev)
-        _lib.check(L.smmd_scaled_loss_fwd(_lib.ptr(jac), n_cols, b, b_total, per,
-                                          _lib.ptr(feat_c), dof, _lib.ptr(base), float(sc),
-                                          variant, sqrt_scale, _lib.ptr(out), _lib.ptr(per_sample),
-                                          _lib.ptr(ws), ws.numel(), s), 'smmd_scaled_loss_fwd')
+        args = (_lib.ptr(jac), n_cols, b, b_total, per, _lib.ptr(feat_c), dof, _lib.ptr(base),
+                float(sc), variant, sqrt_scale, _lib.ptr(out), _lib.ptr(per_sample), _lib.ptr(ws),
+                ws.numel(), s)
+        with _lib.timed('smmd_scaled_loss_fwd'):
+            st = L.smmd_scaled_loss_fwd(*args)
+        _lib.check(st, 'smmd_scaled_loss_fwd')
         if group is not None:
             # J and nD are partial means over the global batch: sum them
             dist.all_reduce(out[3:5], group=group)
@@ -97,10 +101,12 @@ class _ScaledLoss(torch.autograd.Function):
         d_base = torch.empty(1, device=dev, dtype=torch.float32)
         gjac = torch.empty_like(jac)
         gfeat = torch.empty_like(feat) if (feat is not None and variant == 1) else None
-        _lib.check(_lib.lib().smmd_scaled_loss_bwd(
-            _lib.ptr(jac), n_cols, b, b_total, per, _lib.ptr(feat), dof, _lib.ptr(out), sc,
-            variant, sqrt_scale, _lib.ptr(go), _lib.ptr(d_base), _lib.ptr(gjac),
-            _lib.ptr(gfeat), _lib.stream_handle(dev)), 'smmd_scaled_loss_bwd')
+        args = (_lib.ptr(jac), n_cols, b, b_total, per, _lib.ptr(feat), dof, _lib.ptr(out), sc,
+                variant, sqrt_scale, _lib.ptr(go), _lib.ptr(d_base), _lib.ptr(gjac),
+                _lib.ptr(gfeat), _lib.stream_handle(dev))
+        with _lib.timed('smmd_scaled_loss_bwd'):
+            st = _lib.lib().smmd_scaled_loss_bwd(*args)
+        _lib.check(st, 'smmd_scaled_loss_bwd')
         if feat is not None and gfeat is None:
             gfeat = torch.zeros_like(feat)
         return d_base.view(()), gjac, gfeat, None, None, None, None, None

@@ -19,7 +19,8 @@ from . import _lib
 
 
 class FlatAdam:
-    def __init__(self, params, lr, beta1=0.5, beta2=0.9, eps=1e-8, clip_norm=1.0):
+    def __init__(self, params, lr, beta1=0.5, beta2=0.9, eps=1e-8, clip_norm=1.0, name='opt'):
+        self.name = name
         self.params = [p for p in params]
         if not self.params:
             raise ValueError('no parameters')
@@ -29,42 +30,46 @@ class FlatAdam:
         self.clip_norm = clip_norm if clip_norm else 0.0
         sizes = [p.numel() for p in self.params]
         offs = [0]
-        for s in sizes:
-            offs.append(offs[-1] + s)
+        for s in sizes:     # tensor i owns [offs[i], offs[i+1]): size padded to 4 floats
+            offs.append(offs[-1] + (s + 3) // 4 * 4)
         self.numel = offs[-1]
+        self.param_numel = sum(sizes)
         self.offsets = (ctypes.c_int64 * len(offs))(*offs)
-        self.flat_param = torch.empty(self.numel, device=dev, dtype=torch.float32)
+        self.flat_param = torch.zeros(self.numel, device=dev, dtype=torch.float32)
         self.flat_grad = torch.zeros(self.numel, device=dev, dtype=torch.float32)
         self.m = torch.zeros(self.numel, device=dev, dtype=torch.float32)
         self.v = torch.zeros(self.numel, device=dev, dtype=torch.float32)
         with torch.no_grad():
             for p, o, s in zip(self.params, offs, sizes):
-                view = self.flat_param[o:o + s].view_as(p)
+                # keep each parameter's memory format (e.g. channels_last convs)
+                view = self._view(self.flat_param, p, o)
                 view.copy_(p)
                 p.data = view
-                p.grad = self.flat_grad[o:o + s].view_as(p)
+                p.grad = self._view(self.flat_grad, p, o)
         self.step_count = 0
         nbytes = _lib.lib().smmd_opt_workspace_bytes(self.offsets, len(self.params))
         self.ws = torch.zeros(max(nbytes, 256), dtype=torch.uint8, device=dev)
 
+    @staticmethod
+    def _view(flat, p, o):
+        if p.is_contiguous():
+            return flat[o:o + p.numel()].view_as(p)
+        return torch.as_strided(flat, p.shape, p.stride(), o)
+
     def zero_grad(self, set_to_none=False):
         self.flat_grad.zero_()
         # re-attach views in case autograd replaced a .grad tensor
-        o = 0
-        for p in self.params:
-            n = p.numel()
+        for i, p in enumerate(self.params):
+            o, n = self.offsets[i], p.numel()
             if n and (p.grad is None or p.grad.data_ptr() != self.flat_grad[o:o + n].data_ptr()):
-                p.grad = self.flat_grad[o:o + n].view_as(p)
-            o += n
+                p.grad = self._view(self.flat_grad, p, o)
 
     def _check_grads(self):
-        o = 0
-        for p in self.params:
-            n = p.numel()
+        for i, p in enumerate(self.params):
+            o, n = self.offsets[i], p.numel()
             if n and (p.grad is None or p.grad.data_ptr() != self.flat_grad[o:o + n].data_ptr()):
                 raise RuntimeError('a parameter gradient was re-allocated outside flat_grad; '
                                    'call zero_grad() before backward()')
-            o += n
 
     def clip_(self, clip_norm=None):
         """Per-tensor clip_by_norm in place (the per-tower clip)."""
@@ -78,12 +83,14 @@ class FlatAdam:
         self._check_grads()
         self.step_count += 1
         c = float(self.clip_norm) if clip else 0.0
-        _lib.check(_lib.lib().smmd_adam_flat(
-            _lib.ptr(self.flat_param), _lib.ptr(self.flat_grad), _lib.ptr(self.m),
-            _lib.ptr(self.v), self.offsets, len(self.params), float(grad_scale), c,
-            float(self.lr if lr is None else lr), float(self.beta1), float(self.beta2),
-            float(self.eps), self.step_count, _lib.ptr(self.ws), self.ws.numel(),
-            _lib.stream_handle(self.flat_grad.device)), 'smmd_adam_flat')
+        args = (_lib.ptr(self.flat_param), _lib.ptr(self.flat_grad), _lib.ptr(self.m),
+                _lib.ptr(self.v), self.offsets, len(self.params), float(grad_scale), c,
+                float(self.lr if lr is None else lr), float(self.beta1), float(self.beta2),
+                float(self.eps), self.step_count, _lib.ptr(self.ws), self.ws.numel(),
+                _lib.stream_handle(self.flat_grad.device))
+        with _lib.timed('smmd_adam_flat[%s]' % self.name):
+            st = _lib.lib().smmd_adam_flat(*args)
+        _lib.check(st, 'smmd_adam_flat')
 
     def state_dict(self):
         return {'m': self.m.clone(), 'v': self.v.clone(), 'step': self.step_count,

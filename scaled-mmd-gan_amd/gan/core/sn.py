@@ -38,13 +38,15 @@ class _SNBatch(torch.autograd.Function):
         outs = []
         arr = (_lib.SnLayer * n)()
         for i, (e, W, s) in enumerate(zip(bank.entries, Ws, ss)):
-            W2 = W.detach().reshape(e.N, e.K)
-            if not W2.is_contiguous():
-                raise ValueError('SN weight %d is not contiguous' % i)
+            # each output channel's K values must be contiguous: true for the
+            # default and the channels_last layouts (SN is invariant to the
+            # order of K, see the module docstring)
+            if _memfmt(W) is None:
+                raise ValueError('SN weight %d is neither contiguous nor channels_last' % i)
             W_eff = torch.empty_like(W)
             outs.append(W_eff)
             L = arr[i]
-            L.W = W2.data_ptr()
+            L.W = W.data_ptr()
             L.W_eff = W_eff.data_ptr()
             L.u = e.u.data_ptr()
             L.v = e.v.data_ptr()
@@ -53,9 +55,11 @@ class _SNBatch(torch.autograd.Function):
             L.N, L.K = e.N, e.K
         dev = Ws[0].device
         lib = _lib.lib()
-        _lib.check(lib.smmd_sn_power_iter(arr, n, bank.num_iters, SN_EPS, 1 if update_u else 0,
-                                          _lib.ptr(bank.ws), bank.ws.numel(),
-                                          _lib.stream_handle(dev)), 'smmd_sn_power_iter')
+        args = (arr, n, bank.num_iters, SN_EPS, 1 if update_u else 0, _lib.ptr(bank.ws),
+                bank.ws.numel(), _lib.stream_handle(dev))
+        with _lib.timed('smmd_sn_power_iter'):
+            st = lib.smmd_sn_power_iter(*args)
+        _lib.check(st, 'smmd_sn_power_iter')
         ctx.bank = bank
         ctx.save_for_backward(*Ws, *ss)
         return tuple(outs)
@@ -71,7 +75,7 @@ class _SNBatch(torch.autograd.Function):
         for i, (e, W, s, G) in enumerate(zip(bank.entries, Ws, ss, grads)):
             if G is None:
                 G = torch.zeros_like(W)
-            G = G.contiguous()
+            G = G.contiguous(memory_format=_memfmt(W))
             keep.append(G)
             gW = torch.empty_like(W)
             gs = torch.empty(1, device=W.device, dtype=torch.float32)
@@ -87,9 +91,10 @@ class _SNBatch(torch.autograd.Function):
             L.gW = gW.data_ptr()
             L.gs = gs.data_ptr()
             L.N, L.K = e.N, e.K
-        _lib.check(_lib.lib().smmd_sn_weight_bwd(arr, n, _lib.ptr(bank.ws), bank.ws.numel(),
-                                                 _lib.stream_handle(Ws[0].device)),
-                   'smmd_sn_weight_bwd')
+        args = (arr, n, _lib.ptr(bank.ws), bank.ws.numel(), _lib.stream_handle(Ws[0].device))
+        with _lib.timed('smmd_sn_weight_bwd'):
+            st = _lib.lib().smmd_sn_weight_bwd(*args)
+        _lib.check(st, 'smmd_sn_weight_bwd')
         gs_out = []
         for s, gs in zip(ss, gss):
             if gs is None:
@@ -97,6 +102,14 @@ class _SNBatch(torch.autograd.Function):
             else:
                 gs_out.append(gs.view_as(s))
         return (None, None, *gWs, *gs_out)
+
+
+def _memfmt(W):
+    if W.is_contiguous():
+        return torch.contiguous_format
+    if W.dim() == 4 and W.is_contiguous(memory_format=torch.channels_last):
+        return torch.channels_last
+    return None
 
 
 class SNEntry:

@@ -16,6 +16,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .convops import conv2d
+
 
 def same_pad(n_in, k, s):
     """TF 'SAME': total = max((ceil(n/s) - 1) s + k - n, 0), before = total // 2."""
@@ -74,9 +76,9 @@ class Conv2d(nn.Module, _SNMixin):
         ph = same_pad(x.shape[2], self.k, self.stride)
         pw = same_pad(x.shape[3], self.k, self.stride)
         if ph[0] == ph[1] and pw[0] == pw[1]:
-            return F.conv2d(x, w, self.bias, self.stride, (ph[0], pw[0]))
+            return conv2d(x, w, self.bias, self.stride, (ph[0], pw[0]))
         x = F.pad(x, (pw[0], pw[1], ph[0], ph[1]))
-        return F.conv2d(x, w, self.bias, self.stride)
+        return conv2d(x, w, self.bias, self.stride, 0)
 
 
 class Deconv2d(nn.Module, _SNMixin):

@@ -43,7 +43,8 @@ def test_status_strings(L):
 
 def test_workspace_sizing(L):
     from gan.core import _lib
-    assert L.smmd_mmd2_workspace_bytes(64, 64, 1) >= 256 + 32 * 8 * 8
+    assert L.smmd_mmd2_workspace_bytes(64, 64, 1) >= 256            # one-block path
+    assert L.smmd_mmd2_workspace_bytes(2048, 2048, 1) >= 256 + (4096 // 8) * 8 * 8
     assert L.smmd_scaled_loss_workspace_bytes(64, 3 * 64 * 64) >= 64 * 3 * 8
     arr = (_lib.SnLayer * 2)()
     arr[0].N, arr[0].K, arr[1].N, arr[1].K = 64, 27, 1024, 4608

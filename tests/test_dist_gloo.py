@@ -131,11 +131,12 @@ def _worker_exchange(rank, world, port, mode, q):
     params = [torch.nn.Parameter(torch.tensor(p0)), torch.nn.Parameter(torch.tensor(p1))]
     opt = FlatAdam(params, lr=1e-3, clip_norm=1.0)
     g = np.random.default_rng(100 + rank).standard_normal(8).astype(np.float32) * 2
-    opt.flat_grad.copy_(torch.tensor(g))
+    params[0].grad.copy_(torch.tensor(g[:5]))
+    params[1].grad.copy_(torch.tensor(g[5:]))
     m = MMD_GAN.__new__(MMD_GAN)
     m.world, m.group, m.dp_mode = world, dist.group.WORLD, mode
     m._exchange(opt)
-    q.put((rank, opt.flat_param.numpy().copy()))
+    q.put((rank, np.concatenate([p.detach().numpy().ravel() for p in params])))
     dist.barrier()
     dist.destroy_process_group()
 

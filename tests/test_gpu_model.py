@@ -40,14 +40,18 @@ def _mirror_from(model):
     return st
 
 
-@pytest.mark.parametrize('arch,size', [('sngan', 32), ('snresnet', 64)])
-def test_critic_step_matches_tf_mirror(dev, arch, size):
+@pytest.mark.parametrize('arch,size,cl', [('sngan', 32, False), ('snresnet', 64, False),
+                                           ('snresnet', 64, True)])
+def test_critic_step_matches_tf_mirror(dev, arch, size, cl):
     from gan.core.smmd import SMMD
     torch.manual_seed(0)
     cfg = _cfg(architecture=arch, output_size=size, df_dim=16 if arch == 'snresnet' else 64,
                gf_dim=16 if arch == 'snresnet' else 64)
-    model = SMMD(cfg, device=dev)
+    model = SMMD(cfg, device=dev, channels_last=cl)
     mirror = _mirror_from(model)
+    if cl:      # the mirror runs the default layout
+        mirror.G.to(memory_format=torch.contiguous_format)
+        mirror.D.to(memory_format=torch.contiguous_format)
     g = torch.Generator().manual_seed(1)
     images = torch.rand(8, 3, size, size, generator=g)
     z = torch.empty(8, 128).uniform_(-1, 1, generator=g)
@@ -67,17 +71,16 @@ def test_critic_step_matches_tf_mirror(dev, arch, size):
     assert float(d_loss.detach()) == pytest.approx(float(ref_loss), rel=1e-3, abs=1e-6)
     flat = captured['g']
     gmax = max(float(rg.abs().max()) for rg in ref_grads)
-    o = 0
-    for p, rg in zip(model.d_vars, ref_grads):
-        n = p.numel()
-        got = flat[o:o + n].view_as(rg).numpy().astype(np.float64)
+    for i, (p, rg) in enumerate(zip(model.d_vars, ref_grads)):
+        o, n = model.d_optim.offsets[i], p.numel()
+        got = torch.as_strided(flat, p.shape, p.stride(), o).contiguous().view_as(rg)
+        got = got.numpy().astype(np.float64)
         ref = rg.numpy().astype(np.float64)
         # exact zeros (e.g. the output bias: RBF-MMD is translation invariant) are
         # rounding noise in both: absolute floor 1e-5 of the largest gradient
         tol = max(2e-3 * np.abs(ref).max(), 1e-5 * gmax) + 2e-3 * np.abs(ref)
         assert (np.abs(got - ref) <= tol + 1e-12).all(), (p.shape, np.abs(got - ref).max(),
                                                            np.abs(ref).max())
-        o += n
     # u advanced exactly as the reference's u.assign(u') (sn.py:39-46)
     for e, u in zip(model.sn_D.entries, mirror.us):
         np.testing.assert_allclose(e.u.cpu().numpy(), u.numpy()[0], rtol=1e-4, atol=1e-6)

@@ -115,3 +115,61 @@ def test_cpu_mirror_step_runs():
     X, Y = torch.randn(9, 1, dtype=torch.float64), torch.randn(7, 1, dtype=torch.float64)
     assert float(rbf_mmd2_tf(X, Y)) == pytest.approx(O.mmd2(O.kernel_spec('rbf'), X.numpy(),
                                                             Y.numpy()), rel=1e-10)
+
+
+def test_conv_second_order_rule_matches_autograd():
+    """convops.conv2d: value, first and second derivatives equal F.conv2d's
+    (CPU, float64) incl. the weight term of the double backward."""
+    from gan.core.convops import conv2d, mean_pool2
+    torch.manual_seed(0)
+    for stride, pad in ((1, 1), (2, 1), (1, 0)):
+        x = torch.randn(3, 4, 9, 9, dtype=torch.float64, requires_grad=True)
+        w = torch.randn(5, 4, 3, 3, dtype=torch.float64, requires_grad=True)
+        b = torch.randn(5, dtype=torch.float64, requires_grad=True)
+        outs = []
+        for fn in (lambda: conv2d(x, w, b, stride, pad),
+                   lambda: torch.nn.functional.conv2d(x, w, b, stride, pad)):
+            y = fn()
+            g, = torch.autograd.grad(torch.tanh(y).sum(), x, create_graph=True)
+            L = (g * g).sum() + y.pow(2).mean()
+            outs.append((y.detach(),) + torch.autograd.grad(L, (x, w, b)))
+        for a, c in zip(*outs):
+            assert torch.allclose(a, c, rtol=1e-9, atol=1e-10)
+    t = torch.randn(2, 3, 8, 6, dtype=torch.float64)
+    assert torch.allclose(mean_pool2(t), torch.nn.functional.avg_pool2d(t, 2))
+    assert torch.autograd.gradcheck(lambda a, c: conv2d(a, c, None, 1, 1),
+                                    (torch.randn(1, 2, 5, 5, dtype=torch.float64, requires_grad=True),
+                                     torch.randn(3, 2, 3, 3, dtype=torch.float64, requires_grad=True)))
+    assert torch.autograd.gradgradcheck(lambda a, c: conv2d(a, c, None, 2, 1),
+                                        (torch.randn(1, 2, 5, 5, dtype=torch.float64, requires_grad=True),
+                                         torch.randn(3, 2, 3, 3, dtype=torch.float64, requires_grad=True)))
+
+
+def test_input_grad_only_pass_keeps_second_order_exact():
+    """The Jacobian pass under input_grad_only skips weight gradients but the
+    double backward through it still yields the exact parameter gradient."""
+    from gan.core.convops import conv2d, input_grad_only
+    torch.manual_seed(1)
+    x = torch.randn(2, 3, 6, 6, dtype=torch.float64, requires_grad=True)
+    w1 = torch.randn(4, 3, 3, 3, dtype=torch.float64, requires_grad=True)
+    w2 = torch.randn(1, 4, 3, 3, dtype=torch.float64, requires_grad=True)
+    res = []
+    for ctxmgr, conv in ((input_grad_only, conv2d), (None, torch.nn.functional.conv2d)):
+        y = conv(torch.nn.functional.leaky_relu(conv(x, w1, None, 1, 1), 0.2), w2, None, 1, 1).sum()
+        if ctxmgr:
+            with ctxmgr():
+                g, = torch.autograd.grad(y, x, create_graph=True)
+        else:
+            g, = torch.autograd.grad(y, x, create_graph=True)
+        L = (g * g).sum() * y
+        res.append(torch.autograd.grad(L, (x, w1, w2)))
+    for a, b in zip(*res):
+        assert torch.allclose(a, b, rtol=1e-9, atol=1e-10)
+
+
+def test_mean_pool2_first_and_second_order():
+    from gan.core.convops import mean_pool2
+    x = torch.randn(2, 3, 6, 8, dtype=torch.float64, requires_grad=True)
+    assert torch.allclose(mean_pool2(x), torch.nn.functional.avg_pool2d(x, 2))
+    assert torch.autograd.gradcheck(mean_pool2, (x,))
+    assert torch.autograd.gradgradcheck(mean_pool2, (x,))
