@@ -34,6 +34,22 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
 BATCH = 64
 
 
+PMC_TRAFFIC = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', 'r01',
+                           'pmc_traffic.json')
+
+
+def pmc_traffic(entry):
+    """HBM bytes per call of a library entry point from the committed rocprofv3
+    PMC passes (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, tools/pmc_traffic.py,
+    same kernels and sizes via tools/hipbench.py), or None when not measured."""
+    try:
+        with open(PMC_TRAFFIC) as f:
+            rec = json.load(f).get(entry.split('[')[0])
+        return rec['traffic_bytes'] if rec else None
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def imagenet_config():
     """configs/imagenet_smmd.yml over the gan/main.py defaults."""
     from gan.main import default_flags
@@ -98,10 +114,18 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    # test hook: SMMD_DIST_BACKEND=gloo + SMMD_SAME_DEVICE=1 rehearses the N>1
+    # path with every rank on one GPU (RCCL needs one GPU per rank)
+    backend = os.environ.get('SMMD_DIST_BACKEND', 'nccl')
+    if os.environ.get('SMMD_SAME_DEVICE') == '1':
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
     if world > 1:
-        dist.init_process_group('nccl', device_id=dev)
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=dev)
+        else:
+            dist.init_process_group(backend)
     # MIOpen immediate mode: one kernel compile per conv config on a fresh box;
     # benchmark=True would compile every candidate solver (minutes per shape).
     torch.backends.cudnn.benchmark = False
@@ -156,10 +180,10 @@ def main():
         # sqsum pass reads g; update pass reads g, p, m, v and writes p, m, v
         'smmd_adam_flat[D]': model.d_optim.numel * 4 * 8,
         'smmd_adam_flat[G]': model.g_optim.numel * 4 * 8,
-        # P1 read W, P2 read W, P3 read W + write W_eff
-        'smmd_sn_power_iter': sn_kn * 4 * 4,
-        # A read G, W; B read G, write gW
-        'smmd_sn_weight_bwd': sn_kn * 4 * 4,
+        # one read of W + one write of W_eff (2 K N 4 B per iteration)
+        'smmd_sn_power_iter': sn_kn * 4 * 2,
+        # one read of G and W, one write of gW
+        'smmd_sn_weight_bwd': sn_kn * 4 * 3,
         # X, Y rows read, unit gradients written, sums
         'smmd_mmd2_fwd': 2 * m_all * 4 + 2 * BATCH * 4 + 8 * 4,
         'smmd_scaled_loss_fwd': BATCH * per_img * 4,
@@ -200,7 +224,7 @@ def main():
                    'miopen_winograd': bool(args.miopen_winograd)},
         'roofline': {'bound': 'hbm', 'kernel': dom, 'achieved': kernels[dom]['GB_s'],
                      'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': kernels[dom]['frac'],
-                     'traffic': None, 'avg_ms': kernels[dom]['avg_ms'],
+                     'traffic': pmc_traffic(dom), 'avg_ms': kernels[dom]['avg_ms'],
                      'algorithmic_bytes': kernels[dom]['bytes']},
         'mmd_kernel': {'kernel': 'smmd_mmd2_fwd (mmd2_fused_kernel<1,RBF>)',
                        'avg_ms': mk.get('avg_ms'), 'GB_s': mk.get('GB_s'),

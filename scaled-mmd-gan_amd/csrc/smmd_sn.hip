@@ -18,6 +18,9 @@
 // wave-instruction reads 1 KiB of one row.  All reductions have a fixed order.
 #include "smmd_common.hpp"
 
+#include <atomic>
+#include <stdlib.h>
+
 namespace smmd {
 
 constexpr int SN_TR = 64;      // tile rows
@@ -350,12 +353,386 @@ __global__ __launch_bounds__(256) void sn_bwd_b_kernel(SnTable t) {
 }
 
 // ---------------------------------------------------------------------------
+// Resident path: one cooperative launch per call.  Every workgroup (one per
+// CU, 1024 threads) loads its share of 32 x 256 tiles of every layer ONCE into
+// registers and keeps them across the phases of the power iteration, which
+// are separated by grid barriers:
+//
+//   A   resident tiles -> column partials (LDS reduce of the 16 waves) -> P1
+//   A2  P1 -> v_raw, 256-column chunks spread over the grid
+//   B   resident tiles . v_raw -> per-row partials q2
+//   R   one workgroup per layer: the sn_r2 epilogue (norms, v, u', sigma)
+//   C   resident tiles -> W_eff = (W / sigma) * s
+//
+// HBM traffic: one read of W and one write of W_eff (8 B per weight) instead
+// of the three reads + one write of the P1/P2/P3 launch set.  The backward
+// reads G and W once (the <G, W> partials), keeps G, and writes gW after one
+// barrier: 12 B per weight instead of 20.
+// ---------------------------------------------------------------------------
+constexpr int SR_TR = 32;            // tile rows (thread: rows w and w + 16)
+constexpr int SR_THREADS = 1024;
+constexpr int SR_TMAX = 8;           // resident tiles per workgroup
+constexpr int SR_GROUP = 4;          // tiles per LDS reduction round (64 KiB)
+constexpr unsigned SR_SPIN_LIMIT = 1u << 22;   // ~0.2 s of polling, then give up
+
+struct GridBarrier {
+    unsigned count;   // arrivals of the current barrier (returns to 0)
+    unsigned gen;     // completed barriers (monotone, wraps)
+    unsigned err;     // set when a barrier timed out (grid not co-resident)
+    unsigned pad;
+};
+
+// Self-resetting grid barrier for a cooperative (co-resident) launch.  The
+// last arriver resets `count` and bumps `gen`; the others poll `gen`.  A
+// bounded poll guarantees termination even if co-residency were violated.
+__device__ __forceinline__ void grid_sync(GridBarrier *b, unsigned nblocks) {
+    // every wave's global stores must have reached L2 before thread 0 writes
+    // the L2 back (__syncthreads alone does not wait for vmcnt)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned g = __hip_atomic_load(&b->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned old =
+            __hip_atomic_fetch_add(&b->count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == nblocks - 1) {
+            __hip_atomic_store(&b->count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(&b->gen, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            unsigned spins = 0;
+            while (__hip_atomic_load(&b->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > SR_SPIN_LIMIT) {
+                    __hip_atomic_store(&b->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    __syncthreads();
+}
+
+struct SrTile {
+    int layer, rt, ct;
+};
+
+__device__ __forceinline__ SrTile sr_tile(const SnTable &t, int tile) {
+    SrTile o;
+    o.layer = find_layer(t, tile);
+    const int lt = tile - t.L[o.layer].tile_begin;
+    const int nct = t.L[o.layer].nct;
+    o.rt = lt / nct;
+    o.ct = lt - o.rt * nct;
+    return o;
+}
+
+// raw buffer over [p, p + bytes): out-of-range loads return 0 without a branch
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sr_rsrc(const void *p, unsigned bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes,
+                                             0x00020000);
+}
+
+__device__ __forceinline__ float4 sr_bload4(__amdgpu_buffer_rsrc_t r, int elem) {
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, elem * 4, 0, 0);
+    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
+                       __uint_as_float(v.w));
+}
+
+// rows r0 and r0 + 16 of a tile, 4 columns at c0 (zero outside the matrix).
+// vec layers (K % 4 == 0): two unconditional buffer loads (rows >= N are out of
+// range and read 0; a float4 never straddles a row end), columns >= K masked.
+__device__ __forceinline__ void sr_load(const float *__restrict__ base, int N, int K, int vec,
+                                        int r0, int c0, float4 &a, float4 &b) {
+    const int r1 = r0 + 16;
+    if (vec) {
+        const __amdgpu_buffer_rsrc_t rs = sr_rsrc(base, (unsigned)N * (unsigned)K * 4u);
+        const float4 x = sr_bload4(rs, r0 * K + c0), y = sr_bload4(rs, r1 * K + c0);
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+        a = (c0 < K) ? x : z;
+        b = (c0 < K) ? y : z;
+        return;
+    }
+    float x[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (c0 + k < K) {
+            if (r0 < N) x[k] = base[(size_t)r0 * K + c0 + k];
+            if (r1 < N) x[4 + k] = base[(size_t)r1 * K + c0 + k];
+        }
+    }
+    a = make_float4(x[0], x[1], x[2], x[3]);
+    b = make_float4(x[4], x[5], x[6], x[7]);
+}
+
+__device__ __forceinline__ void sr_store(float *__restrict__ base, int N, int K, int vec, int r,
+                                         int c0, float4 o) {
+    if (r >= N) return;
+    float *p = base + (size_t)r * K + c0;
+    if (vec && c0 + 3 < K) {
+        *reinterpret_cast<float4 *>(p) = o;
+        return;
+    }
+    if (c0 + 0 < K) p[0] = o.x;
+    if (c0 + 1 < K) p[1] = o.y;
+    if (c0 + 2 < K) p[2] = o.z;
+    if (c0 + 3 < K) p[3] = o.w;
+}
+
+// the sn_r2 epilogue for layer L, run by one 1024-thread workgroup
+__device__ void sr_layer_epilogue(const SnTable &t, const SnLayerDev &L, int last_iter,
+                                  double *red) {
+    const int tid = threadIdx.x;
+    double a = 0.0;
+    for (int k = tid; k < L.K; k += 1024) {
+        const double x = (double)L.vraw[k];
+        a += x * x;
+    }
+    const float nv = (float)sqrt(block_sum<16>(a, red)) + t.eps;     // sn.py:13
+    for (int k = tid; k < L.K; k += 1024) L.v[k] = L.vraw[k] / nv;
+    double b = 0.0;
+    for (int n = tid; n < L.N; n += 1024) {
+        float s0 = 0.f, s1 = 0.f;
+        int c = 0;
+        for (; c + 1 < L.nct; c += 2) {
+            s0 += L.q2[(size_t)c * L.N + n];
+            s1 += L.q2[(size_t)(c + 1) * L.N + n];
+        }
+        if (c < L.nct) s0 += L.q2[(size_t)c * L.N + n];
+        const float ur = (s0 + s1) / nv;
+        L.ucur[n] = ur;
+        b += (double)ur * (double)ur;
+    }
+    const float nu = (float)sqrt(block_sum<16>(b, red)) + t.eps;
+    double sg = 0.0;
+    for (int n = tid; n < L.N; n += 1024) {
+        const float ur = L.ucur[n];
+        const float un = ur / nu;                               // u' = l2n(v W)
+        sg += (double)ur * (double)un;                          // sigma, sn.py:42
+        L.ucur[n] = un;
+        if (t.update_u && last_iter) L.u[n] = un;
+    }
+    sg = block_sum<16>(sg, red);
+    if (tid == 0) L.sigma[0] = (float)sg;
+}
+
+// tile j of this block (strided over the grid), or false past the end
+#define SR_FOR_TILES(j, q, L)                                                    \
+    for (int j = 0; j < SR_TMAX; ++j)                                            \
+        if (const int tile_ = blockIdx.x + j * gridDim.x; tile_ < t.total_tiles) \
+            if (const SrTile q = sr_tile(t, tile_); true)                        \
+                if (const SnLayerDev &L = t.L[q.layer]; true)
+
+__global__ __launch_bounds__(SR_THREADS) void sn_resident_kernel(SnTable t, GridBarrier *bar,
+                                                                 int num_iters) {
+    const unsigned G = gridDim.x;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    __shared__ float red[SR_GROUP][16][SN_TC];
+    __shared__ double dred[16];
+
+    float4 wa[SR_TMAX], wb[SR_TMAX];
+#pragma unroll
+    for (int j = 0; j < SR_TMAX; ++j) wa[j] = wb[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    SR_FOR_TILES(j, q, L) {
+        sr_load(L.W, L.N, L.K, L.vec, q.rt * SR_TR + w, q.ct * SN_TC + lane * 4, wa[j], wb[j]);
+    }
+
+    for (int it = 0; it < num_iters; ++it) {
+        // ---- A: column partials of u^T W over the tile's 32 rows -> P1
+#pragma unroll
+        for (int g0 = 0; g0 < SR_TMAX; g0 += SR_GROUP) {
+#pragma unroll
+            for (int jj = 0; jj < SR_GROUP && g0 + jj < SR_TMAX; ++jj) {
+                const int j = g0 + jj;
+                const int tile = blockIdx.x + j * G;
+                if (tile >= t.total_tiles) break;
+                const SrTile q = sr_tile(t, tile);
+                const SnLayerDev &L = t.L[q.layer];
+                const float *uin = (it == 0) ? L.u : L.ucur;
+                const int r0 = q.rt * SR_TR + w, r1 = r0 + 16;
+                const float u0 = (r0 < L.N) ? uin[r0] : 0.f;
+                const float u1 = (r1 < L.N) ? uin[r1] : 0.f;
+                float4 acc;
+                acc.x = fmaf(u1, wb[j].x, u0 * wa[j].x);
+                acc.y = fmaf(u1, wb[j].y, u0 * wa[j].y);
+                acc.z = fmaf(u1, wb[j].z, u0 * wa[j].z);
+                acc.w = fmaf(u1, wb[j].w, u0 * wa[j].w);
+                *reinterpret_cast<float4 *>(&red[jj][w][lane * 4]) = acc;
+            }
+            __syncthreads();
+            {
+                const int jj = threadIdx.x >> 8, c = threadIdx.x & 255;
+                const int tile = blockIdx.x + (g0 + jj) * G;
+                if (g0 + jj < SR_TMAX && tile < t.total_tiles) {
+                    const SrTile q = sr_tile(t, tile);
+                    const SnLayerDev &L = t.L[q.layer];
+                    const int col = q.ct * SN_TC + c;
+                    float s = 0.f;
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) s += red[jj][i][c];
+                    if (col < L.K) L.p1[(size_t)q.rt * L.K + col] = s;
+                }
+            }
+            __syncthreads();
+        }
+        grid_sync(bar, G);
+
+        // ---- A2: v_raw = sum over row tiles of P1; 256-column chunks, 4 per block
+        for (int qi = blockIdx.x * 4 + (threadIdx.x >> 8); ; qi += G * 4) {
+            int l = 0, cb = 0;
+            for (; l < t.n_layers; ++l) {
+                if (qi < cb + t.L[l].nct) break;
+                cb += t.L[l].nct;
+            }
+            if (l >= t.n_layers) break;
+            const SnLayerDev &L = t.L[l];
+            const int col = (qi - cb) * SN_TC + (threadIdx.x & 255);
+            if (col < L.K) {
+                float s = 0.f;
+#pragma unroll 8
+                for (int r = 0; r < L.nrt; ++r) s += L.p1[(size_t)r * L.K + col];
+                L.vraw[col] = s;
+            }
+        }
+        grid_sync(bar, G);
+
+        // ---- B: per-row partial dots with v_raw -> q2[ct][row]
+#pragma unroll
+        SR_FOR_TILES(j, q, L) {
+            const int c0 = q.ct * SN_TC + lane * 4;
+            const float v0 = (c0 + 0 < L.K) ? L.vraw[c0 + 0] : 0.f;
+            const float v1 = (c0 + 1 < L.K) ? L.vraw[c0 + 1] : 0.f;
+            const float v2 = (c0 + 2 < L.K) ? L.vraw[c0 + 2] : 0.f;
+            const float v3 = (c0 + 3 < L.K) ? L.vraw[c0 + 3] : 0.f;
+            float d0 = fmaf(v3, wa[j].w, fmaf(v2, wa[j].z, fmaf(v1, wa[j].y, v0 * wa[j].x)));
+            float d1 = fmaf(v3, wb[j].w, fmaf(v2, wb[j].z, fmaf(v1, wb[j].y, v0 * wb[j].x)));
+            d0 = wave_sum(d0);
+            d1 = wave_sum(d1);
+            if (lane == 0) {
+                const int r0 = q.rt * SR_TR + w, r1 = r0 + 16;
+                float *dst = L.q2 + (size_t)q.ct * L.N;
+                if (r0 < L.N) dst[r0] = d0;
+                if (r1 < L.N) dst[r1] = d1;
+            }
+        }
+        grid_sync(bar, G);
+
+        // ---- R: norms, v, u', sigma (one workgroup per layer)
+        const int last = (it == num_iters - 1);
+        for (int l = blockIdx.x; l < t.n_layers; l += G) sr_layer_epilogue(t, t.L[l], last, dred);
+        grid_sync(bar, G);
+    }
+
+    // ---- C: W_eff = (W / sigma) * s from the resident tiles
+#pragma unroll
+    SR_FOR_TILES(j, q, L) {
+        if (!L.W_eff) continue;
+        const float sigma = L.sigma[0];
+        const float s = L.s ? L.s[0] : 1.f;
+        const int r0 = q.rt * SR_TR + w, c0 = q.ct * SN_TC + lane * 4;
+        float4 o;
+        o.x = (wa[j].x / sigma) * s; o.y = (wa[j].y / sigma) * s;
+        o.z = (wa[j].z / sigma) * s; o.w = (wa[j].w / sigma) * s;
+        sr_store(L.W_eff, L.N, L.K, L.vec, r0, c0, o);
+        o.x = (wb[j].x / sigma) * s; o.y = (wb[j].y / sigma) * s;
+        o.z = (wb[j].z / sigma) * s; o.w = (wb[j].w / sigma) * s;
+        sr_store(L.W_eff, L.N, L.K, L.vec, r0 + 16, c0, o);
+    }
+}
+
+// backward: <G, W> partial per tile -> barrier -> per-layer sum (fixed order,
+// every block redoes it for its layers) -> gW from the resident G tiles
+__global__ __launch_bounds__(SR_THREADS) void sn_resident_bwd_kernel(SnTable t, GridBarrier *bar) {
+    const unsigned G = gridDim.x;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    __shared__ float dsh[SR_TMAX][16];
+    __shared__ float dlay[SR_TMAX];
+
+    float4 ga[SR_TMAX], gb[SR_TMAX];
+#pragma unroll
+    for (int j = 0; j < SR_TMAX; ++j) ga[j] = gb[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    SR_FOR_TILES(j, q, L) {
+        const int r0 = q.rt * SR_TR + w, c0 = q.ct * SN_TC + lane * 4;
+        float4 wa, wb;
+        sr_load(L.W, L.N, L.K, L.vec, r0, c0, wa, wb);
+        sr_load(L.G, L.N, L.K, L.vec, r0, c0, ga[j], gb[j]);
+        float acc = 0.f;
+        acc = fmaf(ga[j].x, wa.x, acc); acc = fmaf(ga[j].y, wa.y, acc);
+        acc = fmaf(ga[j].z, wa.z, acc); acc = fmaf(ga[j].w, wa.w, acc);
+        acc = fmaf(gb[j].x, wb.x, acc); acc = fmaf(gb[j].y, wb.y, acc);
+        acc = fmaf(gb[j].z, wb.z, acc); acc = fmaf(gb[j].w, wb.w, acc);
+        acc = wave_sum(acc);
+        if (lane == 0) dsh[j][w] = acc;
+    }
+    __syncthreads();
+    // wave j publishes tile j's partial (sr_tile needs a wave-uniform tile)
+    if (w < SR_TMAX) {
+        const int j = w;
+        const int tile = blockIdx.x + j * G;
+        if (tile < t.total_tiles && lane == 0) {
+            const SrTile q = sr_tile(t, tile);
+            float s = 0.f;
+            for (int i = 0; i < 16; ++i) s += dsh[j][i];
+            t.L[q.layer].dotp[tile - t.L[q.layer].tile_begin] = s;
+        }
+    }
+    grid_sync(bar, G);
+
+    // per-layer <G, W>: wave j sums the dotp of tile j's layer (fixed order)
+    if (w < SR_TMAX) {
+        const int j = w;
+        const int tile = blockIdx.x + j * G;
+        if (tile < t.total_tiles) {
+            const SrTile q = sr_tile(t, tile);
+            const SnLayerDev &L = t.L[q.layer];
+            const int nt = L.nrt * L.nct;
+            double d = 0.0;
+            for (int i = lane; i < nt; i += 64) d += (double)L.dotp[i];
+            d = wave_sum(d);
+            if (lane == 0) dlay[j] = (float)d;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    SR_FOR_TILES(j, q, L) {
+        const float d = dlay[j];                      // <G, W>
+        const float sigma = L.sigma[0];
+        const float s = L.s ? L.s[0] : 1.f;
+        const int r0 = q.rt * SR_TR + w, c0 = q.ct * SN_TC + lane * 4;
+        if (q.rt == 0 && q.ct == 0 && threadIdx.x == 0 && L.gs) L.gs[0] = d / sigma;
+        const float coef = (s * d) / (sigma * sigma);
+        float vv[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) vv[k] = (c0 + k < L.K) ? L.v[c0 + k] : 0.f;
+        const float cu0 = (r0 < L.N) ? coef * L.ucur[r0] : 0.f;
+        const float cu1 = (r0 + 16 < L.N) ? coef * L.ucur[r0 + 16] : 0.f;
+        float4 o;
+        o.x = (s * ga[j].x) / sigma - cu0 * vv[0];
+        o.y = (s * ga[j].y) / sigma - cu0 * vv[1];
+        o.z = (s * ga[j].z) / sigma - cu0 * vv[2];
+        o.w = (s * ga[j].w) / sigma - cu0 * vv[3];
+        sr_store(L.gW, L.N, L.K, L.vec, r0, c0, o);
+        o.x = (s * gb[j].x) / sigma - cu1 * vv[0];
+        o.y = (s * gb[j].y) / sigma - cu1 * vv[1];
+        o.z = (s * gb[j].z) / sigma - cu1 * vv[2];
+        o.w = (s * gb[j].w) / sigma - cu1 * vv[3];
+        sr_store(L.gW, L.N, L.K, L.vec, r0 + 16, c0, o);
+    }
+}
+#undef SR_FOR_TILES
+
+// ---------------------------------------------------------------------------
 // host side: workspace carve and launch sets
 // ---------------------------------------------------------------------------
 static int ceil_div(int a, int b) { return (a + b - 1) / b; }
 
 static size_t layer_ws_bytes(int N, int K) {
-    const int nrt = ceil_div(N, SN_TR), nct = ceil_div(K, SN_TC);
+    // P1 / dotp sized for the finer (resident) row tiling, which also covers SN_TR
+    const int nrt = ceil_div(N, SR_TR), nct = ceil_div(K, SN_TC);
     size_t b = 0;
     b += align_up((size_t)nrt * K * 4, 256);   // p1
     b += align_up((size_t)K * 4, 256);         // vraw
@@ -366,7 +743,7 @@ static size_t layer_ws_bytes(int N, int K) {
 }
 
 static bool build_table(const smmd_sn_layer *layers, int first, int count, char *ws,
-                        SnTable &t) {
+                        SnTable &t, int tile_rows) {
     memset(&t, 0, sizeof(t));
     t.n_layers = count;
     int tiles = 0;
@@ -388,7 +765,7 @@ static bool build_table(const smmd_sn_layer *layers, int first, int count, char 
         L.gs = src.gs;
         L.N = src.N;
         L.K = src.K;
-        L.nrt = ceil_div(src.N, SN_TR);
+        L.nrt = ceil_div(src.N, tile_rows);
         L.nct = ceil_div(src.K, SN_TC);
         L.tile_begin = tiles;
         tiles += L.nrt * L.nct;
@@ -396,15 +773,54 @@ static bool build_table(const smmd_sn_layer *layers, int first, int count, char 
                              (uintptr_t)(src.G ? src.G : src.W) | (uintptr_t)(src.gW ? src.gW : src.W);
         L.vec = (src.K % 4 == 0) && (al % 16 == 0);
         char *p = ws + off;
-        L.p1 = (float *)p;   p += align_up((size_t)L.nrt * L.K * 4, 256);
+        const int nrt_max = ceil_div(src.N, SR_TR);
+        L.p1 = (float *)p;   p += align_up((size_t)nrt_max * L.K * 4, 256);
         L.vraw = (float *)p; p += align_up((size_t)L.K * 4, 256);
         L.q2 = (float *)p;   p += align_up((size_t)L.nct * L.N * 4, 256);
         L.ucur = (float *)p; p += align_up((size_t)L.N * 4, 256);
-        L.dotp = (float *)p; p += align_up((size_t)L.nrt * L.nct * 4, 256);
+        L.dotp = (float *)p; p += align_up((size_t)nrt_max * L.nct * 4, 256);
         off += layer_ws_bytes(L.N, L.K);
     }
     t.total_tiles = tiles;
     return true;
+}
+
+static bool resident_enabled() {
+    const char *e = getenv("SMMD_SN_RESIDENT");
+    return !(e && e[0] == '0');
+}
+
+// co-resident 1024-thread blocks of a resident kernel on the current device
+// (cached per device: the only host state the library keeps)
+template <typename K>
+static int coresident_blocks(K kernel, int slot) {
+    static std::atomic<int> cache[2][64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+    int v = cache[slot][dev].load(std::memory_order_relaxed);
+    if (v) return v;
+    int cus = 0, per_cu = 0, coop = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, SR_THREADS, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    v = coop ? cus * per_cu : 0;
+    cache[slot][dev].store(v > 0 ? v : -1, std::memory_order_relaxed);
+    return v > 0 ? v : -1;
+}
+
+// grid for the resident path, or 0 when it does not apply (too many layers
+// for one table, more tiles than the registers of the co-resident grid hold)
+template <typename K>
+static int resident_grid(K kernel, int slot, int n_layers, const SnTable &t) {
+    if (n_layers > SN_CHUNK || !resident_enabled()) return 0;
+    const int cap = coresident_blocks(kernel, slot);
+    if (cap <= 0) return 0;
+    const int g = t.total_tiles < cap ? t.total_tiles : cap;
+    if ((long)g * SR_TMAX < (long)t.total_tiles) return 0;
+    return g;
 }
 
 }  // namespace smmd
@@ -429,10 +845,25 @@ smmd_status smmd_sn_power_iter(const smmd_sn_layer *layers, int n_layers, int nu
         if (!layers[i].u || !layers[i].v || !layers[i].sigma) return SMMD_EINVAL;
     if (!ws || ws_bytes < smmd_sn_workspace_bytes(layers, n_layers)) return SMMD_EWORKSPACE;
     hipStream_t s = (hipStream_t)stream;
+    {
+        SnTable t;
+        if (n_layers <= SN_CHUNK) {
+            if (!build_table(layers, 0, n_layers, (char *)ws + 256, t, SR_TR)) return SMMD_EINVAL;
+            const int g = resident_grid(sn_resident_kernel, 0, n_layers, t);
+            if (g > 0) {
+                t.eps = eps;
+                t.update_u = update_u ? 1 : 0;
+                GridBarrier *bar = (GridBarrier *)ws;
+                void *args[] = {&t, &bar, &num_iters};
+                return hip_status(hipLaunchCooperativeKernel((const void *)sn_resident_kernel,
+                                                             dim3(g), dim3(SR_THREADS), args, 0, s));
+            }
+        }
+    }
     for (int first = 0; first < n_layers; first += SN_CHUNK) {
         const int count = (n_layers - first < SN_CHUNK) ? n_layers - first : SN_CHUNK;
         SnTable t;
-        if (!build_table(layers, first, count, (char *)ws + 256, t)) return SMMD_EINVAL;
+        if (!build_table(layers, first, count, (char *)ws + 256, t, SN_TR)) return SMMD_EINVAL;
         t.eps = eps;
         t.update_u = update_u ? 1 : 0;
         for (int it = 0; it < num_iters; ++it) {
@@ -458,10 +889,21 @@ smmd_status smmd_sn_weight_bwd(const smmd_sn_layer *layers, int n_layers, void *
         if (!layers[i].G || !layers[i].gW || !layers[i].v || !layers[i].sigma) return SMMD_EINVAL;
     if (!ws || ws_bytes < smmd_sn_workspace_bytes(layers, n_layers)) return SMMD_EWORKSPACE;
     hipStream_t s = (hipStream_t)stream;
+    if (n_layers <= SN_CHUNK) {
+        SnTable t;
+        if (!build_table(layers, 0, n_layers, (char *)ws + 256, t, SR_TR)) return SMMD_EINVAL;
+        const int g = resident_grid(sn_resident_bwd_kernel, 1, n_layers, t);
+        if (g > 0) {
+            GridBarrier *bar = (GridBarrier *)ws;
+            void *args[] = {&t, &bar};
+            return hip_status(hipLaunchCooperativeKernel((const void *)sn_resident_bwd_kernel,
+                                                         dim3(g), dim3(SR_THREADS), args, 0, s));
+        }
+    }
     for (int first = 0; first < n_layers; first += SN_CHUNK) {
         const int count = (n_layers - first < SN_CHUNK) ? n_layers - first : SN_CHUNK;
         SnTable t;
-        if (!build_table(layers, first, count, (char *)ws + 256, t)) return SMMD_EINVAL;
+        if (!build_table(layers, first, count, (char *)ws + 256, t, SN_TR)) return SMMD_EINVAL;
         hipLaunchKernelGGL(sn_bwd_a_kernel, dim3(t.total_tiles), dim3(256), 0, s, t);
         hipLaunchKernelGGL(sn_bwd_b_kernel, dim3(t.total_tiles), dim3(256), 0, s, t);
         smmd_status st = last_launch_status();

@@ -171,35 +171,114 @@ def test_witness_second_order(dev, name):
 
 SN_SHAPES = [(64, 27), (128, 576), (256, 1152), (1, 1024), (1024, 4608), (7, 13), (130, 300)]
 
+# smmd_sn_power_iter / smmd_sn_weight_bwd have two implementations: the
+# resident cooperative kernel (one launch, W held in registers) and the
+# multi-pass launch set it falls back to; SMMD_SN_RESIDENT=0 forces the latter.
+SN_PATHS = ['resident', 'multipass']
 
-def test_sn_bank_vs_oracle(dev):
+
+def _sn_path(monkeypatch, path):
+    monkeypatch.setenv('SMMD_SN_RESIDENT', '1' if path == 'resident' else '0')
+
+
+def _sn_bank(dev, shapes, seed, num_iters=1):
     from gan.core import sn
-    rng = np.random.default_rng(2)
+    rng = np.random.default_rng(seed)
     mods = []
-    for N, K in SN_SHAPES:
+    for N, K in shapes:
         m = torch.nn.Module()
         m.weight = torch.nn.Parameter(torch.tensor(rng.standard_normal((N, K)) * 0.05,
                                                    dtype=torch.float32, device=dev))
         m.sn_scale = torch.nn.Parameter(torch.tensor([1.3], device=dev))
         mods.append(m)
-    bank = sn.SpectralNormBank(mods)
+    return mods, sn.SpectralNormBank(mods, num_iters=num_iters), rng
+
+
+def _check_sn(mods, bank, u0, outs, Gs, num_iters=1):
+    for i, (m, e) in enumerate(zip(mods, bank.entries)):
+        W = m.weight.detach().cpu().numpy().astype(np.float64)
+        sigma, u1, v1 = O.spectral_norm_rows(W, u0[i], num_iters)
+        _close(e.sigma.item(), sigma, 0, 1e-4, 'sigma %d' % i)
+        _close(e.u.cpu().numpy(), u1, 1e-6, 1e-4, 'u %d' % i)
+        _close(e.v.cpu().numpy(), v1, 1e-6, 1e-4, 'v %d' % i)
+        weff = W / sigma * 1.3
+        _close(outs[i].detach().cpu().numpy(), weff, 1e-6 * np.abs(weff).max(), 1e-4, 'Weff')
+        if Gs is None:
+            continue
+        gW, gs = O.sn_weight_backward(W, 1.3, sigma, u1, v1, Gs[i])
+        _close(m.weight.grad.cpu().numpy(), gW, 1e-4 * np.abs(gW).max(), 1e-3, 'gW %d' % i)
+        _close(m.sn_scale.grad.item(), gs, 1e-4 * abs(gs), 1e-3, 'gs %d' % i)
+
+
+@pytest.mark.parametrize('path', SN_PATHS)
+def test_sn_bank_vs_oracle(dev, monkeypatch, path):
+    _sn_path(monkeypatch, path)
+    mods, bank, rng = _sn_bank(dev, SN_SHAPES, 2)
     u0 = [e.u.cpu().numpy().astype(np.float64) for e in bank.entries]
     outs = bank.refresh(update_u=True)
     Gs = [rng.standard_normal((N, K)) for N, K in SN_SHAPES]
     loss = sum((o * torch.tensor(G, device=dev, dtype=torch.float32)).sum()
                for o, G in zip(outs, Gs))
     loss.backward()
-    for i, (m, e) in enumerate(zip(mods, bank.entries)):
-        W = m.weight.detach().cpu().numpy().astype(np.float64)
-        sigma, u1, v1 = O.spectral_norm_rows(W, u0[i])
-        _close(e.sigma.item(), sigma, 0, 1e-4, 'sigma %d' % i)
-        _close(e.u.cpu().numpy(), u1, 1e-6, 1e-4, 'u %d' % i)
-        _close(e.v.cpu().numpy(), v1, 1e-6, 1e-4, 'v %d' % i)
-        weff = W / sigma * 1.3
-        _close(outs[i].detach().cpu().numpy(), weff, 1e-6 * np.abs(weff).max(), 1e-4, 'Weff')
-        gW, gs = O.sn_weight_backward(W, 1.3, sigma, u1, v1, Gs[i])
-        _close(m.weight.grad.cpu().numpy(), gW, 1e-4 * np.abs(gW).max(), 1e-3, 'gW %d' % i)
-        _close(m.sn_scale.grad.item(), gs, 1e-4 * abs(gs), 1e-3, 'gs %d' % i)
+    _check_sn(mods, bank, u0, outs, Gs)
+
+
+@pytest.mark.parametrize('path', SN_PATHS)
+def test_sn_num_iters(dev, monkeypatch, path):
+    """num_iters > 1 (sn.py:24-35): the resident kernel loops its phases with
+    W still in registers."""
+    _sn_path(monkeypatch, path)
+    shapes = [(64, 27), (256, 1152), (33, 70)]
+    mods, bank, rng = _sn_bank(dev, shapes, 5, num_iters=3)
+    u0 = [e.u.cpu().numpy().astype(np.float64) for e in bank.entries]
+    outs = bank.refresh(update_u=True)
+    _check_sn(mods, bank, u0, outs, None, num_iters=3)
+
+
+def test_sn_paths_agree_and_barrier_state(dev, monkeypatch):
+    """Both implementations give the same sigma/W_eff to fp32 rounding on the
+    SNResNet-64 critic shapes; after many resident launches the grid barrier
+    in the workspace header is back at rest (count 0, no timeout flag) with
+    exactly 4 barriers per power iteration and 1 per backward."""
+    from gan.core.architecture import SNResNetDiscriminator
+    from gan.core.snops import sn_modules
+    D = SNResNetDiscriminator(64, 1, False, with_sn=True, with_learnable_sn_scale=True)
+    shapes = [(m.weight.shape[0], m.weight[0].numel()) for m in sn_modules(D)]
+    assert sum(N * K for N, K in shapes) > 10_000_000          # SURVEY 8a a7: 10.10 M
+    res = {}
+    for path in SN_PATHS:
+        _sn_path(monkeypatch, path)
+        mods, bank, rng = _sn_bank(dev, shapes, 11)
+        hdr0 = bank.ws[:16].view(torch.int32).clone()
+        calls = 20
+        for _ in range(calls):
+            outs = bank.refresh(update_u=False)
+            G = [torch.ones_like(o) for o in outs]
+            torch.autograd.backward(outs, G)
+        torch.cuda.synchronize()
+        hdr = bank.ws[:16].view(torch.int32).cpu().tolist()
+        if path == 'resident':
+            assert hdr[0] == 0, hdr            # count back at rest
+            assert hdr[2] == 0, hdr            # no barrier timed out
+            assert hdr[1] - int(hdr0[1]) == calls * (4 + 1), hdr
+        res[path] = (bank.sigmas().cpu().numpy(), [o.detach().cpu().numpy() for o in outs],
+                     [m.weight.grad.cpu().numpy() for m in mods])
+    a, b = res['resident'], res['multipass']
+    _close(a[0], b[0], 0, 2e-6, 'sigma resident vs multipass')
+    for i in range(len(shapes)):
+        _close(a[1][i], b[1][i], 1e-7 * np.abs(b[1][i]).max(), 2e-6, 'Weff %d' % i)
+        _close(a[2][i], b[2][i], 1e-6 * np.abs(b[2][i]).max(), 1e-5, 'gW %d' % i)
+
+
+def test_sn_over_resident_capacity(dev, monkeypatch):
+    """More tiles than the co-resident grid holds in registers: the call falls
+    back to the multi-pass launch set and stays correct."""
+    _sn_path(monkeypatch, 'resident')
+    shapes = [(2048, 9216), (64, 27)]          # 2 * 64 * 36 + 1 tiles of 32 x 256 > 8 * 256
+    mods, bank, rng = _sn_bank(dev, shapes, 4)
+    u0 = [e.u.cpu().numpy().astype(np.float64) for e in bank.entries]
+    outs = bank.refresh(update_u=True)
+    _check_sn(mods, bank, u0, outs, None)
 
 
 def test_sn_reference_layout(dev):

@@ -1,0 +1,88 @@
+"""Library-only microbenchmark: the libsmmd_hip launches of one SNResNet-64
+SMMD training step at bench.py's sizes, without the convolutions.
+
+    python tools/hipbench.py [--iters 200] [--json out.json]
+
+Times each entry point with HIP events on the compute stream (mean over
+iterations after warm-up) and reports algorithmic GB/s and the fraction of the
+8 TB/s HBM peak.  Used for kernel A/B work and for the PMC (FETCH_SIZE /
+WRITE_SIZE) passes, which crash the profiler when MIOpen is in the process.
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, 'scaled-mmd-gan_amd')):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import torch  # noqa: E402
+
+PEAK = 8000.0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--iters', type=int, default=200)
+    ap.add_argument('--json', default='')
+    ap.add_argument('--batch', type=int, default=64)
+    args = ap.parse_args()
+    from gan.core import _lib, mmd, ops
+    from gan.core.architecture import SNResNetDiscriminator
+    from gan.core.optim import FlatAdam
+    from gan.core.sn import SpectralNormBank
+    from gan.core.snops import sn_modules
+    dev = torch.device('cuda:0')
+    torch.manual_seed(0)
+    D = SNResNetDiscriminator(64, 1, False, with_sn=True, with_learnable_sn_scale=True,
+                              input_size=64).to(dev)
+    bank = SpectralNormBank(sn_modules(D))
+    opt = FlatAdam([p for p in D.parameters() if p.requires_grad], 2e-4, name='D')
+    Gs = [torch.randn_like(e.weight) for e in bank.entries]
+    B = args.batch
+    X = torch.randn(B, 1, device=dev, requires_grad=True)
+    Y = torch.randn(B, 1, device=dev, requires_grad=True)
+    jac = torch.randn(1, B, 3, 64, 64, device=dev, requires_grad=True)
+    for p in opt.params:
+        p.grad.normal_()
+
+    def one():
+        outs = bank.refresh(update_u=True)
+        torch.autograd.backward(outs, Gs)
+        opt.step()
+        m2 = mmd.mmd2_fused(X, Y, 'rbf')
+        g, _ = ops.scaled_loss(m2, jac, None, sc=10.0)
+        g.backward()
+
+    for _ in range(20):
+        one()
+    torch.cuda.synchronize()
+    _lib.reset_timing()
+    _lib.enable_timing(True)
+    for _ in range(args.iters):
+        one()
+    _lib.enable_timing(False)
+    tm = _lib.timing_ms()
+    kn = sum(e.N * e.K for e in bank.entries)
+    alg = {'smmd_sn_power_iter': kn * 4 * 2, 'smmd_sn_weight_bwd': kn * 4 * 3,
+           'smmd_adam_flat[D]': opt.numel * 4 * 8,
+           'smmd_mmd2_fwd': 2 * B * 4 * 2 + 32,
+           'smmd_scaled_loss_fwd': B * 3 * 64 * 64 * 4,
+           'smmd_scaled_loss_bwd': 2 * B * 3 * 64 * 64 * 4}
+    res = {}
+    for k, (n, ms) in sorted(tm.items()):
+        b = alg.get(k)
+        res[k] = {'calls': n, 'avg_us': round(ms * 1e3, 2)}
+        if b:
+            gbs = b / (ms * 1e-3) / 1e9
+            res[k].update(bytes=b, GB_s=round(gbs, 1), frac=round(gbs / PEAK, 4))
+    print(json.dumps(res, indent=1))
+    if args.json:
+        with open(args.json, 'w') as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,61 @@
+"""Per-launch HBM traffic of the libsmmd_hip kernels from rocprofv3 PMC passes.
+
+    python tools/pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> [out.json]
+
+FETCH_SIZE and WRITE_SIZE are in KB.  On gfx950 FETCH_SIZE reports exactly
+half of the bytes of a wide coalesced streaming read (MI355X_MICROARCH.md,
+HBM section), so read bytes = 2 * FETCH_SIZE * 1024; WRITE_SIZE is exact for
+16-B-per-lane streaming stores.  Kernels are grouped per library entry point
+(the launches one call issues) and averaged per call.
+"""
+import csv
+import json
+import sys
+from collections import defaultdict
+
+GROUPS = {
+    'smmd_sn_power_iter': ('sn_p1_kernel', 'sn_p2_kernel', 'sn_r2_kernel', 'sn_p3_kernel',
+                           'sn_resident_kernel'),
+    'smmd_sn_weight_bwd': ('sn_bwd_a_kernel', 'sn_bwd_b_kernel', 'sn_resident_bwd_kernel'),
+    'smmd_adam_flat': ('opt_sqsum_kernel', 'opt_adam_kernel'),
+    'smmd_mmd2_fwd': ('mmd2_fused_kernel',),
+    'smmd_scaled_loss_fwd': ('sqnorm_partial_kernel', 'scaled_loss_final_kernel'),
+    'smmd_scaled_loss_bwd': ('scaled_loss_bwd_kernel',),
+}
+
+
+def per_kernel(path):
+    acc = defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if 'smmd::' not in r['Kernel_Name']:
+            continue
+        acc[r['Kernel_Name']].append(float(r['Counter_Value']))
+    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+def main():
+    fetch = per_kernel(sys.argv[1])
+    write = per_kernel(sys.argv[2])
+    out = {'_note': 'bytes per call; read = 2 * FETCH_SIZE(KB) * 1024 (gfx950 correction), '
+                    'write = WRITE_SIZE(KB) * 1024'}
+    for entry, kernels in GROUPS.items():
+        rd = wr = 0.0
+        found = []
+        for kname in fetch:
+            if any(k in kname for k in kernels):
+                rd += 2 * fetch[kname] * 1024
+                found.append(kname.split('(')[0])
+        for kname in write:
+            if any(k in kname for k in kernels):
+                wr += write[kname] * 1024
+        if found:
+            out[entry] = {'read_bytes': round(rd), 'write_bytes': round(wr),
+                          'traffic_bytes': round(rd + wr), 'kernels': sorted(set(found))}
+    print(json.dumps(out, indent=1))
+    if len(sys.argv) > 3:
+        with open(sys.argv[3], 'w') as f:
+            json.dump(out, f, indent=1)
+
+
+if __name__ == '__main__':
+    main()
