@@ -199,9 +199,10 @@ size_t smmd_sn_workspace_bytes(const smmd_sn_layer *layers, int n_layers);
  * 0 mirrors "NO_OPS" (u left untouched). layers[] is a HOST array read during
  * the call; the pointers in it are device pointers. n_layers <= SMMD_SN_MAX_LAYERS.
  * ws: zero-filled at allocation and then reused as is; its first 16 bytes are
- * the grid barrier of the single-launch (cooperative) path, which runs when
- * n_layers <= 16 and the weights fit the registers of the co-resident grid
- * (else a multi-launch path; env SMMD_SN_RESIDENT=0 forces it). */
+ * the grid barrier of the single-launch (cooperative) path.  That path is
+ * opt-in (env SMMD_SN_RESIDENT=1) and runs only when n_layers <= 16 and the
+ * weights fit the registers of the co-resident grid; the default is a
+ * multi-launch path. */
 smmd_status smmd_sn_power_iter(const smmd_sn_layer *layers, int n_layers,
                                int num_iters, float eps, int update_u,
                                void *ws, size_t ws_bytes, smmd_stream_t stream);

@@ -14,84 +14,11 @@
 // slab; the last-arriving block reduces the slab in a fixed order (agent-scope
 // release/acquire, CDNA4 guide G16) and writes the estimator.
 #include "smmd_common.hpp"
+#include "smmd_kern.hpp"
+
+#include <stdlib.h>
 
 namespace smmd {
-
-struct KParams {
-    int n_terms;
-    float c1[SMMD_MAX_TERMS];   // RBF: -gamma_k ; RQ: 2*alpha_k
-    float c2[SMMD_MAX_TERMS];   // RQ: -alpha_k
-    float wt[SMMD_MAX_TERMS];
-    float add_dot;
-};
-
-// d/dz_i K(z_i, z_j) = alpha * z_i + beta * (z_i - z_j)
-template <int KIND>
-struct Kern;
-
-template <>
-struct Kern<SMMD_KIND_RBF> {   // mmd.py:55-116: K = sum wt exp(-gamma max(raw,0))
-    static __device__ __forceinline__ void eval(const KParams &p, float raw, float, float,
-                                                float, float &K, float &al, float &be) {
-        const float R = fmaxf(raw, 0.f);
-        float k = 0.f, dk = 0.f;
-        for (int t = 0; t < p.n_terms; ++t) {
-            const float e = p.wt[t] * expf(p.c1[t] * R);
-            k += e;
-            dk += p.c1[t] * e;
-        }
-        K = k;
-        al = 0.f;
-        be = (raw >= 0.f) ? 2.f * dk : 0.f;   // tf.maximum: ties pass the gradient
-    }
-};
-
-template <>
-struct Kern<SMMD_KIND_RQ> {    // mmd.py:143-188
-    static __device__ __forceinline__ void eval(const KParams &p, float raw, float dot, float,
-                                                float, float &K, float &al, float &be) {
-        const float R = fmaxf(raw, 0.f);
-        float k = 0.f, dk = 0.f;
-        for (int t = 0; t < p.n_terms; ++t) {
-            const float q = 1.f + R / p.c1[t];
-            const float e = p.wt[t] * expf(p.c2[t] * logf(q));
-            k += e;
-            dk += e * p.c2[t] / (q * p.c1[t]);
-        }
-        if (p.add_dot > 0.f) k += p.add_dot * dot;
-        K = k;
-        al = p.add_dot;
-        be = ((raw >= 0.f) ? 2.f * dk : 0.f) - p.add_dot;
-    }
-};
-
-__device__ __forceinline__ float mysqrt(float x) {      // mmd.py:12
-    return sqrtf(fmaxf(x + 1.0e-5f, 0.f));
-}
-__device__ __forceinline__ float mysqrt_grad(float x) {
-    const float xe = x + 1.0e-5f;
-    return (xe >= 0.f) ? 0.5f / sqrtf(xe) : 0.f;
-}
-
-template <>
-struct Kern<SMMD_KIND_DISTANCE> {   // mmd.py:18-37 (no clamp; eps inside sqrt)
-    static __device__ __forceinline__ void eval(const KParams &, float raw, float, float sqr,
-                                                float sqc, float &K, float &al, float &be) {
-        K = (mysqrt(sqr) + mysqrt(sqc)) - mysqrt(raw);
-        al = 2.f * mysqrt_grad(sqr);
-        be = -2.f * mysqrt_grad(raw);
-    }
-};
-
-template <>
-struct Kern<SMMD_KIND_DOT> {   // mmd.py:44-52
-    static __device__ __forceinline__ void eval(const KParams &, float, float dot, float,
-                                                float, float &K, float &al, float &be) {
-        K = dot;
-        al = 1.f;
-        be = -1.f;
-    }
-};
 
 template <int DT>
 __device__ __forceinline__ void load_feat(const float *__restrict__ p, int d, bool tanh_in,
@@ -135,16 +62,6 @@ struct MmdArgs {
     double const_diag;
     KParams kp;
 };
-
-__device__ __forceinline__ double estimator(const double *S, double m, double n, int biased,
-                                            int has_const, double c) {
-    // gan/core/mmd.py:199-220
-    if (biased) return S[0] / (m * m) + S[2] / (n * n) - 2.0 * S[1] / (m * n);
-    const double trX = has_const ? m * c : S[3];
-    const double trY = has_const ? n * c : S[4];
-    return (S[0] - trX) / (m * (m - 1.0)) + (S[2] - trY) / (n * (n - 1.0)) -
-           2.0 * S[1] / (m * n);
-}
 
 // NW waves per block.  A one-block launch (small batches: the configs' 64+64
 // rows) reduces in LDS and writes the outputs directly; larger launches use
@@ -762,8 +679,14 @@ const char *smmd_status_string(smmd_status s) {
 
 int smmd_abi_version(void) { return 1; }
 
+static bool use_gram(int d) {
+    if (pick_dt(d) == 0) return true;
+    const char *e = getenv("SMMD_MMD_GRAM");
+    return e && e[0] == '1';
+}
+
 size_t smmd_mmd2_workspace_bytes(int m, int n, int d) {
-    (void)d;
+    if (use_gram(d)) return 256 + gram_ws_bytes(m, n, d);
     const int rows = (m > 0 ? m : 0) + (n > 0 ? n : 0);
     return 256 + align_up((size_t)mmd2_grid(rows, pick_dt(d)) * 8 * sizeof(double), 256);
 }
@@ -780,11 +703,36 @@ smmd_status smmd_mmd2_fwd(const smmd_kernel_desc *desc, const float *X, int m, c
     KParams kp;
     if (!make_kparams(desc, kp)) return SMMD_EINVAL;
     const int dt = pick_dt(d);
-    if (dt == 0) return SMMD_EUNSUPPORTED;
+    const bool gram = use_gram(d);
     const int rows = (x_end - x_begin) + (y_end - y_begin);
-    const int grid = mmd2_grid(rows, dt);
     if (!ws || ws_bytes < smmd_mmd2_workspace_bytes(m, n, d)) return SMMD_EWORKSPACE;
     if (rows == 0) return SMMD_EINVAL;
+    const double md = m, nd = n;
+    const int is_biased = biased ? 1 : 0;
+    const double wxx = is_biased ? 1.0 / (md * md) : 1.0 / (md * (md - 1.0));
+    const double wyy = is_biased ? 1.0 / (nd * nd) : 1.0 / (nd * (nd - 1.0));
+    if (gram) {
+        GramArgs g;
+        memset(&g, 0, sizeof(g));
+        g.X = X; g.Y = Y; g.m = m; g.n = n; g.d = d;
+        g.nrows = rows; g.nxr = x_end - x_begin; g.x_begin = x_begin; g.y_begin = y_begin;
+        g.tanh_in = desc->tanh_inputs ? 1 : 0;
+        g.biased = is_biased;
+        g.has_const = desc->has_const_diag ? 1 : 0;
+        g.const_diag = desc->const_diag;
+        g.trace_mode = (!is_biased && !g.has_const) ? 1 : 0;
+        g.need_grad = need_grad;
+        g.kind = desc->kind;
+        g.gw_same_x = (float)(2.0 * wxx);
+        g.gw_same_y = (float)(2.0 * wyy);
+        g.gw_cross = (float)(-2.0 / (md * nd));
+        g.counter = (unsigned *)ws;
+        g.out_sums = out_sums; g.out_mmd2 = out_mmd2;
+        g.grad_x = grad_x; g.grad_y = grad_y;
+        g.kp = kp;
+        return gram_mmd2_launch(g, (char *)ws + 256, (hipStream_t)stream);
+    }
+    const int grid = mmd2_grid(rows, dt);
 
     MmdArgs a;
     memset(&a, 0, sizeof(a));
@@ -803,9 +751,6 @@ smmd_status smmd_mmd2_fwd(const smmd_kernel_desc *desc, const float *X, int m, c
     a.const_diag = desc->const_diag;
     a.trace_mode = (!a.biased && !a.has_const) ? 1 : 0;
     a.need_grad = need_grad;
-    const double md = m, nd = n;
-    const double wxx = a.biased ? 1.0 / (md * md) : 1.0 / (md * (md - 1.0));
-    const double wyy = a.biased ? 1.0 / (nd * nd) : 1.0 / (nd * (nd - 1.0));
     a.gw_same_x = (float)(2.0 * wxx);
     a.gw_same_y = (float)(2.0 * wyy);
     a.gw_cross = (float)(-2.0 / (md * nd));

@@ -23,7 +23,10 @@
 
 namespace smmd {
 
-constexpr int SN_TR = 64;      // tile rows
+#ifndef SMMD_SN_TR
+#define SMMD_SN_TR 32
+#endif
+constexpr int SN_TR = SMMD_SN_TR;   // tile rows (multi-launch path)
 constexpr int SN_TC = 256;     // tile cols (64 lanes x 4)
 constexpr int SN_RPW = SN_TR / 4;   // rows per wave
 constexpr int SN_CHUNK = 16;   // layers per launch set
@@ -414,6 +417,16 @@ __device__ __forceinline__ void grid_sync(GridBarrier *b, unsigned nblocks) {
     __syncthreads();
 }
 
+// Phase timestamps (s_memrealtime, 100 MHz) of blocks 0 and G-1 in the spare
+// bytes of the 256-byte workspace header: u64 slots 2+i (block 0) and 16+i
+// (last block).  One store per phase per block; read by tools/diag_sn_phases.py.
+#define SR_STAMP(bar, i)                                                            \
+    do {                                                                            \
+        if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1))   \
+            reinterpret_cast<unsigned long long *>(bar)[(blockIdx.x ? 16 : 2) + (i)] = \
+                __builtin_amdgcn_s_memrealtime();                                   \
+    } while (0)
+
 struct SrTile {
     int layer, rt, ct;
 };
@@ -532,6 +545,7 @@ __global__ __launch_bounds__(SR_THREADS) void sn_resident_kernel(SnTable t, Grid
     __shared__ float red[SR_GROUP][16][SN_TC];
     __shared__ double dred[16];
 
+    SR_STAMP(bar, 0);
     float4 wa[SR_TMAX], wb[SR_TMAX];
 #pragma unroll
     for (int j = 0; j < SR_TMAX; ++j) wa[j] = wb[j] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -578,7 +592,9 @@ __global__ __launch_bounds__(SR_THREADS) void sn_resident_kernel(SnTable t, Grid
             }
             __syncthreads();
         }
+        if (it == 0) SR_STAMP(bar, 1);
         grid_sync(bar, G);
+        if (it == 0) SR_STAMP(bar, 2);
 
         // ---- A2: v_raw = sum over row tiles of P1; 256-column chunks, 4 per block
         for (int qi = blockIdx.x * 4 + (threadIdx.x >> 8); ; qi += G * 4) {
@@ -597,7 +613,9 @@ __global__ __launch_bounds__(SR_THREADS) void sn_resident_kernel(SnTable t, Grid
                 L.vraw[col] = s;
             }
         }
+        if (it == 0) SR_STAMP(bar, 3);
         grid_sync(bar, G);
+        if (it == 0) SR_STAMP(bar, 4);
 
         // ---- B: per-row partial dots with v_raw -> q2[ct][row]
 #pragma unroll
@@ -618,12 +636,16 @@ __global__ __launch_bounds__(SR_THREADS) void sn_resident_kernel(SnTable t, Grid
                 if (r1 < L.N) dst[r1] = d1;
             }
         }
+        if (it == 0) SR_STAMP(bar, 5);
         grid_sync(bar, G);
+        if (it == 0) SR_STAMP(bar, 6);
 
         // ---- R: norms, v, u', sigma (one workgroup per layer)
         const int last = (it == num_iters - 1);
         for (int l = blockIdx.x; l < t.n_layers; l += G) sr_layer_epilogue(t, t.L[l], last, dred);
+        if (it == 0) SR_STAMP(bar, 7);
         grid_sync(bar, G);
+        if (it == 0) SR_STAMP(bar, 8);
     }
 
     // ---- C: W_eff = (W / sigma) * s from the resident tiles
@@ -641,6 +663,7 @@ __global__ __launch_bounds__(SR_THREADS) void sn_resident_kernel(SnTable t, Grid
         o.z = (wb[j].z / sigma) * s; o.w = (wb[j].w / sigma) * s;
         sr_store(L.W_eff, L.N, L.K, L.vec, r0 + 16, c0, o);
     }
+    SR_STAMP(bar, 9);
 }
 
 // backward: <G, W> partial per tile -> barrier -> per-layer sum (fixed order,
@@ -785,9 +808,18 @@ static bool build_table(const smmd_sn_layer *layers, int first, int count, char 
     return true;
 }
 
+static bool coop_launch() {
+    const char *e = getenv("SMMD_SN_COOP");
+    return !(e && e[0] == '0');
+}
+
+// The resident path is opt-in (SMMD_SN_RESIDENT=1): on MI355X its four grid
+// barriers cost 15-20 us each and the cooperative launch ~20 us, so the
+// single-launch kernel (1 read + 1 write of W, 120 us measured on the
+// SNResNet-64 critic) loses to the launch set (3 reads + 1 write, 54 us).
 static bool resident_enabled() {
     const char *e = getenv("SMMD_SN_RESIDENT");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
 }
 
 // co-resident 1024-thread blocks of a resident kernel on the current device
@@ -855,6 +887,11 @@ smmd_status smmd_sn_power_iter(const smmd_sn_layer *layers, int n_layers, int nu
                 t.update_u = update_u ? 1 : 0;
                 GridBarrier *bar = (GridBarrier *)ws;
                 void *args[] = {&t, &bar, &num_iters};
+                if (!coop_launch()) {   // diagnostic: plain launch of the same grid
+                    hipLaunchKernelGGL(sn_resident_kernel, dim3(g), dim3(SR_THREADS), 0, s, t,
+                                       bar, num_iters);
+                    return last_launch_status();
+                }
                 return hip_status(hipLaunchCooperativeKernel((const void *)sn_resident_kernel,
                                                              dim3(g), dim3(SR_THREADS), args, 0, s));
             }

@@ -227,12 +227,16 @@ class MMD_GAN:
         return g_loss, d_loss, aux
 
     def g_step(self, images):
-        self.sn_D.refresh(update_u=True)
-        if self.sn_G.entries:
-            self.sn_G.refresh(update_u=True)
+        # critic weights are constants of the generator update: freeze them
+        # BEFORE the SN refresh so W_eff does not require grad (otherwise the
+        # backward runs every critic conv's weight-gradient kernel and the SN
+        # weight backward, and discards them)
         for p in self.d_vars:
             p.requires_grad_(False)
         try:
+            self.sn_D.refresh(update_u=True)
+            if self.sn_G.entries:
+                self.sn_G.refresh(update_u=True)
             self.g_optim.zero_grad()
             fake = self.generator(self.sample_z(self.batch_size))
             g_loss, d_loss, aux = self._critic_losses(images, fake, need_critic_grad=False)

@@ -69,8 +69,13 @@ def test_argument_validation_without_gpu(L):
                            None) == 1
     assert L.smmd_mmd2_fwd(d, x, 4, x, 4, 1, 0, 0, 4, 0, 4, None, None, None, None, x, 8,
                            None) == 3          # EWORKSPACE
-    assert L.smmd_mmd2_fwd(d, x, 4, x, 4, 64, 0, 0, 4, 0, 4, None, None, None, None, x, 1 << 20,
-                           None) == 4          # EUNSUPPORTED (d > 32 this round)
+    # d > 32 takes the MFMA Gram path, whose workspace holds the padded Z and
+    # the coefficient matrix: one byte short of the query is rejected
+    small = L.smmd_mmd2_workspace_bytes(4, 4, 32)
+    wide = L.smmd_mmd2_workspace_bytes(4, 4, 64)
+    assert wide >= 256 + 64 * 64 * 4 * 2 > small
+    assert L.smmd_mmd2_fwd(d, x, 4, x, 4, 64, 0, 0, 4, 0, 4, None, None, None, None, x, wide - 1,
+                           None) == 3          # EWORKSPACE
     assert L.smmd_sn_power_iter(None, 0, 1, 1e-12, 1, None, 0, None) == 1
     assert L.smmd_witness_bwd(d, x, 4, x, 4, x, 4, 1, None, x, x, x, None) == 1
 

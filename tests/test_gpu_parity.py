@@ -72,6 +72,81 @@ def test_mmd2_fused_vs_oracle(dev, name, shape, biased):
     _grad_close(Yt.grad.cpu().numpy(), rdy, 'dY %s %s' % (name, shape))
 
 
+# MFMA Gram path (smmd_gram.hip): every d > 32; features scaled by 1/sqrt(d)
+# so D2 = O(1) and the kernels are not saturated at 0
+GRAM_SHAPES = [(64, 64, 40), (100, 37, 128), (33, 70, 300)]
+
+
+def _gfeats(m, n, d, seed):
+    """N(0, 1/d) rows, Y shifted by 0.3/sqrt(d) per coordinate: D2 = O(1)."""
+    X, Y = _feats(m, n, d, seed, scale=1.0 / np.sqrt(d))
+    return X, (Y - np.float32(0.3) + np.float32(0.3 / np.sqrt(d))).astype(np.float32)
+
+
+@pytest.mark.parametrize('name', O.KERNEL_NAMES)
+@pytest.mark.parametrize('shape', GRAM_SHAPES)
+def test_mmd2_gram_vs_oracle(dev, name, shape):
+    from gan.core import mmd
+    m, n, d = shape
+    X, Y = _gfeats(m, n, d, seed=zlib.crc32(repr(('gram', name, shape)).encode()))
+    spec = O.kernel_spec(name)
+    g32 = spec.kind == 'distance'          # see test_mmd2_fused_vs_oracle
+    ref = O.mmd2(spec, X, Y, False, gram32=g32)
+    rdx, rdy = O.mmd2_grad(spec, X, Y, False, gram32=g32)
+    Xt = torch.tensor(X, device=dev, requires_grad=True)
+    Yt = torch.tensor(Y, device=dev, requires_grad=True)
+    val, sums = mmd.mmd2_fused(Xt, Yt, name, return_sums=True)
+    val.backward()
+    _close(val.item(), ref, 1e-5, 1e-4, 'mmd2 %s %s' % (name, shape))
+    _close(sums[:5].cpu().numpy(), O.mmd2_sums(spec, X, Y, gram32=g32), 1e-4, 1e-4, 'sums')
+    _grad_close(Xt.grad.cpu().numpy(), rdx, 'dX %s %s' % (name, shape))
+    _grad_close(Yt.grad.cpu().numpy(), rdy, 'dY %s %s' % (name, shape))
+
+
+@pytest.mark.parametrize('biased', [False, True])
+def test_mmd2_gram_wide(dev, biased):
+    """d = 1024 (SURVEY 8d MFMA sweep) at N = 2 x 256, rbf."""
+    from gan.core import mmd
+    X, Y = _gfeats(256, 256, 1024, seed=21)
+    spec = O.kernel_spec('rbf')
+    Xt = torch.tensor(X, device=dev, requires_grad=True)
+    Yt = torch.tensor(Y, device=dev, requires_grad=True)
+    val = mmd.mmd2_fused(Xt, Yt, 'rbf', biased=biased)
+    val.backward()
+    _close(val.item(), O.mmd2(spec, X, Y, biased), 1e-5, 1e-4, 'mmd2 wide')
+    rdx, rdy = O.mmd2_grad(spec, X, Y, biased)
+    _grad_close(Xt.grad.cpu().numpy(), rdx, 'dX wide')
+    _grad_close(Yt.grad.cpu().numpy(), rdy, 'dY wide')
+
+
+@pytest.mark.parametrize('name', ['rbf', 'mix_rq_dot', 'distance', 'dot', 'tanh_mix_rq'])
+@pytest.mark.parametrize('shape', [(64, 64, 1), (33, 70, 16), (17, 9, 32), (130, 127, 2)])
+def test_mmd2_gram_matches_row_sweep(dev, monkeypatch, name, shape):
+    """SMMD_MMD_GRAM=1 forces the MFMA path where the row-sweep kernel also
+    applies: the dot products are the same k-ordered fma chain, so the two
+    paths agree to the order of their final sums."""
+    from gan.core import mmd
+    m, n, d = shape
+    X, Y = _gfeats(m, n, d, seed=zlib.crc32(repr(('g-vs-f', name, shape)).encode()))
+    out = {}
+    for path in ('0', '1'):
+        monkeypatch.setenv('SMMD_MMD_GRAM', path)
+        Xt = torch.tensor(X, device=dev, requires_grad=True)
+        Yt = torch.tensor(Y, device=dev, requires_grad=True)
+        val, sums = mmd.mmd2_fused(Xt, Yt, name, return_sums=True)
+        val.backward()
+        out[path] = (val.item(), sums[:6].cpu().numpy(), Xt.grad.cpu().numpy(),
+                     Yt.grad.cpu().numpy())
+    a, b = out['1'], out['0']
+    _close(a[0], b[0], 1e-6, 1e-5, 'mmd2 gram vs sweep')
+    _close(a[1], b[1], 1e-5, 1e-5, 'sums gram vs sweep')
+    # the gradient is formed as (sum_j c_ij) z_i - sum_j c_ij z_j on the MFMA
+    # path and as sum_j c_ij (z_i - z_j) on the row sweep: the same tolerance
+    # as against the oracle (small entries lose digits to the cancellation)
+    for ga, gb, what in ((a[2], b[2], 'dX'), (a[3], b[3], 'dY')):
+        _grad_close(ga, gb, what + ' gram vs sweep')
+
+
 def test_mmd2_reference_api_path(dev):
     """mmd.mmd2(mmd._rbf_kernel(X, Y)) -- the exact call of SMMD.set_loss."""
     from gan.core import mmd
@@ -248,6 +323,7 @@ def test_sn_paths_agree_and_barrier_state(dev, monkeypatch):
     res = {}
     for path in SN_PATHS:
         _sn_path(monkeypatch, path)
+        torch.manual_seed(0)                   # same initial u for both banks
         mods, bank, rng = _sn_bank(dev, shapes, 11)
         hdr0 = bank.ws[:16].view(torch.int32).clone()
         calls = 20
