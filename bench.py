@@ -92,6 +92,119 @@ def cpu_baseline(cfg, seconds_budget=20.0):
                       (n, BATCH, dt)}
 
 
+MFMA_F32_PEAK_TFS = 157.3     # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense
+
+
+def mmd_sweep(world, rank, dev, group, quick=False):
+    """SURVEY 8d MMD microbench: X, Y ~ N(0,1) [N, D] per side (global N,
+    numpy default_rng(1234)), rank r owning rows [r N/w, (r+1) N/w) of each, run
+    through the product path mmd.mmd2_fused (all-gather mode when w > 1) with
+    its backward; HIP-event time per fwd+bwd, max over ranks.  Algorithmic
+    bytes: fwd (m+n) D 4 + 16, bwd (m+n) D 4 read + (m+n) D 4 written; pairs
+    P = m^2 + mn + n^2 (the reference's three matrices); for D >= 128 the Gram
+    flops 4 D P (forward Gram + backward C Z) against the f32 MFMA peak."""
+    import numpy as np
+    from gan.core import _lib, mmd
+    grid = [(32, 1), (64, 1), (256, 1), (512, 1), (2048, 1), (512, 16), (2048, 16),
+            (256, 128), (512, 128), (2048, 128), (512, 1024), (2048, 1024)]
+    if quick:
+        grid = [(64, 1), (512, 128)]
+    extra = [('mix_rq', 512, 1), ('mix_rbf', 512, 1), ('mix_rq', 512, 128),
+             ('mix_rbf', 512, 128)]
+    rows = []
+    for kern, N, D in [('rbf', N, D) for N, D in grid] + ([] if quick else extra):
+        if N % world:
+            continue
+        rng = np.random.default_rng(1234)
+        X = (rng.standard_normal((N, D)) / np.sqrt(D)).astype(np.float32)
+        Y = (rng.standard_normal((N, D)) / np.sqrt(D)).astype(np.float32)
+        sl = slice(rank * N // world, (rank + 1) * N // world)
+        Xl = torch.tensor(X[sl], device=dev, requires_grad=True)
+        Yl = torch.tensor(Y[sl], device=dev, requires_grad=True)
+
+        def once():
+            v = mmd.mmd2_fused(Xl, Yl, kern, process_group=group)
+            gx, gy = torch.autograd.grad(v, (Xl, Yl))
+            return v
+
+        for _ in range(3):
+            once()
+        iters = 20 if D < 1024 else 8
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        _lib.reset_timing()
+        _lib.enable_timing(True)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            val = once()
+        e1.record()
+        torch.cuda.synchronize()
+        _lib.enable_timing(False)
+        # op_ms: the whole mmd2_fused call + its backward as the training step
+        # issues it (host overhead, collectives); kernel_ms: HIP-event time of
+        # the library call alone (every launch of smmd_mmd2_fwd)
+        t = torch.tensor([e0.elapsed_time(e1) / iters,
+                          _lib.timing_ms().get('smmd_mmd2_fwd', (1, 0.0))[1]], device=dev)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        op_ms, ms = float(t[0]), float(t[1])
+        m = n = N
+        P = m * m + m * n + n * n
+        b = 3 * (m + n) * D * 4 + 16
+        row = {'kernel': kern, 'N': N, 'D': D, 'op_ms': round(op_ms, 5),
+               'kernel_ms': round(ms, 5), 'GB_s': round(b / (ms * 1e-3) / 1e9, 2),
+               'pair_evals_per_s': round(P / (ms * 1e-3), 1),
+               'path': 'row-sweep' if D <= 32 else 'mfma-gram', 'mmd2': float(val.detach())}
+        if D >= 128:
+            tf = 4.0 * D * P / (ms * 1e-3) / 1e12
+            row.update(tflops=round(tf, 2), mfma_frac=round(tf / MFMA_F32_PEAK_TFS, 4))
+        rows.append(row)
+    return rows
+
+
+def cpu_components(cfg, threads):
+    """SURVEY 8d CPU baseline rows (i) and (ii): the torch-CPU mirror of the TF
+    graph for MMD fwd+bwd per N (materialised N x N matrices, D = 1) and the
+    SN power iteration of the SNResNet-64 critic (all layers)."""
+    import numpy as np
+    from gan.core.architecture import SNResNetDiscriminator
+    from gan.core.snops import sn_modules
+    from oracle.tf_mirror import rbf_mmd2_tf, sn_weight_tf
+    torch.set_num_threads(threads)
+    out = {'mmd_fwd_bwd': []}
+    for N in (64, 256, 512, 2048):
+        rng = np.random.default_rng(1234)
+        X = torch.tensor(rng.standard_normal((N, 1)), dtype=torch.float32, requires_grad=True)
+        Y = torch.tensor(rng.standard_normal((N, 1)), dtype=torch.float32, requires_grad=True)
+        rbf_mmd2_tf(X, Y).backward()
+        reps, t0 = 0, time.perf_counter()
+        while reps < 20 and time.perf_counter() - t0 < 2.0:
+            X.grad = Y.grad = None
+            rbf_mmd2_tf(X, Y).backward()
+            reps += 1
+        out['mmd_fwd_bwd'].append({'N': N, 'D': 1, 'kernel': 'rbf',
+                                   'ms': round((time.perf_counter() - t0) / reps * 1e3, 3)})
+    D = SNResNetDiscriminator(64, 1, False, with_sn=True, with_learnable_sn_scale=True)
+    layers = []
+    for mod in sn_modules(D):
+        W = mod.weight.detach()
+        perm = (2, 3, 1, 0) if W.dim() == 4 else (1, 0)
+        layers.append((W, torch.randn(1, W.shape[0]), mod.sn_scale.detach(), perm))
+    for W, u, sc, perm in layers:
+        sn_weight_tf(W, u, sc, perm)
+    reps, t0 = 0, time.perf_counter()
+    while reps < 10 and time.perf_counter() - t0 < 3.0:
+        for W, u, sc, perm in layers:
+            sn_weight_tf(W, u, sc, perm)
+        reps += 1
+    out['sn_power_iter'] = {'architecture': 'snresnet-64 critic', 'layers': len(layers),
+                            'weights': sum(W.numel() for W, *_ in layers),
+                            'ms': round((time.perf_counter() - t0) / reps * 1e3, 3)}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -104,6 +217,11 @@ def main():
                     help='0: disable MIOpen Winograd solvers (immediate mode then picks '
                          'the MFMA implicit-GEMM ones)')
     ap.add_argument('--cpu-seconds', type=float, default=20.0)
+    ap.add_argument('--ref-schedule-steps', type=int, default=30,
+                    help='steps timed with the reference schedule (both gradient sets '
+                         'every step, model.py:514) after the main run; 0: skip')
+    ap.add_argument('--mmd-sweep', type=int, default=1,
+                    help='1: SURVEY 8d MMD microbench grid; 2: two configs; 0: skip')
     args = ap.parse_args()
 
     if not args.miopen_winograd:      # read by MIOpen at its first solver query
@@ -164,15 +282,48 @@ def main():
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     _lib.enable_timing(False)
+    tm = _lib.timing_ms()            # before the extra runs below reset the records
     g_loss, d_loss = model.check_finite()
     if world > 1:
         t = torch.tensor([dt], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t)
 
+    # the reference-schedule variant (both gradient sets every step)
+    ref_sched = None
+    if args.ref_schedule_steps > 0:
+        model.schedule = 'reference'
+        for i in range(6):                        # covers one generator step
+            model.train_step(images[i % len(images)])
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for i in range(args.ref_schedule_steps):
+            model.train_step(images[i % len(images)])
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        dtr = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([dtr], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dtr = float(t)
+        model.schedule = 'lean'
+        ref_sched = {'value': round(world * BATCH * args.ref_schedule_steps / dtr, 2),
+                     'unit': 'images/s', 'steps': args.ref_schedule_steps, 'warmup': 6,
+                     'ms_per_step': round(dtr / args.ref_schedule_steps * 1e3, 3),
+                     'note': 'every step also computes the other network\'s gradient set '
+                             'and discards it, as each sess.run of the reference does '
+                             '(model.py:514); value above is the lean schedule'}
+    sweep = None
+    if args.mmd_sweep:
+        sweep = mmd_sweep(world, rank, dev, dist.group.WORLD if world > 1 else None,
+                          quick=args.mmd_sweep == 2)
+
     # every libsmmd_hip entry point of the timed region: HIP-event time on the
     # compute stream and its algorithmic HBM bytes per call
-    tm = _lib.timing_ms()
     m_all = BATCH * world
     sn_kn = sum(e.N * e.K for e in model.sn_D.entries)
     per_img = 3 * 64 * 64
@@ -231,11 +382,15 @@ def main():
                        'pair_evals_per_s': round(pairs / (mk['avg_ms'] * 1e-3), 1) if mk else None,
                        'bound': 'latency (D=1: %s B algorithmic per call)' % mk.get('bytes')},
         'hip_kernels': kernels,
+        'schedule_reference': ref_sched,
+        'mmd_sweep': sweep,
         'losses': {'g_loss': g_loss, 'd_loss': d_loss},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             result['cpu_baseline'] = cpu_baseline(cfg, args.cpu_seconds)
+            result['cpu_baseline']['components'] = cpu_components(
+                cfg, result['cpu_baseline']['cores'])
         except Exception as e:   # report, never hide the GPU number
             result['cpu_baseline'] = {'error': repr(e)}
     if rank == 0:

@@ -57,7 +57,7 @@ typedef struct {
 } smmd_kernel_desc;
 
 const char *smmd_status_string(smmd_status s);
-int smmd_abi_version(void);         /* bumped on any ABI change                  */
+int smmd_abi_version(void);         /* bumped on any ABI change (2: Gram/poly) */
 
 /* ---------------------------------------------------------------------------
  * Fused pairwise MMD^2 (forward + unit gradient).
@@ -249,6 +249,51 @@ smmd_status smmd_adam_flat(float *param, const float *grad, float *m, float *v,
                            const int64_t *offsets, int n_tensors, float grad_scale,
                            float clip_norm, float lr, float beta1, float beta2, float eps,
                            int64_t step, void *ws, size_t ws_bytes, smmd_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * Polynomial-kernel MMD statistics of the KID scorer and the 3-sample LR
+ * scheduler, on the f32 matrix cores.
+ * Replaces polynomial_kernel + _mmd2_and_variance (gan/compute_scores.py:
+ * 232-335, via polynomial_mmd_averages :211-229 from gan/utils/scorer.py:103)
+ * and _np_get_sums / _np_diff_mmd2_and_ratio_from_sums (gan/core/mmd.py:
+ * 429-539, from gan/utils/scorer.py:124-162).
+ *
+ * smmd_poly_kernel_sums: K = (gamma A B^T + coef0)^degree for A [na, dim],
+ *   B [nb, dim] (row-major fp32; K is never materialised).  Outputs (device,
+ *   double, each may be NULL): row_sums [na] = K 1, col_sums [nb] = K^T 1,
+ *   diag [min(na, nb)] = K_ii, stats [4] = { sum K, sum K^2, sum_i K_ii,
+ *   sum_i K_ii^2 }.  degree 1..8.  ws: zero-filled at allocation.
+ * A "sums record" below is (rows, cols, diag, stats) of one such call.
+ * smmd_poly_mmd2_var: mmd2 and its variance estimate (_mmd2_and_variance)
+ *   from the XX, YY and XY records (m = na = nb): estimator 0 'unbiased',
+ *   1 'biased', 2 'u-statistic'; var_at_m <= 0 means m.
+ *   out [2] (device, double) = { mmd2, var_est }.
+ * smmd_poly_diff_ratio: mmd2(X,Y) - mmd2(X,Z) and its ratio to the estimated
+ *   std (the 3-sample test statistic, _np_diff_mmd2_and_ratio_from_sums) from
+ *   the YY, XY, ZZ, XZ records.  out [2] = { mmd2_diff, ratio }.
+ * ------------------------------------------------------------------------- */
+size_t smmd_poly_sums_workspace_bytes(int na, int nb, int dim);
+
+smmd_status smmd_poly_kernel_sums(const float *A, int na, const float *B, int nb, int dim,
+                                  double gamma, double coef0, int degree,
+                                  double *row_sums, double *col_sums, double *diag,
+                                  double *stats, void *ws, size_t ws_bytes,
+                                  smmd_stream_t stream);
+
+typedef struct {
+    const double *rows;   /* [m] */
+    const double *cols;   /* [m] */
+    const double *diag;   /* [m] */
+    const double *stats;  /* [4] */
+} smmd_poly_sums;
+
+smmd_status smmd_poly_mmd2_var(const smmd_poly_sums *xx, const smmd_poly_sums *yy,
+                               const smmd_poly_sums *xy, int m, double var_at_m,
+                               int estimator, double *out, smmd_stream_t stream);
+
+smmd_status smmd_poly_diff_ratio(const smmd_poly_sums *yy, const smmd_poly_sums *xy,
+                                 const smmd_poly_sums *zz, const smmd_poly_sums *xz, int m,
+                                 double *out, smmd_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -463,3 +463,124 @@ def smmd_objective(spec, x_fake, x_real, W1, W2, sc=10.0, variant='grad', biased
     nD = float(np.mean(dI ** 2))
     sc_ = scale_factor(J, sc, nD, variant)
     return m2 * sc_, m2, sc_
+
+
+# ---------------------------------------------------------------------------
+# Polynomial-kernel MMD of the KID scorer and the 3-sample LR scheduler.
+# The reference computes these in numpy (float64 sums over float32 kernel
+# matrices); restated here in float64 throughout.
+# ---------------------------------------------------------------------------
+def polynomial_kernel(X, Y=None, degree=3, gamma=None, coef0=1):
+    """sklearn.metrics.pairwise.polynomial_kernel (scikit_learn==0.19.1,
+    /root/reference requirements.txt:12; called at gan/compute_scores.py:237-239):
+    K = (gamma X Y^T + coef0)^degree, gamma None -> 1 / n_features."""
+    X = np.asarray(X, np.float64)
+    Y = X if Y is None else np.asarray(Y, np.float64)
+    g = 1.0 / X.shape[1] if gamma is None else gamma
+    return (g * (X @ Y.T) + coef0) ** degree
+
+
+def _sqn(a):
+    f = np.ravel(a)
+    return float(f @ f)
+
+
+def mmd2_and_variance(K_XX, K_XY, K_YY, unit_diagonal=False, mmd_est='unbiased',
+                      var_at_m=None, ret_var=True):
+    """gan/compute_scores.py:246-335 (_mmd2_and_variance)."""
+    m = K_XX.shape[0]
+    if var_at_m is None:
+        var_at_m = m
+    if unit_diagonal:
+        diag_X = diag_Y = 1
+        sum_diag_X = sum_diag_Y = m
+        sum_diag2_X = sum_diag2_Y = m
+    else:
+        diag_X, diag_Y = np.diagonal(K_XX), np.diagonal(K_YY)
+        sum_diag_X, sum_diag_Y = diag_X.sum(), diag_Y.sum()
+        sum_diag2_X, sum_diag2_Y = _sqn(diag_X), _sqn(diag_Y)
+    Kt_XX_sums = K_XX.sum(axis=1) - diag_X
+    Kt_YY_sums = K_YY.sum(axis=1) - diag_Y
+    K_XY_sums_0 = K_XY.sum(axis=0)
+    K_XY_sums_1 = K_XY.sum(axis=1)
+    Kt_XX_sum, Kt_YY_sum, K_XY_sum = Kt_XX_sums.sum(), Kt_YY_sums.sum(), K_XY_sums_0.sum()
+    if mmd_est == 'biased':
+        mmd2 = ((Kt_XX_sum + sum_diag_X) / (m * m) + (Kt_YY_sum + sum_diag_Y) / (m * m)
+                - 2 * K_XY_sum / (m * m))
+    else:
+        mmd2 = (Kt_XX_sum + Kt_YY_sum) / (m * (m - 1))
+        if mmd_est == 'unbiased':
+            mmd2 -= 2 * K_XY_sum / (m * m)
+        else:
+            mmd2 -= 2 * (K_XY_sum - np.trace(K_XY)) / (m * (m - 1))
+    if not ret_var:
+        return mmd2
+    Kt_XX_2_sum = _sqn(K_XX) - sum_diag2_X
+    Kt_YY_2_sum = _sqn(K_YY) - sum_diag2_Y
+    K_XY_2_sum = _sqn(K_XY)
+    dot_XX_XY = Kt_XX_sums.dot(K_XY_sums_1)
+    dot_YY_YX = Kt_YY_sums.dot(K_XY_sums_0)
+    m1, m2 = m - 1, m - 2
+    zeta1 = (1 / (m * m1 * m2) * (_sqn(Kt_XX_sums) - Kt_XX_2_sum + _sqn(Kt_YY_sums) - Kt_YY_2_sum)
+             - 1 / (m * m1) ** 2 * (Kt_XX_sum ** 2 + Kt_YY_sum ** 2)
+             + 1 / (m * m * m1) * (_sqn(K_XY_sums_1) + _sqn(K_XY_sums_0) - 2 * K_XY_2_sum)
+             - 2 / m ** 4 * K_XY_sum ** 2
+             - 2 / (m * m * m1) * (dot_XX_XY + dot_YY_YX)
+             + 2 / (m ** 3 * m1) * (Kt_XX_sum + Kt_YY_sum) * K_XY_sum)
+    zeta2 = (1 / (m * m1) * (Kt_XX_2_sum + Kt_YY_2_sum)
+             - 1 / (m * m1) ** 2 * (Kt_XX_sum ** 2 + Kt_YY_sum ** 2)
+             + 2 / (m * m) * K_XY_2_sum
+             - 2 / m ** 4 * K_XY_sum ** 2
+             - 4 / (m * m * m1) * (dot_XX_XY + dot_YY_YX)
+             + 4 / (m ** 3 * m1) * (Kt_XX_sum + Kt_YY_sum) * K_XY_sum)
+    var_est = (4 * (var_at_m - 2) / (var_at_m * (var_at_m - 1)) * zeta1
+               + 2 / (var_at_m * (var_at_m - 1)) * zeta2)
+    return mmd2, var_est
+
+
+def np_get_sums(K_XY, K_YY):
+    """gan/core/mmd.py:515-539 (_np_get_sums, const_diagonal=False)."""
+    diag_Y = np.diag(K_YY)
+    sum_diag2_Y = diag_Y @ diag_Y
+    return (K_YY.sum(axis=1) - diag_Y, (K_YY ** 2).sum() - sum_diag2_Y, K_XY.sum(axis=0),
+            K_XY.sum(axis=1), (K_XY ** 2).sum())
+
+
+def diff_mmd2_and_ratio_from_sums(Y_sums, Z_sums, m):
+    """gan/core/mmd.py:444-512 (_np_diff_mmd2_and_ratio_from_sums), _eps = 1e-5 (:6)."""
+    Kt_YY_sums, Kt_YY_2_sum, K_XY_sums_0, K_XY_sums_1, K_XY_2_sum = Y_sums
+    Kt_ZZ_sums, Kt_ZZ_2_sum, K_XZ_sums_0, K_XZ_sums_1, K_XZ_2_sum = Z_sums
+    Kt_YY_sum, Kt_ZZ_sum = Kt_YY_sums.sum(), Kt_ZZ_sums.sum()
+    K_XY_sum, K_XZ_sum = K_XY_sums_0.sum(), K_XZ_sums_0.sum()
+    muY_muY = Kt_YY_sum / (m * (m - 1))
+    muZ_muZ = Kt_ZZ_sum / (m * (m - 1))
+    muX_muY = K_XY_sum / (m * m)
+    muX_muZ = K_XZ_sum / (m * m)
+    E_y_muY_sq = (Kt_YY_sums @ Kt_YY_sums - Kt_YY_2_sum) / (m * (m - 1) * (m - 2))
+    E_z_muZ_sq = (Kt_ZZ_sums @ Kt_ZZ_sums - Kt_ZZ_2_sum) / (m * (m - 1) * (m - 2))
+    E_x_muY_sq = (K_XY_sums_1 @ K_XY_sums_1 - K_XY_2_sum) / (m * m * (m - 1))
+    E_x_muZ_sq = (K_XZ_sums_1 @ K_XZ_sums_1 - K_XZ_2_sum) / (m * m * (m - 1))
+    E_y_muX_sq = (K_XY_sums_0 @ K_XY_sums_0 - K_XY_2_sum) / (m * m * (m - 1))
+    E_z_muX_sq = (K_XZ_sums_0 @ K_XZ_sums_0 - K_XZ_2_sum) / (m * m * (m - 1))
+    E_y_muY_y_muX = Kt_YY_sums @ K_XY_sums_0 / (m * m * (m - 1))
+    E_z_muZ_z_muX = Kt_ZZ_sums @ K_XZ_sums_0 / (m * m * (m - 1))
+    E_x_muY_x_muZ = K_XY_sums_1 @ K_XZ_sums_1 / (m * m * m)
+    E_kyy2 = Kt_YY_2_sum / (m * (m - 1))
+    E_kzz2 = Kt_ZZ_2_sum / (m * (m - 1))
+    E_kxy2 = K_XY_2_sum / (m * m)
+    E_kxz2 = K_XZ_2_sum / (m * m)
+    mmd2_diff = muY_muY - 2 * muX_muY - muZ_muZ + 2 * muX_muZ
+    first_order = 4 * (m - 2) / (m * (m - 1)) * (
+        E_y_muY_sq - muY_muY ** 2 + E_x_muY_sq - muX_muY ** 2 + E_y_muX_sq - muX_muY ** 2
+        + E_z_muZ_sq - muZ_muZ ** 2 + E_x_muZ_sq - muX_muZ ** 2 + E_z_muX_sq - muX_muZ ** 2
+        - 2 * E_y_muY_y_muX + 2 * muY_muY * muX_muY
+        - 2 * E_x_muY_x_muZ + 2 * muX_muY * muX_muZ
+        - 2 * E_z_muZ_z_muX + 2 * muZ_muZ * muX_muZ)
+    second_order = 2 / (m * (m - 1)) * (
+        E_kyy2 - muY_muY ** 2 + 2 * E_kxy2 - 2 * muX_muY ** 2 + E_kzz2 - muZ_muZ ** 2
+        + 2 * E_kxz2 - 2 * muX_muZ ** 2
+        - 4 * E_y_muY_y_muX + 4 * muY_muY * muX_muY
+        - 4 * E_x_muY_x_muZ + 4 * muX_muY * muX_muZ
+        - 4 * E_z_muZ_z_muX + 4 * muZ_muZ * muX_muZ)
+    var_est = first_order + second_order
+    return mmd2_diff, mmd2_diff / np.sqrt(max(var_est, 1.0e-5))

@@ -677,7 +677,7 @@ const char *smmd_status_string(smmd_status s) {
     return "SMMD_?: unknown status";
 }
 
-int smmd_abi_version(void) { return 1; }
+int smmd_abi_version(void) { return 2; }
 
 static bool use_gram(int d) {
     if (pick_dt(d) == 0) return true;

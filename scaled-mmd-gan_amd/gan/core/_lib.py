@@ -21,7 +21,7 @@ LIB_PATH = os.environ.get('SMMD_HIP_LIB', os.path.join(_PKG_ROOT, 'lib', 'libsmm
 
 SMMD_MAX_TERMS = 8
 SMMD_SN_MAX_LAYERS = 32
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 KIND_RBF, KIND_RQ, KIND_DISTANCE, KIND_DOT = 0, 1, 2, 3
 
@@ -59,6 +59,14 @@ class SnLayer(ctypes.Structure):
                 ('K', ctypes.c_int32)]
 
 
+class PolySums(ctypes.Structure):
+    """smmd_poly_sums: (rows, cols, diag, stats) of one smmd_poly_kernel_sums call."""
+    _fields_ = [('rows', ctypes.c_void_p),
+                ('cols', ctypes.c_void_p),
+                ('diag', ctypes.c_void_p),
+                ('stats', ctypes.c_void_p)]
+
+
 _P = ctypes.c_void_p
 _I = ctypes.c_int
 _I64 = ctypes.c_int64
@@ -92,6 +100,14 @@ _SIGS = {
     'smmd_clip_by_norm_flat': (_I, [_P, ctypes.POINTER(ctypes.c_int64), _I, _F, _P, _SZ, _P]),
     'smmd_adam_flat': (_I, [_P, _P, _P, _P, ctypes.POINTER(ctypes.c_int64), _I, _F, _F, _F, _F,
                             _F, _F, _I64, _P, _SZ, _P]),
+    'smmd_poly_sums_workspace_bytes': (_SZ, [_I, _I, _I]),
+    'smmd_poly_kernel_sums': (_I, [_P, _I, _P, _I, _I, ctypes.c_double, ctypes.c_double, _I, _P,
+                                   _P, _P, _P, _P, _SZ, _P]),
+    'smmd_poly_mmd2_var': (_I, [ctypes.POINTER(PolySums), ctypes.POINTER(PolySums),
+                                ctypes.POINTER(PolySums), _I, ctypes.c_double, _I, _P, _P]),
+    'smmd_poly_diff_ratio': (_I, [ctypes.POINTER(PolySums), ctypes.POINTER(PolySums),
+                                  ctypes.POINTER(PolySums), ctypes.POINTER(PolySums), _I, _P,
+                                  _P]),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS)

@@ -20,6 +20,7 @@ from __future__ import annotations
 
 from dataclasses import dataclass, field
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -373,3 +374,103 @@ def witness_and_grad(H, R, F, kernel='rbf', **kw):
     """(d sum_i w_i / dH, w) with w_i = mean_j K(H_i,R_j) - mean_j K(H_i,F_j)."""
     dH, w = _WitnessGrad.apply(H, R, F, _as_spec(kernel, **kw))
     return dH, w
+
+
+# ---------------------------------------------------------------------------
+# Polynomial-kernel MMD statistics: the KID scorer and the 3-sample test of
+# the learning-rate scheduler (gan/core/mmd.py:296-539 numpy/TF versions,
+# gan/compute_scores.py:232-335).  K = (gamma <a, b> + coef0)^degree is
+# evaluated tile by tile on the f32 matrix cores (smmd_poly_kernel_sums) and
+# never materialised; the estimators run in double on the device.
+# ---------------------------------------------------------------------------
+class PolySums:
+    """Row sums, column sums, diagonal and {sum K, sum K^2, sum diag,
+    sum diag^2} of one polynomial kernel matrix (device float64 tensors)."""
+
+    __slots__ = ('rows', 'cols', 'diag', 'stats', 'shape')
+
+    def __init__(self, rows, cols, diag, stats, shape):
+        self.rows, self.cols, self.diag, self.stats, self.shape = rows, cols, diag, stats, shape
+
+    def c_struct(self):
+        return _lib.PolySums(self.rows.data_ptr(), self.cols.data_ptr(), self.diag.data_ptr(),
+                             self.stats.data_ptr())
+
+
+def _codes(x, device=None):
+    if not torch.is_tensor(x):
+        x = torch.from_numpy(np.ascontiguousarray(x, dtype=np.float32))
+    dev = device or (x.device if x.is_cuda else torch.device('cuda', torch.cuda.current_device()))
+    return x.to(device=dev, dtype=torch.float32).contiguous()
+
+
+def polynomial_kernel_sums(A, B, degree=3, gamma=None, coef0=1):
+    """Sums of K = (gamma A B^T + coef0)^degree (sklearn polynomial_kernel;
+    gamma None -> 1 / dim) without forming K."""
+    A = _codes(A)
+    B = _codes(B, A.device)
+    _lib.require_cuda(A, B)
+    na, dim = A.shape
+    nb = B.shape[0]
+    if B.shape[1] != dim:
+        raise ValueError('feature widths differ: %d vs %d' % (dim, B.shape[1]))
+    g = 1.0 / dim if gamma is None else float(gamma)
+    dev = A.device
+    rows = torch.empty(na, device=dev, dtype=torch.float64)
+    cols = torch.empty(nb, device=dev, dtype=torch.float64)
+    diag = torch.zeros(min(na, nb), device=dev, dtype=torch.float64)
+    stats = torch.empty(4, device=dev, dtype=torch.float64)
+    L = _lib.lib()
+    nbytes = L.smmd_poly_sums_workspace_bytes(na, nb, dim)
+    ws = _lib.workspace('poly', nbytes, dev)
+    with _lib.timed('smmd_poly_kernel_sums'):
+        _lib.check(L.smmd_poly_kernel_sums(_lib.ptr(A), na, _lib.ptr(B), nb, dim, g, float(coef0),
+                                           int(degree), _lib.ptr(rows), _lib.ptr(cols),
+                                           _lib.ptr(diag), _lib.ptr(stats), _lib.ptr(ws),
+                                           ws.numel(), _lib.stream_handle(dev)),
+                   'smmd_poly_kernel_sums')
+    return PolySums(rows, cols, diag, stats, (na, nb))
+
+
+_ESTIMATORS = {'unbiased': 0, 'biased': 1, 'u-statistic': 2}
+
+
+def poly_mmd2_and_variance(xx, yy, xy, var_at_m=None, mmd_est='unbiased'):
+    """mmd2 and var_est of gan/compute_scores.py:246-335 from three PolySums
+    records (device double tensor [2])."""
+    m = xx.shape[0]
+    if not (xx.shape == yy.shape == xy.shape == (m, m)):
+        raise ValueError('KID statistics need equal sample sizes')
+    out = torch.empty(2, device=xx.rows.device, dtype=torch.float64)
+    _lib.check(_lib.lib().smmd_poly_mmd2_var(
+        xx.c_struct(), yy.c_struct(), xy.c_struct(), m,
+        float(var_at_m) if var_at_m is not None else -1.0, _ESTIMATORS[mmd_est],
+        _lib.ptr(out), _lib.stream_handle(xx.rows.device)), 'smmd_poly_mmd2_var')
+    return out
+
+
+class YRelatedSums(tuple):
+    """(K_XY sums, K_YY sums) of gan/core/mmd.py:436 -- the record the
+    3-sample scheduler keeps for an earlier sample Z."""
+
+
+def np_diff_polynomial_mmd2_and_ratio_with_saving(X, Y, saved_sums_for_Z):
+    """gan/core/mmd.py:429-441: K = (<.,.>/dim + 1)^3.  Returns the Y-related
+    sums when saved_sums_for_Z is None, else (mmd2(X,Y) - mmd2(X,Z), the test
+    statistic, Y-related sums)."""
+    X = _codes(X)
+    Y = _codes(Y, X.device)
+    xy = polynomial_kernel_sums(X, Y)
+    yy = polynomial_kernel_sums(Y, Y)
+    mine = YRelatedSums((xy, yy))
+    if saved_sums_for_Z is None:
+        return mine
+    xz, zz = saved_sums_for_Z
+    m = yy.shape[0]
+    out = torch.empty(2, device=X.device, dtype=torch.float64)
+    _lib.check(_lib.lib().smmd_poly_diff_ratio(yy.c_struct(), xy.c_struct(), zz.c_struct(),
+                                               xz.c_struct(), m, _lib.ptr(out),
+                                               _lib.stream_handle(X.device)),
+               'smmd_poly_diff_ratio')
+    diff, ratio = out.tolist()
+    return diff, ratio, mine

@@ -61,8 +61,15 @@ class MMD_GAN:
     (:352-364)."""
 
     def __init__(self, config, device=None, process_group=None, dp_mode='tower',
-                 batch_size=None, output_size=None, c_dim=3, channels_last=False):
+                 batch_size=None, output_size=None, c_dim=3, channels_last=False,
+                 schedule='lean'):
         c = config
+        # 'lean': a step computes only the gradient set it applies.
+        # 'reference': every step also computes the other set and discards it,
+        # as each sess.run of the reference does (model.py:514, SURVEY App. B 4)
+        if schedule not in ('lean', 'reference'):
+            raise ValueError('schedule must be lean or reference')
+        self.schedule = schedule
         if getattr(c, 'learning_rate_D', -1) < 0:               # model.py:18-19
             c.learning_rate_D = c.learning_rate
         if getattr(c, 'real_batch_size', -1) == -1:             # model.py:42-43
@@ -216,13 +223,18 @@ class MMD_GAN:
         self.sn_D.refresh(update_u=True)
         if self.sn_G.entries:
             self.sn_G.refresh(update_u=True)
-        with torch.no_grad():
+        ref = self.schedule == 'reference'
+        with torch.set_grad_enabled(ref):
             fake = self.generator(self.sample_z(self.batch_size))
         for p in self.d_vars:
             p.requires_grad_(True)
         self.d_optim.zero_grad()
         g_loss, d_loss, aux = self._critic_losses(images, fake, need_critic_grad=True)
-        d_loss.backward()
+        if ref:       # the generator's gradient set, computed and discarded
+            torch.autograd.grad(g_loss, self.g_vars, retain_graph=True)
+            d_loss.backward(inputs=self.d_vars)
+        else:
+            d_loss.backward()
         self._exchange(self.d_optim)
         return g_loss, d_loss, aux
 
@@ -231,16 +243,20 @@ class MMD_GAN:
         # BEFORE the SN refresh so W_eff does not require grad (otherwise the
         # backward runs every critic conv's weight-gradient kernel and the SN
         # weight backward, and discards them)
-        for p in self.d_vars:
-            p.requires_grad_(False)
+        ref = self.schedule == 'reference'
+        if not ref:
+            for p in self.d_vars:
+                p.requires_grad_(False)
         try:
             self.sn_D.refresh(update_u=True)
             if self.sn_G.entries:
                 self.sn_G.refresh(update_u=True)
             self.g_optim.zero_grad()
             fake = self.generator(self.sample_z(self.batch_size))
-            g_loss, d_loss, aux = self._critic_losses(images, fake, need_critic_grad=False)
-            g_loss.backward()
+            g_loss, d_loss, aux = self._critic_losses(images, fake, need_critic_grad=ref)
+            if ref:   # the critic's gradient set, computed and discarded
+                torch.autograd.grad(d_loss, self.d_vars, retain_graph=True)
+            g_loss.backward(inputs=self.g_vars)
             self._exchange(self.g_optim)
         finally:
             for p in self.d_vars:

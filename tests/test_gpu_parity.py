@@ -474,3 +474,78 @@ def test_missing_inputs_fail_loudly(dev):
     from gan.core import mmd, _lib
     with pytest.raises(_lib.SmmdError):
         mmd.mmd2_fused(torch.zeros(4, 1), torch.zeros(4, 1))   # CPU tensors: no CPU path
+
+
+# ---- polynomial-kernel MMD: KID scorer and 3-sample test -------------------
+def _codes(n, dim, seed, scale=1.0):
+    """Synthetic pool3-like codes: |N(0, 1)| (Inception is unavailable offline)."""
+    rng = np.random.default_rng(seed)
+    return (np.abs(rng.standard_normal((n, dim))) * scale).astype(np.float32)
+
+
+@pytest.mark.parametrize('na,nb,dim', [(100, 100, 64), (257, 130, 2048), (64, 64, 33)])
+def test_poly_kernel_sums_vs_oracle(dev, na, nb, dim):
+    from gan.core import mmd
+    A, B = _codes(na, dim, 1), _codes(nb, dim, 2, 1.1)
+    s = mmd.polynomial_kernel_sums(torch.tensor(A, device=dev), torch.tensor(B, device=dev))
+    K = O.polynomial_kernel(A, B)
+    d = np.diagonal(K)
+    # each K is an fp32 dot over dim features then cubed (as the reference's
+    # float32 sklearn call): ~3e-6 relative per element at dim 2048; the
+    # double sums average that down
+    _close(s.diag.cpu().numpy(), d, 0, 2e-5, 'diag')
+    _close(s.rows.cpu().numpy(), K.sum(1), 0, 1e-5, 'rows')
+    _close(s.cols.cpu().numpy(), K.sum(0), 0, 1e-5, 'cols')
+    _close(s.stats.cpu().numpy(), [K.sum(), (K * K).sum(), d.sum(), (d * d).sum()], 0, 1e-5,
+           'stats')
+
+
+@pytest.mark.parametrize('mmd_est', ['unbiased', 'biased', 'u-statistic'])
+def test_polynomial_mmd_vs_oracle(dev, mmd_est):
+    """KID of gan/compute_scores.py:232-335 at 512 x 2048 codes."""
+    from gan import compute_scores as cs
+    from gan.core import mmd
+    X, Y = _codes(512, 2048, 3), _codes(512, 2048, 4, 1.05)
+    Kxx, Kyy, Kxy = (O.polynomial_kernel(a, b) for a, b in ((X, X), (Y, Y), (X, Y)))
+    ref_m, ref_v = O.mmd2_and_variance(Kxx, Kxy, Kyy, mmd_est=mmd_est, var_at_m=1000)
+    Xt, Yt = torch.tensor(X, device=dev), torch.tensor(Y, device=dev)
+    sums = [mmd.polynomial_kernel_sums(a, b) for a, b in ((Xt, Xt), (Yt, Yt), (Xt, Yt))]
+    got = mmd.poly_mmd2_and_variance(*sums, var_at_m=1000, mmd_est=mmd_est).cpu().numpy()
+    scale = Kxy.mean()              # the estimator is a difference of O(mean K) terms
+    _close(got[0], ref_m, 1e-6 * scale, 1e-4, 'mmd2 %s' % mmd_est)
+    _close(got[1], ref_v, 1e-6 * abs(ref_v) + 1e-9 * scale ** 2, 1e-2, 'var %s' % mmd_est)
+    if mmd_est == 'unbiased':
+        m2, v2 = cs.polynomial_mmd(X, Y, var_at_m=1000)
+        _close([m2, v2], got, 0, 1e-12, 'polynomial_mmd')
+        # the materialised-matrix entry point on the same matrices
+        m3, v3 = cs._mmd2_and_variance(Kxx.astype(np.float32), Kxy.astype(np.float32),
+                                       Kyy.astype(np.float32), var_at_m=1000)
+        _close(m3, ref_m, 1e-6 * scale, 1e-4, '_mmd2_and_variance')
+
+
+def test_polynomial_mmd_averages_subsets(dev):
+    from gan import compute_scores as cs
+    G, R = _codes(1500, 2048, 5), _codes(1200, 2048, 6)
+    np.random.seed(0)
+    got = cs.polynomial_mmd_averages(G, R, n_subsets=3, subset_size=1000, ret_var=False)
+    np.random.seed(0)
+    for i in range(3):
+        g = G[np.random.choice(len(G), 1000, replace=False)]
+        r = R[np.random.choice(len(R), 1000, replace=False)]
+        Ks = [O.polynomial_kernel(a, b) for a, b in ((g, g), (g, r), (r, r))]
+        ref = O.mmd2_and_variance(*Ks, var_at_m=1200, ret_var=False)
+        _close(got[i], ref, 1e-6 * Ks[1].mean(), 1e-4, 'subset %d' % i)
+
+
+def test_three_sample_diff_and_ratio(dev):
+    """gan/core/mmd.py:429-512 as the LR scheduler calls it (gan/utils/scorer.py:124-162)."""
+    from gan.core import mmd
+    X, Y, Z = _codes(300, 2048, 7), _codes(300, 2048, 8, 1.02), _codes(300, 2048, 9, 1.08)
+    saved = mmd.np_diff_polynomial_mmd2_and_ratio_with_saving(X, Z, None)
+    diff, ratio, _ = mmd.np_diff_polynomial_mmd2_and_ratio_with_saving(X, Y, saved)
+    K = lambda a, b: O.polynomial_kernel(a, b)
+    ref = O.diff_mmd2_and_ratio_from_sums(O.np_get_sums(K(X, Y), K(Y, Y)),
+                                          O.np_get_sums(K(X, Z), K(Z, Z)), 300)
+    scale = K(X, Y).mean()
+    _close(diff, ref[0], 1e-6 * scale, 1e-4, 'mmd2_diff')
+    _close(ratio, ref[1], 1e-3 * abs(ref[1]) + 1e-3, 1e-3, 'ratio')

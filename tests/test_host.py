@@ -173,3 +173,39 @@ def test_mean_pool2_first_and_second_order():
     assert torch.allclose(mean_pool2(x), torch.nn.functional.avg_pool2d(x, 2))
     assert torch.autograd.gradcheck(mean_pool2, (x,))
     assert torch.autograd.gradgradcheck(mean_pool2, (x,))
+
+
+def test_three_sample_lr_scheduler_logic(monkeypatch):
+    """gan/utils/scorer.py:119-162 decision rules on scripted statistics:
+    p = Phi(stat) > .1 for MMD_sdlr_num_test consecutive scorings -> decay."""
+    import argparse
+    import numpy as np
+    from gan.utils import scorer as S
+    stats = iter([-3.0, 2.0, 2.0, 2.0, 2.0])          # p ~ 0.001, then p ~ 0.98 x 4
+    kids = iter([0.5, 0.4, 0.6, 0.3, 0.7, 0.7, 0.7, 0.7, 0.7, 0.7])
+    monkeypatch.setattr(S.cs, 'polynomial_mmd_averages',
+                        lambda *a, **k: np.full(2, next(kids)))
+
+    def fake_diff(X, Y, saved):
+        if saved is None:
+            return ('sums',)
+        return 0.0, next(stats), ('sums',)
+    monkeypatch.setattr(S.mmd, 'np_diff_polynomial_mmd2_and_ratio_with_saving', fake_diff)
+
+    class Gan:
+        config = argparse.Namespace(MMD_sdlr_freq=1, MMD_sdlr_past_sample=2, MMD_sdlr_num_test=3,
+                                    with_scaling=True)
+        lr, sc, decays = 1e-4, 10.0, 0
+
+        def decay_ops(self):
+            self.decays += 1
+            self.lr *= .8
+    gan = Gan()
+    best = []
+    sc = S.Scorer(np.zeros((10, 4)), n_subsets=2, subset_size=5)
+    for step in range(6):
+        sc.compute(gan, step, np.zeros((10, 4)), save_checkpoint=lambda: best.append(step))
+    # scorings 0,1 fill the memory; 2: p small -> keep; 3,4,5: p > .1 three times -> decay
+    assert gan.decays == 1 and abs(gan.lr - 0.8e-4) < 1e-12
+    assert sc.three_sample_chances == 0
+    assert best == [1, 3]                      # KID improved at scorings 1 and 3

@@ -177,3 +177,36 @@ def test_golden_sn_regression():
         sigma, u1, _ = O.spectral_norm_rows(z[key + '__W'], z[key + '__u'])
         assert sigma == pytest.approx(float(z[key + '__sigma']), rel=1e-12)
         np.testing.assert_allclose(u1, z[key + '__u1'], rtol=1e-12, atol=1e-15)
+
+
+# ---- polynomial-kernel MMD (KID scorer / 3-sample scheduler) --------------
+def test_polynomial_kernel_matches_sklearn():
+    """The reference calls sklearn's polynomial_kernel (compute_scores.py:237-239)."""
+    from sklearn.metrics.pairwise import polynomial_kernel as sk
+    rng = np.random.default_rng(0)
+    X, Y = rng.standard_normal((7, 5)), rng.standard_normal((4, 5))
+    np.testing.assert_allclose(O.polynomial_kernel(X, Y), sk(X, Y), rtol=1e-12)
+    np.testing.assert_allclose(O.polynomial_kernel(X, Y, degree=2, gamma=.3, coef0=.5),
+                               sk(X, Y, degree=2, gamma=.3, coef0=.5), rtol=1e-12)
+
+
+def test_poly_mmd2_known_answers():
+    rng = np.random.default_rng(1)
+    X, Y = np.abs(rng.standard_normal((9, 6))), np.abs(rng.standard_normal((9, 6))) * 1.3
+    Kxx, Kyy, Kxy = (O.polynomial_kernel(a, b) for a, b in ((X, X), (Y, Y), (X, Y)))
+    # biased MMD^2 of a sample with itself is 0
+    assert abs(O.mmd2_and_variance(Kxx, Kxx, Kxx, mmd_est='biased', ret_var=False)) < 1e-12
+    # unbiased: off-diagonal means minus twice the cross mean, by brute force
+    m = 9
+    off = lambda K: sum(K[i, j] for i in range(m) for j in range(m) if i != j) / (m * (m - 1))
+    ref = off(Kxx) + off(Kyy) - 2 * Kxy.mean()
+    mmd2, var = O.mmd2_and_variance(Kxx, Kxy, Kyy)
+    assert abs(mmd2 - ref) < 1e-12 and var > 0
+    # the 3-sample difference equals the difference of the two unbiased MMDs
+    Z = np.abs(rng.standard_normal((9, 6))) * 0.8
+    Kzz, Kxz = O.polynomial_kernel(Z, Z), O.polynomial_kernel(X, Z)
+    diff, ratio = O.diff_mmd2_and_ratio_from_sums(O.np_get_sums(Kxy, Kyy),
+                                                  O.np_get_sums(Kxz, Kzz), m)
+    d_ref = (O.mmd2_and_variance(Kxx, Kxy, Kyy, ret_var=False)
+             - O.mmd2_and_variance(Kxx, Kxz, Kzz, ret_var=False))
+    assert abs(diff - d_ref) < 1e-10 and np.isfinite(ratio)
