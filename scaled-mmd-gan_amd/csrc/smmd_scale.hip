@@ -127,16 +127,25 @@ __global__ __launch_bounds__(256) void scaled_loss_bwd_kernel(
 
 // ---------------------------------------------------------------------------
 // flat multi-tensor clip / Adam.  Tensors are [off[i], off[i+1]) of one flat
-// buffer; each tensor is cut into OPT_CHUNK-element blocks.
+// buffer.  The norm pass cuts each tensor into OPT_SQ_CHUNK-element blocks
+// (one double partial each); the update / clip pass into OPT_UP_CHUNK-element
+// blocks, small enough that the ~2.5k blocks of a 10 M-parameter critic spread
+// evenly over 256 CUs (16 K-element blocks left 105 CUs with one block more
+// than the rest), each thread issuing all of its loads before any update.
 // ---------------------------------------------------------------------------
-constexpr int OPT_CHUNK = 16384;
+constexpr int OPT_SQ_CHUNK = 8192;
+constexpr int OPT_UP_CHUNK = 4096;
+constexpr int OPT_SQ_IT = OPT_SQ_CHUNK / 4 / 256;   // float4 per thread, full block
+constexpr int OPT_UP_IT = OPT_UP_CHUNK / 4 / 256;
 constexpr int OPT_MAX = 96;     // tensors per launch set (kernel-arg budget)
 
 struct OptTable {
     int n;
-    int total_blocks;
+    int total_blocks;            // blocks of the pass this table drives
+    int chunk;                   // elements per block of that pass
     int64_t off[OPT_MAX + 1];
-    int blk[OPT_MAX + 1];        // first block of each tensor
+    int blk[OPT_MAX + 1];        // first block of each tensor (this pass)
+    int sblk[OPT_MAX + 1];       // first norm-pass block of each tensor (partial slab)
 };
 
 __device__ __forceinline__ int opt_find(const OptTable &t, int b) {
@@ -151,14 +160,31 @@ __device__ __forceinline__ int opt_find(const OptTable &t, int b) {
 // every tensor range [off[i], off[i+1]) of the flat buffer is walked as float4
 // when all offsets are multiples of 4 and the buffers 16-byte aligned (vec);
 // FlatAdam pads its tensors to that.
+__device__ __forceinline__ void opt_range(const OptTable &t, int ti, int64_t &lo, int64_t &hi) {
+    lo = t.off[ti] + (int64_t)(blockIdx.x - t.blk[ti]) * t.chunk;
+    hi = (lo + t.chunk < t.off[ti + 1]) ? lo + t.chunk : t.off[ti + 1];
+}
+
 __global__ __launch_bounds__(256) void opt_sqsum_kernel(OptTable t, const float *__restrict__ g,
                                                         float gscale, int vec,
                                                         double *__restrict__ part) {
     const int ti = opt_find(t, blockIdx.x);
-    const int64_t lo = t.off[ti] + (int64_t)(blockIdx.x - t.blk[ti]) * OPT_CHUNK;
-    const int64_t hi = (lo + OPT_CHUNK < t.off[ti + 1]) ? lo + OPT_CHUNK : t.off[ti + 1];
+    int64_t lo, hi;
+    opt_range(t, ti, lo, hi);
     float acc0 = 0.f, acc1 = 0.f;
-    if (vec) {
+    if (vec && hi - lo == OPT_SQ_CHUNK) {     // full block: every load in flight at once
+        const float4 *g4 = reinterpret_cast<const float4 *>(g) + lo / 4 + threadIdx.x;
+        float4 x[OPT_SQ_IT];
+#pragma unroll
+        for (int k = 0; k < OPT_SQ_IT; ++k) x[k] = g4[k * 256];
+#pragma unroll
+        for (int k = 0; k < OPT_SQ_IT; ++k) {
+            acc0 = fmaf(x[k].x * gscale, x[k].x * gscale, acc0);
+            acc1 = fmaf(x[k].y * gscale, x[k].y * gscale, acc1);
+            acc0 = fmaf(x[k].z * gscale, x[k].z * gscale, acc0);
+            acc1 = fmaf(x[k].w * gscale, x[k].w * gscale, acc1);
+        }
+    } else if (vec) {
         const float4 *g4 = reinterpret_cast<const float4 *>(g);
         for (int64_t i = lo / 4 + threadIdx.x; i < hi / 4; i += 256) {
             const float4 x = g4[i];
@@ -183,7 +209,7 @@ __device__ __forceinline__ float clip_factor(const OptTable &t, int ti, const do
                                              float clip, float *sh) {
     if (threadIdx.x < 64) {
         double s = 0.0;
-        for (int b = t.blk[ti] + (int)threadIdx.x; b < t.blk[ti + 1]; b += 64) s += part[b];
+        for (int b = t.sblk[ti] + (int)threadIdx.x; b < t.sblk[ti + 1]; b += 64) s += part[b];
         s = wave_sum(s);
         if (threadIdx.x == 0) {
             const float ss = (float)s;
@@ -201,8 +227,8 @@ __global__ __launch_bounds__(256) void opt_clip_kernel(OptTable t, float *__rest
     const int ti = opt_find(t, blockIdx.x);
     __shared__ float sh[1];
     const float f = clip_factor(t, ti, part, clip, sh);
-    const int64_t lo = t.off[ti] + (int64_t)(blockIdx.x - t.blk[ti]) * OPT_CHUNK;
-    const int64_t hi = (lo + OPT_CHUNK < t.off[ti + 1]) ? lo + OPT_CHUNK : t.off[ti + 1];
+    int64_t lo, hi;
+    opt_range(t, ti, lo, hi);
     if (vec) {
         float4 *g4 = reinterpret_cast<float4 *>(g);
         for (int64_t i = lo / 4 + threadIdx.x; i < hi / 4; i += 256) {
@@ -243,9 +269,33 @@ __global__ __launch_bounds__(256) void opt_adam_kernel(OptTable t, float *__rest
     k.b1c = 1.f - b1;
     k.b2c = 1.f - b2;
     k.eps = eps;
-    const int64_t lo = t.off[ti] + (int64_t)(blockIdx.x - t.blk[ti]) * OPT_CHUNK;
-    const int64_t hi = (lo + OPT_CHUNK < t.off[ti + 1]) ? lo + OPT_CHUNK : t.off[ti + 1];
-    if (vec) {
+    int64_t lo, hi;
+    opt_range(t, ti, lo, hi);
+    if (vec && hi - lo == OPT_UP_CHUNK) {     // full block: 4 x OPT_UP_IT float4 loads in flight
+        const int64_t b4 = lo / 4 + threadIdx.x;
+        float4 *p4 = reinterpret_cast<float4 *>(p) + b4;
+        const float4 *g4 = reinterpret_cast<const float4 *>(g) + b4;
+        float4 *m4 = reinterpret_cast<float4 *>(m) + b4;
+        float4 *v4 = reinterpret_cast<float4 *>(v) + b4;
+        float4 pp[OPT_UP_IT], gg[OPT_UP_IT], mm[OPT_UP_IT], vv[OPT_UP_IT];
+#pragma unroll
+        for (int j = 0; j < OPT_UP_IT; ++j) {
+            gg[j] = g4[j * 256];
+            pp[j] = p4[j * 256];
+            mm[j] = m4[j * 256];
+            vv[j] = v4[j * 256];
+        }
+#pragma unroll
+        for (int j = 0; j < OPT_UP_IT; ++j) {
+            k.upd(pp[j].x, gg[j].x, mm[j].x, vv[j].x);
+            k.upd(pp[j].y, gg[j].y, mm[j].y, vv[j].y);
+            k.upd(pp[j].z, gg[j].z, mm[j].z, vv[j].z);
+            k.upd(pp[j].w, gg[j].w, mm[j].w, vv[j].w);
+            p4[j * 256] = pp[j];
+            m4[j * 256] = mm[j];
+            v4[j * 256] = vv[j];
+        }
+    } else if (vec) {
         float4 *p4 = reinterpret_cast<float4 *>(p);
         const float4 *g4 = reinterpret_cast<const float4 *>(g);
         float4 *m4 = reinterpret_cast<float4 *>(m);
@@ -280,22 +330,31 @@ static int opt_vec(const int64_t *off, int n, const void *a, const void *b, cons
     return (al % 16) == 0;
 }
 
-static bool build_opt(const int64_t *off, int first, int count, OptTable &t) {
+// blocks of a tensor of n elements at `chunk` elements per block (an empty
+// tensor keeps one block so the block -> tensor map stays strictly increasing)
+static int64_t opt_blocks(int64_t n, int chunk) { return n == 0 ? 1 : (n + chunk - 1) / chunk; }
+
+// table of tensors [first, first + count) for a pass of `chunk`-element blocks
+static bool build_opt(const int64_t *off, int first, int count, int chunk, OptTable &t) {
     memset(&t, 0, sizeof(t));
     t.n = count;
-    int blocks = 0;
+    t.chunk = chunk;
+    int64_t blocks = 0, sblocks = 0;
     for (int i = 0; i <= count; ++i) {
         t.off[i] = off[first + i];
         if (i > 0 && t.off[i] < t.off[i - 1]) return false;
     }
     for (int i = 0; i < count; ++i) {
-        t.blk[i] = blocks;
+        t.blk[i] = (int)blocks;
+        t.sblk[i] = (int)sblocks;
         const int64_t n = t.off[i + 1] - t.off[i];
-        blocks += (int)((n + OPT_CHUNK - 1) / OPT_CHUNK);
-        if (n == 0) blocks += 1;   // keep blk strictly increasing
+        blocks += opt_blocks(n, chunk);
+        sblocks += opt_blocks(n, OPT_SQ_CHUNK);
+        if (blocks > INT32_MAX / 2) return false;
     }
-    t.blk[count] = blocks;
-    t.total_blocks = blocks;
+    t.blk[count] = (int)blocks;
+    t.sblk[count] = (int)sblocks;
+    t.total_blocks = (int)blocks;
     return true;
 }
 
@@ -363,10 +422,7 @@ smmd_status smmd_scaled_loss_bwd(const float *jac, int n_cols, int b, int b_tota
 size_t smmd_opt_workspace_bytes(const int64_t *offsets, int n_tensors) {
     if (!offsets || n_tensors < 1) return 0;
     int64_t blocks = 0;
-    for (int i = 0; i < n_tensors; ++i) {
-        const int64_t n = offsets[i + 1] - offsets[i];
-        blocks += (n + OPT_CHUNK - 1) / OPT_CHUNK + (n == 0 ? 1 : 0);
-    }
+    for (int i = 0; i < n_tensors; ++i) blocks += opt_blocks(offsets[i + 1] - offsets[i], OPT_SQ_CHUNK);
     return align_up((size_t)blocks * sizeof(double) + 256, 256);
 }
 
@@ -378,12 +434,14 @@ smmd_status smmd_clip_by_norm_flat(float *grad, const int64_t *offsets, int n_te
     hipStream_t s = (hipStream_t)stream;
     for (int first = 0; first < n_tensors; first += OPT_MAX) {
         const int count = (n_tensors - first < OPT_MAX) ? n_tensors - first : OPT_MAX;
-        OptTable t;
-        if (!build_opt(offsets, first, count, t)) return SMMD_EINVAL;
+        OptTable ts, tu;
+        if (!build_opt(offsets, first, count, OPT_SQ_CHUNK, ts) ||
+            !build_opt(offsets, first, count, OPT_UP_CHUNK, tu))
+            return SMMD_EINVAL;
         const int vec = opt_vec(offsets + first, count, grad, grad, grad, grad);
-        hipLaunchKernelGGL(opt_sqsum_kernel, dim3(t.total_blocks), dim3(256), 0, s, t,
+        hipLaunchKernelGGL(opt_sqsum_kernel, dim3(ts.total_blocks), dim3(256), 0, s, ts,
                            (const float *)grad, 1.f, vec, (double *)ws);
-        hipLaunchKernelGGL(opt_clip_kernel, dim3(t.total_blocks), dim3(256), 0, s, t, grad,
+        hipLaunchKernelGGL(opt_clip_kernel, dim3(tu.total_blocks), dim3(256), 0, s, tu, grad,
                            (const double *)ws, clip_norm, vec);
         smmd_status st = last_launch_status();
         if (st != SMMD_OK) return st;
@@ -404,13 +462,15 @@ smmd_status smmd_adam_flat(float *param, const float *grad, float *m, float *v,
     hipStream_t s = (hipStream_t)stream;
     for (int first = 0; first < n_tensors; first += OPT_MAX) {
         const int count = (n_tensors - first < OPT_MAX) ? n_tensors - first : OPT_MAX;
-        OptTable t;
-        if (!build_opt(offsets, first, count, t)) return SMMD_EINVAL;
+        OptTable ts, tu;
+        if (!build_opt(offsets, first, count, OPT_SQ_CHUNK, ts) ||
+            !build_opt(offsets, first, count, OPT_UP_CHUNK, tu))
+            return SMMD_EINVAL;
         const int vec = opt_vec(offsets + first, count, param, grad, m, v);
         if (clip_norm > 0.f)
-            hipLaunchKernelGGL(opt_sqsum_kernel, dim3(t.total_blocks), dim3(256), 0, s, t, grad,
+            hipLaunchKernelGGL(opt_sqsum_kernel, dim3(ts.total_blocks), dim3(256), 0, s, ts, grad,
                                grad_scale, vec, (double *)ws);
-        hipLaunchKernelGGL(opt_adam_kernel, dim3(t.total_blocks), dim3(256), 0, s, t, param, grad,
+        hipLaunchKernelGGL(opt_adam_kernel, dim3(tu.total_blocks), dim3(256), 0, s, tu, param, grad,
                            m, v, (const double *)ws, grad_scale, clip_norm, (float)lr_t, beta1,
                            beta2, eps, vec);
         smmd_status st = last_launch_status();
