@@ -54,6 +54,44 @@ __device__ __forceinline__ double block_sum(double x, double *red) {
     return t;
 }
 
+// ---- in-launch hand-off to a last-arriving workgroup (CDNA4 guide G16) -----
+// Producers store the published words WRITE-THROUGH (sc1: a relaxed
+// agent-scope atomic store), so no release fence (an L2 write-back per block,
+// which made a 1233-block pass 4x slower); the storing wave drains, then lane 0
+// takes a ticket.  The last arriver acquires once and reads with plain loads.
+__device__ __forceinline__ void store_wt(float *p, float x) {
+    __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void store_wt(double *p, double x) {
+    __hip_atomic_store(reinterpret_cast<unsigned long long *>(p),
+                       (unsigned long long)__double_as_longlong(x), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Called by every lane of the one wave that made all the write-through stores
+// being published.  Returns 1 in every lane for the arrivals-th arriver.
+__device__ __forceinline__ int wave_ticket(unsigned *ctr, unsigned arrivals) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned prev = 0;
+    if ((threadIdx.x & 63) == 0)
+        prev = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    prev = __shfl(prev, 0, SMMD_WAVE);
+    return prev == arrivals - 1;
+}
+
+// Last arriver: one lane's agent-scope acquire (drops this CU's stale L1
+// lines), its drain, then the barrier; afterwards every wave may load.
+__device__ __forceinline__ void acquire_block() {
+    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+}
+
+__device__ __forceinline__ void ticket_reset(unsigned *ctr) {
+    if (threadIdx.x == 0) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 inline smmd_status hip_status(hipError_t e) {
     return e == hipSuccess ? SMMD_OK : SMMD_EHIP;
 }

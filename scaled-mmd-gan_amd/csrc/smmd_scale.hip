@@ -10,10 +10,28 @@ namespace smmd {
 
 constexpr int SQ_CHUNK = 4096;   // floats per block of the squared-norm pass
 
-// ---- per-(row, chunk) partial sum of squares -------------------------------
-__global__ __launch_bounds__(256) void sqnorm_partial_kernel(const float *__restrict__ jac,
-                                                             int64_t per_sample, int nchunk,
-                                                             int vec, double *__restrict__ part) {
+struct ScaledLossArgs {
+    const float *jac;
+    int64_t per_sample;
+    int nchunk, vec;
+    double *part;        // ws + 256: [rows * nchunk] partials
+    unsigned *counter;   // ws + 0: arrival ticket (zero at rest)
+    int n_cols, b, b_total, dof, variant, sqrt_scale;
+    const float *feat;
+    const float *base_loss;
+    float sc;
+    float *out;
+    float *per_sample_out;
+};
+
+__device__ void scaled_loss_final(const ScaledLossArgs &a);
+
+// ---- per-(row, chunk) partial sum of squares; the last block to arrive runs
+// the finalize (per-sample norms, J, nD, scale, losses) ---------------------
+__global__ __launch_bounds__(256) void sqnorm_partial_kernel(ScaledLossArgs a) {
+    const float *__restrict__ jac = a.jac;
+    const int64_t per_sample = a.per_sample;
+    const int nchunk = a.nchunk, vec = a.vec;
     const int row = blockIdx.x / nchunk, ch = blockIdx.x % nchunk;
     const float *p = jac + (size_t)row * per_sample;
     const int64_t b0 = (int64_t)ch * SQ_CHUNK;
@@ -31,15 +49,30 @@ __global__ __launch_bounds__(256) void sqnorm_partial_kernel(const float *__rest
         for (int64_t i = b0 + threadIdx.x; i < e0; i += 256) acc = fmaf(p[i], p[i], acc);
     }
     __shared__ double red[4];
+    __shared__ int last;
     const double s = block_sum<4>((double)acc, red);
-    if (threadIdx.x == 0) part[blockIdx.x] = s;
+    if (threadIdx.x < 64) {      // wave 0: publish the partial write-through, then the ticket
+        if (threadIdx.x == 0) store_wt(a.part + blockIdx.x, s);
+        const int l = wave_ticket(a.counter, gridDim.x);
+        if (threadIdx.x == 0) last = l;
+    }
+    __syncthreads();
+    if (!last) return;
+    acquire_block();
+    scaled_loss_final(a);
+    ticket_reset(a.counter);
 }
 
-// ---- finalize: per-sample norms, J, nD, scale, losses (one block) ----------
-__global__ __launch_bounds__(256) void scaled_loss_final_kernel(
-    const double *__restrict__ part, int n_cols, int b, int b_total, int nchunk,
-    const float *feat, int dof, const float *base_loss, float sc, int variant, int sqrt_scale,
-    float *out, float *per_sample_out) {
+// ---- finalize: per-sample norms, J, nD, scale, losses (one 256-thread block;
+// partials summed in fixed order) --------------------------------------------
+__device__ void scaled_loss_final(const ScaledLossArgs &a) {
+    const double *__restrict__ part = a.part;
+    const int n_cols = a.n_cols, b = a.b, b_total = a.b_total, nchunk = a.nchunk;
+    const float *feat = a.feat;
+    const int dof = a.dof, variant = a.variant, sqrt_scale = a.sqrt_scale;
+    const float *base_loss = a.base_loss;
+    const float sc = a.sc;
+    float *out = a.out, *per_sample_out = a.per_sample_out;
     __shared__ double red[4];
     double jsum = 0.0;
     for (int s = threadIdx.x; s < b; s += 256) {
@@ -56,10 +89,10 @@ __global__ __launch_bounds__(256) void scaled_loss_final_kernel(
     jsum = block_sum<4>(jsum, red);
     double nd = 0.0;
     if (variant == 1 && feat) {
-        double a = 0.0;
-        for (int i = threadIdx.x; i < b * dof; i += 256) a += (double)feat[i] * (double)feat[i];
-        a = block_sum<4>(a, red);
-        nd = a / ((double)b_total * dof);               // model.py:385
+        double fs = 0.0;
+        for (int i = threadIdx.x; i < b * dof; i += 256) fs += (double)feat[i] * (double)feat[i];
+        fs = block_sum<4>(fs, red);
+        nd = fs / ((double)b_total * dof);              // model.py:385
     }
     if (threadIdx.x == 0) {
         const float J = (float)(jsum / (double)b_total); // model.py:384
@@ -367,7 +400,7 @@ extern "C" {
 size_t smmd_scaled_loss_workspace_bytes(int rows, int64_t per_sample) {
     if (rows < 1 || per_sample < 1) return 0;
     const int64_t nchunk = (per_sample + SQ_CHUNK - 1) / SQ_CHUNK;
-    return align_up((size_t)rows * nchunk * sizeof(double), 256);
+    return 256 + align_up((size_t)rows * nchunk * sizeof(double), 256);   // ticket + partials
 }
 
 smmd_status smmd_scaled_loss_fwd(const float *jac, int n_cols, int b, int b_total,
@@ -383,12 +416,28 @@ smmd_status smmd_scaled_loss_fwd(const float *jac, int n_cols, int b, int b_tota
     if (!ws || ws_bytes < smmd_scaled_loss_workspace_bytes(rows, per_sample)) return SMMD_EWORKSPACE;
     const int nchunk = (int)((per_sample + SQ_CHUNK - 1) / SQ_CHUNK);
     const int vec = (per_sample % 4 == 0) && ((uintptr_t)jac % 16 == 0);
-    hipStream_t s = (hipStream_t)stream;
-    hipLaunchKernelGGL(sqnorm_partial_kernel, dim3(rows * nchunk), dim3(256), 0, s, jac,
-                       per_sample, nchunk, vec, (double *)ws);
-    hipLaunchKernelGGL(scaled_loss_final_kernel, dim3(1), dim3(256), 0, s, (const double *)ws,
-                       n_cols, b, b_total, nchunk, feat, dof, base_loss, sc, variant, sqrt_scale,
-                       out, per_sample_out);
+    ScaledLossArgs a;
+    a.jac = jac;
+    a.per_sample = per_sample;
+    a.nchunk = nchunk;
+    a.vec = vec;
+    // ticket first, at a fixed offset: a cached workspace reused for fewer rows
+    // must not find its counter inside an earlier call's partials
+    a.counter = (unsigned *)ws;
+    a.part = (double *)((char *)ws + 256);
+    a.n_cols = n_cols;
+    a.b = b;
+    a.b_total = b_total;
+    a.dof = dof;
+    a.variant = variant;
+    a.sqrt_scale = sqrt_scale;
+    a.feat = feat;
+    a.base_loss = base_loss;
+    a.sc = sc;
+    a.out = out;
+    a.per_sample_out = per_sample_out;
+    hipLaunchKernelGGL(sqnorm_partial_kernel, dim3(rows * nchunk), dim3(256), 0,
+                       (hipStream_t)stream, a);
     return last_launch_status();
 }
 

@@ -190,9 +190,10 @@ def test_reference_schedule_applies_the_lean_update(dev):
         scale = float(ga.abs().max())
         # The two schedules run different autograd graphs, so MIOpen picks other
         # backward solvers (combined data+weight calls, bwd-data for the fake
-        # batch): measured differences up to 1e-3 of max for D and 8e-4 for G
-        # (amplified through the generator's BatchNorm backward).  A schedule
-        # bug (a leaked or missing gradient set) is O(1).
-        rtol, atol = 1e-3, 2e-3 * scale
+        # batch): measured differences up to 9.5e-3 of max for D and 6.2e-3 for
+        # G (amplified through the generator's BatchNorm backward), in some runs
+        # of the same build and not in others.  A schedule bug (a leaked or
+        # missing gradient set) is O(1).
+        rtol, atol = 1e-3, 2e-2 * scale
         assert torch.allclose(gb, ga, rtol=rtol, atol=atol), (
             name, scale, float((gb - ga).abs().max()))

@@ -346,6 +346,22 @@ def test_sn_paths_agree_and_barrier_state(dev, monkeypatch):
         _close(a[2][i], b[2][i], 1e-6 * np.abs(b[2][i]).max(), 1e-5, 'gW %d' % i)
 
 
+def test_sn_repeated_calls_track_weights(dev, monkeypatch):
+    """Workspace state carried between calls (slabs, u') never leaks into the
+    next call: new weights each call, checked against the oracle from the u
+    the previous call left."""
+    _sn_path(monkeypatch, 'multipass')
+    shapes = [(1024, 4608), (64, 27), (1, 1024), (130, 300)]
+    mods, bank, rng = _sn_bank(dev, shapes, 21)
+    for _ in range(4):
+        with torch.no_grad():
+            for m in mods:
+                m.weight.add_(torch.randn_like(m.weight) * 0.01)
+        u0 = [e.u.cpu().numpy().astype(np.float64) for e in bank.entries]
+        outs = bank.refresh(update_u=True)
+        _check_sn(mods, bank, u0, outs, None)
+
+
 def test_sn_over_resident_capacity(dev, monkeypatch):
     """More tiles than the co-resident grid holds in registers: the call falls
     back to the multi-pass launch set and stays correct."""
@@ -399,6 +415,23 @@ def test_scaled_loss_vs_oracle(dev, variant, sqrt_scale):
     if variant == 'value_and_grad':
         _grad_close(ft.grad.cpu().numpy(), coefq * 2.0 / (b * 2) * feat.astype(np.float64),
                     'd feat')
+
+
+def test_scaled_loss_workspace_reuse(dev):
+    """The squared-norm pass elects its finalizing block by a ticket at a fixed
+    offset of the cached workspace; calls with fewer rows reuse the buffer
+    (whose partial slab then holds an earlier call's values) and must still
+    finalize once, correctly."""
+    from gan.core import ops
+    rng = np.random.default_rng(17)
+    for b, per in ((24, (3, 64, 64)), (5, (3, 9, 7)), (64, (3, 32, 32)), (1, (3, 4, 4))):
+        jac = rng.standard_normal((1, b) + per).astype(np.float32) * 0.1
+        jt = torch.tensor(jac, device=dev)
+        bt = torch.tensor(np.float32(0.5), device=dev)
+        g, aux = ops.scaled_loss(bt, jt, None, sc=10.0)
+        J = np.mean(O.squared_norm_per_sample(jac[0]))
+        _close(aux[3].item(), J, 0, 1e-5, 'J b=%d' % b)
+        _close(g.item(), 0.5 * O.scale_factor(J, 10.0, 0.0, 'grad'), 0, 1e-5, 'g_loss b=%d' % b)
 
 
 def test_smmd_objective_end_to_end(dev):
