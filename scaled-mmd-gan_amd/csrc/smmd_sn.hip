@@ -49,10 +49,11 @@ struct SnLayerDev {
     float *gs;
     float *p1;       // ws [nrt][K]
     float *vraw;     // ws [K]
-    float *q2;       // ws [nct][N]
+    float *q2;       // ws [N][nctp] row partials, one contiguous 16-B aligned row per n
     float *ucur;     // ws [N]  u' of the last iteration
     float *dotp;     // ws [ntiles] backward partial <G, W>
     int N, K, nrt, nct;
+    int nctp;        // nct rounded up to a multiple of 4
     int tile_begin;
     int vec;         // K % 4 == 0 and 16-byte aligned rows
 };
@@ -178,75 +179,119 @@ __global__ __launch_bounds__(256) void sn_p2_kernel(SnTable t) {
 #pragma unroll
     for (int i = 0; i < SN_RPW; ++i) part[i] = wave_sum(part[i]);
     if (lane == 0) {
-        float *dst = L.q2 + (size_t)ct * L.N;
 #pragma unroll
         for (int i = 0; i < SN_RPW; ++i)
-            if (r0 + i < L.N) dst[r0 + i] = part[i];
+            if (r0 + i < L.N) L.q2[(size_t)(r0 + i) * L.nctp + ct] = part[i];
     }
 }
 
-// one block (1024 threads) per layer: norms, v, u', sigma.  Every loop body
-// issues independent loads (unrolled) so the block is not a latency chain.
-__global__ __launch_bounds__(1024) void sn_r2_kernel(SnTable t) {
-    const SnLayerDev &L = t.L[blockIdx.x];
-    __shared__ double red[16];
-    const int tid = threadIdx.x;
-    // ||v_raw||
-    double a = 0.0;
-#pragma unroll 4
-    for (int k = tid; k < L.K; k += 1024) {
+// u_raw[n] * ||v_raw|| = sum over column tiles c < nct of q2[n][c], in order.
+// The row is contiguous and 16-B aligned, so all of its loads are issued
+// before the first add (the [nct][N] layout cost one L2 round trip per pair).
+__device__ __forceinline__ float q2_row_sum(const SnLayerDev &L, int n) {
+    const float4 *q = reinterpret_cast<const float4 *>(L.q2 + (size_t)n * L.nctp);
+    const int n4 = L.nctp >> 2;
+    float s = 0.f;
+    for (int j0 = 0; j0 < n4; j0 += 8) {
+        float4 b[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            b[j] = (j0 + j < n4) ? q[j0 + j] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int c = (j0 + j) * 4;
+            if (c + 0 < L.nct) s += b[j].x;
+            if (c + 1 < L.nct) s += b[j].y;
+            if (c + 2 < L.nct) s += b[j].z;
+            if (c + 3 < L.nct) s += b[j].w;
+        }
+    }
+    return s;
+}
+
+// norms, v, u', sigma of one layer (sn.py:12-13, :38-42) by one 1024-thread
+// block, from v_raw [K] and the row partials q2.  With r_n = (W v_raw)_n:
+//   nv = ||v_raw|| + eps, u_raw = r / nv, nu = ||u_raw|| + eps,
+//   u' = u_raw / nu, sigma = u_raw . u' = ||u_raw||^2 / nu.
+// Every input is loaded up front and the two norms share ONE block
+// reduction (||u_raw||^2 = sum r_n^2 / nv^2), so the block makes one round
+// of dependent global loads instead of four.
+constexpr int EP_KREG = 8;    // v_raw values per thread kept in registers (K <= 8192)
+constexpr int EP_NREG = 2;    // rows per thread kept in registers (N <= 2048)
+
+__device__ void sn_layer_epilogue(const SnTable &t, const SnLayerDev &L, int last_iter,
+                                  double *red) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    float vr[EP_KREG], rs[EP_NREG];
+#pragma unroll
+    for (int j = 0; j < EP_KREG; ++j) {
+        const int k = tid + j * 1024;
+        vr[j] = (k < L.K) ? L.vraw[k] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < EP_NREG; ++j) {
+        const int n = tid + j * 1024;
+        rs[j] = (n < L.N) ? q2_row_sum(L, n) : 0.f;
+    }
+    double a = 0.0, b = 0.0;
+#pragma unroll
+    for (int j = 0; j < EP_KREG; ++j) a += (double)vr[j] * (double)vr[j];
+    for (int k = tid + EP_KREG * 1024; k < L.K; k += 1024) {
         const double x = (double)L.vraw[k];
         a += x * x;
     }
-    const float nv = (float)sqrt(block_sum<16>(a, red)) + t.eps;     // sn.py:13
-#pragma unroll 4
-    for (int k = tid; k < L.K; k += 1024) L.v[k] = L.vraw[k] / nv;
-    // u_raw = W v = (W v_raw) / nv, summed over column tiles in fixed order
-    float ur[2] = {0.f, 0.f};
-    double b = 0.0;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < EP_NREG; ++j) b += (double)rs[j] * (double)rs[j];
+    for (int n = tid + EP_NREG * 1024; n < L.N; n += 1024) {      // rare: N > 2048
+        const float r = q2_row_sum(L, n);
+        L.ucur[n] = r;
+        b += (double)r * (double)r;
+    }
+    a = wave_sum(a);
+    b = wave_sum(b);
+    __syncthreads();
+    if (lane == 0) {
+        red[w] = a;
+        red[16 + w] = b;
+    }
+    __syncthreads();
+    double sa = 0.0, sb = 0.0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        sa += red[i];
+        sb += red[16 + i];
+    }
+    const float nv = (float)sqrt(sa) + t.eps;                   // sn.py:13
+    const double uu = sb / ((double)nv * (double)nv);           // ||u_raw||^2
+    const float nu = (float)sqrt(uu) + t.eps;
+#pragma unroll
+    for (int j = 0; j < EP_KREG; ++j) {
+        const int k = tid + j * 1024;
+        if (k < L.K) L.v[k] = vr[j] / nv;
+    }
+    for (int k = tid + EP_KREG * 1024; k < L.K; k += 1024) L.v[k] = L.vraw[k] / nv;
+    const bool upd = t.update_u && last_iter;
+#pragma unroll
+    for (int j = 0; j < EP_NREG; ++j) {
         const int n = tid + j * 1024;
         if (n < L.N) {
-            float s0 = 0.f, s1 = 0.f;
-            int c = 0;
-            for (; c + 1 < L.nct; c += 2) {
-                s0 += L.q2[(size_t)c * L.N + n];
-                s1 += L.q2[(size_t)(c + 1) * L.N + n];
-            }
-            if (c < L.nct) s0 += L.q2[(size_t)c * L.N + n];
-            ur[j] = (s0 + s1) / nv;
-            b += (double)ur[j] * (double)ur[j];
-        }
-    }
-    for (int n = tid + 2048; n < L.N; n += 1024) {          // N > 2048: rare, simple path
-        float s0 = 0.f;
-        for (int c = 0; c < L.nct; ++c) s0 += L.q2[(size_t)c * L.N + n];
-        s0 /= nv;
-        L.ucur[n] = s0;
-        b += (double)s0 * (double)s0;
-    }
-    const float nu = (float)sqrt(block_sum<16>(b, red)) + t.eps;
-    double sg = 0.0;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const int n = tid + j * 1024;
-        if (n < L.N) {
-            const float un = ur[j] / nu;                    // u' = l2n(v W)
-            sg += (double)ur[j] * (double)un;               // sigma = (v W) . u'  sn.py:42
+            const float un = (rs[j] / nv) / nu;                 // u' = l2n(v W)
             L.ucur[n] = un;
-            if (t.update_u && t.last_iter) L.u[n] = un;
+            if (upd) L.u[n] = un;
         }
     }
-    for (int n = tid + 2048; n < L.N; n += 1024) {
-        const float r = L.ucur[n];
-        const float un = r / nu;
-        sg += (double)r * (double)un;
+    for (int n = tid + EP_NREG * 1024; n < L.N; n += 1024) {
+        const float un = (L.ucur[n] / nv) / nu;
         L.ucur[n] = un;
-        if (t.update_u && t.last_iter) L.u[n] = un;
+        if (upd) L.u[n] = un;
     }
-    sg = block_sum<16>(sg, red);
-    if (tid == 0 && t.last_iter) L.sigma[0] = (float)sg;
+    if (tid == 0) L.sigma[0] = (float)(uu / (double)nu);     // (v W) . u', sn.py:42
+}
+
+// R2: one 1024-thread block per layer runs the epilogue
+__global__ __launch_bounds__(1024) void sn_r2_kernel(SnTable t) {
+    __shared__ double red[32];
+    sn_layer_epilogue(t, t.L[blockIdx.x], t.last_iter, red);
 }
 
 __global__ __launch_bounds__(256) void sn_p3_kernel(SnTable t) {
@@ -500,43 +545,6 @@ __device__ __forceinline__ void sr_store(float *__restrict__ base, int N, int K,
     if (c0 + 3 < K) p[3] = o.w;
 }
 
-// the sn_r2 epilogue for layer L, run by one 1024-thread workgroup
-__device__ void sr_layer_epilogue(const SnTable &t, const SnLayerDev &L, int last_iter,
-                                  double *red) {
-    const int tid = threadIdx.x;
-    double a = 0.0;
-    for (int k = tid; k < L.K; k += 1024) {
-        const double x = (double)L.vraw[k];
-        a += x * x;
-    }
-    const float nv = (float)sqrt(block_sum<16>(a, red)) + t.eps;     // sn.py:13
-    for (int k = tid; k < L.K; k += 1024) L.v[k] = L.vraw[k] / nv;
-    double b = 0.0;
-    for (int n = tid; n < L.N; n += 1024) {
-        float s0 = 0.f, s1 = 0.f;
-        int c = 0;
-        for (; c + 1 < L.nct; c += 2) {
-            s0 += L.q2[(size_t)c * L.N + n];
-            s1 += L.q2[(size_t)(c + 1) * L.N + n];
-        }
-        if (c < L.nct) s0 += L.q2[(size_t)c * L.N + n];
-        const float ur = (s0 + s1) / nv;
-        L.ucur[n] = ur;
-        b += (double)ur * (double)ur;
-    }
-    const float nu = (float)sqrt(block_sum<16>(b, red)) + t.eps;
-    double sg = 0.0;
-    for (int n = tid; n < L.N; n += 1024) {
-        const float ur = L.ucur[n];
-        const float un = ur / nu;                               // u' = l2n(v W)
-        sg += (double)ur * (double)un;                          // sigma, sn.py:42
-        L.ucur[n] = un;
-        if (t.update_u && last_iter) L.u[n] = un;
-    }
-    sg = block_sum<16>(sg, red);
-    if (tid == 0) L.sigma[0] = (float)sg;
-}
-
 // tile j of this block (strided over the grid), or false past the end
 #define SR_FOR_TILES(j, q, L)                                                    \
     for (int j = 0; j < SR_TMAX; ++j)                                            \
@@ -549,7 +557,7 @@ __global__ __launch_bounds__(SR_THREADS) void sn_resident_kernel(SnTable t, Grid
     const unsigned G = gridDim.x;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     __shared__ float red[SR_GROUP][16][SN_TC];
-    __shared__ double dred[16];
+    __shared__ double dred[32];
 
     SR_STAMP(bar, 0);
     float4 wa[SR_TMAX], wb[SR_TMAX];
@@ -623,7 +631,7 @@ __global__ __launch_bounds__(SR_THREADS) void sn_resident_kernel(SnTable t, Grid
         grid_sync(bar, G);
         if (it == 0) SR_STAMP(bar, 4);
 
-        // ---- B: per-row partial dots with v_raw -> q2[ct][row]
+        // ---- B: per-row partial dots with v_raw -> q2[row][ct]
 #pragma unroll
         SR_FOR_TILES(j, q, L) {
             const int c0 = q.ct * SN_TC + lane * 4;
@@ -637,9 +645,8 @@ __global__ __launch_bounds__(SR_THREADS) void sn_resident_kernel(SnTable t, Grid
             d1 = wave_sum(d1);
             if (lane == 0) {
                 const int r0 = q.rt * SR_TR + w, r1 = r0 + 16;
-                float *dst = L.q2 + (size_t)q.ct * L.N;
-                if (r0 < L.N) dst[r0] = d0;
-                if (r1 < L.N) dst[r1] = d1;
+                if (r0 < L.N) L.q2[(size_t)r0 * L.nctp + q.ct] = d0;
+                if (r1 < L.N) L.q2[(size_t)r1 * L.nctp + q.ct] = d1;
             }
         }
         if (it == 0) SR_STAMP(bar, 5);
@@ -648,7 +655,7 @@ __global__ __launch_bounds__(SR_THREADS) void sn_resident_kernel(SnTable t, Grid
 
         // ---- R: norms, v, u', sigma (one workgroup per layer)
         const int last = (it == num_iters - 1);
-        for (int l = blockIdx.x; l < t.n_layers; l += G) sr_layer_epilogue(t, t.L[l], last, dred);
+        for (int l = blockIdx.x; l < t.n_layers; l += G) sn_layer_epilogue(t, t.L[l], last, dred);
         if (it == 0) SR_STAMP(bar, 7);
         grid_sync(bar, G);
         if (it == 0) SR_STAMP(bar, 8);
@@ -765,7 +772,7 @@ static size_t layer_ws_bytes(int N, int K) {
     size_t b = 0;
     b += align_up((size_t)nrt * K * 4, 256);   // p1
     b += align_up((size_t)K * 4, 256);         // vraw
-    b += align_up((size_t)nct * N * 4, 256);   // q2
+    b += align_up((size_t)((nct + 3) & ~3) * N * 4, 256);   // q2
     b += align_up((size_t)N * 4, 256);         // ucur
     b += align_up((size_t)nrt * nct * 4, 256); // dotp
     return b;
@@ -805,7 +812,8 @@ static bool build_table(const smmd_sn_layer *layers, int first, int count, char 
         const int nrt_max = ceil_div(src.N, SR_TR);
         L.p1 = (float *)p;   p += align_up((size_t)nrt_max * L.K * 4, 256);
         L.vraw = (float *)p; p += align_up((size_t)L.K * 4, 256);
-        L.q2 = (float *)p;   p += align_up((size_t)L.nct * L.N * 4, 256);
+        L.nctp = (L.nct + 3) & ~3;
+        L.q2 = (float *)p;   p += align_up((size_t)L.nctp * L.N * 4, 256);
         L.ucur = (float *)p; p += align_up((size_t)L.N * 4, 256);
         L.dotp = (float *)p; p += align_up((size_t)nrt_max * L.nct * 4, 256);
         off += layer_ws_bytes(L.N, L.K);
