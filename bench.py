@@ -216,6 +216,10 @@ def main():
     ap.add_argument('--miopen-winograd', type=int, default=1,
                     help='0: disable MIOpen Winograd solvers (immediate mode then picks '
                          'the MFMA implicit-GEMM ones)')
+    ap.add_argument('--miopen-find', type=int, default=0,
+                    help='1: torch.backends.cudnn.benchmark (MIOpen Find: times every '
+                         'applicable solver per conv problem during warmup); the find '
+                         'results persist in MIOPEN_USER_DB_PATH when set')
     ap.add_argument('--cpu-seconds', type=float, default=20.0)
     ap.add_argument('--ref-schedule-steps', type=int, default=30,
                     help='steps timed with the reference schedule (both gradient sets '
@@ -244,9 +248,13 @@ def main():
             dist.init_process_group('nccl', device_id=dev)
         else:
             dist.init_process_group(backend)
+    # MIOpen solver choice: the committed find db (gan/core/miopen_db.py),
+    # installed before the first convolution
+    from gan.core import miopen_db
+    miopen_db.install()
     # MIOpen immediate mode: one kernel compile per conv config on a fresh box;
     # benchmark=True would compile every candidate solver (minutes per shape).
-    torch.backends.cudnn.benchmark = False
+    torch.backends.cudnn.benchmark = bool(args.miopen_find)
 
     from gan.core.smmd import SMMD
     cfg = imagenet_config()
@@ -372,7 +380,9 @@ def main():
                    'model': 'snresnet', 'global_batch': BATCH * world, 'seq_len': None,
                    'parallelism': 'dp%d' % world, 'dp_mode': args.dp_mode,
                    'memory_format': 'channels_last' if args.channels_last else 'nchw',
-                   'miopen_winograd': bool(args.miopen_winograd)},
+                   'miopen_winograd': bool(args.miopen_winograd),
+                   'miopen_find': bool(args.miopen_find),
+                   'miopen_db': os.environ.get('MIOPEN_USER_DB_PATH')},
         'roofline': {'bound': 'hbm', 'kernel': dom, 'achieved': kernels[dom]['GB_s'],
                      'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': kernels[dom]['frac'],
                      'traffic': pmc_traffic(dom), 'avg_ms': kernels[dom]['avg_ms'],

@@ -123,6 +123,8 @@ def main(argv=None):
 
     flags = make_flags(argv=argv)
     flags.num_gpus = num_gpus_from_env()
+    from gan.core import miopen_db
+    miopen_db.install()                    # before the first convolution
     world = int(os.environ.get('WORLD_SIZE', '1'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     torch.cuda.set_device(local)

@@ -209,3 +209,20 @@ def test_three_sample_lr_scheduler_logic(monkeypatch):
     assert gan.decays == 1 and abs(gan.lr - 0.8e-4) < 1e-12
     assert sc.three_sample_chances == 0
     assert best == [1, 3]                      # KID improved at scorings 1 and 3
+
+
+def test_miopen_db_install(monkeypatch):
+    """The committed MIOpen find db is copied to a writable per-process dir
+    and MIOPEN_USER_DB_PATH points at it; a user setting is left alone."""
+    import os
+    from gan.core import miopen_db
+    monkeypatch.delenv('MIOPEN_USER_DB_PATH', raising=False)
+    monkeypatch.delenv('SMMD_MIOPEN_DB', raising=False)
+    d = miopen_db.install()
+    assert d and os.environ['MIOPEN_USER_DB_PATH'] == d
+    names = sorted(os.listdir(d))
+    assert any(n.endswith('.ufdb.txt') for n in names), names
+    assert all(n.startswith('gfx950') for n in names)
+    monkeypatch.setenv('MIOPEN_USER_DB_PATH', '/somewhere/else')
+    assert miopen_db.install() is None
+    assert os.environ['MIOPEN_USER_DB_PATH'] == '/somewhere/else'
