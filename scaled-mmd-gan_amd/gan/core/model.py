@@ -293,6 +293,39 @@ class MMD_GAN:
             self.sc *= c.sc_decay_rate
 
     # checkpoint: torch state (the TF Saver format is out of scope)
+    def save_checkpoint(self, checkpoint_dir, step=None):
+        """model.py:585-593: 'MMDGAN.model-<step>' (every 2000 steps) or
+        'best.model' (step None, the scorer's best KID); the 'checkpoint' file
+        names the latest save, as TF's checkpoint state does."""
+        import os
+        os.makedirs(checkpoint_dir, exist_ok=True)
+        name = 'best.model' if step is None else 'MMDGAN.model-%d' % step
+        path = os.path.join(checkpoint_dir, name + '.pt')
+        torch.save(self.state_dict(), path + '.tmp')
+        os.replace(path + '.tmp', path)                      # never a torn checkpoint
+        with open(os.path.join(checkpoint_dir, 'checkpoint.tmp'), 'w') as f:
+            f.write(name + '\n')
+        os.replace(os.path.join(checkpoint_dir, 'checkpoint.tmp'),
+                   os.path.join(checkpoint_dir, 'checkpoint'))
+        return path
+
+    def load_checkpoint(self, checkpoint_dir, ckpt_name=''):
+        """model.py:595-606: ``ckpt_name`` or the latest save; False if none."""
+        import os
+        if not ckpt_name:
+            state = os.path.join(checkpoint_dir, 'checkpoint')
+            if not os.path.exists(state):
+                return False
+            with open(state) as f:
+                ckpt_name = f.read().strip()
+        path = os.path.join(checkpoint_dir, ckpt_name)
+        if not path.endswith('.pt'):
+            path += '.pt'
+        if not os.path.exists(path):
+            return False
+        self.load_state_dict(torch.load(path, map_location=self.device, weights_only=True))
+        return True
+
     def state_dict(self):
         return {'G': self.generator.state_dict(), 'D': self.discriminator.state_dict(),
                 'sn_D': self.sn_D.state_dict(), 'sn_G': self.sn_G.state_dict(),
@@ -309,3 +342,5 @@ class MMD_GAN:
         self.d_optim.load_state_dict(sd['d_optim'])
         self.step, self.lr, self.sc = sd['step'], sd['lr'], sd['sc']
         self.d_counter, self.g_counter = sd['counters']
+        self.g_optim.lr = self.lr
+        self.d_optim.lr = self.lr * self.config.learning_rate_D / self.config.learning_rate

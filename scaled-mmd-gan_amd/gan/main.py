@@ -5,10 +5,15 @@ trainer.
     python scaled-mmd-gan_amd/gan/main.py -config_file configs/imagenet_smmd.yml
     torchrun --nproc-per-node 8 scaled-mmd-gan_amd/gan/main.py -config_file ... -dp_mode global
 
-Data: datasets are not shipped (no network); ``-dataset synthetic`` (or any
-dataset whose files are absent, with a warning) feeds U[0,1] images of the
-configured size, matching the reference pipeline's value range
-(gan/core/pipeline.py:201, :403).
+Data (gan/core/pipeline.py): cifar10 (python or binary batches under
+-data_dir), imagenet / celebA (TFRecord shards tf_records_train/train-*).
+Datasets are not shipped (no network); ``-dataset synthetic`` (or any dataset
+whose files are absent, with a warning) feeds U[0,1] images of the configured
+size, matching the reference pipeline's value range (pipeline.py:201, :403).
+
+Checkpoints (model.py:559-566, :585-617): resumed from -checkpoint_dir/-name
+(-ckpt_name or the latest save) at start; saved every 2000 steps after a
+generator update.
 """
 from __future__ import annotations
 
@@ -116,6 +121,26 @@ def output_size_for(flags):
     return flags.output_size, flags.c_dim
 
 
+CHECKPOINT_FREQ = 2000                   # model.py:609
+
+
+def make_pipeline(flags, size, c_dim, dev, rank=0, world=1):
+    """The dataset's pipeline (gan/core/pipeline.py:458-476), or synthetic
+    U[0,1] images when the dataset's files are absent."""
+    import warnings
+    from gan.core import pipeline as P
+    args = (size, c_dim, flags.real_batch_size, flags.data_dir)
+    kw = dict(device=dev, rank=rank, world=world)
+    try:
+        cls = P.get_pipeline(flags.dataset)
+        return cls(*args, **kw)
+    except (ValueError, FileNotFoundError) as e:
+        if flags.dataset != 'synthetic':
+            warnings.warn('dataset %r unavailable (%s): synthetic U[0,1] images'
+                          % (flags.dataset, e))
+        return P.Synthetic(*args, **kw)
+
+
 def main(argv=None):
     import torch
     import torch.distributed as dist
@@ -141,16 +166,25 @@ def main(argv=None):
     gan = Model(flags, device=dev, process_group=dist.group.WORLD if world > 1 else None,
                 dp_mode=flags.dp_mode, output_size=size, c_dim=c_dim)
     if flags.is_train:
-        gen = torch.Generator(device=dev).manual_seed(rank)
-        step = 0
-        while step <= flags.max_iteration:
-            images = torch.rand(flags.real_batch_size, c_dim, size, size, device=dev,
-                                generator=gen)
-            _, _, step = gan.train_step(images)
-            if gan.d_counter == 0 and (step % 100 == 0 or step <= 10):
-                g, d = gan.check_finite()
-                if rank == 0:
-                    gan.timer(step, '%s, G: %.8f, D: %.8f' % (gan.optim_name, g, d))
+        pipe = make_pipeline(flags, size, c_dim, dev, rank, world)
+        ckpt_dir = os.path.join(flags.checkpoint_dir, flags.name)
+        if gan.load_checkpoint(ckpt_dir, flags.ckpt_name):
+            print(' [*] Load SUCCESS, re-starting at step %d with learning rate %.7f'
+                  % (gan.step, gan.lr))
+        else:
+            print(' [!] Load failed...')
+        step = gan.step
+        try:
+            while step <= flags.max_iteration:
+                _, _, step = gan.train_step(pipe.next())
+                if gan.d_counter == 0 and (step % 100 == 0 or step <= 10):
+                    g, d = gan.check_finite()
+                    if rank == 0:
+                        gan.timer(step, '%s, G: %.8f, D: %.8f' % (gan.optim_name, g, d))
+                if gan.d_counter == 0 and step % CHECKPOINT_FREQ == 0 and rank == 0:
+                    gan.save_checkpoint(ckpt_dir, step)          # model.py:608-612
+        finally:
+            pipe.stop()
     if world > 1:
         dist.destroy_process_group()
 
