@@ -24,6 +24,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
+from .collectives import all_reduce_, gather_rows
 from . import _lib
 
 _eps = 1.0e-5   # gan/core/mmd.py:6
@@ -129,10 +130,11 @@ class _MMD2Fused(torch.autograd.Function):
         if group is not None and dist.get_world_size(group) > 1:
             world, rank = dist.get_world_size(group), dist.get_rank(group)
             ml, nl = X.shape[0], Y.shape[0]
-            Xa = torch.empty((world * ml, d), device=dev, dtype=torch.float32)
-            Ya = torch.empty((world * nl, d), device=dev, dtype=torch.float32)
-            dist.all_gather_into_tensor(Xa, X, group=group)
-            dist.all_gather_into_tensor(Ya, Y, group=group)
+            # ONE all-gather of the packed local rows [X; Y] (latency-bound:
+            # 2 x 256 B per rank at batch 64), then each side's rows in rank order
+            Za = gather_rows(torch.cat([X, Y], 0), group).view(world, ml + nl, d)
+            Xa = Za[:, :ml].reshape(world * ml, d)
+            Ya = Za[:, ml:].reshape(world * nl, d)
             rows = (rank * ml, (rank + 1) * ml, rank * nl, (rank + 1) * nl)
         else:
             group = None
@@ -153,7 +155,7 @@ class _MMD2Fused(torch.autograd.Function):
             st = L.smmd_mmd2_fwd(*args)
         _lib.check(st, 'smmd_mmd2_fwd')
         if group is not None:
-            dist.all_reduce(sums, group=group)
+            all_reduce_(sums, group)
             _lib.check(L.smmd_mmd2_combine(desc, _lib.ptr(sums), m, n, 1 if biased else 0,
                                            _lib.ptr(out), _lib.stream_handle(dev)),
                        'smmd_mmd2_combine')

@@ -29,6 +29,7 @@ import torch.distributed as dist
 
 from . import mmd, ops
 from .architecture import get_networks
+from .collectives import all_reduce_
 from .optim import FlatAdam
 from .sn import SpectralNormBank
 from .snops import sn_modules
@@ -213,10 +214,10 @@ class MMD_GAN:
             # per-tower clip (model.py:449,455), then the tower mean (:257-258)
             if opt.clip_norm > 0:
                 opt.clip_()
-            dist.all_reduce(opt.flat_grad, group=self.group)
+            all_reduce_(opt.flat_grad, self.group)
             opt.step(grad_scale=1.0 / self.world, clip=False)
         else:
-            dist.all_reduce(opt.flat_grad, group=self.group)
+            all_reduce_(opt.flat_grad, self.group)
             opt.step()
 
     def d_step(self, images):

@@ -14,6 +14,7 @@ import torch
 import torch.distributed as dist
 
 from . import _lib
+from .collectives import all_reduce_
 from .convops import input_grad_only
 from .mmd import _eps
 
@@ -84,7 +85,7 @@ class _ScaledLoss(torch.autograd.Function):
         _lib.check(st, 'smmd_scaled_loss_fwd')
         if group is not None:
             # J and nD are partial means over the global batch: sum them
-            dist.all_reduce(out[3:5], group=group)
+            all_reduce_(out[3:5], group)
             _lib.check(L.smmd_scaled_loss_finalize(_lib.ptr(out), float(sc), variant,
                                                    sqrt_scale, s), 'smmd_scaled_loss_finalize')
         ctx.save_for_backward(jac, feat_c, out)

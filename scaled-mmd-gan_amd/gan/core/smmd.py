@@ -5,6 +5,7 @@ import torch
 import torch.distributed as dist
 
 from . import mmd, ops
+from .collectives import all_reduce_
 from .model import MMD_GAN
 
 
@@ -40,7 +41,7 @@ class SWGAN(MMD_GAN):
         base = d_images.mean() - d_G.mean()          # g_loss = -(mean G - mean images)
         if self.dp_mode == 'global' and self.world > 1:
             base = base.clone()
-            dist.all_reduce(base, group=self.group)
+            all_reduce_(base, self.group)
             base = base / self.world
         return base
 

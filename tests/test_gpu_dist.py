@@ -1,0 +1,117 @@
+"""Two data-parallel ranks on ONE GPU (gloo: RCCL needs a GPU per rank), real
+libsmmd_hip kernels: one critic update in the all-gather ('global') mode
+equals one process on the concatenated batch:
+  * the same mmd2 / J / d_loss (the full (2n) x (2n) pairwise kernel),
+  * the same all-reduced critic gradient (the loss is global: SUM, no mean),
+  * the same parameters after clip + Adam on every rank.
+The generator has no BatchNorm here (batch_norm False): replica-local BN
+statistics would differ from the one-process batch by design (towers).
+Tolerances: MIOpen picks other kernels for batch 8 and 16, d_loss rtol 1e-4,
+gradients |d| <= 2e-3 max|ref| + 1e-3 |ref|."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip('torch')
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+N_PER_RANK = 8
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _cfg():
+    import argparse
+    from gan.main import default_flags
+    c = default_flags()
+    c.update(dict(batch_size=N_PER_RANK, output_size=32, architecture='sngan', kernel='rbf',
+                  model='smmd', batch_norm=False, with_sn=True, with_learnable_sn_scale=True,
+                  with_scaling=True, dof_dim=1, learning_rate=1e-4, dataset='cifar10'))
+    return argparse.Namespace(**c)
+
+
+def _inputs(world):
+    g = torch.Generator().manual_seed(7)
+    images = torch.rand(N_PER_RANK * world, 3, 32, 32, generator=g)
+    z = torch.empty(N_PER_RANK * world, 128).uniform_(-1, 1, generator=g)
+    return images, z
+
+
+def _critic_update(model, images, z):
+    """One d_step; returns (d_loss, aux, the gradient Adam applies, params after).
+    The critic's last SN scale is raised to 50 so its outputs spread and mmd2
+    is not a cancellation residue at the fp32 rounding of its sums."""
+    with torch.no_grad():
+        model.discriminator.l4.sn_scale.fill_(50.0)
+    model.sample_z = lambda n: z
+    cap = {}
+    step = model.d_optim.step
+
+    def hooked(*a, **k):
+        cap['g'] = model.d_optim.flat_grad.detach().clone()
+        return step(*a, **k)
+    model.d_optim.step = hooked
+    _, d_loss, aux = model.d_step(images)
+    torch.cuda.synchronize()
+    return (float(d_loss), aux.detach().cpu().numpy(), cap['g'].cpu().numpy(),
+            model.d_optim.flat_param.detach().cpu().numpy())
+
+
+def _worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, 'scaled-mmd-gan_amd')):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    torch.cuda.set_device(0)
+    dev = torch.device('cuda:0')
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from gan.core.smmd import SMMD
+    torch.manual_seed(0)
+    model = SMMD(_cfg(), device=dev, process_group=dist.group.WORLD, dp_mode='global')
+    images, z = _inputs(world)
+    sl = slice(rank * N_PER_RANK, (rank + 1) * N_PER_RANK)
+    res = _critic_update(model, images[sl].to(dev), z[sl].to(dev))
+    q.put((rank,) + res)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_global_mode_two_ranks_equal_one_process(dev):
+    from gan.core.smmd import SMMD
+    world = 2
+    torch.manual_seed(0)
+    single = SMMD(_cfg(), device=dev, batch_size=N_PER_RANK * world)
+    images, z = _inputs(world)
+    ref = _critic_update(single, images.to(dev), z.to(dev))
+
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = sorted([q.get(timeout=300) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, d_loss, aux, grad, params in outs:
+        np.testing.assert_allclose(d_loss, ref[0], rtol=1e-4)
+        np.testing.assert_allclose(aux[3], ref[1][3], rtol=1e-4)         # J, global batch
+        scale = np.abs(ref[2]).max()
+        np.testing.assert_allclose(grad, ref[2], rtol=1e-3, atol=2e-3 * scale)
+    # every rank applied the same update
+    np.testing.assert_array_equal(outs[0][4], outs[1][4])

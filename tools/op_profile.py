@@ -1,0 +1,50 @@
+"""Per-aten-op GPU time of the bench workload (torch.profiler), to attribute
+the non-convolution kernels of the step to the ops that launch them.
+
+    python tools/op_profile.py [--steps 6] [--out gpurun_out/ops.txt]
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, 'scaled-mmd-gan_amd')):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--steps', type=int, default=6)
+    ap.add_argument('--out', default='gpurun_out/ops.txt')
+    args = ap.parse_args()
+    import bench
+    from gan.core import miopen_db
+    from gan.core.smmd import SMMD
+    miopen_db.install()
+    dev = torch.device('cuda:0')
+    cfg = bench.imagenet_config()
+    torch.manual_seed(2)
+    model = SMMD(cfg, device=dev)
+    images = torch.rand(64, 3, 64, 64, device=dev)
+    model.step = 21
+    for _ in range(12):
+        model.train_step(images)
+    torch.cuda.synchronize()
+    from torch.profiler import ProfilerActivity, profile
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+        for _ in range(args.steps):
+            model.train_step(images)
+        torch.cuda.synchronize()
+    tab = prof.key_averages().table(sort_by='self_cuda_time_total', row_limit=60,
+                                    max_name_column_width=60)
+    os.makedirs(os.path.dirname(args.out) or '.', exist_ok=True)
+    with open(args.out, 'w') as f:
+        f.write(tab)
+    print(tab[:6000])
+
+
+if __name__ == '__main__':
+    main()
