@@ -208,6 +208,9 @@ def cpu_components(cfg, threads):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--batch', type=int, default=64,
+                    help='images per GPU: 64 is the headline (imagenet_smmd.yml); 256 is '
+                         'BASELINE configs[4] (the 256 x 256 pairwise tile per GPU)')
     ap.add_argument('--steps', type=int, default=60)
     ap.add_argument('--warmup', type=int, default=12)
     ap.add_argument('--dp-mode', default='global', choices=['global', 'tower'])
@@ -227,6 +230,8 @@ def main():
     ap.add_argument('--mmd-sweep', type=int, default=1,
                     help='1: SURVEY 8d MMD microbench grid; 2: two configs; 0: skip')
     args = ap.parse_args()
+    global BATCH
+    BATCH = args.batch
 
     if not args.miopen_winograd:      # read by MIOpen at its first solver query
         for k in ('MIOPEN_DEBUG_AMD_WINOGRAD_RXS_F2X3', 'MIOPEN_DEBUG_AMD_WINOGRAD_RXS_F3X2',
@@ -376,7 +381,7 @@ def main():
         'dtype': 'fp32',
         'data': 'synthetic (U[0,1] images in HBM, z~U(-1,1), random-init weights)',
         'config': {'workload': 'imagenet_smmd 64x64 SNResNet G/D, rbf kernel, scaling, SN, '
-                               'batch 64/GPU, 5D+1G schedule',
+                               'batch %d/GPU, 5D+1G schedule' % BATCH,
                    'model': 'snresnet', 'global_batch': BATCH * world, 'seq_len': None,
                    'parallelism': 'dp%d' % world, 'dp_mode': args.dp_mode,
                    'memory_format': 'channels_last' if args.channels_last else 'nchw',
