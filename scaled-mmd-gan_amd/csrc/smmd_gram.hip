@@ -23,6 +23,8 @@
 // 'FP32-input MFMA'), i.e. the dot products equal smmd_mmd.hip's dotk().
 #include "smmd_kern.hpp"
 
+#include <stdlib.h>
+
 namespace smmd {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
@@ -63,11 +65,12 @@ __global__ __launch_bounds__(256) void gram_prep_kernel(GramArgs g) {
     }
 }
 
-// stage a [64 rows][32 k] tile: 512 float4, two per thread (rows < 0: zero)
+// stage a [TM rows][32 k] tile: TM * 8 float4, TM / 32 per thread (rows < 0: zero)
+template <int TM>
 __device__ __forceinline__ void gram_fetch(const float *__restrict__ base, int ld, const int *rows,
-                                           int k0, float4 (&v)[2]) {
+                                           int k0, float4 (&v)[TM / 32]) {
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
+    for (int q = 0; q < TM / 32; ++q) {
         const int idx = threadIdx.x + 256 * q;
         const int r = rows[idx >> 3];
         v[q] = (r >= 0) ? *reinterpret_cast<const float4 *>(base + (size_t)r * ld + k0 + (idx & 7) * 4)
@@ -75,85 +78,112 @@ __device__ __forceinline__ void gram_fetch(const float *__restrict__ base, int l
     }
 }
 
-__device__ __forceinline__ void gram_stash(float (*T)[GLD], const float4 (&v)[2]) {
+template <int TM>
+__device__ __forceinline__ void gram_stash(float (*T)[GLD], const float4 (&v)[TM / 32]) {
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
+    for (int q = 0; q < TM / 32; ++q) {
         const int idx = threadIdx.x + 256 * q;
         float *p = &T[idx >> 3][(idx & 7) * 4];
         p[0] = v[q].x; p[1] = v[q].y; p[2] = v[q].z; p[3] = v[q].w;
     }
 }
 
-template <int KIND>
+// S = Z_rows Z^T on TM x TM block tiles: 4 waves in 2 x 2, each wave TM/2 x TM/2
+// = NS x NS MFMA tiles of 32 x 32 (NS accumulators per operand fragment, so a
+// 128 tile reads each LDS fragment once per 2 MFMAs and fetches half the L2 /
+// Infinity-Cache bytes per flop of a 64 tile)
+template <int KIND, int TM>
 __global__ __launch_bounds__(256) void gram_nt_kernel(GramArgs g) {
-    __shared__ float As[GT][GLD], Bs[GT][GLD];
-    __shared__ int arow[GT], brow[GT];
+    constexpr int NS = TM / 64;
+    __shared__ float As[TM][GLD], Bs[TM][GLD];
+    __shared__ int arow[TM], brow[TM];
     __shared__ double red[4][8];
     __shared__ int is_last;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int wm = w >> 1, wn = w & 1;
-    const int e0 = blockIdx.y * GT, j0 = blockIdx.x * GT;
-    if (threadIdx.x < GT) {
+    const int e0 = blockIdx.y * TM, j0 = blockIdx.x * TM;
+    if (threadIdx.x < TM) {
         const int e = e0 + threadIdx.x;
         arow[threadIdx.x] = (e < g.nrows) ? gram_zrow(g, e) : -1;
         brow[threadIdx.x] = j0 + threadIdx.x;          // < Rp: padded rows are zero
     }
     __syncthreads();
 
-    floatx16 acc;
+    floatx16 acc[NS][NS];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    float4 va[2], vb[2];
-    gram_fetch(g.Zp, g.dp, arow, 0, va);
-    gram_fetch(g.Zp, g.dp, brow, 0, vb);
+    for (int a = 0; a < NS; ++a)
+#pragma unroll
+        for (int b = 0; b < NS; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+    float4 va[TM / 32], vb[TM / 32];
+    gram_fetch<TM>(g.Zp, g.dp, arow, 0, va);
+    gram_fetch<TM>(g.Zp, g.dp, brow, 0, vb);
     for (int k0 = 0; k0 < g.dp; k0 += GK) {
-        gram_stash(As, va);
-        gram_stash(Bs, vb);
+        gram_stash<TM>(As, va);
+        gram_stash<TM>(Bs, vb);
         __syncthreads();
         if (k0 + GK < g.dp) {                            // next chunk in flight
-            gram_fetch(g.Zp, g.dp, arow, k0 + GK, va);
-            gram_fetch(g.Zp, g.dp, brow, k0 + GK, vb);
+            gram_fetch<TM>(g.Zp, g.dp, arow, k0 + GK, va);
+            gram_fetch<TM>(g.Zp, g.dp, brow, k0 + GK, vb);
         }
-        const float *ar = &As[wm * 32 + (lane & 31)][lane >> 5];
-        const float *br = &Bs[wn * 32 + (lane & 31)][lane >> 5];
+        const float *ar = &As[wm * (TM / 2) + (lane & 31)][lane >> 5];
+        const float *br = &Bs[wn * (TM / 2) + (lane & 31)][lane >> 5];
 #pragma unroll
-        for (int kk = 0; kk < GK / 2; ++kk)
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ar[2 * kk], br[2 * kk], acc, 0, 0, 0);
+        for (int kk = 0; kk < GK / 2; ++kk) {
+            float af[NS], bf[NS];
+#pragma unroll
+            for (int a = 0; a < NS; ++a) af[a] = ar[a * 32 * GLD + 2 * kk];
+#pragma unroll
+            for (int b = 0; b < NS; ++b) bf[b] = br[b * 32 * GLD + 2 * kk];
+#pragma unroll
+            for (int a = 0; a < NS; ++a)
+#pragma unroll
+                for (int b = 0; b < NS; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a], bf[b], acc[a][b], 0, 0, 0);
+        }
         __syncthreads();
     }
 
     // epilogue: C/D map of 32x32 MFMA: col = lane & 31, row = (r&3) + 8(r>>2) + 4(lane>>5)
     float s[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // XX XY YY trXX trYY YX
-    const int j = j0 + wn * 32 + (lane & 31);
-    const float sqc = g.sq[j];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int rs = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        const int e = e0 + wm * 32 + rs;
-        if (e >= g.nrows) continue;
-        const int i = arow[wm * 32 + rs];
-        float c = 0.f;
-        if (j < g.R) {
-            const float dot = acc[r];
-            const float sqi = g.sq[i];
-            const float raw = (-2.f * dot + sqi) + sqc;          // mmd.py:67 order
-            float K, al, be;
-            Kern<KIND>::eval(g.kp, raw, dot, sqi, sqc, K, al, be);
-            const bool isx = e < g.nxr, colx = j < g.m;
-            const bool diag = (j == i);
-            if (isx) {
-                if (colx) { s[0] += K; if (diag) s[3] += K; }
-                else s[1] += K;
-            } else {
-                if (colx) s[5] += K;
-                else { s[2] += K; if (diag) s[4] += K; }
-            }
-            if (g.need_grad && !(diag && g.trace_mode)) {
-                const float wgt = (isx == colx) ? (isx ? g.gw_same_x : g.gw_same_y) : g.gw_cross;
-                c = wgt * be;
+    for (int b = 0; b < NS; ++b) {
+        const int j = j0 + wn * (TM / 2) + b * 32 + (lane & 31);
+        const float sqc = g.sq[j];
+#pragma unroll
+        for (int a = 0; a < NS; ++a) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int rl = wm * (TM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                const int e = e0 + rl;
+                if (e >= g.nrows) continue;
+                const int i = arow[rl];
+                float c = 0.f;
+                if (j < g.R) {
+                    const float dot = acc[a][b][r];
+                    const float sqi = g.sq[i];
+                    const float raw = (-2.f * dot + sqi) + sqc;          // mmd.py:67 order
+                    float K, al, be;
+                    Kern<KIND>::eval(g.kp, raw, dot, sqi, sqc, K, al, be);
+                    const bool isx = e < g.nxr, colx = j < g.m;
+                    const bool diag = (j == i);
+                    if (isx) {
+                        if (colx) { s[0] += K; if (diag) s[3] += K; }
+                        else s[1] += K;
+                    } else {
+                        if (colx) s[5] += K;
+                        else { s[2] += K; if (diag) s[4] += K; }
+                    }
+                    if (g.need_grad && !(diag && g.trace_mode)) {
+                        const float wgt = (isx == colx) ? (isx ? g.gw_same_x : g.gw_same_y)
+                                                        : g.gw_cross;
+                        c = wgt * be;
+                    }
+                }
+                if (g.need_grad) g.C[(size_t)e * g.Rp + j] = c;
             }
         }
-        if (g.need_grad) g.C[(size_t)e * g.Rp + j] = c;
     }
 
     // block sums (fixed order, double) -> slab -> last arriver
@@ -202,89 +232,112 @@ __global__ __launch_bounds__(256) void gram_nt_kernel(GramArgs g) {
     }
 }
 
-// G = C Z over the Rp columns; grad_i = (a_i + sum_j c_ij) z_i - G_i
+// G = C Z over the Rp columns; grad_i = (a_i + sum_j c_ij) z_i - G_i, on TM x TM
+// output tiles (rows x feature columns), the same wave layout as gram_nt
+template <int TM>
 __global__ __launch_bounds__(256) void gram_nn_kernel(GramArgs g) {
-    constexpr int BLD = GT + 4;
-    __shared__ float As[GT][GLD];
+    constexpr int NS = TM / 64;
+    constexpr int BLD = TM + 4;
+    __shared__ float As[TM][GLD];
     __shared__ float Bs[GK][BLD];
-    __shared__ int arow[GT];
-    __shared__ float rsum[GT];
+    __shared__ int arow[TM];
+    __shared__ float rsum[TM];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int wm = w >> 1, wn = w & 1;
-    const int e0 = blockIdx.y * GT, k0c = blockIdx.x * GT;
-    if (threadIdx.x < GT) arow[threadIdx.x] = (e0 + threadIdx.x < g.nrows) ? e0 + threadIdx.x : -1;
+    const int e0 = blockIdx.y * TM, k0c = blockIdx.x * TM;
+    if (threadIdx.x < TM) arow[threadIdx.x] = (e0 + threadIdx.x < g.nrows) ? e0 + threadIdx.x : -1;
     __syncthreads();
 
-    floatx16 acc;
+    floatx16 acc[NS][NS];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    float rs = 0.f;                                   // thread t < 64: row t's sum_j c_ij
-    // B tile [32 j][64 cols] of Zp: 512 float4, two per thread
-    auto fetch_b = [&](int jb, float4 (&v)[2]) {
+    for (int a = 0; a < NS; ++a)
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
+        for (int b = 0; b < NS; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+    float rs = 0.f;                                   // thread t < TM: row t's sum_j c_ij
+    // B tile [32 j][TM cols] of Zp: 8 * TM float4, TM / 32 per thread
+    auto fetch_b = [&](int jb, float4 (&v)[TM / 32]) {
+#pragma unroll
+        for (int q = 0; q < TM / 32; ++q) {
             const int idx = threadIdx.x + 256 * q;
-            const int jr = idx >> 4, c = k0c + (idx & 15) * 4;
+            const int jr = idx / (TM / 4), c = k0c + (idx % (TM / 4)) * 4;
             v[q] = (c < g.dp) ? *reinterpret_cast<const float4 *>(g.Zp + (size_t)(jb + jr) * g.dp + c)
                               : make_float4(0.f, 0.f, 0.f, 0.f);
         }
     };
-    float4 va[2], vb[2];
-    gram_fetch(g.C, g.Rp, arow, 0, va);
+    float4 va[TM / 32], vb[TM / 32];
+    gram_fetch<TM>(g.C, g.Rp, arow, 0, va);
     fetch_b(0, vb);
     for (int jb = 0; jb < g.Rp; jb += GK) {
-        gram_stash(As, va);
+        gram_stash<TM>(As, va);
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
+        for (int q = 0; q < TM / 32; ++q) {
             const int idx = threadIdx.x + 256 * q;
-            *reinterpret_cast<float4 *>(&Bs[idx >> 4][(idx & 15) * 4]) = vb[q];
+            *reinterpret_cast<float4 *>(&Bs[idx / (TM / 4)][(idx % (TM / 4)) * 4]) = vb[q];
         }
         __syncthreads();
         if (jb + GK < g.Rp) {
-            gram_fetch(g.C, g.Rp, arow, jb + GK, va);
+            gram_fetch<TM>(g.C, g.Rp, arow, jb + GK, va);
             fetch_b(jb + GK, vb);
         }
-        if (threadIdx.x < GT) {
+        if (threadIdx.x < TM) {
 #pragma unroll
             for (int c = 0; c < GK; ++c) rs += As[threadIdx.x][c];
         }
-        const float *ar = &As[wm * 32 + (lane & 31)][lane >> 5];
-        const float *br = &Bs[lane >> 5][wn * 32 + (lane & 31)];
+        const float *ar = &As[wm * (TM / 2) + (lane & 31)][lane >> 5];
+        const float *br = &Bs[lane >> 5][wn * (TM / 2) + (lane & 31)];
 #pragma unroll
-        for (int kk = 0; kk < GK / 2; ++kk)
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ar[2 * kk], br[2 * kk * BLD], acc, 0, 0, 0);
+        for (int kk = 0; kk < GK / 2; ++kk) {
+            float af[NS], bf[NS];
+#pragma unroll
+            for (int a = 0; a < NS; ++a) af[a] = ar[a * 32 * GLD + 2 * kk];
+#pragma unroll
+            for (int b = 0; b < NS; ++b) bf[b] = br[2 * kk * BLD + b * 32];
+#pragma unroll
+            for (int a = 0; a < NS; ++a)
+#pragma unroll
+                for (int b = 0; b < NS; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a], bf[b], acc[a][b], 0, 0, 0);
+        }
         __syncthreads();
     }
-    if (threadIdx.x < GT) rsum[threadIdx.x] = rs;
+    if (threadIdx.x < TM) rsum[threadIdx.x] = rs;
     __syncthreads();
 
-    const int k = k0c + wn * 32 + (lane & 31);
-    if (k >= g.d) return;
     const double md = g.m, nd = g.n;
     const int tm = g.trace_mode ? 1 : 0;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int rsi = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        const int e = e0 + rsi;
-        if (e >= g.nrows) continue;
-        const int i = gram_zrow(g, e);
-        const bool isx = e < g.nxr;
-        // a_i = al_i * sum_j w_ij over the columns the gradient includes
-        float a = 0.f;
-        if (g.kind != SMMD_KIND_RBF) {
-            const float W = isx ? (float)(g.gw_same_x * (md - tm) + g.gw_cross * nd)
-                                : (float)(g.gw_same_y * (nd - tm) + g.gw_cross * md);
-            float al = 0.f;
-            if (g.kind == SMMD_KIND_RQ) al = g.kp.add_dot;
-            else if (g.kind == SMMD_KIND_DOT) al = 1.f;
-            else al = 2.f * mysqrt_grad(g.sq[i]);
-            a = al * W;
+    for (int b = 0; b < NS; ++b) {
+        const int k = k0c + wn * (TM / 2) + b * 32 + (lane & 31);
+        if (k >= g.d) continue;
+#pragma unroll
+        for (int a = 0; a < NS; ++a) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int rsi = wm * (TM / 2) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                const int e = e0 + rsi;
+                if (e >= g.nrows) continue;
+                const int i = gram_zrow(g, e);
+                const bool isx = e < g.nxr;
+                // a_i = al_i * sum_j w_ij over the columns the gradient includes
+                float av = 0.f;
+                if (g.kind != SMMD_KIND_RBF) {
+                    const float W = isx ? (float)(g.gw_same_x * (md - tm) + g.gw_cross * nd)
+                                        : (float)(g.gw_same_y * (nd - tm) + g.gw_cross * md);
+                    float al = 0.f;
+                    if (g.kind == SMMD_KIND_RQ) al = g.kp.add_dot;
+                    else if (g.kind == SMMD_KIND_DOT) al = 1.f;
+                    else al = 2.f * mysqrt_grad(g.sq[i]);
+                    av = al * W;
+                }
+                const float zk = g.Zp[(size_t)i * g.dp + k];
+                float gk = (av + rsum[rsi]) * zk - acc[a][b][r];
+                if (g.tanh_in) gk *= 1.f - zk * zk;
+                float *dst = isx ? g.grad_x + (size_t)e * g.d : g.grad_y + (size_t)(e - g.nxr) * g.d;
+                dst[k] = gk;
+            }
         }
-        const float zk = g.Zp[(size_t)i * g.dp + k];
-        float gk = (a + rsum[rsi]) * zk - acc[r];
-        if (g.tanh_in) gk *= 1.f - zk * zk;
-        float *dst = isx ? g.grad_x + (size_t)e * g.d : g.grad_y + (size_t)(e - g.nxr) * g.d;
-        dst[k] = gk;
     }
 }
 
@@ -293,10 +346,20 @@ __global__ __launch_bounds__(256) void gram_nn_kernel(GramArgs g) {
 // ---------------------------------------------------------------------------
 static int gram_pad(int x, int q) { return (x + q - 1) / q * q; }
 
+// 128 x 128 tiles (2 x 2 MFMA tiles per wave, half the operand bytes per flop)
+// only where the K loop dominates and 1024+ blocks remain: measured on MI355X
+// (tools/gram_bench.py, fwd + grad, rbf) 75.5 -> 80.6 TF at 2 x 2048 rows,
+// d = 1024 and 79 -> 91 TF at 2 x 4096, d = 512; but 50 -> 42 TF at 2 x 1024,
+// d = 1024 and 25 -> 18 TF at 2 x 2048, d = 128, where the per-pair epilogue
+// and the block count matter more
+static int gram_tile(int R, int d) {
+    return (R >= 4096 && d >= 512) ? 128 : 64;
+}
+
 size_t gram_ws_bytes(int m, int n, int d) {
     const size_t R = (size_t)(m > 0 ? m : 0) + (n > 0 ? n : 0);
-    const size_t Rp = gram_pad((int)R, GT), dp = gram_pad(d > 0 ? d : 1, GK);
-    const size_t blocks = (Rp / GT) * (Rp / GT);
+    const size_t Rp = gram_pad((int)R, 128), dp = gram_pad(d > 0 ? d : 1, GK);   // covers both tiles
+    const size_t blocks = (Rp / 64) * (Rp / 64);
     size_t b = 0;
     b += align_up(Rp * dp * 4, 256);        // Zp
     b += align_up(Rp * 4, 256);             // sq
@@ -305,29 +368,37 @@ size_t gram_ws_bytes(int m, int n, int d) {
     return b;
 }
 
+template <int TM>
+static smmd_status gram_launch_tiles(const GramArgs &g, hipStream_t s) {
+    const int nrt = (g.nrows + TM - 1) / TM;
+    const dim3 grid_nt(g.Rp / TM, nrt);
+    switch (g.kind) {
+        case SMMD_KIND_RBF: hipLaunchKernelGGL((gram_nt_kernel<SMMD_KIND_RBF, TM>), grid_nt, dim3(256), 0, s, g); break;
+        case SMMD_KIND_RQ: hipLaunchKernelGGL((gram_nt_kernel<SMMD_KIND_RQ, TM>), grid_nt, dim3(256), 0, s, g); break;
+        case SMMD_KIND_DISTANCE: hipLaunchKernelGGL((gram_nt_kernel<SMMD_KIND_DISTANCE, TM>), grid_nt, dim3(256), 0, s, g); break;
+        case SMMD_KIND_DOT: hipLaunchKernelGGL((gram_nt_kernel<SMMD_KIND_DOT, TM>), grid_nt, dim3(256), 0, s, g); break;
+        default: return SMMD_EINVAL;
+    }
+    if (g.need_grad)
+        hipLaunchKernelGGL((gram_nn_kernel<TM>), dim3((g.dp + TM - 1) / TM, nrt), dim3(256), 0, s, g);
+    return last_launch_status();
+}
+
 smmd_status gram_mmd2_launch(const GramArgs &proto, void *ws_body, hipStream_t s) {
     GramArgs g = proto;
     g.R = g.m + g.n;
-    g.Rp = gram_pad(g.R, GT);
+    const char *force = getenv("SMMD_GRAM_TILE");          // 64 / 128: A/B and tests
+    int tm = gram_tile(g.R, g.d);
+    if (force && (atoi(force) == 64 || atoi(force) == 128)) tm = atoi(force);
+    g.Rp = gram_pad(g.R, tm);
     g.dp = gram_pad(g.d, GK);
     char *p = (char *)ws_body;
     g.Zp = (float *)p;   p += align_up((size_t)g.Rp * g.dp * 4, 256);
     g.sq = (float *)p;   p += align_up((size_t)g.Rp * 4, 256);
     g.C = (float *)p;    p += align_up((size_t)g.Rp * g.Rp * 4, 256);
     g.slab = (double *)p;
-    const int nrt = (g.nrows + GT - 1) / GT;
     hipLaunchKernelGGL(gram_prep_kernel, dim3((g.Rp + 3) / 4), dim3(256), 0, s, g);
-    const dim3 grid_nt(g.Rp / GT, nrt);
-    switch (g.kind) {
-        case SMMD_KIND_RBF: hipLaunchKernelGGL(gram_nt_kernel<SMMD_KIND_RBF>, grid_nt, dim3(256), 0, s, g); break;
-        case SMMD_KIND_RQ: hipLaunchKernelGGL(gram_nt_kernel<SMMD_KIND_RQ>, grid_nt, dim3(256), 0, s, g); break;
-        case SMMD_KIND_DISTANCE: hipLaunchKernelGGL(gram_nt_kernel<SMMD_KIND_DISTANCE>, grid_nt, dim3(256), 0, s, g); break;
-        case SMMD_KIND_DOT: hipLaunchKernelGGL(gram_nt_kernel<SMMD_KIND_DOT>, grid_nt, dim3(256), 0, s, g); break;
-        default: return SMMD_EINVAL;
-    }
-    if (g.need_grad)
-        hipLaunchKernelGGL(gram_nn_kernel, dim3((g.dp + GT - 1) / GT, nrt), dim3(256), 0, s, g);
-    return last_launch_status();
+    return tm == 128 ? gram_launch_tiles<128>(g, s) : gram_launch_tiles<64>(g, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -377,15 +448,15 @@ __global__ __launch_bounds__(256) void poly_tile_kernel(PolyArgs p) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
     float4 va[2], vb[2];
-    gram_fetch(p.Ap, p.dimp, arow, 0, va);
-    gram_fetch(p.Bp, p.dimp, brow, 0, vb);
+    gram_fetch<GT>(p.Ap, p.dimp, arow, 0, va);
+    gram_fetch<GT>(p.Bp, p.dimp, brow, 0, vb);
     for (int k0 = 0; k0 < p.dimp; k0 += GK) {
-        gram_stash(As, va);
-        gram_stash(Bs, vb);
+        gram_stash<GT>(As, va);
+        gram_stash<GT>(Bs, vb);
         __syncthreads();
         if (k0 + GK < p.dimp) {
-            gram_fetch(p.Ap, p.dimp, arow, k0 + GK, va);
-            gram_fetch(p.Bp, p.dimp, brow, k0 + GK, vb);
+            gram_fetch<GT>(p.Ap, p.dimp, arow, k0 + GK, va);
+            gram_fetch<GT>(p.Bp, p.dimp, brow, k0 + GK, vb);
         }
         const float *ar = &As[wm * 32 + (lane & 31)][lane >> 5];
         const float *br = &Bs[wn * 32 + (lane & 31)][lane >> 5];

@@ -85,8 +85,13 @@ def _gfeats(m, n, d, seed):
 
 @pytest.mark.parametrize('name', O.KERNEL_NAMES)
 @pytest.mark.parametrize('shape', GRAM_SHAPES)
-def test_mmd2_gram_vs_oracle(dev, name, shape):
+@pytest.mark.parametrize('tile', ['64', '128'])
+def test_mmd2_gram_vs_oracle(dev, monkeypatch, name, shape, tile):
+    """Both block tilings of the Gram path (64 x 64 with one 32 x 32 MFMA tile
+    per wave; 128 x 128 with 2 x 2 per wave), forced by SMMD_GRAM_TILE on
+    ragged shapes (partial row and column tiles, padded K)."""
     from gan.core import mmd
+    monkeypatch.setenv('SMMD_GRAM_TILE', tile)
     m, n, d = shape
     X, Y = _gfeats(m, n, d, seed=zlib.crc32(repr(('gram', name, shape)).encode()))
     spec = O.kernel_spec(name)
@@ -104,10 +109,13 @@ def test_mmd2_gram_vs_oracle(dev, name, shape):
 
 
 @pytest.mark.parametrize('biased', [False, True])
-def test_mmd2_gram_wide(dev, biased):
-    """d = 1024 (SURVEY 8d MFMA sweep) at N = 2 x 256, rbf."""
+@pytest.mark.parametrize('shape', [(256, 256, 1024), (1100, 1000, 200)])
+def test_mmd2_gram_wide(dev, biased, shape):
+    """d = 1024 (SURVEY 8d MFMA sweep) at N = 2 x 256, and 2100 rows (the
+    128 x 128 tiling's own choice, a partial last tile) at d = 200, rbf."""
     from gan.core import mmd
-    X, Y = _gfeats(256, 256, 1024, seed=21)
+    m, n, d = shape
+    X, Y = _gfeats(m, n, d, seed=21)
     spec = O.kernel_spec('rbf')
     Xt = torch.tensor(X, device=dev, requires_grad=True)
     Yt = torch.tensor(Y, device=dev, requires_grad=True)

@@ -1,0 +1,66 @@
+"""MFMA Gram path of smmd_mmd2_fwd (d > 32): HIP-event time of the library call
+per (N per side, D), for the 64 x 64 and 128 x 128 block tilings
+(SMMD_GRAM_TILE), with TFLOP/s against the f32 MFMA peak (157.3 TF).
+
+    python tools/gram_bench.py [--json out.json]
+
+Flops counted as executed: the Gram S = Z Z^T over all (2N)^2 pairs plus
+G = C Z, 2 * D * (2N)^2 each (the bench's mmd_sweep counts the reference's
+three blocks, P = 3 N^2 pairs, i.e. 3/4 of these)."""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, 'scaled-mmd-gan_amd')):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+PEAK = 157.3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--json', default='')
+    args = ap.parse_args()
+    from gan.core import _lib, mmd
+    dev = torch.device('cuda:0')
+    rows = []
+    for N, D in [(512, 128), (512, 1024), (1024, 1024), (2048, 128), (2048, 1024), (4096, 512)]:
+        rng = np.random.default_rng(1234)
+        X = torch.tensor(rng.standard_normal((N, D)) / np.sqrt(D), dtype=torch.float32,
+                         device=dev, requires_grad=True)
+        Y = torch.tensor(rng.standard_normal((N, D)) / np.sqrt(D), dtype=torch.float32,
+                         device=dev, requires_grad=True)
+        for tile in ('64', '128'):
+            os.environ['SMMD_GRAM_TILE'] = tile
+            for _ in range(3):
+                v = mmd.mmd2_fused(X, Y, 'rbf')
+                torch.autograd.grad(v, (X, Y))
+            torch.cuda.synchronize()
+            _lib.reset_timing()
+            _lib.enable_timing(True)
+            iters = 10
+            for _ in range(iters):
+                v = mmd.mmd2_fused(X, Y, 'rbf')
+                torch.autograd.grad(v, (X, Y))
+            _lib.enable_timing(False)
+            ms = _lib.timing_ms()['smmd_mmd2_fwd'][1]
+            fl = 4.0 * D * (2 * N) ** 2
+            tf = fl / (ms * 1e-3) / 1e12
+            rows.append({'N': N, 'D': D, 'tile': int(tile), 'ms': round(ms, 4),
+                         'tflops': round(tf, 2), 'mfma_frac': round(tf / PEAK, 4),
+                         'mmd2': float(v)})
+            print(json.dumps(rows[-1]), flush=True)
+    os.environ.pop('SMMD_GRAM_TILE', None)
+    if args.json:
+        with open(args.json, 'w') as f:
+            json.dump(rows, f, indent=1)
+
+
+if __name__ == '__main__':
+    main()
