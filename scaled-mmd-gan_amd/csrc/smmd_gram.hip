@@ -38,31 +38,50 @@ __device__ __forceinline__ int gram_zrow(const GramArgs &g, int e) {
 }
 
 // one wave per row of Zp: copy (tanh), zero padding, then lane 0 forms the
-// squared norm as a k-ordered fma chain over the row it just wrote
+// squared norm as a k-ordered fma chain over the row.  The chain is inherently
+// serial (it must equal the MFMA's k-ordered accumulation bit for bit, so raw
+// D2 is exactly 0 on the diagonal); lane 0 reads the row back from LDS four
+// values per ds_read_b128 instead of from global memory one load per step
+// (that form took 140 us at 4096 x 1024, a sixth of the whole MMD call)
+constexpr int GP_CHUNK = 256;   // floats of a row staged per wave per step
+
 __global__ __launch_bounds__(256) void gram_prep_kernel(GramArgs g) {
-    const int lane = threadIdx.x & 63;
-    const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (r < g.Rp) {
-        const float *src = nullptr;
-        if (r < g.m) src = g.X + (size_t)r * g.d;
-        else if (r < g.R) src = g.Y + (size_t)(r - g.m) * g.d;
-        float *dst = g.Zp + (size_t)r * g.dp;
-        for (int k = lane; k < g.dp; k += 64) {
+    __shared__ float4 rowbuf[4][GP_CHUNK / 4];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int r = blockIdx.x * 4 + w;
+    const bool live = r < g.Rp;
+    const float *src = nullptr;
+    if (live && r < g.m) src = g.X + (size_t)r * g.d;
+    else if (live && r < g.R) src = g.Y + (size_t)(r - g.m) * g.d;
+    float *dst = live ? g.Zp + (size_t)r * g.dp : nullptr;
+    float *rb = reinterpret_cast<float *>(rowbuf[w]);
+    float s = 0.f;
+    for (int k0 = 0; k0 < g.dp; k0 += GP_CHUNK) {          // dp: same for every wave
+        const int n = (g.dp - k0 < GP_CHUNK) ? g.dp - k0 : GP_CHUNK;   // multiple of 32
+        for (int kk = lane; kk < n; kk += 64) {
+            const int k = k0 + kk;
             float v = 0.f;
             if (src && k < g.d) {
                 v = src[k];
                 if (g.tanh_in) v = tanhf(v);
             }
-            dst[k] = v;
+            if (live) dst[k] = v;
+            rb[kk] = v;
         }
+        __syncthreads();
+        if (live && lane == 0) {
+#pragma unroll 4
+            for (int q = 0; q < n / 4; ++q) {
+                const float4 x = rowbuf[w][q];
+                s = (k0 == 0 && q == 0) ? x.x * x.x : fmaf(x.x, x.x, s);
+                s = fmaf(x.y, x.y, s);
+                s = fmaf(x.z, x.z, s);
+                s = fmaf(x.w, x.w, s);
+            }
+        }
+        __syncthreads();
     }
-    __syncthreads();
-    if (r < g.Rp && lane == 0) {
-        const float *row = g.Zp + (size_t)r * g.dp;
-        float s = row[0] * row[0];
-        for (int k = 1; k < g.dp; ++k) s = fmaf(row[k], row[k], s);
-        g.sq[r] = s;
-    }
+    if (live && lane == 0) g.sq[r] = s;
 }
 
 // stage a [TM rows][32 k] tile: TM * 8 float4, TM / 32 per thread (rows < 0: zero)

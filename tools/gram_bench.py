@@ -26,17 +26,22 @@ PEAK = 157.3
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--json', default='')
+    ap.add_argument('--only', default='', help='N,D: one size (PMC passes)')
+    ap.add_argument('--tiles', default='64,128')
     args = ap.parse_args()
     from gan.core import _lib, mmd
     dev = torch.device('cuda:0')
     rows = []
-    for N, D in [(512, 128), (512, 1024), (1024, 1024), (2048, 128), (2048, 1024), (4096, 512)]:
+    sizes = [(512, 128), (512, 1024), (1024, 1024), (2048, 128), (2048, 1024), (4096, 512)]
+    if args.only:
+        sizes = [tuple(int(v) for v in args.only.split(','))]
+    for N, D in sizes:
         rng = np.random.default_rng(1234)
         X = torch.tensor(rng.standard_normal((N, D)) / np.sqrt(D), dtype=torch.float32,
                          device=dev, requires_grad=True)
         Y = torch.tensor(rng.standard_normal((N, D)) / np.sqrt(D), dtype=torch.float32,
                          device=dev, requires_grad=True)
-        for tile in ('64', '128'):
+        for tile in args.tiles.split(','):
             os.environ['SMMD_GRAM_TILE'] = tile
             for _ in range(3):
                 v = mmd.mmd2_fused(X, Y, 'rbf')
