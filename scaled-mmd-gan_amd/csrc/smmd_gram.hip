@@ -84,25 +84,27 @@ __global__ __launch_bounds__(256) void gram_prep_kernel(GramArgs g) {
     if (live && lane == 0) g.sq[r] = s;
 }
 
-// stage a [TM rows][32 k] tile: TM * 8 float4, TM / 32 per thread (rows < 0: zero)
-template <int TM>
+// stage a [TM rows][KC k] tile: TM * KC / 4 float4, TM * KC / 1024 per thread
+// (rows < 0: zero); LDS rows padded to KC + 1 floats (conflict-free fragment reads)
+template <int TM, int KC>
 __device__ __forceinline__ void gram_fetch(const float *__restrict__ base, int ld, const int *rows,
-                                           int k0, float4 (&v)[TM / 32]) {
+                                           int k0, float4 (&v)[TM * KC / 1024]) {
 #pragma unroll
-    for (int q = 0; q < TM / 32; ++q) {
+    for (int q = 0; q < TM * KC / 1024; ++q) {
         const int idx = threadIdx.x + 256 * q;
-        const int r = rows[idx >> 3];
-        v[q] = (r >= 0) ? *reinterpret_cast<const float4 *>(base + (size_t)r * ld + k0 + (idx & 7) * 4)
+        const int r = rows[idx / (KC / 4)];
+        v[q] = (r >= 0) ? *reinterpret_cast<const float4 *>(base + (size_t)r * ld + k0 +
+                                                            (idx % (KC / 4)) * 4)
                         : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 }
 
-template <int TM>
-__device__ __forceinline__ void gram_stash(float (*T)[GLD], const float4 (&v)[TM / 32]) {
+template <int TM, int KC>
+__device__ __forceinline__ void gram_stash(float (*T)[KC + 1], const float4 (&v)[TM * KC / 1024]) {
 #pragma unroll
-    for (int q = 0; q < TM / 32; ++q) {
+    for (int q = 0; q < TM * KC / 1024; ++q) {
         const int idx = threadIdx.x + 256 * q;
-        float *p = &T[idx >> 3][(idx & 7) * 4];
+        float *p = &T[idx / (KC / 4)][(idx % (KC / 4)) * 4];
         p[0] = v[q].x; p[1] = v[q].y; p[2] = v[q].z; p[3] = v[q].w;
     }
 }
@@ -111,10 +113,11 @@ __device__ __forceinline__ void gram_stash(float (*T)[GLD], const float4 (&v)[TM
 // = NS x NS MFMA tiles of 32 x 32 (NS accumulators per operand fragment, so a
 // 128 tile reads each LDS fragment once per 2 MFMAs and fetches half the L2 /
 // Infinity-Cache bytes per flop of a 64 tile)
-template <int KIND, int TM>
+template <int KIND, int TM, int KC>
 __global__ __launch_bounds__(256) void gram_nt_kernel(GramArgs g) {
     constexpr int NS = TM / 64;
-    __shared__ float As[TM][GLD], Bs[TM][GLD];
+    constexpr int LD = KC + 1;
+    __shared__ float As[TM][LD], Bs[TM][LD];
     __shared__ int arow[TM], brow[TM];
     __shared__ double red[4][8];
     __shared__ int is_last;
@@ -135,26 +138,26 @@ __global__ __launch_bounds__(256) void gram_nt_kernel(GramArgs g) {
         for (int b = 0; b < NS; ++b)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-    float4 va[TM / 32], vb[TM / 32];
-    gram_fetch<TM>(g.Zp, g.dp, arow, 0, va);
-    gram_fetch<TM>(g.Zp, g.dp, brow, 0, vb);
-    for (int k0 = 0; k0 < g.dp; k0 += GK) {
-        gram_stash<TM>(As, va);
-        gram_stash<TM>(Bs, vb);
+    float4 va[TM * KC / 1024], vb[TM * KC / 1024];
+    gram_fetch<TM, KC>(g.Zp, g.dp, arow, 0, va);
+    gram_fetch<TM, KC>(g.Zp, g.dp, brow, 0, vb);
+    for (int k0 = 0; k0 < g.dp; k0 += KC) {
+        gram_stash<TM, KC>(As, va);
+        gram_stash<TM, KC>(Bs, vb);
         __syncthreads();
-        if (k0 + GK < g.dp) {                            // next chunk in flight
-            gram_fetch<TM>(g.Zp, g.dp, arow, k0 + GK, va);
-            gram_fetch<TM>(g.Zp, g.dp, brow, k0 + GK, vb);
+        if (k0 + KC < g.dp) {                            // next chunk in flight
+            gram_fetch<TM, KC>(g.Zp, g.dp, arow, k0 + KC, va);
+            gram_fetch<TM, KC>(g.Zp, g.dp, brow, k0 + KC, vb);
         }
         const float *ar = &As[wm * (TM / 2) + (lane & 31)][lane >> 5];
         const float *br = &Bs[wn * (TM / 2) + (lane & 31)][lane >> 5];
 #pragma unroll
-        for (int kk = 0; kk < GK / 2; ++kk) {
+        for (int kk = 0; kk < KC / 2; ++kk) {
             float af[NS], bf[NS];
 #pragma unroll
-            for (int a = 0; a < NS; ++a) af[a] = ar[a * 32 * GLD + 2 * kk];
+            for (int a = 0; a < NS; ++a) af[a] = ar[a * 32 * LD + 2 * kk];
 #pragma unroll
-            for (int b = 0; b < NS; ++b) bf[b] = br[b * 32 * GLD + 2 * kk];
+            for (int b = 0; b < NS; ++b) bf[b] = br[b * 32 * LD + 2 * kk];
 #pragma unroll
             for (int a = 0; a < NS; ++a)
 #pragma unroll
@@ -253,12 +256,13 @@ __global__ __launch_bounds__(256) void gram_nt_kernel(GramArgs g) {
 
 // G = C Z over the Rp columns; grad_i = (a_i + sum_j c_ij) z_i - G_i, on TM x TM
 // output tiles (rows x feature columns), the same wave layout as gram_nt
-template <int TM>
+template <int TM, int KC>
 __global__ __launch_bounds__(256) void gram_nn_kernel(GramArgs g) {
     constexpr int NS = TM / 64;
+    constexpr int LD = KC + 1;
     constexpr int BLD = TM + 4;
-    __shared__ float As[TM][GLD];
-    __shared__ float Bs[GK][BLD];
+    __shared__ float As[TM][LD];
+    __shared__ float Bs[KC][BLD];
     __shared__ int arow[TM];
     __shared__ float rsum[TM];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -275,42 +279,42 @@ __global__ __launch_bounds__(256) void gram_nn_kernel(GramArgs g) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
     float rs = 0.f;                                   // thread t < TM: row t's sum_j c_ij
-    // B tile [32 j][TM cols] of Zp: 8 * TM float4, TM / 32 per thread
-    auto fetch_b = [&](int jb, float4 (&v)[TM / 32]) {
+    // B tile [KC j][TM cols] of Zp: KC * TM / 4 float4, TM * KC / 1024 per thread
+    auto fetch_b = [&](int jb, float4 (&v)[TM * KC / 1024]) {
 #pragma unroll
-        for (int q = 0; q < TM / 32; ++q) {
+        for (int q = 0; q < TM * KC / 1024; ++q) {
             const int idx = threadIdx.x + 256 * q;
             const int jr = idx / (TM / 4), c = k0c + (idx % (TM / 4)) * 4;
             v[q] = (c < g.dp) ? *reinterpret_cast<const float4 *>(g.Zp + (size_t)(jb + jr) * g.dp + c)
                               : make_float4(0.f, 0.f, 0.f, 0.f);
         }
     };
-    float4 va[TM / 32], vb[TM / 32];
-    gram_fetch<TM>(g.C, g.Rp, arow, 0, va);
+    float4 va[TM * KC / 1024], vb[TM * KC / 1024];
+    gram_fetch<TM, KC>(g.C, g.Rp, arow, 0, va);
     fetch_b(0, vb);
-    for (int jb = 0; jb < g.Rp; jb += GK) {
-        gram_stash<TM>(As, va);
+    for (int jb = 0; jb < g.Rp; jb += KC) {
+        gram_stash<TM, KC>(As, va);
 #pragma unroll
-        for (int q = 0; q < TM / 32; ++q) {
+        for (int q = 0; q < TM * KC / 1024; ++q) {
             const int idx = threadIdx.x + 256 * q;
             *reinterpret_cast<float4 *>(&Bs[idx / (TM / 4)][(idx % (TM / 4)) * 4]) = vb[q];
         }
         __syncthreads();
-        if (jb + GK < g.Rp) {
-            gram_fetch<TM>(g.C, g.Rp, arow, jb + GK, va);
-            fetch_b(jb + GK, vb);
+        if (jb + KC < g.Rp) {
+            gram_fetch<TM, KC>(g.C, g.Rp, arow, jb + KC, va);
+            fetch_b(jb + KC, vb);
         }
         if (threadIdx.x < TM) {
 #pragma unroll
-            for (int c = 0; c < GK; ++c) rs += As[threadIdx.x][c];
+            for (int c = 0; c < KC; ++c) rs += As[threadIdx.x][c];
         }
         const float *ar = &As[wm * (TM / 2) + (lane & 31)][lane >> 5];
         const float *br = &Bs[lane >> 5][wn * (TM / 2) + (lane & 31)];
 #pragma unroll
-        for (int kk = 0; kk < GK / 2; ++kk) {
+        for (int kk = 0; kk < KC / 2; ++kk) {
             float af[NS], bf[NS];
 #pragma unroll
-            for (int a = 0; a < NS; ++a) af[a] = ar[a * 32 * GLD + 2 * kk];
+            for (int a = 0; a < NS; ++a) af[a] = ar[a * 32 * LD + 2 * kk];
 #pragma unroll
             for (int b = 0; b < NS; ++b) bf[b] = br[2 * kk * BLD + b * 32];
 #pragma unroll
@@ -377,7 +381,7 @@ static int gram_tile(int R, int d) {
 
 size_t gram_ws_bytes(int m, int n, int d) {
     const size_t R = (size_t)(m > 0 ? m : 0) + (n > 0 ? n : 0);
-    const size_t Rp = gram_pad((int)R, 128), dp = gram_pad(d > 0 ? d : 1, GK);   // covers both tiles
+    const size_t Rp = gram_pad((int)R, 128), dp = gram_pad(d > 0 ? d : 1, 64);   // covers both tilings
     const size_t blocks = (Rp / 64) * (Rp / 64);
     size_t b = 0;
     b += align_up(Rp * dp * 4, 256);        // Zp
@@ -387,19 +391,19 @@ size_t gram_ws_bytes(int m, int n, int d) {
     return b;
 }
 
-template <int TM>
+template <int TM, int KC>
 static smmd_status gram_launch_tiles(const GramArgs &g, hipStream_t s) {
     const int nrt = (g.nrows + TM - 1) / TM;
     const dim3 grid_nt(g.Rp / TM, nrt);
     switch (g.kind) {
-        case SMMD_KIND_RBF: hipLaunchKernelGGL((gram_nt_kernel<SMMD_KIND_RBF, TM>), grid_nt, dim3(256), 0, s, g); break;
-        case SMMD_KIND_RQ: hipLaunchKernelGGL((gram_nt_kernel<SMMD_KIND_RQ, TM>), grid_nt, dim3(256), 0, s, g); break;
-        case SMMD_KIND_DISTANCE: hipLaunchKernelGGL((gram_nt_kernel<SMMD_KIND_DISTANCE, TM>), grid_nt, dim3(256), 0, s, g); break;
-        case SMMD_KIND_DOT: hipLaunchKernelGGL((gram_nt_kernel<SMMD_KIND_DOT, TM>), grid_nt, dim3(256), 0, s, g); break;
+        case SMMD_KIND_RBF: hipLaunchKernelGGL((gram_nt_kernel<SMMD_KIND_RBF, TM, KC>), grid_nt, dim3(256), 0, s, g); break;
+        case SMMD_KIND_RQ: hipLaunchKernelGGL((gram_nt_kernel<SMMD_KIND_RQ, TM, KC>), grid_nt, dim3(256), 0, s, g); break;
+        case SMMD_KIND_DISTANCE: hipLaunchKernelGGL((gram_nt_kernel<SMMD_KIND_DISTANCE, TM, KC>), grid_nt, dim3(256), 0, s, g); break;
+        case SMMD_KIND_DOT: hipLaunchKernelGGL((gram_nt_kernel<SMMD_KIND_DOT, TM, KC>), grid_nt, dim3(256), 0, s, g); break;
         default: return SMMD_EINVAL;
     }
     if (g.need_grad)
-        hipLaunchKernelGGL((gram_nn_kernel<TM>), dim3((g.dp + TM - 1) / TM, nrt), dim3(256), 0, s, g);
+        hipLaunchKernelGGL((gram_nn_kernel<TM, KC>), dim3((g.dp + TM - 1) / TM, nrt), dim3(256), 0, s, g);
     return last_launch_status();
 }
 
@@ -409,15 +413,18 @@ smmd_status gram_mmd2_launch(const GramArgs &proto, void *ws_body, hipStream_t s
     const char *force = getenv("SMMD_GRAM_TILE");          // 64 / 128: A/B and tests
     int tm = gram_tile(g.R, g.d);
     if (force && (atoi(force) == 64 || atoi(force) == 128)) tm = atoi(force);
+    // K chunk staged per step: 32 for both tilings (64 for the 128 tile measured
+    // 3-9 % slower: 66 KB of LDS per block halves the blocks per CU)
+    const int kc = GK;
     g.Rp = gram_pad(g.R, tm);
-    g.dp = gram_pad(g.d, GK);
+    g.dp = gram_pad(g.d, kc);
     char *p = (char *)ws_body;
     g.Zp = (float *)p;   p += align_up((size_t)g.Rp * g.dp * 4, 256);
     g.sq = (float *)p;   p += align_up((size_t)g.Rp * 4, 256);
     g.C = (float *)p;    p += align_up((size_t)g.Rp * g.Rp * 4, 256);
     g.slab = (double *)p;
     hipLaunchKernelGGL(gram_prep_kernel, dim3((g.Rp + 3) / 4), dim3(256), 0, s, g);
-    return tm == 128 ? gram_launch_tiles<128>(g, s) : gram_launch_tiles<64>(g, s);
+    return tm == 128 ? gram_launch_tiles<128, GK>(g, s) : gram_launch_tiles<64, GK>(g, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -467,15 +474,15 @@ __global__ __launch_bounds__(256) void poly_tile_kernel(PolyArgs p) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
     float4 va[2], vb[2];
-    gram_fetch<GT>(p.Ap, p.dimp, arow, 0, va);
-    gram_fetch<GT>(p.Bp, p.dimp, brow, 0, vb);
+    gram_fetch<GT, GK>(p.Ap, p.dimp, arow, 0, va);
+    gram_fetch<GT, GK>(p.Bp, p.dimp, brow, 0, vb);
     for (int k0 = 0; k0 < p.dimp; k0 += GK) {
-        gram_stash<GT>(As, va);
-        gram_stash<GT>(Bs, vb);
+        gram_stash<GT, GK>(As, va);
+        gram_stash<GT, GK>(Bs, vb);
         __syncthreads();
         if (k0 + GK < p.dimp) {
-            gram_fetch<GT>(p.Ap, p.dimp, arow, k0 + GK, va);
-            gram_fetch<GT>(p.Bp, p.dimp, brow, k0 + GK, vb);
+            gram_fetch<GT, GK>(p.Ap, p.dimp, arow, k0 + GK, va);
+            gram_fetch<GT, GK>(p.Bp, p.dimp, brow, k0 + GK, vb);
         }
         const float *ar = &As[wm * 32 + (lane & 31)][lane >> 5];
         const float *br = &Bs[wn * 32 + (lane & 31)][lane >> 5];
