@@ -95,6 +95,12 @@ def cpu_baseline(cfg, seconds_budget=20.0):
 MFMA_F32_PEAK_TFS = 157.3     # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense
 
 
+def mmd_path(rows, d):
+    """The implementation smmd_mmd2_fwd picks (csrc/smmd_mmd.hip use_gram)."""
+    gram = d > 32 or (d >= 16 and rows >= 1024) or (d >= 32 and rows >= 512)
+    return 'mfma-gram' if gram else 'row-sweep'
+
+
 def mmd_sweep(world, rank, dev, group, quick=False):
     """SURVEY 8d MMD microbench: X, Y ~ N(0,1) [N, D] per side (global N,
     numpy default_rng(1234)), rank r owning rows [r N/w, (r+1) N/w) of each, run
@@ -156,7 +162,7 @@ def mmd_sweep(world, rank, dev, group, quick=False):
         row = {'kernel': kern, 'N': N, 'D': D, 'op_ms': round(op_ms, 5),
                'kernel_ms': round(ms, 5), 'GB_s': round(b / (ms * 1e-3) / 1e9, 2),
                'pair_evals_per_s': round(P / (ms * 1e-3), 1),
-               'path': 'row-sweep' if D <= 32 else 'mfma-gram', 'mmd2': float(val.detach())}
+               'path': mmd_path(2 * N, D), 'mmd2': float(val.detach())}
         if D >= 128:
             tf = 4.0 * D * P / (ms * 1e-3) / 1e12
             row.update(tflops=round(tf, 2), mfma_frac=round(tf / MFMA_F32_PEAK_TFS, 4))

@@ -679,14 +679,24 @@ const char *smmd_status_string(smmd_status s) {
 
 int smmd_abi_version(void) { return 2; }
 
-static bool use_gram(int d) {
+// Path choice.  d > 32: the MFMA Gram path (the row sweep holds a row in
+// registers up to 32 features).  d <= 32: the row sweep, except where the
+// Gram path measured faster on MI355X (tools/gram_bench.py --paths, rbf fwd +
+// grad): d >= 16 from 2 x 512 rows (0.115 vs 0.158 ms at 2 x 1024, d = 16;
+// 0.303 vs 0.408 ms at 2 x 2048) and d = 32 from 2 x 256 rows (0.040 vs
+// 0.068 ms); d <= 8 stays on the row sweep at every size (0.114 vs 0.303 ms at
+// 2 x 2048, d = 1).  SMMD_MMD_GRAM=1 / 0 forces either path (d <= 32).
+static bool use_gram(int m, int n, int d) {
     if (pick_dt(d) == 0) return true;
     const char *e = getenv("SMMD_MMD_GRAM");
-    return e && e[0] == '1';
+    if (e && e[0] == '1') return true;
+    if (e && e[0] == '0') return false;
+    const long rows = (long)(m > 0 ? m : 0) + (n > 0 ? n : 0);
+    return (d >= 16 && rows >= 1024) || (d >= 32 && rows >= 512);
 }
 
 size_t smmd_mmd2_workspace_bytes(int m, int n, int d) {
-    if (use_gram(d)) return 256 + gram_ws_bytes(m, n, d);
+    if (use_gram(m, n, d)) return 256 + gram_ws_bytes(m, n, d);
     const int rows = (m > 0 ? m : 0) + (n > 0 ? n : 0);
     return 256 + align_up((size_t)mmd2_grid(rows, pick_dt(d)) * 8 * sizeof(double), 256);
 }
@@ -703,7 +713,7 @@ smmd_status smmd_mmd2_fwd(const smmd_kernel_desc *desc, const float *X, int m, c
     KParams kp;
     if (!make_kparams(desc, kp)) return SMMD_EINVAL;
     const int dt = pick_dt(d);
-    const bool gram = use_gram(d);
+    const bool gram = use_gram(m, n, d);
     const int rows = (x_end - x_begin) + (y_end - y_begin);
     if (!ws || ws_bytes < smmd_mmd2_workspace_bytes(m, n, d)) return SMMD_EWORKSPACE;
     if (rows == 0) return SMMD_EINVAL;

@@ -155,6 +155,26 @@ def test_mmd2_gram_matches_row_sweep(dev, monkeypatch, name, shape):
         _grad_close(ga, gb, what + ' gram vs sweep')
 
 
+@pytest.mark.parametrize('shape', [(600, 500, 16), (300, 300, 32), (600, 500, 8)])
+def test_mmd2_default_path_choice(dev, monkeypatch, shape):
+    """Without SMMD_MMD_GRAM the library picks the path by size (the Gram path
+    for d >= 16 from 1024 rows and d = 32 from 512 rows, else the row sweep):
+    each choice against the oracle."""
+    from gan.core import mmd
+    monkeypatch.delenv('SMMD_MMD_GRAM', raising=False)
+    m, n, d = shape
+    X, Y = _gfeats(m, n, d, seed=zlib.crc32(repr(('auto', shape)).encode()))
+    spec = O.kernel_spec('mix_rbf')
+    Xt = torch.tensor(X, device=dev, requires_grad=True)
+    Yt = torch.tensor(Y, device=dev, requires_grad=True)
+    val = mmd.mmd2_fused(Xt, Yt, 'mix_rbf')
+    val.backward()
+    _close(val.item(), O.mmd2(spec, X, Y), 1e-5, 1e-4, 'mmd2 auto %s' % (shape,))
+    rdx, rdy = O.mmd2_grad(spec, X, Y)
+    _grad_close(Xt.grad.cpu().numpy(), rdx, 'dX auto')
+    _grad_close(Yt.grad.cpu().numpy(), rdy, 'dY auto')
+
+
 def test_mmd2_reference_api_path(dev):
     """mmd.mmd2(mmd._rbf_kernel(X, Y)) -- the exact call of SMMD.set_loss."""
     from gan.core import mmd

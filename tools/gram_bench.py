@@ -28,7 +28,11 @@ def main():
     ap.add_argument('--json', default='')
     ap.add_argument('--only', default='', help='N,D: one size (PMC passes)')
     ap.add_argument('--tiles', default='64,128')
+    ap.add_argument('--paths', action='store_true',
+                    help='row sweep vs Gram path (SMMD_MMD_GRAM=0/1) at small d')
     args = ap.parse_args()
+    if args.paths:
+        return path_sweep(args)
     from gan.core import _lib, mmd
     dev = torch.device('cuda:0')
     rows = []
@@ -62,6 +66,41 @@ def main():
                          'mmd2': float(v)})
             print(json.dumps(rows[-1]), flush=True)
     os.environ.pop('SMMD_GRAM_TILE', None)
+    if args.json:
+        with open(args.json, 'w') as f:
+            json.dump(rows, f, indent=1)
+
+
+def path_sweep(args):
+    """smmd_mmd2_fwd time, row-sweep kernel vs MFMA Gram path, d <= 32."""
+    from gan.core import _lib, mmd
+    dev = torch.device('cuda:0')
+    rows = []
+    for N in (256, 1024, 2048):
+        for D in (1, 2, 4, 8, 16, 32):
+            rng = np.random.default_rng(1234)
+            X = torch.tensor(rng.standard_normal((N, D)) / np.sqrt(D), dtype=torch.float32,
+                             device=dev, requires_grad=True)
+            Y = torch.tensor(rng.standard_normal((N, D)) / np.sqrt(D), dtype=torch.float32,
+                             device=dev, requires_grad=True)
+            rec = {'N': N, 'D': D}
+            for path in ('0', '1'):
+                os.environ['SMMD_MMD_GRAM'] = path
+                for _ in range(3):
+                    v = mmd.mmd2_fused(X, Y, 'rbf')
+                    torch.autograd.grad(v, (X, Y))
+                torch.cuda.synchronize()
+                _lib.reset_timing()
+                _lib.enable_timing(True)
+                for _ in range(10):
+                    v = mmd.mmd2_fused(X, Y, 'rbf')
+                    torch.autograd.grad(v, (X, Y))
+                _lib.enable_timing(False)
+                rec['sweep_ms' if path == '0' else 'gram_ms'] = round(
+                    _lib.timing_ms()['smmd_mmd2_fwd'][1], 4)
+            rows.append(rec)
+            print(json.dumps(rec), flush=True)
+    os.environ.pop('SMMD_MMD_GRAM', None)
     if args.json:
         with open(args.json, 'w') as f:
             json.dump(rows, f, indent=1)
