@@ -350,6 +350,10 @@ def main():
         # sqsum pass reads g; update pass reads g, p, m, v and writes p, m, v
         'smmd_adam_flat[D]': model.d_optim.numel * 4 * 8,
         'smmd_adam_flat[G]': model.g_optim.numel * 4 * 8,
+        # the same update with the SN weights' first power-iteration pass folded
+        # in (its column-partial writes are < 0.1 % of these bytes)
+        'smmd_adam_flat_sn[D]': model.d_optim.numel * 4 * 8,
+        'smmd_adam_flat_sn[G]': model.g_optim.numel * 4 * 8,
         # one read of W + one write of W_eff (2 K N 4 B per iteration)
         'smmd_sn_power_iter': sn_kn * 4 * 2,
         # one read of G and W, one write of gW

@@ -207,6 +207,16 @@ smmd_status smmd_sn_power_iter(const smmd_sn_layer *layers, int n_layers,
                                int num_iters, float eps, int update_u,
                                void *ws, size_t ws_bytes, smmd_stream_t stream);
 
+/* flags = SMMD_SN_P1_READY: the column partials of the first iteration (u^T W
+ * per 32-row tile) are already in ws, written by smmd_adam_flat_sn from the
+ * current W and u; the call skips that pass (one read of every W).  The
+ * caller guarantees neither W nor u changed since.  flags = 0 is
+ * smmd_sn_power_iter.  The resident path ignores the flag. */
+#define SMMD_SN_P1_READY 1
+smmd_status smmd_sn_power_iter_ex(const smmd_sn_layer *layers, int n_layers,
+                                  int num_iters, float eps, int update_u, int flags,
+                                  void *ws, size_t ws_bytes, smmd_stream_t stream);
+
 /* dL/dW = (s/sigma) (G - (<G,W>/sigma) u' v^T),  dL/ds = <G,W>/sigma,
  * u', v, sigma from the last smmd_sn_power_iter (stop_gradient, sn.py:32-34);
  * ws must be the workspace that call used (it holds u'). */
@@ -249,6 +259,20 @@ smmd_status smmd_adam_flat(float *param, const float *grad, float *m, float *v,
                            const int64_t *offsets, int n_tensors, float grad_scale,
                            float clip_norm, float lr, float beta1, float beta2, float eps,
                            int64_t step, void *ws, size_t ws_bytes, smmd_stream_t stream);
+
+/* smmd_adam_flat whose SN weight tensors are updated tile by tile together
+ * with the first pass of the next power iteration (layers[i].W must be tensor
+ * sn_tensor[i] of param, layers[i].u the u the next smmd_sn_power_iter_ex
+ * reads; sn_ws that call's workspace).  Same bits as smmd_adam_flat followed
+ * by that pass, in one launch after the norm pass.  n_tensors <= 96 and
+ * n_layers <= 16 (else SMMD_EUNSUPPORTED: use smmd_adam_flat). */
+smmd_status smmd_adam_flat_sn(float *param, const float *grad, float *m, float *v,
+                              const int64_t *offsets, int n_tensors, float grad_scale,
+                              float clip_norm, float lr, float beta1, float beta2, float eps,
+                              int64_t step, void *ws, size_t ws_bytes,
+                              const smmd_sn_layer *layers, const int32_t *sn_tensor,
+                              int n_layers, void *sn_ws, size_t sn_ws_bytes,
+                              smmd_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * Polynomial-kernel MMD statistics of the KID scorer and the 3-sample LR

@@ -92,6 +92,42 @@ __device__ __forceinline__ void ticket_reset(unsigned *ctr) {
     if (threadIdx.x == 0) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// tf.train.AdamOptimizer element update (Eigen ApplyAdam), shared by the flat
+// optimizer and the SN-fused update so both give the same bits:
+//   m += (g - m)(1-b1); v += (g^2 - v)(1-b2); var -= lr_t m / (sqrt(v) + eps)
+// Every operation rounds on its own: with contraction on, the compiler fused
+// different products into the subtractions in the two kernels (g has several
+// uses), and the updates differed in the last bit from the second step on.
+struct AdamK {
+    float gscale, f, lr_t, b1c, b2c, eps;   // f: clip factor; b1c = 1 - b1, b2c = 1 - b2
+    __device__ __forceinline__ void upd(float &p, float g, float &m, float &v) const {
+#pragma clang fp contract(off)
+        g = (g * gscale) * f;
+        m += (g - m) * b1c;
+        v += (g * g - v) * b2c;
+        p -= (m * lr_t) / (sqrtf(v) + eps);
+    }
+};
+
+// clip factor of tf.clip_by_norm (TF 1.x form): clip * min(rsqrt(ss), 1/clip),
+// ss = the norm pass's double partials [b0, b1) summed by wave 0 in a fixed
+// order; every thread of the block gets it (sh: one float of LDS)
+__device__ __forceinline__ float clip_factor_slab(const double *part, int b0, int b1, float clip,
+                                                  float *sh) {
+    if (threadIdx.x < 64) {
+        double s = 0.0;
+        for (int b = b0 + (int)threadIdx.x; b < b1; b += 64) s += part[b];
+        s = wave_sum(s);
+        if (threadIdx.x == 0) {
+            const float ss = (float)s;
+            const float inv = (ss > 0.f) ? rsqrtf(ss) : INFINITY;
+            sh[0] = clip * fminf(inv, 1.f / clip);
+        }
+    }
+    __syncthreads();
+    return sh[0];
+}
+
 inline smmd_status hip_status(hipError_t e) {
     return e == hipSuccess ? SMMD_OK : SMMD_EHIP;
 }

@@ -4,7 +4,9 @@
 // Reference: gan/core/ops.py:228-233 (squared_norm_jacobian),
 // gan/core/model.py:366-403 (add_scaling), gan/core/smmd.py:21-23, :40-42
 // (apply_scaling), gan/core/model.py:444-468 (clip_by_norm + Adam).
-#include "smmd_common.hpp"
+#include "smmd_sn_tile.hpp"
+
+#include <stdlib.h>
 
 namespace smmd {
 
@@ -179,6 +181,7 @@ struct OptTable {
     int64_t off[OPT_MAX + 1];
     int blk[OPT_MAX + 1];        // first block of each tensor (this pass)
     int sblk[OPT_MAX + 1];       // first norm-pass block of each tensor (partial slab)
+    unsigned char skip[OPT_MAX]; // tensor updated elsewhere (the SN-fused update)
 };
 
 __device__ __forceinline__ int opt_find(const OptTable &t, int b) {
@@ -193,8 +196,9 @@ __device__ __forceinline__ int opt_find(const OptTable &t, int b) {
 // every tensor range [off[i], off[i+1]) of the flat buffer is walked as float4
 // when all offsets are multiples of 4 and the buffers 16-byte aligned (vec);
 // FlatAdam pads its tensors to that.
-__device__ __forceinline__ void opt_range(const OptTable &t, int ti, int64_t &lo, int64_t &hi) {
-    lo = t.off[ti] + (int64_t)(blockIdx.x - t.blk[ti]) * t.chunk;
+__device__ __forceinline__ void opt_range(const OptTable &t, int ti, int b, int64_t &lo,
+                                          int64_t &hi) {
+    lo = t.off[ti] + (int64_t)(b - t.blk[ti]) * t.chunk;
     hi = (lo + t.chunk < t.off[ti + 1]) ? lo + t.chunk : t.off[ti + 1];
 }
 
@@ -203,7 +207,7 @@ __global__ __launch_bounds__(256) void opt_sqsum_kernel(OptTable t, const float 
                                                         double *__restrict__ part) {
     const int ti = opt_find(t, blockIdx.x);
     int64_t lo, hi;
-    opt_range(t, ti, lo, hi);
+    opt_range(t, ti, blockIdx.x, lo, hi);
     float acc0 = 0.f, acc1 = 0.f;
     if (vec && hi - lo == OPT_SQ_CHUNK) {     // full block: every load in flight at once
         const float4 *g4 = reinterpret_cast<const float4 *>(g) + lo / 4 + threadIdx.x;
@@ -237,21 +241,9 @@ __global__ __launch_bounds__(256) void opt_sqsum_kernel(OptTable t, const float 
     if (threadIdx.x == 0) part[blockIdx.x] = s;
 }
 
-// clip factor of tf.clip_by_norm (TF 1.x form): clip * min(rsqrt(ss), 1/clip)
 __device__ __forceinline__ float clip_factor(const OptTable &t, int ti, const double *part,
                                              float clip, float *sh) {
-    if (threadIdx.x < 64) {
-        double s = 0.0;
-        for (int b = t.sblk[ti] + (int)threadIdx.x; b < t.sblk[ti + 1]; b += 64) s += part[b];
-        s = wave_sum(s);
-        if (threadIdx.x == 0) {
-            const float ss = (float)s;
-            const float inv = (ss > 0.f) ? rsqrtf(ss) : INFINITY;
-            sh[0] = clip * fminf(inv, 1.f / clip);
-        }
-    }
-    __syncthreads();
-    return sh[0];
+    return clip_factor_slab(part, t.sblk[ti], t.sblk[ti + 1], clip, sh);
 }
 
 __global__ __launch_bounds__(256) void opt_clip_kernel(OptTable t, float *__restrict__ g,
@@ -261,7 +253,7 @@ __global__ __launch_bounds__(256) void opt_clip_kernel(OptTable t, float *__rest
     __shared__ float sh[1];
     const float f = clip_factor(t, ti, part, clip, sh);
     int64_t lo, hi;
-    opt_range(t, ti, lo, hi);
+    opt_range(t, ti, blockIdx.x, lo, hi);
     if (vec) {
         float4 *g4 = reinterpret_cast<float4 *>(g);
         for (int64_t i = lo / 4 + threadIdx.x; i < hi / 4; i += 256) {
@@ -274,36 +266,29 @@ __global__ __launch_bounds__(256) void opt_clip_kernel(OptTable t, float *__rest
     }
 }
 
-struct AdamK {
-    float gscale, f, lr_t, b1c, b2c, eps;   // b1c = 1 - b1, b2c = 1 - b2
-    __device__ __forceinline__ void upd(float &p, float g, float &m, float &v) const {
-        // Eigen ApplyAdam: m += (g - m)(1-b1); v += (g^2 - v)(1-b2);
-        //                  var -= lr_t m / (sqrt(v) + eps)
-        g = (g * gscale) * f;
-        m += (g - m) * b1c;
-        v += (g * g - v) * b2c;
-        p -= (m * lr_t) / (sqrtf(v) + eps);
-    }
+struct AdamArgs {
+    float *p, *m, *v;
+    const float *g;
+    const double *part;     // norm-pass partials
+    float clip;             // > 0: per-tensor clip_by_norm
+    int vec;
+    AdamK k;                // k.f set per tensor
 };
 
-__global__ __launch_bounds__(256) void opt_adam_kernel(OptTable t, float *__restrict__ p,
-                                                       const float *__restrict__ g,
-                                                       float *__restrict__ m,
-                                                       float *__restrict__ v,
-                                                       const double *__restrict__ part,
-                                                       float gscale, float clip, float lr_t,
-                                                       float b1, float b2, float eps, int vec) {
-    const int ti = opt_find(t, blockIdx.x);
+// update block b of the table (blocks of skipped tensors return at once)
+__device__ __forceinline__ void opt_adam_block(const OptTable &t, int b, const AdamArgs &a) {
+    const int ti = opt_find(t, b);
+    if (t.skip[ti]) return;             // block-uniform
+    float *__restrict__ p = a.p;
+    float *__restrict__ m = a.m;
+    float *__restrict__ v = a.v;
+    const float *__restrict__ g = a.g;
+    const int vec = a.vec;
     __shared__ float sh[1];
-    AdamK k;
-    k.gscale = gscale;
-    k.f = (clip > 0.f) ? clip_factor(t, ti, part, clip, sh) : 1.f;
-    k.lr_t = lr_t;
-    k.b1c = 1.f - b1;
-    k.b2c = 1.f - b2;
-    k.eps = eps;
+    AdamK k = a.k;
+    k.f = (a.clip > 0.f) ? clip_factor(t, ti, a.part, a.clip, sh) : 1.f;
     int64_t lo, hi;
-    opt_range(t, ti, lo, hi);
+    opt_range(t, ti, b, lo, hi);
     if (vec && hi - lo == OPT_UP_CHUNK) {     // full block: 4 x OPT_UP_IT float4 loads in flight
         const int64_t b4 = lo / 4 + threadIdx.x;
         float4 *p4 = reinterpret_cast<float4 *>(p) + b4;
@@ -355,6 +340,53 @@ __global__ __launch_bounds__(256) void opt_adam_kernel(OptTable t, float *__rest
     }
 }
 
+__global__ __launch_bounds__(256) void opt_adam_kernel(OptTable t, AdamArgs a) {
+    opt_adam_block(t, blockIdx.x, a);
+}
+
+// one launch for a critic update with SN layers: the SN weight tiles first
+// (tile-shaped, with the next power iteration's P1), then the blocks of every
+// other tensor
+template <int H>
+__global__ __launch_bounds__(256) void opt_adam_sn_kernel(OptTable t, SnAdamTable st,
+                                                          AdamArgs a) {
+    if ((int)blockIdx.x < st.total_tiles)
+        sn_adam_tile<H>(st, blockIdx.x, a.k, a.part, a.clip);
+    else
+        opt_adam_block(t, blockIdx.x - st.total_tiles, a);
+}
+
+// row groups of the fused SN tile (env SMMD_SN_ADAM_H = 1 | 2 | 4, default 2)
+static int sn_adam_groups() {
+    const char *e = getenv("SMMD_SN_ADAM_H");
+    return (e && (e[0] == '1' || e[0] == '4')) ? e[0] - '0' : 2;
+}
+static_assert(sizeof(OptTable) + sizeof(SnAdamTable) + sizeof(AdamArgs) <= 4000,
+              "kernel argument budget");
+
+static AdamArgs adam_args(float *p, const float *g, float *m, float *v, const void *ws,
+                          float gscale, float clip, double lr_t, float b1, float b2, float eps,
+                          int vec) {
+    AdamArgs a;
+    a.p = p;
+    a.m = m;
+    a.v = v;
+    a.g = g;
+    a.part = (const double *)ws;
+    a.clip = clip;
+    a.vec = vec;
+    a.k.gscale = gscale;
+    a.k.f = 1.f;
+    a.k.lr_t = (float)lr_t;
+    a.k.b1c = 1.f - b1;
+    a.k.b2c = 1.f - b2;
+    a.k.eps = eps;
+    return a;
+}
+
+// the update pass skips skipped tensors' blocks without launching them: a
+// skipped tensor keeps one block (the map stays strictly increasing) that
+// returns at once
 static int opt_vec(const int64_t *off, int n, const void *a, const void *b, const void *c,
                    const void *d) {
     for (int i = 0; i <= n; ++i)
@@ -368,7 +400,8 @@ static int opt_vec(const int64_t *off, int n, const void *a, const void *b, cons
 static int64_t opt_blocks(int64_t n, int chunk) { return n == 0 ? 1 : (n + chunk - 1) / chunk; }
 
 // table of tensors [first, first + count) for a pass of `chunk`-element blocks
-static bool build_opt(const int64_t *off, int first, int count, int chunk, OptTable &t) {
+static bool build_opt(const int64_t *off, int first, int count, int chunk, OptTable &t,
+                      const unsigned char *skip = nullptr) {
     memset(&t, 0, sizeof(t));
     t.n = count;
     t.chunk = chunk;
@@ -381,7 +414,8 @@ static bool build_opt(const int64_t *off, int first, int count, int chunk, OptTa
         t.blk[i] = (int)blocks;
         t.sblk[i] = (int)sblocks;
         const int64_t n = t.off[i + 1] - t.off[i];
-        blocks += opt_blocks(n, chunk);
+        blocks += skip && skip[first + i] ? 1 : opt_blocks(n, chunk);
+        t.skip[i] = skip && skip[first + i] ? 1 : 0;
         sblocks += opt_blocks(n, OPT_SQ_CHUNK);
         if (blocks > INT32_MAX / 2) return false;
     }
@@ -519,13 +553,65 @@ smmd_status smmd_adam_flat(float *param, const float *grad, float *m, float *v,
         if (clip_norm > 0.f)
             hipLaunchKernelGGL(opt_sqsum_kernel, dim3(ts.total_blocks), dim3(256), 0, s, ts, grad,
                                grad_scale, vec, (double *)ws);
-        hipLaunchKernelGGL(opt_adam_kernel, dim3(tu.total_blocks), dim3(256), 0, s, tu, param, grad,
-                           m, v, (const double *)ws, grad_scale, clip_norm, (float)lr_t, beta1,
-                           beta2, eps, vec);
+        hipLaunchKernelGGL(opt_adam_kernel, dim3(tu.total_blocks), dim3(256), 0, s, tu,
+                           adam_args(param, grad, m, v, ws, grad_scale, clip_norm, lr_t, beta1,
+                                     beta2, eps, vec));
         smmd_status st = last_launch_status();
         if (st != SMMD_OK) return st;
     }
     return SMMD_OK;
+}
+
+smmd_status smmd_adam_flat_sn(float *param, const float *grad, float *m, float *v,
+                              const int64_t *offsets, int n_tensors, float grad_scale,
+                              float clip_norm, float lr, float beta1, float beta2, float eps,
+                              int64_t step, void *ws, size_t ws_bytes,
+                              const smmd_sn_layer *layers, const int32_t *sn_tensor,
+                              int n_layers, void *sn_ws, size_t sn_ws_bytes,
+                              smmd_stream_t stream) {
+    if (!param || !grad || !m || !v || !offsets || n_tensors < 1 || step < 1) return SMMD_EINVAL;
+    if (!layers || !sn_tensor || n_layers < 1 || n_layers > SMMD_SN_MAX_LAYERS) return SMMD_EINVAL;
+    if (n_tensors > OPT_MAX) return SMMD_EUNSUPPORTED;     // one partial slab for every tensor
+    if (clip_norm > 0.f && (!ws || ws_bytes < smmd_opt_workspace_bytes(offsets, n_tensors)))
+        return SMMD_EWORKSPACE;
+    unsigned char skip[OPT_MAX] = {0};
+    for (int i = 0; i < n_layers; ++i) {
+        const int ti = sn_tensor[i];
+        if (ti < 0 || ti >= n_tensors || skip[ti]) return SMMD_EINVAL;
+        skip[ti] = 1;
+    }
+    const double lr_t = (double)lr * sqrt(1.0 - pow((double)beta2, (double)step)) /
+                        (1.0 - pow((double)beta1, (double)step));
+    hipStream_t s = (hipStream_t)stream;
+    OptTable ts, tu;
+    if (!build_opt(offsets, 0, n_tensors, OPT_SQ_CHUNK, ts) ||
+        !build_opt(offsets, 0, n_tensors, OPT_UP_CHUNK, tu, skip))
+        return SMMD_EINVAL;
+    const int vec = opt_vec(offsets, n_tensors, param, grad, m, v);
+    SnAdamHost h;
+    h.param = param;
+    h.m = m;
+    h.v = v;
+    h.grad = grad;
+    h.offsets = offsets;
+    h.sblk = ts.sblk;
+    SnAdamTable snt;
+    const smmd_status r = sn_adam_table(layers, sn_tensor, n_layers, h, sn_ws, sn_ws_bytes, snt);
+    if (r != SMMD_OK) return r;
+    if (clip_norm > 0.f)
+        hipLaunchKernelGGL(opt_sqsum_kernel, dim3(ts.total_blocks), dim3(256), 0, s, ts, grad,
+                           grad_scale, vec, (double *)ws);
+    const AdamArgs aa = adam_args(param, grad, m, v, ws, grad_scale, clip_norm, lr_t, beta1, beta2,
+                                  eps, vec);
+    const dim3 grid(snt.total_tiles + tu.total_blocks);
+    const int hg = sn_adam_groups();
+    if (hg == 1)
+        hipLaunchKernelGGL(opt_adam_sn_kernel<1>, grid, dim3(256), 0, s, tu, snt, aa);
+    else if (hg == 4)
+        hipLaunchKernelGGL(opt_adam_sn_kernel<4>, grid, dim3(256), 0, s, tu, snt, aa);
+    else
+        hipLaunchKernelGGL(opt_adam_sn_kernel<2>, grid, dim3(256), 0, s, tu, snt, aa);
+    return last_launch_status();
 }
 
 }  // extern "C"

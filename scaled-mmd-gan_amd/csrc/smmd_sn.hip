@@ -22,20 +22,12 @@
 // (arrival tickets, write-through partials).  It removes the R2 launch but puts
 // each reducer's serial chain of dependent L2 loads at the tail of its kernel:
 // P1 11 -> 19 us, P2 + R2 20 -> 34 us on the SNResNet-64 critic.
-#include "smmd_common.hpp"
+#include "smmd_sn_tile.hpp"
 
 #include <atomic>
 #include <stdlib.h>
 
 namespace smmd {
-
-#ifndef SMMD_SN_TR
-#define SMMD_SN_TR 32
-#endif
-constexpr int SN_TR = SMMD_SN_TR;   // tile rows (multi-launch path)
-constexpr int SN_TC = 256;     // tile cols (64 lanes x 4)
-constexpr int SN_RPW = SN_TR / 4;   // rows per wave
-constexpr int SN_CHUNK = 16;   // layers per launch set
 
 struct SnLayerDev {
     const float *W;
@@ -79,33 +71,6 @@ __device__ __forceinline__ int find_layer(const SnTable &t, int tile) {
     return __builtin_amdgcn_readfirstlane(l);
 }
 
-// load the 16 rows x 4 cols this thread owns (zero outside the matrix).
-// Interior tiles of 16-B aligned layers take one branch-free path: 16
-// independent float4 loads issued back to back.
-__device__ __forceinline__ void load_tile(const float *__restrict__ base, int N, int K, int vec,
-                                          int r0, int c0, float4 (&w)[SN_RPW]) {
-    if (vec && r0 + SN_RPW <= N && c0 + 3 < K) {
-        const float4 *p = reinterpret_cast<const float4 *>(base + (size_t)r0 * K + c0);
-        const int stride4 = K / 4;
-#pragma unroll
-        for (int i = 0; i < SN_RPW; ++i) w[i] = p[(size_t)i * stride4];
-        return;
-    }
-#pragma unroll
-    for (int i = 0; i < SN_RPW; ++i) {
-        const int r = r0 + i;
-        float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (r < N) {
-            const float *p = base + (size_t)r * K + c0;
-            if (c0 + 0 < K) x.x = p[0];
-            if (c0 + 1 < K) x.y = p[1];
-            if (c0 + 2 < K) x.z = p[2];
-            if (c0 + 3 < K) x.w = p[3];
-        }
-        w[i] = x;
-    }
-}
-
 __global__ __launch_bounds__(256) void sn_p1_kernel(SnTable t) {
     const int tile = blockIdx.x;
     const SnLayerDev L = t.L[find_layer(t, tile)];
@@ -115,34 +80,9 @@ __global__ __launch_bounds__(256) void sn_p1_kernel(SnTable t) {
     const int r0 = rt * SN_TR + w * SN_RPW;
     const int c0 = ct * SN_TC + lane * 4;
     const float *uin = (t.iter == 0) ? L.u : L.ucur;
-
     float4 wt[SN_RPW];
     load_tile(L.W, L.N, L.K, L.vec, r0, c0, wt);
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int i = 0; i < SN_RPW; ++i) {
-        const float un = (r0 + i < L.N) ? uin[r0 + i] : 0.f;
-        acc.x = fmaf(un, wt[i].x, acc.x);
-        acc.y = fmaf(un, wt[i].y, acc.y);
-        acc.z = fmaf(un, wt[i].z, acc.z);
-        acc.w = fmaf(un, wt[i].w, acc.w);
-    }
-    __shared__ float4 red[4][64];
-    red[w][lane] = acc;
-    __syncthreads();
-    if (w == 0) {
-        float4 s = red[0][lane];
-#pragma unroll
-        for (int i = 1; i < 4; ++i) {
-            s.x += red[i][lane].x; s.y += red[i][lane].y;
-            s.z += red[i][lane].z; s.w += red[i][lane].w;
-        }
-        float *dst = L.p1 + (size_t)rt * L.K;
-        const float sv[4] = {s.x, s.y, s.z, s.w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (c0 + k < L.K) dst[c0 + k] = sv[k];
-    }
+    p1_tile(uin, L.p1, L.N, L.K, rt, r0, c0, wt);
 }
 
 __global__ __launch_bounds__(256) void sn_p2_kernel(SnTable t) {
@@ -869,6 +809,41 @@ static int resident_grid(K kernel, int slot, int n_layers, const SnTable &t) {
     return g;
 }
 
+smmd_status sn_adam_table(const smmd_sn_layer *layers, const int32_t *sn_tensor, int n_layers,
+                          const SnAdamHost &a, void *sn_ws, size_t sn_ws_bytes, SnAdamTable &t) {
+    if (n_layers < 1 || n_layers > SN_CHUNK) return SMMD_EUNSUPPORTED;
+    if (!sn_ws || sn_ws_bytes < smmd_sn_workspace_bytes(layers, n_layers)) return SMMD_EWORKSPACE;
+    SnTable st;
+    if (!build_table(layers, 0, n_layers, (char *)sn_ws + 256, st, SN_TR)) return SMMD_EINVAL;
+    memset(&t, 0, sizeof(t));
+    t.n_layers = n_layers;
+    t.total_tiles = st.total_tiles;
+    for (int i = 0; i < n_layers; ++i) {
+        const smmd_sn_layer &src = layers[i];
+        const int ti = sn_tensor[i];
+        const int64_t off = a.offsets[ti];
+        // the SN weight must be tensor ti of the flat buffer, N x K rows
+        if (!src.u || src.W != a.param + off || a.offsets[ti + 1] - off < (int64_t)src.N * src.K)
+            return SMMD_EINVAL;
+        SnAdamLayerDev &L = t.L[i];
+        L.p = const_cast<float *>(a.param) + off;
+        L.m = const_cast<float *>(a.m) + off;
+        L.v = const_cast<float *>(a.v) + off;
+        L.g = a.grad + off;
+        L.u = src.u;
+        L.p1 = st.L[i].p1;
+        L.N = src.N;
+        L.K = src.K;
+        L.nct = st.L[i].nct;
+        L.tile_begin = st.L[i].tile_begin;
+        const uintptr_t al = (uintptr_t)L.p | (uintptr_t)L.m | (uintptr_t)L.v | (uintptr_t)L.g;
+        L.vec = (src.K % 4 == 0) && (al % 16 == 0);
+        L.sb0 = a.sblk[ti];
+        L.sb1 = a.sblk[ti + 1];
+    }
+    return SMMD_OK;
+}
+
 }  // namespace smmd
 
 using namespace smmd;
@@ -885,6 +860,14 @@ size_t smmd_sn_workspace_bytes(const smmd_sn_layer *layers, int n_layers) {
 smmd_status smmd_sn_power_iter(const smmd_sn_layer *layers, int n_layers, int num_iters,
                                float eps, int update_u, void *ws, size_t ws_bytes,
                                smmd_stream_t stream) {
+    return smmd_sn_power_iter_ex(layers, n_layers, num_iters, eps, update_u, 0, ws, ws_bytes,
+                                 stream);
+}
+
+smmd_status smmd_sn_power_iter_ex(const smmd_sn_layer *layers, int n_layers, int num_iters,
+                                  float eps, int update_u, int flags, void *ws, size_t ws_bytes,
+                                  smmd_stream_t stream) {
+    if (flags & ~SMMD_SN_P1_READY) return SMMD_EINVAL;
     if (!layers || n_layers < 1 || n_layers > SMMD_SN_MAX_LAYERS || num_iters < 1)
         return SMMD_EINVAL;
     for (int i = 0; i < n_layers; ++i)
@@ -920,7 +903,8 @@ smmd_status smmd_sn_power_iter(const smmd_sn_layer *layers, int n_layers, int nu
         for (int it = 0; it < num_iters; ++it) {
             t.iter = it;
             t.last_iter = (it == num_iters - 1);
-            hipLaunchKernelGGL(sn_p1_kernel, dim3(t.total_tiles), dim3(256), 0, s, t);
+            if (it > 0 || !(flags & SMMD_SN_P1_READY))   // else written by smmd_adam_flat_sn
+                hipLaunchKernelGGL(sn_p1_kernel, dim3(t.total_tiles), dim3(256), 0, s, t);
             hipLaunchKernelGGL(sn_p2_kernel, dim3(t.total_tiles), dim3(256), 0, s, t);
             hipLaunchKernelGGL(sn_r2_kernel, dim3(t.n_layers), dim3(1024), 0, s, t);
         }

@@ -110,6 +110,10 @@ class MMD_GAN:
                                 name='G')
         self.d_optim = FlatAdam(self.d_vars, c.learning_rate_D, c.beta1, c.beta2, clip_norm=clip,
                                 name='D')
+        # each optimizer step also writes the first power-iteration pass of
+        # the next refresh of its network's SN bank
+        self.d_optim.attach_sn(self.sn_D)
+        self.g_optim.attach_sn(self.sn_G)
         self.lr = float(c.learning_rate)
         self.sc = float(c.scaling_coeff) if c.with_scaling else None
         self.gp = float(c.gradient_penalty)

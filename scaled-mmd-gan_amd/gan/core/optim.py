@@ -8,10 +8,16 @@ fp32 buffer, and so is its gradient, so
 * the data-parallel gradient exchange is a single RCCL all_reduce over
   ``flat_grad`` (one bucket of ~40 MB for the SNResNet critic), and
 * clip + Adam for all tensors is one ``smmd_adam_flat`` launch set.
+
+With a spectral-norm bank attached (``attach_sn``) the step is
+``smmd_adam_flat_sn``: the SN weights are updated tile by tile together with
+the first pass of the bank's next power iteration, which the next
+``refresh`` then skips (one read of every SN weight less per step).
 """
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -47,6 +53,7 @@ class FlatAdam:
                 p.data = view
                 p.grad = self._view(self.flat_grad, p, o)
         self.step_count = 0
+        self._sn = None
         nbytes = _lib.lib().smmd_opt_workspace_bytes(self.offsets, len(self.params))
         self.ws = torch.zeros(max(nbytes, 256), dtype=torch.uint8, device=dev)
 
@@ -79,6 +86,37 @@ class FlatAdam:
             _lib.ptr(self.ws), self.ws.numel(), _lib.stream_handle(self.flat_grad.device)),
             'smmd_clip_by_norm_flat')
 
+    def attach_sn(self, bank):
+        """Fuse the first power-iteration pass of ``bank`` (a
+        SpectralNormBank whose weights are parameters of this optimizer) into
+        ``step``.  Returns False, leaving the plain update, when the fused
+        call does not apply (env SMMD_SN_FUSE_P1=0, no SN layers, too many
+        tensors, a weight outside this optimizer)."""
+        self._sn = None
+        if os.environ.get('SMMD_SN_FUSE_P1', '1') == '0' or bank is None or not bank.entries:
+            return False
+        if len(self.params) > _lib.OPT_MAX_FUSED or len(bank.entries) > _lib.SN_MAX_FUSED:
+            return False
+        index = {id(p): i for i, p in enumerate(self.params)}
+        idx = [index.get(id(e.weight)) for e in bank.entries]
+        if any(i is None for i in idx):
+            return False
+        self._sn = (bank, (ctypes.c_int32 * len(idx))(*idx))
+        return True
+
+    def _sn_layers(self):
+        bank, idx = self._sn
+        base = self.flat_param.data_ptr()
+        arr = (_lib.SnLayer * len(bank.entries))()
+        for k, e in enumerate(bank.entries):
+            W = e.weight
+            if W.data_ptr() != base + 4 * self.offsets[idx[k]]:
+                return None         # re-pointed since attach_sn: plain update
+            arr[k].W = W.data_ptr()
+            arr[k].u = e.u.data_ptr()
+            arr[k].N, arr[k].K = e.N, e.K
+        return arr
+
     def step(self, grad_scale=1.0, clip=True, lr=None):
         self._check_grads()
         self.step_count += 1
@@ -86,10 +124,19 @@ class FlatAdam:
         args = (_lib.ptr(self.flat_param), _lib.ptr(self.flat_grad), _lib.ptr(self.m),
                 _lib.ptr(self.v), self.offsets, len(self.params), float(grad_scale), c,
                 float(self.lr if lr is None else lr), float(self.beta1), float(self.beta2),
-                float(self.eps), self.step_count, _lib.ptr(self.ws), self.ws.numel(),
-                _lib.stream_handle(self.flat_grad.device))
+                float(self.eps), self.step_count, _lib.ptr(self.ws), self.ws.numel())
+        stream = _lib.stream_handle(self.flat_grad.device)
+        layers = self._sn_layers() if self._sn is not None else None
+        if layers is not None:
+            bank, idx = self._sn
+            with _lib.timed('smmd_adam_flat_sn[%s]' % self.name):
+                st = _lib.lib().smmd_adam_flat_sn(*args, layers, idx, len(bank.entries),
+                                                  _lib.ptr(bank.ws), bank.ws.numel(), stream)
+            _lib.check(st, 'smmd_adam_flat_sn')
+            bank.mark_p1_ready()
+            return
         with _lib.timed('smmd_adam_flat[%s]' % self.name):
-            st = _lib.lib().smmd_adam_flat(*args)
+            st = _lib.lib().smmd_adam_flat(*args, stream)
         _lib.check(st, 'smmd_adam_flat')
 
     def state_dict(self):

@@ -32,7 +32,7 @@ def truncated_normal_(t, std=1.0):
 
 class _SNBatch(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, bank, update_u, *tensors):
+    def forward(ctx, bank, update_u, flags, *tensors):
         n = len(bank.entries)
         Ws, ss = tensors[:n], tensors[n:]
         outs = []
@@ -55,11 +55,11 @@ class _SNBatch(torch.autograd.Function):
             L.N, L.K = e.N, e.K
         dev = Ws[0].device
         lib = _lib.lib()
-        args = (arr, n, bank.num_iters, SN_EPS, 1 if update_u else 0, _lib.ptr(bank.ws),
+        args = (arr, n, bank.num_iters, SN_EPS, 1 if update_u else 0, flags, _lib.ptr(bank.ws),
                 bank.ws.numel(), _lib.stream_handle(dev))
         with _lib.timed('smmd_sn_power_iter'):
-            st = lib.smmd_sn_power_iter(*args)
-        _lib.check(st, 'smmd_sn_power_iter')
+            st = lib.smmd_sn_power_iter_ex(*args)
+        _lib.check(st, 'smmd_sn_power_iter_ex')
         ctx.bank = bank
         ctx.save_for_backward(*Ws, *ss)
         return tuple(outs)
@@ -101,7 +101,7 @@ class _SNBatch(torch.autograd.Function):
                 gs_out.append(None)
             else:
                 gs_out.append(gs.view_as(s))
-        return (None, None, *gWs, *gs_out)
+        return (None, None, None, *gWs, *gs_out)
 
 
 def _memfmt(W):
@@ -154,7 +154,23 @@ class SpectralNormBank:
         self.entries = [SNEntry(m) for m in modules]
         self.num_iters = num_iters
         self.ws = None
+        self._p1_token = None
         self._alloc_ws()
+
+    def _state_token(self):
+        # storage and version of every W and u: an in-place write through
+        # torch (copy_, load_state_dict, broadcast into the parameter) bumps a
+        # version; the fused optimizer's own write does not
+        return tuple((e.weight.data_ptr(), e.weight._version, e.u.data_ptr(), e.u._version)
+                     for e in self.entries)
+
+    def mark_p1_ready(self):
+        """Called by FlatAdam right after smmd_adam_flat_sn wrote the first
+        pass of the next power iteration into ``ws``."""
+        self._p1_token = self._state_token()
+
+    def invalidate(self):
+        self._p1_token = None
 
     def _alloc_ws(self):
         if not self.entries:
@@ -169,6 +185,7 @@ class SpectralNormBank:
     def to(self, device):
         for e in self.entries:
             e.to(device)
+        self._p1_token = None
         self._alloc_ws()
 
     def refresh(self, update_u=True):
@@ -178,7 +195,9 @@ class SpectralNormBank:
         ss = [e.scale if e.scale is not None else torch.empty(0, device=Ws[0].device)
               for e in self.entries]
         _lib.require_cuda(*Ws)
-        outs = _SNBatch.apply(self, bool(update_u), *Ws, *ss)
+        ready = self._p1_token is not None and self._p1_token == self._state_token()
+        self._p1_token = None
+        outs = _SNBatch.apply(self, bool(update_u), _lib.SN_P1_READY if ready else 0, *Ws, *ss)
         for e, w in zip(self.entries, outs):
             e.module.w_eff = w
         return list(outs)
@@ -190,6 +209,7 @@ class SpectralNormBank:
         return {'u': [e.u.clone() for e in self.entries]}
 
     def load_state_dict(self, sd):
+        self._p1_token = None
         for e, u in zip(self.entries, sd['u']):
             e.u.copy_(u)
 
@@ -220,7 +240,7 @@ def spectral_normed_weight(W, u=None, num_iters=1, update_collection=None, with_
     e.sigma = torch.ones(1, device=W.device, dtype=torch.float32)
     bank.entries, bank.num_iters, bank.ws = [e], num_iters, None
     bank._alloc_ws()
-    W_eff_t, = _SNBatch.apply(bank, True, Wt, torch.empty(0, device=W.device))
+    W_eff_t, = _SNBatch.apply(bank, True, 0, Wt, torch.empty(0, device=W.device))
     if update_collection is None:
         with torch.no_grad():
             u.copy_(e.u.view_as(u))

@@ -78,6 +78,20 @@ def test_argument_validation_without_gpu(L):
     assert L.smmd_mmd2_fwd(d, x, 4, x, 4, 64, 0, 0, 4, 0, 4, None, None, None, None, x, wide - 1,
                            None) == 3          # EWORKSPACE
     assert L.smmd_sn_power_iter(None, 0, 1, 1e-12, 1, None, 0, None) == 1
+    arr = (_lib.SnLayer * 1)()
+    arr[0].N, arr[0].K = 4, 4
+    assert L.smmd_sn_power_iter_ex(arr, 1, 1, 1e-12, 1, 2, x, 1 << 20, None) == 1   # bad flag
+    offs = (ctypes.c_int64 * 3)(0, 16, 32)
+    idx = (ctypes.c_int32 * 1)(5)                                 # tensor index out of range
+    assert L.smmd_adam_flat_sn(x, x, x, x, offs, 2, 1.0, 1.0, 1e-4, 0.5, 0.9, 1e-8, 1, x,
+                               1 << 20, arr, idx, 1, x, 1 << 20, None) == 1
+    idx2 = (ctypes.c_int32 * 2)(1, 1)                             # one tensor twice
+    arr2 = (_lib.SnLayer * 2)()
+    assert L.smmd_adam_flat_sn(x, x, x, x, offs, 2, 1.0, 1.0, 1e-4, 0.5, 0.9, 1e-8, 1, x,
+                               1 << 20, arr2, idx2, 2, x, 1 << 20, None) == 1
+    big = (ctypes.c_int64 * 98)(*range(0, 98 * 4, 4))            # > 96 tensors: unsupported
+    assert L.smmd_adam_flat_sn(x, x, x, x, big, 97, 1.0, 1.0, 1e-4, 0.5, 0.9, 1e-8, 1, x,
+                               1 << 20, arr, (ctypes.c_int32 * 1)(0), 1, x, 1 << 20, None) == 4
     assert L.smmd_witness_bwd(d, x, 4, x, 4, x, 4, 1, None, x, x, x, None) == 1
 
 

@@ -109,7 +109,9 @@ def test_global_mode_two_ranks_equal_one_process(dev):
         p.join(timeout=60)
         assert p.exitcode == 0
     for _, d_loss, aux, grad, params in outs:
-        np.testing.assert_allclose(d_loss, ref[0], rtol=1e-4)
+        # d_loss ~ -5e-5 is a difference of O(1e-2) kernel means: the summation
+        # order of two ranks vs one process moves it by ~1e-4 relative
+        np.testing.assert_allclose(d_loss, ref[0], rtol=1e-3)
         np.testing.assert_allclose(aux[3], ref[1][3], rtol=1e-4)         # J, global batch
         scale = np.abs(ref[2]).max()
         np.testing.assert_allclose(grad, ref[2], rtol=1e-3, atol=2e-3 * scale)

@@ -28,6 +28,8 @@ def main():
     ap.add_argument('--iters', type=int, default=200)
     ap.add_argument('--json', default='')
     ap.add_argument('--batch', type=int, default=64)
+    ap.add_argument('--no-fuse', action='store_true',
+                    help='plain smmd_adam_flat + full refresh (no SN-fused update)')
     args = ap.parse_args()
     from gan.core import _lib, mmd, ops
     from gan.core.architecture import SNResNetDiscriminator
@@ -40,6 +42,8 @@ def main():
                               input_size=64).to(dev)
     bank = SpectralNormBank(sn_modules(D))
     opt = FlatAdam([p for p in D.parameters() if p.requires_grad], 2e-4, name='D')
+    if not args.no_fuse:     # as MMD_GAN: the critic step of the bench's 5 D + 1 G schedule
+        assert opt.attach_sn(bank)
     Gs = [torch.randn_like(e.weight) for e in bank.entries]
     B = args.batch
     X = torch.randn(B, 1, device=dev, requires_grad=True)
@@ -68,6 +72,7 @@ def main():
     kn = sum(e.N * e.K for e in bank.entries)
     alg = {'smmd_sn_power_iter': kn * 4 * 2, 'smmd_sn_weight_bwd': kn * 4 * 3,
            'smmd_adam_flat[D]': opt.numel * 4 * 8,
+           'smmd_adam_flat_sn[D]': opt.numel * 4 * 8,
            'smmd_mmd2_fwd': 2 * B * 4 * 2 + 32,
            'smmd_scaled_loss_fwd': B * 3 * 64 * 64 * 4,
            'smmd_scaled_loss_bwd': 2 * B * 3 * 64 * 64 * 4}

@@ -18,6 +18,7 @@ GROUPS = {
                            'sn_resident_kernel'),
     'smmd_sn_weight_bwd': ('sn_bwd_a_kernel', 'sn_bwd_b_kernel', 'sn_resident_bwd_kernel'),
     'smmd_adam_flat': ('opt_sqsum_kernel', 'opt_adam_kernel'),
+    'smmd_adam_flat_sn': ('opt_sqsum_kernel', 'opt_adam_kernel', 'sn_adam_p1_kernel'),
     'smmd_mmd2_fwd': ('mmd2_fused_kernel',),
     'smmd_scaled_loss_fwd': ('sqnorm_partial_kernel', 'scaled_loss_final_kernel'),
     'smmd_scaled_loss_bwd': ('scaled_loss_bwd_kernel',),
@@ -38,7 +39,10 @@ def main():
     write = per_kernel(sys.argv[2])
     out = {'_note': 'bytes per call; read = 2 * FETCH_SIZE(KB) * 1024 (gfx950 correction), '
                     'write = WRITE_SIZE(KB) * 1024'}
+    fused = any('sn_adam_p1_kernel' in k for k in fetch)
     for entry, kernels in GROUPS.items():
+        if entry == ('smmd_adam_flat' if fused else 'smmd_adam_flat_sn'):
+            continue        # the opt_* kernels belong to whichever entry the run used
         rd = wr = 0.0
         found = []
         for kname in fetch:
