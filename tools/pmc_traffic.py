@@ -18,7 +18,7 @@ GROUPS = {
                            'sn_resident_kernel'),
     'smmd_sn_weight_bwd': ('sn_bwd_a_kernel', 'sn_bwd_b_kernel', 'sn_resident_bwd_kernel'),
     'smmd_adam_flat': ('opt_sqsum_kernel', 'opt_adam_kernel'),
-    'smmd_adam_flat_sn': ('opt_sqsum_kernel', 'opt_adam_kernel', 'sn_adam_p1_kernel'),
+    'smmd_adam_flat_sn': ('opt_sqsum_kernel', 'opt_adam_sn_kernel'),
     'smmd_mmd2_fwd': ('mmd2_fused_kernel',),
     'smmd_scaled_loss_fwd': ('sqnorm_partial_kernel', 'scaled_loss_final_kernel'),
     'smmd_scaled_loss_bwd': ('scaled_loss_bwd_kernel',),
@@ -26,12 +26,13 @@ GROUPS = {
 
 
 def per_kernel(path):
+    """kernel name -> (sum of the counter over its launches, launches)"""
     acc = defaultdict(list)
     for r in csv.DictReader(open(path)):
         if 'smmd::' not in r['Kernel_Name']:
             continue
         acc[r['Kernel_Name']].append(float(r['Counter_Value']))
-    return {k: sum(v) / len(v) for k, v in acc.items()}
+    return {k: (sum(v), len(v)) for k, v in acc.items()}
 
 
 def main():
@@ -39,20 +40,27 @@ def main():
     write = per_kernel(sys.argv[2])
     out = {'_note': 'bytes per call; read = 2 * FETCH_SIZE(KB) * 1024 (gfx950 correction), '
                     'write = WRITE_SIZE(KB) * 1024'}
-    fused = any('sn_adam_p1_kernel' in k for k in fetch)
+    fused = any('opt_adam_sn_kernel' in k for k in fetch)
     for entry, kernels in GROUPS.items():
         if entry == ('smmd_adam_flat' if fused else 'smmd_adam_flat_sn'):
             continue        # the opt_* kernels belong to whichever entry the run used
         rd = wr = 0.0
         found = []
+        calls = 0
         for kname in fetch:
             if any(k in kname for k in kernels):
-                rd += 2 * fetch[kname] * 1024
+                rd += 2 * fetch[kname][0] * 1024
+                calls = max(calls, fetch[kname][1])
                 found.append(kname.split('(')[0])
         for kname in write:
             if any(k in kname for k in kernels):
-                wr += write[kname] * 1024
+                wr += write[kname][0] * 1024
+        # per call of the entry point = launches of its most frequent kernel
+        # (the SN refresh skips P1 after a fused update: P1's bytes are spread
+        # over the calls that did run it and those that did not)
         if found:
+            rd /= calls
+            wr /= calls
             out[entry] = {'read_bytes': round(rd), 'write_bytes': round(wr),
                           'traffic_bytes': round(rd + wr), 'kernels': sorted(set(found))}
     print(json.dumps(out, indent=1))
