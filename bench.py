@@ -261,7 +261,7 @@ def main():
             dist.init_process_group(backend)
     # MIOpen solver choice: the committed find db (gan/core/miopen_db.py),
     # installed before the first convolution
-    from gan.core import miopen_db
+    from gan.core import architecture, miopen_db
     miopen_db.install()
     # MIOpen immediate mode: one kernel compile per conv config on a fresh box;
     # benchmark=True would compile every candidate solver (minutes per shape).
@@ -397,6 +397,8 @@ def main():
                    'memory_format': 'channels_last' if args.channels_last else 'nchw',
                    'miopen_winograd': bool(args.miopen_winograd),
                    'miopen_find': bool(args.miopen_find),
+                   'conv_mean_pool': ('folded 4x4 stride-2 conv' if architecture.FOLD_POOL
+                                      else 'conv3x3 + mean pool'),
                    'miopen_db': os.environ.get('MIOPEN_USER_DB_PATH')},
         'roofline': {'bound': 'hbm', 'kernel': dom, 'achieved': kernels[dom]['GB_s'],
                      'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': kernels[dom]['frac'],

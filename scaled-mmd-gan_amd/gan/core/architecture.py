@@ -9,11 +9,13 @@ plain dcgan / dcgan5 / sngan-dcgan5 / resnet5 variants.  The conditional
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .convops import mean_pool2
+from .convops import conv2d, fold_pool_weight, mean_pool2
 from .snops import Conv2d, Deconv2d, Linear, batch_norm, lrelu
 
 
@@ -48,6 +50,10 @@ class _Up(nn.Module):
         return self.conv(F.interpolate(x, scale_factor=2, mode='nearest'))
 
 
+# SMMD_FOLD_POOL=0 restores the literal conv -> mean-pool order (A/B, tests)
+FOLD_POOL = os.environ.get('SMMD_FOLD_POOL', '1') != '0'
+
+
 class _ConvMeanPool(nn.Module):
     """block.py:63-66."""
 
@@ -56,7 +62,15 @@ class _ConvMeanPool(nn.Module):
         self.conv = Conv2d(cin, cout, k, 1, bias=bias, init='glorot_uniform', **sn)
 
     def forward(self, x):
-        return mean_pool2(self.conv(x))
+        c = self.conv
+        if FOLD_POOL and c.k == 3 and c.stride == 1 and x.shape[2] % 2 == 0 \
+                and x.shape[3] % 2 == 0:
+            # meanpool2(conv3x3(x)) as ONE 4x4 stride-2 conv on the folded
+            # weight: same value, a quarter of the output rows, no pool and no
+            # upsample in the backward; MIOpen runs fwd / Dx / Dw of it in about
+            # half the time of the 3x3 + pool (tools/fold_bench.py, r02 profiles)
+            return conv2d(x, fold_pool_weight(c.effective_weight()), c.bias, 2, 1)
+        return mean_pool2(c(x))
 
 
 class _MeanPoolConv(nn.Module):

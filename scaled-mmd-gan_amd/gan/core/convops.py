@@ -140,6 +140,15 @@ class _MeanPool2(torch.autograd.Function):
         return _Up2Quarter.apply(g.contiguous())
 
 
+def fold_pool_weight(w):
+    """W [cout, cin, 3, 3] -> W' [cout, cin, 4, 4] with
+    meanpool2(conv(x, W, stride 1, pad 1)) == conv(x, W', stride 2, pad 1):
+    W'[s, t] = 1/4 sum_{a, b in {0, 1}} W[s - a, t - b], i.e. a 2x2 stride-1
+    mean over W zero-padded by one (ConvMeanPool, gan/core/resnet/block.py:63-66,
+    as one strided conv; linear, so differentiable to any order)."""
+    return F.avg_pool2d(F.pad(w, (1, 1, 1, 1)), 2, stride=1)
+
+
 def mean_pool2(x):
     """2x2 mean pool, the reference's add_n of the four strided slices / 4
     (gan/core/resnet/block.py:65, :71), as a linear op whose backward is one

@@ -175,6 +175,31 @@ def test_mean_pool2_first_and_second_order():
     assert torch.autograd.gradgradcheck(mean_pool2, (x,))
 
 
+def test_folded_conv_mean_pool_first_and_second_order():
+    """ConvMeanPool as one 4x4 stride-2 conv on the folded weight equals the
+    literal conv3x3 -> mean pool (block.py:63-66) in value, input gradient and
+    the parameter gradient of a gradient penalty through it (float64)."""
+    from gan.core import architecture
+    torch.manual_seed(2)
+    blk = architecture._ConvMeanPool(3, 5, 3, True).double()
+    x = torch.randn(2, 3, 8, 6, dtype=torch.float64, requires_grad=True)
+    res = []
+    saved = architecture.FOLD_POOL
+    try:
+        for fold in (True, False):
+            architecture.FOLD_POOL = fold
+            y = blk(x)
+            g, = torch.autograd.grad(torch.tanh(y).sum(), x, create_graph=True)
+            L = (g * g).sum() + y.pow(2).mean()
+            res.append((y.detach(),) + torch.autograd.grad(
+                L, (x, blk.conv.weight, blk.conv.bias)))
+    finally:
+        architecture.FOLD_POOL = saved
+    assert res[0][0].shape == (2, 5, 4, 3)
+    for a, c in zip(*res):
+        assert torch.allclose(a, c, rtol=1e-9, atol=1e-11)
+
+
 def test_three_sample_lr_scheduler_logic(monkeypatch):
     """gan/utils/scorer.py:119-162 decision rules on scripted statistics:
     p = Phi(stat) > .1 for MMD_sdlr_num_test consecutive scorings -> decay."""
