@@ -16,8 +16,8 @@ materialises everything the TF graph materialises:
 The convolution stack is the product's PyTorch module graph
 (gan.core.architecture) with its convolutions and mean pools swapped back to
 stock F.conv2d / F.avg_pool2d while the mirror runs (plain autograd, as the
-TF graph is; ConvMeanPool in its literal conv -> pool order, not the product's
-folded stride-2 conv), and its SN weights produced here instead of by the HIP bank.
+TF graph is; ConvMeanPool and UpsampleConv in their literal conv -> pool and
+upsample -> conv orders, not the product's folded stride-2 convs), and its SN weights produced here instead of by the HIP bank.
 """
 from __future__ import annotations
 
@@ -69,14 +69,17 @@ def rbf_mmd2_tf(X, Y, sigma=1.0, wt=1.0):
 def stock_torch_ops():
     """Run the product modules with stock PyTorch conv / pool autograd."""
     from gan.core import architecture, snops
-    saved = snops.conv2d, architecture.mean_pool2, architecture.FOLD_POOL
+    saved = (snops.conv2d, architecture.mean_pool2, architecture.FOLD_POOL,
+             architecture.FOLD_UP)
     snops.conv2d = lambda x, w, b=None, stride=1, padding=0: F.conv2d(x, w, b, stride, padding)
     architecture.mean_pool2 = lambda x: F.avg_pool2d(x, 2)
     architecture.FOLD_POOL = False       # the reference's literal conv -> mean-pool order
+    architecture.FOLD_UP = False         # and upsample -> conv order
     try:
         yield
     finally:
-        snops.conv2d, architecture.mean_pool2, architecture.FOLD_POOL = saved
+        (snops.conv2d, architecture.mean_pool2, architecture.FOLD_POOL,
+         architecture.FOLD_UP) = saved
 
 
 class TFMirrorStep:

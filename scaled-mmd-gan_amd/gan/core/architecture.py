@@ -15,7 +15,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .convops import conv2d, fold_pool_weight, mean_pool2
+from .convops import conv2d, fold_pool_weight, fold_up_weight, mean_pool2
 from .snops import Conv2d, Deconv2d, Linear, batch_norm, lrelu
 
 
@@ -39,6 +39,12 @@ def _bn_or_id(use, c):
 # ---------------------------------------------------------------------------
 # ResNet blocks (gan/core/resnet/block.py:9-86)
 # ---------------------------------------------------------------------------
+# SMMD_FOLD_POOL=0 restores the literal conv -> mean-pool order (A/B, tests)
+FOLD_POOL = os.environ.get('SMMD_FOLD_POOL', '1') != '0'
+# SMMD_FOLD_UP=0 restores the literal upsample -> conv order of UpsampleConv
+FOLD_UP = os.environ.get('SMMD_FOLD_UP', '1') != '0'
+
+
 class _Up(nn.Module):
     """UpsampleConv (block.py:53-60): concat x4 + depth_to_space(2) = nearest x2."""
 
@@ -47,11 +53,16 @@ class _Up(nn.Module):
         self.conv = Conv2d(cin, cout, k, 1, bias=bias, init='glorot_uniform', **sn)
 
     def forward(self, x):
-        return self.conv(F.interpolate(x, scale_factor=2, mode='nearest'))
+        c = self.conv
+        if FOLD_UP and c.stride == 1:
+            if c.k == 1:     # a 1x1 conv commutes with the nearest upsample: 4x fewer flops
+                return F.interpolate(c(x), scale_factor=2, mode='nearest')
+            if c.k == 3:     # one 4x4 stride-2 transposed conv on the folded weight
+                return F.conv_transpose2d(x, fold_up_weight(c.effective_weight()), c.bias,
+                                          stride=2, padding=1)
+        return c(F.interpolate(x, scale_factor=2, mode='nearest'))
 
 
-# SMMD_FOLD_POOL=0 restores the literal conv -> mean-pool order (A/B, tests)
-FOLD_POOL = os.environ.get('SMMD_FOLD_POOL', '1') != '0'
 
 
 class _ConvMeanPool(nn.Module):

@@ -149,6 +149,17 @@ def fold_pool_weight(w):
     return F.avg_pool2d(F.pad(w, (1, 1, 1, 1)), 2, stride=1)
 
 
+def fold_up_weight(w):
+    """W [cout, cin, 3, 3] -> K [cin, cout, 4, 4] with
+    conv(upsample_nearest2(x), W, stride 1, pad 1) == conv_transpose(x, K, stride 2, pad 1):
+    per axis the two output phases see taps (W0, W1 + W2) and (W0 + W1, W2) of
+    x, i.e. K = flip([W0, W0 + W1, W1 + W2, W2]) = flip(4 fold_pool_weight(W))
+    (UpsampleConv, gan/core/resnet/block.py:53-60, without the 4x larger
+    upsampled input; linear, so differentiable to any order)."""
+    return torch.flip(F.avg_pool2d(F.pad(w, (1, 1, 1, 1)), 2, stride=1) * 4.0,
+                      (2, 3)).transpose(0, 1)
+
+
 def mean_pool2(x):
     """2x2 mean pool, the reference's add_n of the four strided slices / 4
     (gan/core/resnet/block.py:65, :71), as a linear op whose backward is one

@@ -200,6 +200,32 @@ def test_folded_conv_mean_pool_first_and_second_order():
         assert torch.allclose(a, c, rtol=1e-9, atol=1e-11)
 
 
+def test_folded_upsample_conv_matches_literal():
+    """UpsampleConv (block.py:53-60) as one 4x4 stride-2 transposed conv on the
+    folded weight (3x3) and as conv1x1 -> upsample (1x1) equals the literal
+    upsample -> conv in value and first / second-order gradients (float64)."""
+    from gan.core import architecture
+    torch.manual_seed(3)
+    for k, bias in ((3, False), (3, True), (1, True)):
+        blk = architecture._Up(4, 3, k, bias).double()
+        x = torch.randn(2, 4, 5, 3, dtype=torch.float64, requires_grad=True)
+        params = [p for p in blk.parameters()]
+        res = []
+        saved = architecture.FOLD_UP
+        try:
+            for fold in (True, False):
+                architecture.FOLD_UP = fold
+                y = blk(x)
+                g, = torch.autograd.grad(torch.tanh(y).sum(), x, create_graph=True)
+                L = (g * g).sum() + y.pow(2).mean()
+                res.append((y.detach(),) + torch.autograd.grad(L, [x] + params))
+        finally:
+            architecture.FOLD_UP = saved
+        assert res[0][0].shape == (2, 3, 10, 6)
+        for a, c in zip(*res):
+            assert torch.allclose(a, c, rtol=1e-9, atol=1e-11)
+
+
 def test_three_sample_lr_scheduler_logic(monkeypatch):
     """gan/utils/scorer.py:119-162 decision rules on scripted statistics:
     p = Phi(stat) > .1 for MMD_sdlr_num_test consecutive scorings -> decay."""
