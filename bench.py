@@ -361,6 +361,11 @@ def main():
         # X, Y rows read, unit gradients written, sums
         'smmd_mmd2_fwd': 2 * m_all * 4 + 2 * BATCH * 4 + 8 * 4,
         'smmd_scaled_loss_fwd': BATCH * per_img * 4,
+        # ConvMeanPool filter fold / adjoint: 9 floats read + 16 written (or
+        # back) per filter, every ConvMeanPool layer of the critic per call
+        'smmd_fold_pool_weights': sum(m.conv.weight.shape[0] * m.conv.weight.shape[1]
+                                      for m in model.discriminator.modules()
+                                      if isinstance(m, architecture._ConvMeanPool)) * 25 * 4,
         'smmd_scaled_loss_bwd': 2 * BATCH * per_img * 4,
     }
     kernels = {}

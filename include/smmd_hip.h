@@ -319,6 +319,22 @@ smmd_status smmd_poly_diff_ratio(const smmd_poly_sums *yy, const smmd_poly_sums 
                                  const smmd_poly_sums *zz, const smmd_poly_sums *xz, int m,
                                  double *out, smmd_stream_t stream);
 
+/* ---------------------------------------------------------------------------
+ * ConvMeanPool filter fold (gan/core/resnet/block.py:63-66: conv3x3 SAME, then
+ * the mean of the four strided slices), run by the product as ONE 4x4
+ * stride-2 conv.  A filter is one (cout, cin) pair, row-major.  One launch
+ * covers n_layers <= 16 layers (host arrays of device pointers / counts; a
+ * zero count skips the layer).
+ *  adjoint = 0: src [n_filters, 3, 3] -> dst [n_filters, 4, 4],
+ *               dst[s,t] = 1/4 sum_{a,b in {0,1}} src[s-a, t-b]
+ *  adjoint = 1: src [n_filters, 4, 4] -> dst [n_filters, 3, 3],
+ *               dst[u,v] = 1/4 sum_{a,b in {0,1}} src[u+a, v+b]  (the gradient)
+ * Every src / dst must be 16-byte aligned.
+ * ------------------------------------------------------------------------- */
+smmd_status smmd_fold_pool_weights(const float *const *src, float *const *dst,
+                                   const int64_t *n_filters, int n_layers, int adjoint,
+                                   smmd_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

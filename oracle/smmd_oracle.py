@@ -584,3 +584,26 @@ def diff_mmd2_and_ratio_from_sums(Y_sums, Z_sums, m):
         - 4 * E_z_muZ_z_muX + 4 * muZ_muZ * muX_muZ)
     var_est = first_order + second_order
     return mmd2_diff, mmd2_diff / np.sqrt(max(var_est, 1.0e-5))
+
+
+def fold_pool_weight(W):
+    """ConvMeanPool (gan/core/resnet/block.py:63-66): mean_pool2(conv3x3_same(x, W))
+    == conv4x4_stride2_pad1(x, W'), W'[s,t] = 1/4 sum_{a,b in {0,1}} W[s-a, t-b].
+    W [..., 3, 3] -> [..., 4, 4], float64."""
+    W = np.asarray(W, np.float64)
+    out = np.zeros(W.shape[:-2] + (4, 4))
+    for a in (0, 1):
+        for b in (0, 1):
+            out[..., a:a + 3, b:b + 3] += W
+    return out * 0.25
+
+
+def fold_pool_weight_adjoint(G):
+    """Adjoint of fold_pool_weight: G [..., 4, 4] -> [..., 3, 3],
+    g[u,v] = 1/4 sum_{a,b in {0,1}} G[u+a, v+b] (the gradient w.r.t. W)."""
+    G = np.asarray(G, np.float64)
+    out = np.zeros(G.shape[:-2] + (3, 3))
+    for a in (0, 1):
+        for b in (0, 1):
+            out += G[..., a:a + 3, b:b + 3]
+    return out * 0.25

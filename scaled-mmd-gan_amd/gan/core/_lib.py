@@ -112,6 +112,8 @@ _SIGS = {
                                    _P, _P, _P, _P, _SZ, _P]),
     'smmd_poly_mmd2_var': (_I, [ctypes.POINTER(PolySums), ctypes.POINTER(PolySums),
                                 ctypes.POINTER(PolySums), _I, ctypes.c_double, _I, _P, _P]),
+    'smmd_fold_pool_weights': (_I, [ctypes.POINTER(_P), ctypes.POINTER(_P),
+                                    ctypes.POINTER(ctypes.c_int64), _I, _I, _P]),
     'smmd_poly_diff_ratio': (_I, [ctypes.POINTER(PolySums), ctypes.POINTER(PolySums),
                                   ctypes.POINTER(PolySums), ctypes.POINTER(PolySums), _I, _P,
                                   _P]),

@@ -15,7 +15,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .convops import conv2d, fold_pool_weight, fold_up_weight, mean_pool2
+from .convops import conv2d, fold_pool_weight, fold_pool_weights, fold_up_weight, mean_pool2
 from .snops import Conv2d, Deconv2d, Linear, batch_norm, lrelu
 
 
@@ -72,16 +72,57 @@ class _ConvMeanPool(nn.Module):
         super().__init__()
         self.conv = Conv2d(cin, cout, k, 1, bias=bias, init='glorot_uniform', **sn)
 
+    _w4 = None      # set by prefolded(): this call's folded weight
+
+    def foldable(self):
+        return FOLD_POOL and self.conv.k == 3 and self.conv.stride == 1
+
     def forward(self, x):
         c = self.conv
-        if FOLD_POOL and c.k == 3 and c.stride == 1 and x.shape[2] % 2 == 0 \
-                and x.shape[3] % 2 == 0:
+        if self.foldable() and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0:
             # meanpool2(conv3x3(x)) as ONE 4x4 stride-2 conv on the folded
             # weight: same value, a quarter of the output rows, no pool and no
             # upsample in the backward; MIOpen runs fwd / Dx / Dw of it in about
-            # half the time of the 3x3 + pool (tools/fold_bench.py, r02 profiles)
-            return conv2d(x, fold_pool_weight(c.effective_weight()), c.bias, 2, 1)
+            # half the time of the 3x3 + pool (tools/fold_bench.py, r03 profiles)
+            w4 = self._w4 if self._w4 is not None else fold_pool_weight(c.effective_weight())
+            return conv2d(x, w4, c.bias, 2, 1)
         return mean_pool2(c(x))
+
+
+class prefolded:
+    """Fold every ConvMeanPool filter of a critic in ONE launch (and one
+    adjoint launch in the backward) for the duration of one forward.
+
+    The folded weights are reused while the effective weights are the same
+    tensors, unmodified (same objects and _version) under the same grad mode:
+    the critic's calls on the real and the fake batch within one step share
+    one fold, and autograd sums both uses' gradients before the single adjoint
+    launch.  The fold nodes save no tensors, so reuse never backs through a
+    freed buffer; a new SN refresh or an in-place update misses the cache."""
+
+    def __init__(self, net):
+        self.net = net
+        self.mods = [m for m in net.modules() if isinstance(m, _ConvMeanPool) and m.foldable()]
+
+    def __enter__(self):
+        if self.mods:
+            ws = [m.conv.effective_weight() for m in self.mods]
+            key = (torch.is_grad_enabled(), tuple((w._version, w.requires_grad) for w in ws))
+            cache = getattr(self.net, '_fold_cache', None)
+            if (cache is not None and cache[0] == key
+                    and all(a is b for a, b in zip(cache[1], ws))):
+                ws4 = cache[2]
+            else:
+                ws4 = fold_pool_weights(ws)
+                self.net._fold_cache = (key, ws, ws4)
+            for m, w4 in zip(self.mods, ws4):
+                m._w4 = w4
+        return self
+
+    def __exit__(self, *a):
+        for m in self.mods:
+            m._w4 = None
+        return False
 
 
 class _MeanPoolConv(nn.Module):
@@ -309,6 +350,10 @@ class SNResNetDiscriminator(nn.Module):
         self.h5_lin = Linear(16 * dim, o_dim, **sn)
 
     def forward(self, x, return_layers=False):
+        with prefolded(self):
+            return self._forward(x, return_layers)
+
+    def _forward(self, x, return_layers):
         layers = {}
         h = lrelu(self.h0(x))
         layers['h0'] = h
@@ -335,6 +380,10 @@ class ResNetDiscriminator(nn.Module):
         self.h5_lin = Linear(4 * 4 * 8 * dim, o_dim)
 
     def forward(self, x, return_layers=False):
+        with prefolded(self):
+            return self._forward(x, return_layers)
+
+    def _forward(self, x, return_layers):
         layers = {}
         h = lrelu(self.h0(x))
         layers['h0'] = h

@@ -140,13 +140,78 @@ class _MeanPool2(torch.autograd.Function):
         return _Up2Quarter.apply(g.contiguous())
 
 
+def _fold_launch(srcs, adjoint):
+    """smmd_fold_pool_weights over a list of layers, ONE launch on the current
+    stream (device tensors only)."""
+    from . import _lib
+    import ctypes
+    _lib.require_cuda(*srcs)
+    srcs = [t.contiguous() for t in srcs]
+    dsts = [torch.empty(t.shape[:2] + ((3, 3) if adjoint else (4, 4)), dtype=t.dtype,
+                        device=t.device) for t in srcs]
+    n = len(srcs)
+    P = ctypes.c_void_p * n
+    nf = (ctypes.c_int64 * n)(*[t.numel() // (16 if adjoint else 9) for t in srcs])
+    with _lib.timed('smmd_fold_pool_weights'):
+        st = _lib.lib().smmd_fold_pool_weights(P(*[t.data_ptr() for t in srcs]),
+                                               P(*[t.data_ptr() for t in dsts]), nf, n,
+                                               int(adjoint), _lib.stream_handle(srcs[0].device))
+    _lib.check(st, 'smmd_fold_pool_weights')
+    return tuple(dsts)
+
+
+def _fold_torch(w):
+    return F.avg_pool2d(F.pad(w, (1, 1, 1, 1)), 2, stride=1)
+
+
+def _fold_adj_torch(g):
+    return F.avg_pool2d(g, 2, stride=1)
+
+
+class _FoldPool(torch.autograd.Function):
+    """W_l [cout, cin, 3, 3] -> W'_l [cout, cin, 4, 4] for every listed layer."""
+
+    @staticmethod
+    def forward(ctx, *ws):
+        if ws[0].is_cuda:
+            return _fold_launch(ws, 0)
+        return tuple(_fold_torch(w) for w in ws)
+
+    @staticmethod
+    def backward(ctx, *gs):
+        return _FoldPoolAdj.apply(*gs)
+
+
+class _FoldPoolAdj(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, *gs):
+        # 1/4 sum_{a,b} g[u+a, v+b] = the 2x2 stride-1 mean of the 4x4 gradient
+        if gs[0].is_cuda:
+            return _fold_launch(gs, 1)
+        return tuple(_fold_adj_torch(g) for g in gs)
+
+    @staticmethod
+    def backward(ctx, *ggs):
+        return _FoldPool.apply(*ggs)
+
+
+def fold_pool_weights(ws):
+    """fold_pool_weight over a list of layers: one HIP launch forward, one for
+    the adjoint in the backward."""
+    out = _FoldPool.apply(*ws)
+    return list(out) if isinstance(out, tuple) else [out]
+
+
 def fold_pool_weight(w):
     """W [cout, cin, 3, 3] -> W' [cout, cin, 4, 4] with
     meanpool2(conv(x, W, stride 1, pad 1)) == conv(x, W', stride 2, pad 1):
     W'[s, t] = 1/4 sum_{a, b in {0, 1}} W[s - a, t - b], i.e. a 2x2 stride-1
     mean over W zero-padded by one (ConvMeanPool, gan/core/resnet/block.py:63-66,
-    as one strided conv; linear, so differentiable to any order)."""
-    return F.avg_pool2d(F.pad(w, (1, 1, 1, 1)), 2, stride=1)
+    as one strided conv).  Device tensors run the HIP fold
+    (`smmd_fold_pool_weights`, csrc/smmd_fold.hip) and its adjoint, each the
+    other's backward, so the op is differentiable to any order; host tensors
+    (CPU module tests, the oracle's mirror) use the same sums in torch."""
+    return fold_pool_weights([w])[0]
 
 
 def fold_up_weight(w):
@@ -156,8 +221,7 @@ def fold_up_weight(w):
     x, i.e. K = flip([W0, W0 + W1, W1 + W2, W2]) = flip(4 fold_pool_weight(W))
     (UpsampleConv, gan/core/resnet/block.py:53-60, without the 4x larger
     upsampled input; linear, so differentiable to any order)."""
-    return torch.flip(F.avg_pool2d(F.pad(w, (1, 1, 1, 1)), 2, stride=1) * 4.0,
-                      (2, 3)).transpose(0, 1)
+    return torch.flip(_fold_torch(w) * 4.0, (2, 3)).transpose(0, 1)
 
 
 def mean_pool2(x):

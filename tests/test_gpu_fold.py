@@ -1,0 +1,107 @@
+"""ConvMeanPool filter fold on the GPU (`smmd_fold_pool_weight`,
+csrc/smmd_fold.hip) against the float64 oracle (oracle.smmd_oracle
+fold_pool_weight / _adjoint, block.py:63-66), on the SNResNet-64 critic's
+ConvMeanPool filter counts and ragged counts (not a multiple of the 256-filter
+block), plus the folded conv block end to end against the literal
+conv3x3 -> mean pool (first and second order)."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip('torch')
+
+from oracle import smmd_oracle as O  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [(128, 64), (1024, 512), (3, 5), (1, 1), (257, 3), (7, 300)]
+
+
+def test_fold_and_adjoint_match_oracle():
+    """All SHAPES as the layers of ONE launch each way (ragged block splits)."""
+    from gan.core.convops import _FoldPool, _FoldPoolAdj
+    rng = np.random.default_rng(7)
+    Ws = [rng.standard_normal((co, ci, 3, 3)).astype(np.float32) for co, ci in SHAPES]
+    Gs = [rng.standard_normal((co, ci, 4, 4)).astype(np.float32) for co, ci in SHAPES]
+    dev = torch.device('cuda:0')
+    w4s = _FoldPool.apply(*[torch.tensor(W, device=dev) for W in Ws])
+    g3s = _FoldPoolAdj.apply(*[torch.tensor(G, device=dev) for G in Gs])
+    torch.cuda.synchronize()
+    for (co, ci), W, G, w4, g3 in zip(SHAPES, Ws, Gs, w4s, g3s):
+        assert w4.shape == (co, ci, 4, 4) and g3.shape == (co, ci, 3, 3)
+        np.testing.assert_allclose(w4.cpu().numpy(), O.fold_pool_weight(W), rtol=1e-6,
+                                   atol=1e-7)
+        np.testing.assert_allclose(g3.cpu().numpy(), O.fold_pool_weight_adjoint(G),
+                                   rtol=1e-6, atol=1e-7)
+        # <fold(W), G> == <W, fold^T(G)>
+        lhs = float((O.fold_pool_weight(W) * G).sum())
+        rhs = float((W * g3.cpu().numpy().astype(np.float64)).sum())
+        assert abs(lhs - rhs) <= 1e-4 * (1 + abs(lhs))
+
+
+@pytest.mark.parametrize('cout,cin', SHAPES)
+def test_fold_single_layer_matches_oracle(cout, cin):
+    from gan.core.convops import fold_pool_weight
+    rng = np.random.default_rng(cout * 1000 + cin)
+    W = rng.standard_normal((cout, cin, 3, 3)).astype(np.float32)
+    w4 = fold_pool_weight(torch.tensor(W, device='cuda:0'))
+    np.testing.assert_allclose(w4.cpu().numpy(), O.fold_pool_weight(W), rtol=1e-6, atol=1e-7)
+
+
+def test_fold_rejects_bad_arguments():
+    from gan.core import _lib
+    import ctypes
+    L = _lib.lib()
+    nf = (ctypes.c_int64 * 1)(-1)
+    P = ctypes.c_void_p * 1
+    assert L.smmd_fold_pool_weights(P(None), P(None), nf, 1, 0, None) == 1      # EINVAL
+    assert L.smmd_fold_pool_weights(P(None), P(None), nf, 17, 0, None) == 1
+    nf0 = (ctypes.c_int64 * 1)(0)
+    assert L.smmd_fold_pool_weights(P(None), P(None), nf0, 1, 0, None) == 0     # empty: OK
+    x = torch.zeros(64, device='cuda:0')
+    w4 = (ctypes.c_int64 * 1)(1)
+    # misaligned 4x4 side
+    assert L.smmd_fold_pool_weights(P(x.data_ptr()), P(x.data_ptr() + 4), w4, 1, 0, None) == 1
+
+
+def test_fold_autograd_second_order_on_device():
+    from gan.core.convops import fold_pool_weight
+    dev = torch.device('cuda:0')
+    torch.manual_seed(0)
+    w = torch.randn(6, 5, 3, 3, device=dev, requires_grad=True)
+    c = torch.randn(6, 5, 4, 4, device=dev)
+    y = (fold_pool_weight(w) * c).pow(2).sum()
+    g, = torch.autograd.grad(y, w, create_graph=True)
+    gg, = torch.autograd.grad(g.pow(2).sum(), w)
+    wc = w.detach().cpu().double().requires_grad_(True)
+    from gan.core.convops import _fold_torch
+    y2 = (_fold_torch(wc) * c.cpu().double()).pow(2).sum()
+    g2, = torch.autograd.grad(y2, wc, create_graph=True)
+    gg2, = torch.autograd.grad(g2.pow(2).sum(), wc)
+    assert torch.allclose(g.cpu().double(), g2, rtol=1e-4, atol=1e-5)
+    assert torch.allclose(gg.cpu().double(), gg2, rtol=1e-4, atol=1e-4)
+
+
+def test_folded_conv_mean_pool_block_on_device():
+    """_ConvMeanPool (folded, HIP fold + MIOpen stride-2 conv) vs the literal
+    conv3x3 -> mean pool on the same device: value, input gradient and the
+    parameter gradients of a gradient penalty through it."""
+    from gan.core import architecture
+    dev = torch.device('cuda:0')
+    torch.manual_seed(1)
+    blk = architecture._ConvMeanPool(16, 32, 3, True).to(dev)
+    x = torch.randn(4, 16, 16, 16, device=dev, requires_grad=True)
+    res = []
+    saved = architecture.FOLD_POOL
+    try:
+        for fold in (True, False):
+            architecture.FOLD_POOL = fold
+            y = blk(x)
+            g, = torch.autograd.grad(torch.tanh(y).sum(), x, create_graph=True)
+            L = (g * g).sum() + y.pow(2).mean()
+            res.append((y.detach(),) + torch.autograd.grad(
+                L, (x, blk.conv.weight, blk.conv.bias)))
+    finally:
+        architecture.FOLD_POOL = saved
+    for a, c in zip(*res):
+        tol = 1e-4 * float(c.abs().max()) + 1e-6
+        assert float((a - c).abs().max()) <= tol

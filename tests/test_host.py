@@ -277,3 +277,49 @@ def test_miopen_db_install(monkeypatch):
     monkeypatch.setenv('MIOPEN_USER_DB_PATH', '/somewhere/else')
     assert miopen_db.install() is None
     assert os.environ['MIOPEN_USER_DB_PATH'] == '/somewhere/else'
+
+
+def test_oracle_fold_pins_to_literal_conv_mean_pool():
+    """The oracle's fold (and its adjoint) against the reference's literal
+    conv3x3 SAME -> mean of the four strided slices (block.py:63-66), float64."""
+    from oracle import smmd_oracle as O
+    F = torch.nn.functional
+    rng = np.random.default_rng(4)
+    x = torch.tensor(rng.standard_normal((2, 3, 10, 8)))
+    W = rng.standard_normal((5, 3, 3, 3))
+    y = F.conv2d(x, torch.tensor(W), None, 1, 1)
+    lit = (y[:, :, ::2, ::2] + y[:, :, 1::2, ::2] + y[:, :, ::2, 1::2] + y[:, :, 1::2, 1::2]) / 4.
+    fol = F.conv2d(x, torch.tensor(O.fold_pool_weight(W)), None, 2, 1)
+    assert torch.allclose(lit, fol, rtol=1e-12, atol=1e-12)
+    G = rng.standard_normal((5, 3, 4, 4))
+    assert abs(float((O.fold_pool_weight(W) * G).sum())
+               - float((W * O.fold_pool_weight_adjoint(G)).sum())) < 1e-10
+
+
+def test_prefold_cache_reuse_and_invalidation():
+    """A critic's ConvMeanPool folds are shared by calls on the same effective
+    weights and recomputed after an in-place update (SN off: W_eff is W)."""
+    from gan.core import architecture
+    torch.manual_seed(5)
+    D = architecture.ResNetDiscriminator(4, 1, False).double()
+    x1 = torch.randn(2, 3, 64, 64, dtype=torch.float64)
+    x2 = torch.randn(2, 3, 64, 64, dtype=torch.float64)
+    (D(x1).sum() + D(x2).sum()).backward()
+    c1 = D._fold_cache
+    D(x1)
+    assert D._fold_cache is c1                       # same weights: reused
+    g_shared = [p.grad.clone() for p in D.parameters()]
+    saved = architecture.FOLD_POOL
+    try:
+        architecture.FOLD_POOL = False
+        D.zero_grad()
+        (D(x1).sum() + D(x2).sum()).backward()
+    finally:
+        architecture.FOLD_POOL = saved
+    for a, b in zip(g_shared, [p.grad for p in D.parameters()]):
+        assert torch.allclose(a, b, rtol=1e-9, atol=1e-12)
+    with torch.no_grad():
+        for p in D.parameters():
+            p.add_(0.01)
+    D(x1)
+    assert D._fold_cache is not c1                   # in-place update: refolded
