@@ -53,6 +53,11 @@ class _ConvBackward(torch.autograd.Function):
     def forward(ctx, x, w, gy, stride, padding, want_w):
         ctx.save_for_backward(x, w, gy)
         ctx.cfg = (stride, padding)
+        # an output nobody differentiates (the placeholder gw of the input-only
+        # Jacobian pass, or gx/gw unused by the loss) arrives as None instead
+        # of a materialised zero tensor: otherwise every critic conv of the
+        # double backward ran conv(x, 0) and Dx(gy, 0) on it
+        ctx.set_materialize_grads(False)
         gx, gw = _bwd(gy, x, w, stride, padding, (True, want_w))
         if gw is None:          # placeholder, discarded by the caller: no allocation
             gw = w.new_zeros(()).expand_as(w)
