@@ -105,3 +105,30 @@ def test_folded_conv_mean_pool_block_on_device():
     for a, c in zip(*res):
         tol = 1e-4 * float(c.abs().max()) + 1e-6
         assert float((a - c).abs().max()) <= tol
+
+
+@pytest.mark.parametrize('k,bias', [(3, False), (1, True)])
+def test_folded_upsample_conv_on_device(k, bias):
+    """_Up (UpsampleConv, block.py:53-60) folded (4x4 stride-2 transposed conv /
+    1x1 before the upsample, MIOpen) vs the literal upsample -> conv on the same
+    device: value and the first-order gradients the generator step uses."""
+    from gan.core import architecture
+    dev = torch.device('cuda:0')
+    torch.manual_seed(2)
+    blk = architecture._Up(32, 16, k, bias).to(dev)
+    x = torch.randn(4, 32, 8, 8, device=dev, requires_grad=True)
+    params = list(blk.parameters())
+    res = []
+    saved = architecture.FOLD_UP
+    try:
+        for fold in (True, False):
+            architecture.FOLD_UP = fold
+            y = blk(x)
+            L = (torch.tanh(y) * torch.arange(y.numel(), device=dev).view_as(y).sin()).sum()
+            res.append((y.detach(),) + torch.autograd.grad(L, [x] + params))
+    finally:
+        architecture.FOLD_UP = saved
+    assert res[0][0].shape == (4, 16, 16, 16)
+    for a, c in zip(*res):
+        tol = 1e-4 * float(c.abs().max()) + 1e-6
+        assert float((a - c).abs().max()) <= tol

@@ -51,6 +51,12 @@ def main():
     jac = torch.randn(1, B, 3, 64, 64, device=dev, requires_grad=True)
     for p in opt.params:
         p.grad.normal_()
+    # ConvMeanPool filter fold + adjoint of the critic's 4 down blocks (one
+    # launch each way per critic step, as architecture.prefolded runs it)
+    from gan.core.architecture import _ConvMeanPool
+    from gan.core.convops import _FoldPool, _FoldPoolAdj
+    cmp_w = [m.conv.weight.detach() for m in D.modules() if isinstance(m, _ConvMeanPool)]
+    cmp_g = [torch.randn(w.shape[0], w.shape[1], 4, 4, device=dev) for w in cmp_w]
 
     def one():
         outs = bank.refresh(update_u=True)
@@ -59,6 +65,8 @@ def main():
         m2 = mmd.mmd2_fused(X, Y, 'rbf')
         g, _ = ops.scaled_loss(m2, jac, None, sc=10.0)
         g.backward()
+        _FoldPool.apply(*cmp_w)
+        _FoldPoolAdj.apply(*cmp_g)
 
     for _ in range(20):
         one()
@@ -75,7 +83,8 @@ def main():
            'smmd_adam_flat_sn[D]': opt.numel * 4 * 8,
            'smmd_mmd2_fwd': 2 * B * 4 * 2 + 32,
            'smmd_scaled_loss_fwd': B * 3 * 64 * 64 * 4,
-           'smmd_scaled_loss_bwd': 2 * B * 3 * 64 * 64 * 4}
+           'smmd_scaled_loss_bwd': 2 * B * 3 * 64 * 64 * 4,
+           'smmd_fold_pool_weights': sum(w.shape[0] * w.shape[1] for w in cmp_w) * 25 * 4}
     res = {}
     for k, (n, ms) in sorted(tm.items()):
         b = alg.get(k)
