@@ -335,6 +335,18 @@ smmd_status smmd_fold_pool_weights(const float *const *src, float *const *dst,
                                    const int64_t *n_filters, int n_layers, int adjoint,
                                    smmd_stream_t stream);
 
+/* ---------------------------------------------------------------------------
+ * Convolution bias gradient: out[c] = sum_{n, hw} gy[n, c, hw] over an NCHW
+ * tensor [N, C, HW] (TF's BiasAddGrad of the bias_add in snops.conv2d,
+ * gan/core/snops.py:79-80, and resnet Conv2D, gan/core/resnet/ops/conv2d.py:34-35).
+ * Fixed-order two-stage sum; workspace from smmd_channel_sum_workspace_bytes.
+ * gy must be 16-byte aligned when HW % 4 == 0.
+ * ------------------------------------------------------------------------- */
+size_t smmd_channel_sum_workspace_bytes(int N, int C);
+
+smmd_status smmd_channel_sum(const float *gy, int N, int C, int HW, float *out, void *ws,
+                             size_t ws_bytes, smmd_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -114,6 +114,8 @@ _SIGS = {
                                 ctypes.POINTER(PolySums), _I, ctypes.c_double, _I, _P, _P]),
     'smmd_fold_pool_weights': (_I, [ctypes.POINTER(_P), ctypes.POINTER(_P),
                                     ctypes.POINTER(ctypes.c_int64), _I, _I, _P]),
+    'smmd_channel_sum_workspace_bytes': (_SZ, [_I, _I]),
+    'smmd_channel_sum': (_I, [_P, _I, _I, _I, _P, _P, _SZ, _P]),
     'smmd_poly_diff_ratio': (_I, [ctypes.POINTER(PolySums), ctypes.POINTER(PolySums),
                                   ctypes.POINTER(PolySums), ctypes.POINTER(PolySums), _I, _P,
                                   _P]),

@@ -111,9 +111,32 @@ class _Conv2d(torch.autograd.Function):
                 gw = None
         else:
             gx, gw = _bwd(gy, x, w, stride, padding, (ctx.needs_input_grad[0], want_w))
-        gb = (gy.sum(dim=(0, 2, 3)) if (has_b and ctx.needs_input_grad[2] and _input_only[0] == 0)
+        gb = (bias_grad(gy) if (has_b and ctx.needs_input_grad[2] and _input_only[0] == 0)
               else None)
         return gx, gw, gb, None, None
+
+
+def bias_grad(gy):
+    """sum of gy over (N, H, W): the conv bias gradient (TF BiasAddGrad,
+    snops.py:79-80).  An NCHW device tensor outside a create_graph pass runs
+    `smmd_channel_sum` (csrc/smmd_bias.hip, fixed-order two-stage sum); a
+    gradient that must itself be differentiable (create_graph, e.g. the
+    witness penalty), channels_last or host tensors use torch's reduction."""
+    if (not gy.is_cuda or torch.is_grad_enabled() or gy.dim() != 4
+            or not gy.is_contiguous()):
+        return gy.sum(dim=(0, 2, 3))
+    from . import _lib
+    _lib.require_cuda(gy)
+    N, C, H, W = gy.shape
+    L = _lib.lib()
+    nbytes = L.smmd_channel_sum_workspace_bytes(N, C)
+    ws = _lib.workspace('channel_sum', nbytes, gy.device)
+    out = torch.empty(C, dtype=gy.dtype, device=gy.device)
+    with _lib.timed('smmd_channel_sum'):
+        st = L.smmd_channel_sum(_lib.ptr(gy), N, C, H * W, _lib.ptr(out), _lib.ptr(ws),
+                                ws.numel(), _lib.stream_handle(gy.device))
+    _lib.check(st, 'smmd_channel_sum')
+    return out
 
 
 def conv2d(x, w, b=None, stride=1, padding=0):

@@ -132,3 +132,24 @@ def test_folded_upsample_conv_on_device(k, bias):
     for a, c in zip(*res):
         tol = 1e-4 * float(c.abs().max()) + 1e-6
         assert float((a - c).abs().max()) <= tol
+
+
+@pytest.mark.parametrize('shape', [(64, 64, 64, 64), (64, 128, 32, 32), (64, 1024, 4, 4),
+                                   (3, 5, 3, 3), (7, 1, 1, 1), (2, 2000, 2, 2), (0, 4, 2, 2)])
+def test_channel_sum_matches_oracle(shape):
+    """smmd_channel_sum (conv bias gradient, BiasAddGrad of snops.py:79-80)
+    against a float64 sum over (N, H, W); odd HW takes the scalar path."""
+    from gan.core.convops import bias_grad
+    rng = np.random.default_rng(sum(shape))
+    g = rng.standard_normal(shape).astype(np.float32)
+    with torch.no_grad():
+        out = bias_grad(torch.tensor(g, device='cuda:0'))
+    torch.cuda.synchronize()
+    ref = g.astype(np.float64).sum(axis=(0, 2, 3))
+    tol = 1e-5 * np.sqrt(shape[0] * shape[2] * shape[3] + 1) + 1e-6
+    assert out.shape == (shape[1],)
+    np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=0, atol=tol)
+    if shape[0]:
+        with torch.no_grad():
+            b2 = bias_grad(torch.tensor(g, device='cuda:0'))
+        assert torch.equal(out, b2)           # fixed order: bit-identical
