@@ -302,6 +302,7 @@ def main():
     dt = time.perf_counter() - t0
     _lib.enable_timing(False)
     tm = _lib.timing_ms()            # before the extra runs below reset the records
+    tb = _lib.timing_bytes()
     g_loss, d_loss = model.check_finite()
     if world > 1:
         t = torch.tensor([dt], device=dev)
@@ -368,6 +369,9 @@ def main():
                                       if isinstance(m, architecture._ConvMeanPool)) * 25 * 4,
         'smmd_scaled_loss_bwd': 2 * BATCH * per_img * 4,
     }
+    # entry points whose size varies per call: mean algorithmic bytes per call
+    # (the conv bias gradient: 4 B per element of gy + 4 B per channel)
+    alg.update({k: int(v) for k, v in tb.items()})
     kernels = {}
     for name, (calls, ms) in tm.items():
         b = alg.get(name)

@@ -185,6 +185,7 @@ def require_cuda(*tensors):
 class _Timing:
     enabled = False
     records = {}
+    nbytes = {}       # entry point -> algorithmic bytes summed over its timed calls
 
 
 class _NullCtx:
@@ -219,6 +220,19 @@ def timed(name):
     return _EventCtx(name) if _Timing.enabled else _NULL
 
 
+def add_bytes(name, n):
+    """Algorithmic HBM bytes of one call of an entry point whose size varies
+    call to call (bench.py reports the mean per call)."""
+    if _Timing.enabled:
+        _Timing.nbytes[name] = _Timing.nbytes.get(name, 0) + int(n)
+
+
+def timing_bytes():
+    """{entry point: mean algorithmic bytes per timed call} (add_bytes users)."""
+    return {k: b / len(_Timing.records[k]) for k, b in _Timing.nbytes.items()
+            if _Timing.records.get(k)}
+
+
 def enable_timing(on=True):
     _Timing.enabled = on
 
@@ -232,6 +246,7 @@ def timing_ms():
 
 def reset_timing():
     _Timing.records = {}
+    _Timing.nbytes = {}
 
 
 # ---------------------------------------------------------------------------

@@ -39,6 +39,26 @@ class input_grad_only:
         _input_only[0] -= 1
 
 
+# storages whose gradient a backward pass does not need although they require
+# grad: the critic step's real images (a leaf only for the Jacobian of the
+# scaling regulariser; the parameter backward never reads their gradient)
+_no_dx = set()
+
+
+class no_input_grad:
+    """Within the block, convolutions whose input IS `t` skip their input
+    gradient (returned as None: the engine treats it as zero)."""
+
+    def __init__(self, t):
+        self.key = t.data_ptr()
+
+    def __enter__(self):
+        _no_dx.add(self.key)
+
+    def __exit__(self, *a):
+        _no_dx.discard(self.key)
+
+
 def _bwd(gy, x, w, stride, padding, mask):
     """(Dx, Dw) of conv(x, w) at upstream gy via the native backward kernels."""
     gx, gw, _ = _aten.convolution_backward(gy, x, w, None, stride, padding, [1, 1], False,
@@ -105,12 +125,15 @@ class _Conv2d(torch.autograd.Function):
         stride, padding, has_b = ctx.cfg
         gy = gy.contiguous(memory_format=_fmt(x))
         want_w = ctx.needs_input_grad[1] and _input_only[0] == 0
+        want_x = ctx.needs_input_grad[0] and not (_no_dx and x.data_ptr() in _no_dx)
         if torch.is_grad_enabled():          # create_graph: keep it differentiable
             gx, gw = _ConvBackward.apply(x, w, gy, stride, padding, want_w)
             if not want_w:
                 gw = None
+        elif want_x or want_w:
+            gx, gw = _bwd(gy, x, w, stride, padding, (want_x, want_w))
         else:
-            gx, gw = _bwd(gy, x, w, stride, padding, (ctx.needs_input_grad[0], want_w))
+            gx = gw = None
         gb = (bias_grad(gy) if (has_b and ctx.needs_input_grad[2] and _input_only[0] == 0)
               else None)
         return gx, gw, gb, None, None
@@ -132,6 +155,7 @@ def bias_grad(gy):
     nbytes = L.smmd_channel_sum_workspace_bytes(N, C)
     ws = _lib.workspace('channel_sum', nbytes, gy.device)
     out = torch.empty(C, dtype=gy.dtype, device=gy.device)
+    _lib.add_bytes('smmd_channel_sum', (gy.numel() + C) * 4)
     with _lib.timed('smmd_channel_sum'):
         st = L.smmd_channel_sum(_lib.ptr(gy), N, C, H * W, _lib.ptr(out), _lib.ptr(ws),
                                 ws.numel(), _lib.stream_handle(gy.device))

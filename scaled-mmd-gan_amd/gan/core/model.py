@@ -27,7 +27,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from . import mmd, ops
+from . import convops, mmd, ops
 from .architecture import get_networks
 from .collectives import all_reduce_
 from .optim import FlatAdam
@@ -177,6 +177,7 @@ class MMD_GAN:
             images = images.contiguous(memory_format=self.memory_format)
         if scaling:
             images = images.detach().requires_grad_(True)
+        self._last_images = images
         d_images = D(images)
         d_G = D(fake)
         base = self.base_loss(d_G, d_images)
@@ -239,7 +240,10 @@ class MMD_GAN:
             torch.autograd.grad(g_loss, self.g_vars, retain_graph=True)
             d_loss.backward(inputs=self.d_vars)
         else:
-            d_loss.backward()
+            # the real images are a leaf only for the Jacobian: the critic's
+            # first conv skips the input gradient nobody reads
+            with convops.no_input_grad(self._last_images):
+                d_loss.backward()
         self._exchange(self.d_optim)
         return g_loss, d_loss, aux
 

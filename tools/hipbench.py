@@ -57,6 +57,20 @@ def main():
     from gan.core.convops import _FoldPool, _FoldPoolAdj
     cmp_w = [m.conv.weight.detach() for m in D.modules() if isinstance(m, _ConvMeanPool)]
     cmp_g = [torch.randn(w.shape[0], w.shape[1], 4, 4, device=dev) for w in cmp_w]
+    # conv bias gradients: every biased conv output of one critic forward
+    # (real and fake batches: two calls per shape per critic step)
+    from gan.core.convops import bias_grad
+    from gan.core.snops import Conv2d as _SNConv
+    shapes = []
+    hooks = [m.register_forward_hook(lambda m, i, o: shapes.append(tuple(o.shape)))
+             for m in D.modules()
+             if (isinstance(m, _SNConv) and m.bias is not None) or isinstance(m, _ConvMeanPool)]
+    with torch.no_grad():
+        bank.refresh(update_u=False)
+        D(torch.rand(B, 3, 64, 64, device=dev))
+    for h in hooks:
+        h.remove()
+    gys = [torch.randn(sh, device=dev) for sh in shapes for _ in range(2)]
 
     def one():
         outs = bank.refresh(update_u=True)
@@ -67,6 +81,9 @@ def main():
         g.backward()
         _FoldPool.apply(*cmp_w)
         _FoldPoolAdj.apply(*cmp_g)
+        with torch.no_grad():
+            for gy in gys:
+                bias_grad(gy)
 
     for _ in range(20):
         one()
@@ -77,6 +94,7 @@ def main():
         one()
     _lib.enable_timing(False)
     tm = _lib.timing_ms()
+    tb = _lib.timing_bytes()
     kn = sum(e.N * e.K for e in bank.entries)
     alg = {'smmd_sn_power_iter': kn * 4 * 2, 'smmd_sn_weight_bwd': kn * 4 * 3,
            'smmd_adam_flat[D]': opt.numel * 4 * 8,
@@ -85,6 +103,7 @@ def main():
            'smmd_scaled_loss_fwd': B * 3 * 64 * 64 * 4,
            'smmd_scaled_loss_bwd': 2 * B * 3 * 64 * 64 * 4,
            'smmd_fold_pool_weights': sum(w.shape[0] * w.shape[1] for w in cmp_w) * 25 * 4}
+    alg.update({k: int(v) for k, v in tb.items()})
     res = {}
     for k, (n, ms) in sorted(tm.items()):
         b = alg.get(k)

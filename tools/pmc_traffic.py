@@ -23,6 +23,7 @@ GROUPS = {
     'smmd_scaled_loss_fwd': ('sqnorm_partial_kernel', 'scaled_loss_final_kernel'),
     'smmd_scaled_loss_bwd': ('scaled_loss_bwd_kernel',),
     'smmd_fold_pool_weights': ('fold_fwd_kernel', 'fold_adj_kernel'),
+    'smmd_channel_sum': ('chan_sum_partial_kernel', 'chan_sum_final_kernel'),
 }
 # entry points whose calls each run ONE of their kernels (fold or adjoint):
 # calls = the sum of the kernels' launches, not the most frequent one's
