@@ -59,7 +59,7 @@ __global__ __launch_bounds__(CS_T) void chan_sum_partial_kernel(const float *__r
     }
     __shared__ float red[CS_T / SMMD_WAVE];
     acc = block_sum<CS_T / SMMD_WAVE>(acc, red);
-    if (threadIdx.x == 0) part[(size_t)c * S + s] = acc;
+    if (threadIdx.x == 0) part[(size_t)s * C + c] = acc;     // [S][C]: coalesced final
 }
 
 __global__ __launch_bounds__(256) void chan_sum_final_kernel(const float *__restrict__ part,
@@ -67,9 +67,19 @@ __global__ __launch_bounds__(256) void chan_sum_final_kernel(const float *__rest
                                                              float *__restrict__ out) {
     const int c = blockIdx.x * 256 + threadIdx.x;
     if (c >= C) return;
-    const float *p = part + (size_t)c * S;
+    // partials of channel c at stride C: a wave's loads of one s are one
+    // coalesced run, and the unrolled loads are all in flight before the adds
+    const float *p = part + c;
     float acc = 0.f;
-    for (int s = 0; s < S; ++s) acc += p[s];
+    int s = 0;
+    for (; s + 8 <= S; s += 8) {
+        float v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = p[(size_t)(s + k) * C];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc += v[k];
+    }
+    for (; s < S; ++s) acc += p[(size_t)s * C];
     out[c] = acc;
 }
 
