@@ -11,7 +11,8 @@
 // fixed order (per-thread sums, then the fixed wave/block tree).  Rows shorter
 // than the block are packed several per step so every lane loads.
 // Stage 2: one thread per channel adds its S partials in order.  S is chosen
-// so stage 1 has >= 2048 blocks (8 per CU) whenever N allows.
+// so stage 1 has >= 2048 blocks (8 per CU) whenever N allows; from 512
+// channels on S = 1 and stage 1 writes the result (one launch).
 #include "smmd_common.hpp"
 
 namespace smmd {
@@ -84,6 +85,7 @@ __global__ __launch_bounds__(256) void chan_sum_final_kernel(const float *__rest
 }
 
 inline int chan_sum_split(int N, int C) {
+    if (C >= 512) return 1;        // >= 2 blocks per CU already: one launch, no partials
     int S = (2048 + C - 1) / C;
     if (S > N) S = N;
     if (S < 1) S = 1;
@@ -114,6 +116,10 @@ extern "C" smmd_status smmd_channel_sum(const float *gy, int N, int C, int HW, f
     const int S = chan_sum_split(N, C);
     if (!ws || ws_bytes < (size_t)C * S * sizeof(float)) return SMMD_EWORKSPACE;
     if (S > 65535) return SMMD_EINVAL;
+    if (S == 1) {                  // each block owns a whole channel: write the result
+        chan_sum_partial_kernel<<<dim3(C, 1), dim3(CS_T), 0, st>>>(gy, N, C, HW, 1, out);
+        return last_launch_status();
+    }
     float *part = static_cast<float *>(ws);
     chan_sum_partial_kernel<<<dim3(C, S), dim3(CS_T), 0, st>>>(gy, N, C, HW, S, part);
     smmd_status e = last_launch_status();
