@@ -15,6 +15,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import optim as _optim
 from .convops import conv2d, fold_pool_weight, fold_pool_weights, fold_up_weight, mean_pool2
 from .snops import Conv2d, Deconv2d, Linear, batch_norm, lrelu
 
@@ -51,6 +52,20 @@ class _Up(nn.Module):
     def __init__(self, cin, cout, k, bias, **sn):
         super().__init__()
         self.conv = Conv2d(cin, cout, k, 1, bias=bias, init='glorot_uniform', **sn)
+        self._kcache = None
+
+    def _folded(self, w):
+        """fold_up_weight(w), contiguous, reused while w is the same unmodified
+        tensor under the same grad mode and no FlatAdam step ran (the
+        generator's weights change once per 5 + 1 steps; its forward runs in
+        every critic step)."""
+        key = (torch.is_grad_enabled(), _optim.param_epoch(w), w._version, w.requires_grad)
+        c = self._kcache
+        if c is not None and c[0] == key and c[1] is w:
+            return c[2]
+        K = fold_up_weight(w).contiguous()
+        self._kcache = (key, w, K)
+        return K
 
     def forward(self, x):
         c = self.conv
@@ -58,7 +73,7 @@ class _Up(nn.Module):
             if c.k == 1:     # a 1x1 conv commutes with the nearest upsample: 4x fewer flops
                 return F.interpolate(c(x), scale_factor=2, mode='nearest')
             if c.k == 3:     # one 4x4 stride-2 transposed conv on the folded weight
-                return F.conv_transpose2d(x, fold_up_weight(c.effective_weight()), c.bias,
+                return F.conv_transpose2d(x, self._folded(c.effective_weight()), c.bias,
                                           stride=2, padding=1)
         return c(F.interpolate(x, scale_factor=2, mode='nearest'))
 
@@ -94,7 +109,9 @@ class prefolded:
     adjoint launch in the backward) for the duration of one forward.
 
     The folded weights are reused while the effective weights are the same
-    tensors, unmodified (same objects and _version) under the same grad mode:
+    tensors, unmodified (same objects and _version, no FlatAdam step since:
+    the library's update does not advance torch's version counters) under the
+    same grad mode:
     the critic's calls on the real and the fake batch within one step share
     one fold, and autograd sums both uses' gradients before the single adjoint
     launch.  The fold nodes save no tensors, so reuse never backs through a
@@ -107,7 +124,8 @@ class prefolded:
     def __enter__(self):
         if self.mods:
             ws = [m.conv.effective_weight() for m in self.mods]
-            key = (torch.is_grad_enabled(), tuple((w._version, w.requires_grad) for w in ws))
+            key = (torch.is_grad_enabled(),
+                   tuple((w._version, _optim.param_epoch(w), w.requires_grad) for w in ws))
             cache = getattr(self.net, '_fold_cache', None)
             if (cache is not None and cache[0] == key
                     and all(a is b for a, b in zip(cache[1], ws))):

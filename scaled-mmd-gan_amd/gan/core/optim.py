@@ -24,6 +24,18 @@ import torch
 from . import _lib
 
 
+# Step count per parameter storage, bumped by every FlatAdam step: the update
+# writes the parameters through the library, which does not advance torch's
+# version counters, so caches of tensors derived from parameters
+# (architecture.prefolded, _Up) key on param_epoch(w) as well.
+_EPOCH = {}
+
+
+def param_epoch(t):
+    """FlatAdam steps applied so far to the storage `t` lives in (0 if none)."""
+    return _EPOCH.get(t.untyped_storage().data_ptr(), 0)
+
+
 class FlatAdam:
     def __init__(self, params, lr, beta1=0.5, beta2=0.9, eps=1e-8, clip_norm=1.0, name='opt'):
         self.name = name
@@ -120,6 +132,8 @@ class FlatAdam:
     def step(self, grad_scale=1.0, clip=True, lr=None):
         self._check_grads()
         self.step_count += 1
+        key = self.flat_param.untyped_storage().data_ptr()
+        _EPOCH[key] = _EPOCH.get(key, 0) + 1
         c = float(self.clip_norm) if clip else 0.0
         args = (_lib.ptr(self.flat_param), _lib.ptr(self.flat_grad), _lib.ptr(self.m),
                 _lib.ptr(self.v), self.offsets, len(self.params), float(grad_scale), c,

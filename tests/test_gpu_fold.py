@@ -153,3 +153,37 @@ def test_channel_sum_matches_oracle(shape):
         with torch.no_grad():
             b2 = bias_grad(torch.tensor(g, device='cuda:0'))
         assert torch.equal(out, b2)           # fixed order: bit-identical
+
+
+def test_fold_caches_follow_flat_adam_updates():
+    """The prefold (critic) and folded-UpsampleConv (generator) caches must
+    miss after a FlatAdam step: the library writes the parameters without
+    advancing torch's version counters (optim.param_epoch keys the caches)."""
+    from gan.core import architecture
+    from gan.core.optim import FlatAdam
+    dev = torch.device('cuda:0')
+    torch.manual_seed(3)
+    D = architecture.ResNetDiscriminator(4, 1, False).to(dev)       # no SN: W_eff is W
+    up = architecture._Up(8, 4, 3, False).to(dev)
+    x = torch.rand(2, 3, 64, 64, device=dev)
+    z = torch.randn(2, 8, 4, 4, device=dev)
+    opt_d = FlatAdam(list(D.parameters()), 1e-2, name='D')
+    opt_g = FlatAdam(list(up.parameters()), 1e-2, name='G')
+    for _ in range(2):
+        with torch.no_grad():
+            D(x)
+            up(z)                                    # fill the caches
+        for p in list(D.parameters()) + list(up.parameters()):
+            p.grad.normal_()
+        opt_d.step()
+        opt_g.step()
+        with torch.no_grad():
+            d_c, u_c = D(x), up(z)
+            saved = architecture.FOLD_POOL, architecture.FOLD_UP
+            try:
+                architecture.FOLD_POOL = architecture.FOLD_UP = False
+                d_l, u_l = D(x), up(z)
+            finally:
+                architecture.FOLD_POOL, architecture.FOLD_UP = saved
+        assert torch.allclose(d_c, d_l, rtol=1e-4, atol=1e-5 * float(d_l.abs().max()) + 1e-6)
+        assert torch.allclose(u_c, u_l, rtol=1e-4, atol=1e-5 * float(u_l.abs().max()) + 1e-6)
