@@ -10,10 +10,19 @@ value = images/s of the whole job = N * batch * K / (max over ranks of the
 timed region).  Multi-GPU uses the all-gather ('global') MMD mode: every rank
 sees the full (N*64) x (N*64) pairwise kernel (weak scaling).
 
-Extra fields: roofline of the dominant HIP launch set (the clip+Adam update of
-the critic, HBM-bound) timed with HIP events on the compute stream, the
-fused-MMD kernel's rate, and a CPU baseline (the oracle's op-by-op mirror of
-the TF graph, timed on a bounded sample on this host).
+Order of the run:
+  1. prime (untimed): one critic and one generator update in each schedule
+     (lean and reference), so every distinct autograd graph -- and every
+     MIOpen kernel it needs -- is built before anything is timed;
+  2. W warmup steps, then the schedule is re-aligned to the start of a
+     5D + 1G cycle;
+  3. EXACTLY K timed steps (no events, no per-call instrumentation inside);
+     the line reports how many were critic / generator updates;
+  4. the reference schedule (both gradient sets every step, model.py:514);
+  5. a separate instrumented pass over whole cycles: HIP-event time of every
+     libsmmd_hip entry point and of each D / G step (the `roofline`,
+     `hip_kernels` and `roofline_hot_path` blocks come from here);
+  6. the MMD microbench and the CPU baseline (rank 0, N = 1).
 """
 import argparse
 import json
@@ -31,68 +40,128 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
+FP32_PEAK_TFS = 157.3          # MI355X_MICROARCH.md: FP32 vector = f32 MFMA peak (dense)
+MFMA_F32_PEAK_TFS = 157.3      # v_mfma_f32_32x32x2_f32 dense
+# FP32 VALU lane-operations per second: 157.3 TFLOP/s counts an FMA as two
+# flops, so one lane-op (add, mul, fma, cmp, ...) issues at half that rate
+VALU_LANE_OPS = FP32_PEAK_TFS / 2 * 1e12
+TRANS_SLOTS = 4                # v_exp_f32 / v_log_f32: quarter rate (MI355X_MICROARCH.md)
 BATCH = 64
 
+PMC_TRAFFIC = os.path.join(ROOT, 'profiles', 'r04', 'pmc_traffic.json')
+PMC_FALLBACK = os.path.join(ROOT, 'profiles', 'r03', 'pmc_traffic.json')
 
-PMC_TRAFFIC = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', 'r03',
-                           'pmc_traffic.json')
+# the hot-path rows a1-a9 and the library entry points that
+# implement them (the roofline kernel is chosen among these)
+HOT_PATH = ('smmd_mmd2_fwd', 'smmd_scaled_loss_fwd', 'smmd_scaled_loss_bwd',
+            'smmd_sn_power_iter', 'smmd_sn_weight_bwd', 'smmd_adam_flat[D]',
+            'smmd_adam_flat[G]', 'smmd_adam_flat_sn[D]', 'smmd_adam_flat_sn[G]')
 
 
 def pmc_traffic(entry):
     """HBM bytes per call of a library entry point from the committed rocprofv3
     PMC passes (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, tools/pmc_traffic.py,
-    same kernels and sizes via tools/hipbench.py), or None when not measured."""
-    try:
-        with open(PMC_TRAFFIC) as f:
-            rec = json.load(f).get(entry.split('[')[0])
-        return rec['traffic_bytes'] if rec else None
-    except (OSError, ValueError, KeyError):
-        return None
+    same kernels and sizes via tools/hipbench.py), or None when not measured.
+    Returns (bytes, source file)."""
+    for path in (PMC_TRAFFIC, PMC_FALLBACK):
+        try:
+            with open(path) as f:
+                rec = json.load(f).get(entry.split('[')[0])
+            if rec:
+                return rec['traffic_bytes'], os.path.relpath(path, ROOT)
+        except (OSError, ValueError, KeyError):
+            continue
+    return None, None
 
 
-def imagenet_config():
+def imagenet_config(batch=BATCH):
     """configs/imagenet_smmd.yml over the gan/main.py defaults."""
-    from gan.main import default_flags
-    c = default_flags()
-    c.update(dict(max_iteration=150000, learning_rate=2e-4, beta1=0.5, beta2=0.9, decay_rate=.8,
-                  dsteps=5, gsteps=1, start_dsteps=10, batch_size=BATCH, output_size=64,
-                  c_dim=3, z_dim=128, df_dim=64, dof_dim=1, gf_dim=64, architecture='snresnet',
-                  kernel='rbf', model='smmd', batch_norm=True, with_sn=True,
-                  with_learnable_sn_scale=True, with_scaling=True, dataset='imagenet'))
-    return argparse.Namespace(**c)
+    from gan.main import make_flags
+    f = make_flags(argv=['-config_file', os.path.join(PKG, 'configs', 'imagenet_smmd.yml'),
+                         '-dataset', 'imagenet'])
+    f.batch_size = batch
+    return f
 
 
-def cpu_baseline(cfg, seconds_budget=20.0):
-    """Oracle mirror of the TF graph on the host CPU (bounded sample)."""
+def cifar_config(batch):
+    """configs/cifar10_smmd.yml (BASELINE configs[0]: batch 32, CPU)."""
+    from gan.main import make_flags
+    f = make_flags(argv=['-config_file', os.path.join(PKG, 'configs', 'cifar10_smmd.yml')])
+    f.batch_size = batch
+    return f
+
+
+def _pct(xs, q):
+    xs = sorted(xs)
+    if not xs:
+        return None
+    k = (len(xs) - 1) * q
+    lo, hi = int(k), min(int(k) + 1, len(xs) - 1)
+    return xs[lo] + (xs[hi] - xs[lo]) * (k - lo)
+
+
+def _mirror_trainer(cfg, batch, seed=2):
     from gan.core.architecture import get_networks
     from gan.core.snops import sn_modules
-    from oracle.tf_mirror import TFMirrorStep
-    threads = min(len(os.sched_getaffinity(0)), 16)
-    torch.set_num_threads(threads)
-    torch.manual_seed(2)
+    from oracle.tf_mirror import TFMirrorTrainer
+    torch.manual_seed(seed)
     G_cls, D_cls = get_networks(cfg.architecture)
     G = G_cls(cfg.gf_dim, 3, cfg.output_size, cfg.batch_norm, z_dim=cfg.z_dim)
     D = D_cls(cfg.df_dim, cfg.dof_dim, False, with_sn=True, with_learnable_sn_scale=True,
               input_size=cfg.output_size)
-    step = TFMirrorStep(G, D, sn_modules(D), lr=cfg.learning_rate, sc=cfg.scaling_coeff)
+    tr = TFMirrorTrainer(G, D, sn_modules(D), lr=cfg.learning_rate, sc=cfg.scaling_coeff)
+    tr.step_no = 21              # steady-state 5 D + 1 G (model.py:474-475)
     g = torch.Generator().manual_seed(0)
-    imgs = torch.rand(BATCH, 3, cfg.output_size, cfg.output_size, generator=g)
-    step.step(imgs)                                    # warm-up
-    t0 = time.perf_counter()
-    n = 0
-    while True:
-        step.step(imgs)
-        n += 1
-        if time.perf_counter() - t0 > seconds_budget or n >= 3:
+    imgs = torch.rand(batch, 3, cfg.output_size, cfg.output_size, generator=g)
+    return tr, imgs
+
+
+def _time_cycles(tr, imgs, cycles, budget_s):
+    """Per-step wall times over whole 5 D + 1 G cycles (at least one)."""
+    tr.train_step(imgs)                       # warm-up (allocator, threads)
+    tr.d_counter = tr.g_counter = 0           # cycle start
+    times, kinds = [], []
+    t_start = time.perf_counter()
+    for c in range(cycles):
+        for _ in range(6):
+            t0 = time.perf_counter()
+            kinds.append(tr.train_step(imgs))
+            times.append(time.perf_counter() - t0)
+        if time.perf_counter() - t_start > budget_s:
             break
-    dt = (time.perf_counter() - t0) / n
-    return {'value': BATCH / dt, 'unit': 'images/s', 'cores': threads, 'kind': 'port',
-            'sample': '%d critic steps (SNResNet-64 SMMD, batch %d) of the oracle torch-CPU '
-                      'mirror of the TF graph (oracle/tf_mirror.py), %.2f s/step' %
-                      (n, BATCH, dt)}
+    return times, kinds
 
 
-MFMA_F32_PEAK_TFS = 157.3     # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense
+def cpu_baseline(seconds_budget=20.0):
+    """The oracle's CPU mirror of the TF graph (oracle/tf_mirror.py), the
+    reference's training loop: both gradient sets every step, 5 D + 1 G.
+    Headline: the bench's own workload (ImageNet SNResNet-64, batch 64) over
+    one full cycle; beside it BASELINE configs[0] (CIFAR-10 SNGAN 32x32,
+    batch 32, the reference's CPU case) over as many cycles as fit."""
+    affinity = len(os.sched_getaffinity(0))
+    threads = min(affinity, 16)     # the box's CPU share for one GPU (16)
+    torch.set_num_threads(threads)
+    out = {'unit': 'images/s', 'cores': threads, 'kind': 'port',
+           'host_cpus': os.cpu_count(), 'affinity_cpus': affinity, 'threads_used': threads}
+    tr, imgs = _mirror_trainer(imagenet_config(BATCH), BATCH)
+    times, kinds = _time_cycles(tr, imgs, 1, seconds_budget)
+    mean = sum(times) / len(times)
+    out.update(value=round(BATCH / mean, 3),
+               sample='%d steps (%s) of the reference loop on the torch-CPU mirror of the TF '
+                      'graph (oracle/tf_mirror.py TFMirrorTrainer; both gradient sets per step '
+                      'as model.py:514), ImageNet SNResNet-64 SMMD, batch %d; value = batch / '
+                      'mean step time' % (len(times), ''.join(kinds), BATCH),
+               step_s={'median': round(_pct(times, .5), 4), 'p10': round(_pct(times, .1), 4),
+                       'p90': round(_pct(times, .9), 4), 'mean': round(mean, 4)})
+    tr, imgs = _mirror_trainer(cifar_config(32), 32)
+    times, kinds = _time_cycles(tr, imgs, 4, seconds_budget / 2)
+    mean = sum(times) / len(times)
+    out['configs0_cifar10_sngan_b32'] = {
+        'value': round(32 / mean, 3), 'unit': 'images/s', 'steps': len(times),
+        'schedule': ''.join(kinds),
+        'step_s': {'median': round(_pct(times, .5), 4), 'p10': round(_pct(times, .1), 4),
+                   'p90': round(_pct(times, .9), 4), 'mean': round(mean, 4)}}
+    return out
 
 
 def mmd_path(rows, d):
@@ -101,22 +170,38 @@ def mmd_path(rows, d):
     return 'mfma-gram' if gram else 'row-sweep'
 
 
+def mmd_valu_ops_per_pair(kernel, D):
+    """Algorithmic VALU lane-ops per pair of the reference's three matrices
+    (SURVEY 8d): forward P (2D + 6) flops + one exp, backward P (3D + 4) flops
+    reusing K; mix_rq adds 3 (4 flops + log + exp), mix_rbf 5 more (2 flops +
+    exp).  A transcendental costs TRANS_SLOTS lane-op slots."""
+    base = (2 * D + 6) + (3 * D + 4)
+    if kernel == 'rbf':
+        return base + TRANS_SLOTS
+    if kernel == 'mix_rbf':
+        return base + 6 * TRANS_SLOTS + 5 * 2
+    if kernel == 'mix_rq':
+        return base + 3 * (4 + 2 * TRANS_SLOTS)
+    return base
+
+
 def mmd_sweep(world, rank, dev, group, quick=False):
     """SURVEY 8d MMD microbench: X, Y ~ N(0,1) [N, D] per side (global N,
     numpy default_rng(1234)), rank r owning rows [r N/w, (r+1) N/w) of each, run
     through the product path mmd.mmd2_fused (all-gather mode when w > 1) with
     its backward; HIP-event time per fwd+bwd, max over ranks.  Algorithmic
     bytes: fwd (m+n) D 4 + 16, bwd (m+n) D 4 read + (m+n) D 4 written; pairs
-    P = m^2 + mn + n^2 (the reference's three matrices); for D >= 128 the Gram
-    flops 4 D P (forward Gram + backward C Z) against the f32 MFMA peak."""
+    P = m^2 + mn + n^2 (the reference's three matrices).  D <= 32: VALU
+    fraction (mmd_valu_ops_per_pair); D >= 128: the Gram flops 4 D P
+    (forward Gram + backward C Z) against the f32 MFMA peak."""
     import numpy as np
     from gan.core import _lib, mmd
     grid = [(32, 1), (64, 1), (256, 1), (512, 1), (2048, 1), (512, 16), (2048, 16),
             (256, 128), (512, 128), (2048, 128), (512, 1024), (2048, 1024)]
     if quick:
-        grid = [(64, 1), (512, 128)]
-    extra = [('mix_rq', 512, 1), ('mix_rbf', 512, 1), ('mix_rq', 512, 128),
-             ('mix_rbf', 512, 128)]
+        grid = [(64, 1), (512, 1), (2048, 1), (512, 128)]
+    extra = [('mix_rq', 512, 1), ('mix_rbf', 512, 1), ('mix_rq', 2048, 1),
+             ('mix_rq', 512, 128), ('mix_rbf', 512, 128)]
     rows = []
     for kern, N, D in [('rbf', N, D) for N, D in grid] + ([] if quick else extra):
         if N % world:
@@ -130,7 +215,7 @@ def mmd_sweep(world, rank, dev, group, quick=False):
 
         def once():
             v = mmd.mmd2_fused(Xl, Yl, kern, process_group=group)
-            gx, gy = torch.autograd.grad(v, (Xl, Yl))
+            torch.autograd.grad(v, (Xl, Yl))
             return v
 
         for _ in range(3):
@@ -166,49 +251,143 @@ def mmd_sweep(world, rank, dev, group, quick=False):
         if D >= 128:
             tf = 4.0 * D * P / (ms * 1e-3) / 1e12
             row.update(tflops=round(tf, 2), mfma_frac=round(tf / MFMA_F32_PEAK_TFS, 4))
+        else:
+            ops = mmd_valu_ops_per_pair(kern, D) * P
+            row.update(valu_ops_per_pair=mmd_valu_ops_per_pair(kern, D),
+                       valu_frac=round(ops / (ms * 1e-3) / VALU_LANE_OPS, 4))
         rows.append(row)
     return rows
 
 
-def cpu_components(cfg, threads):
-    """SURVEY 8d CPU baseline rows (i) and (ii): the torch-CPU mirror of the TF
-    graph for MMD fwd+bwd per N (materialised N x N matrices, D = 1) and the
-    SN power iteration of the SNResNet-64 critic (all layers)."""
-    import numpy as np
-    from gan.core.architecture import SNResNetDiscriminator
-    from gan.core.snops import sn_modules
-    from oracle.tf_mirror import rbf_mmd2_tf, sn_weight_tf
-    torch.set_num_threads(threads)
-    out = {'mmd_fwd_bwd': []}
-    for N in (64, 256, 512, 2048):
-        rng = np.random.default_rng(1234)
-        X = torch.tensor(rng.standard_normal((N, 1)), dtype=torch.float32, requires_grad=True)
-        Y = torch.tensor(rng.standard_normal((N, 1)), dtype=torch.float32, requires_grad=True)
-        rbf_mmd2_tf(X, Y).backward()
-        reps, t0 = 0, time.perf_counter()
-        while reps < 20 and time.perf_counter() - t0 < 2.0:
-            X.grad = Y.grad = None
-            rbf_mmd2_tf(X, Y).backward()
-            reps += 1
-        out['mmd_fwd_bwd'].append({'N': N, 'D': 1, 'kernel': 'rbf',
-                                   'ms': round((time.perf_counter() - t0) / reps * 1e3, 3)})
-    D = SNResNetDiscriminator(64, 1, False, with_sn=True, with_learnable_sn_scale=True)
-    layers = []
-    for mod in sn_modules(D):
-        W = mod.weight.detach()
-        perm = (2, 3, 1, 0) if W.dim() == 4 else (1, 0)
-        layers.append((W, torch.randn(1, W.shape[0]), mod.sn_scale.detach(), perm))
-    for W, u, sc, perm in layers:
-        sn_weight_tf(W, u, sc, perm)
-    reps, t0 = 0, time.perf_counter()
-    while reps < 10 and time.perf_counter() - t0 < 3.0:
-        for W, u, sc, perm in layers:
-            sn_weight_tf(W, u, sc, perm)
-        reps += 1
-    out['sn_power_iter'] = {'architecture': 'snresnet-64 critic', 'layers': len(layers),
-                            'weights': sum(W.numel() for W, *_ in layers),
-                            'ms': round((time.perf_counter() - t0) / reps * 1e3, 3)}
-    return out
+def literal_macs(net, x):
+    """Forward multiply-accumulates per image of `net` on input x in the
+    REFERENCE's literal layer order (gan/core/resnet/block.py:53-73,
+    architecture.py:178-230, :334-343, :395-434): ConvMeanPool as a full
+    resolution 3x3 conv then the pool, UpsampleConv as nearest-upsample then
+    the 3x3 conv -- not the product's folded stride-2 forms, which do 4/9 of
+    that work.  Counted from the layer shapes met by one forward."""
+    from gan.core import architecture as A
+    from gan.core import snops
+    macs = [0]
+    inner = set()
+    for m in net.modules():
+        if isinstance(m, (A._ConvMeanPool, A._Up, A._MeanPoolConv)):
+            inner.add(id(m.conv))
+
+    def conv_hook(mod, inp, out):
+        if id(mod) in inner:
+            return
+        h, w = out.shape[2], out.shape[3]
+        macs[0] += h * w * mod.cout * mod.cin * mod.k * mod.k
+
+    def cmp_hook(mod, inp, out):          # conv at the input's resolution, then pool
+        c = mod.conv
+        h, w = inp[0].shape[2], inp[0].shape[3]
+        macs[0] += h * w * c.cout * c.cin * c.k * c.k
+
+    def mpc_hook(mod, inp, out):          # pool, then conv at half resolution
+        c = mod.conv
+        macs[0] += out.shape[2] * out.shape[3] * c.cout * c.cin * c.k * c.k
+
+    def up_hook(mod, inp, out):           # upsample, then conv at 2x resolution
+        c = mod.conv
+        macs[0] += out.shape[2] * out.shape[3] * c.cout * c.cin * c.k * c.k
+
+    def deconv_hook(mod, inp, out):
+        macs[0] += inp[0].shape[2] * inp[0].shape[3] * mod.cin * mod.cout * mod.k * mod.k
+
+    def lin_hook(mod, inp, out):
+        macs[0] += mod.weight.shape[0] * mod.weight.shape[1]
+
+    hooks = []
+    for m in net.modules():
+        if isinstance(m, snops.Conv2d):
+            hooks.append(m.register_forward_hook(conv_hook))
+        elif isinstance(m, A._ConvMeanPool):
+            hooks.append(m.register_forward_hook(cmp_hook))
+        elif isinstance(m, A._MeanPoolConv):
+            hooks.append(m.register_forward_hook(mpc_hook))
+        elif isinstance(m, A._Up):
+            hooks.append(m.register_forward_hook(up_hook))
+        elif isinstance(m, snops.Deconv2d):
+            hooks.append(m.register_forward_hook(deconv_hook))
+        elif isinstance(m, snops.Linear):
+            hooks.append(m.register_forward_hook(lin_hook))
+    try:
+        with torch.no_grad():
+            net(x[:1])
+    finally:
+        for h in hooks:
+            h.remove()
+    return macs[0]
+
+
+def step_flops(model, images):
+    """Algorithmic FLOPs of the lean schedule per averaged step:
+    per image, D step = G_f + 9 D_f (G forward; critic forward on real and
+    fake; the Jacobian pass Dx; first-order Dx + Dw through both critic calls;
+    the double backward's conv + Dw through the Jacobian pass), G step =
+    3 G_f + 4 D_f (G forward + Dx + Dw; critic forward x2, its Jacobian pass
+    for the scale, Dx through the fake call); a cycle is 5 D + 1 G."""
+    model.sn_D.refresh(update_u=False)
+    if model.sn_G.entries:
+        model.sn_G.refresh(update_u=False)
+    z = model.sample_z(2)
+    d_f = literal_macs(model.discriminator, images)
+    g_f = literal_macs(model.generator, z)
+    per_img_d = 2 * (g_f + 9 * d_f)
+    per_img_g = 2 * (3 * g_f + 4 * d_f)
+    return {'D_fwd_macs_per_image': d_f, 'G_fwd_macs_per_image': g_f,
+            'flops_per_D_step': per_img_d * BATCH, 'flops_per_G_step': per_img_g * BATCH,
+            'flops_per_avg_step': (5 * per_img_d + per_img_g) * BATCH / 6}
+
+
+def run_steps(model, images, k, counts=None):
+    for i in range(k):
+        before = model.step
+        model.train_step(images[i % len(images)])
+        if counts is not None:
+            counts['G' if model.step != before else 'D'] += 1
+
+
+def sync(world):
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def max_over_ranks(x, world, dev):
+    if world == 1:
+        return x
+    t = torch.tensor([x], device=dev, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t)
+
+
+def instrumented_pass(model, images, cycles, world, dev):
+    """Whole 5 D + 1 G cycles with HIP events around every libsmmd_hip call
+    (on the compute stream) and around each step: per entry point calls, mean
+    time and algorithmic bytes; D and G step times."""
+    from gan.core import _lib
+    model.d_counter = model.g_counter = 0
+    sync(world)
+    _lib.reset_timing()
+    _lib.enable_timing(True)
+    ev = {'D': [], 'G': []}
+    for i in range(6 * cycles):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        before = model.step
+        s.record()
+        model.train_step(images[i % len(images)])
+        e.record()
+        ev['G' if model.step != before else 'D'].append((s, e))
+    sync(world)
+    _lib.enable_timing(False)
+    tm = _lib.timing_ms()
+    tb = _lib.timing_bytes()
+    step_ms = {k: sum(a.elapsed_time(b) for a, b in v) / len(v) for k, v in ev.items() if v}
+    return tm, tb, step_ms, 6 * cycles
 
 
 def main():
@@ -233,8 +412,11 @@ def main():
     ap.add_argument('--ref-schedule-steps', type=int, default=30,
                     help='steps timed with the reference schedule (both gradient sets '
                          'every step, model.py:514) after the main run; 0: skip')
+    ap.add_argument('--instrument-cycles', type=int, default=3,
+                    help='5 D + 1 G cycles of the instrumented pass (per-call HIP events); '
+                         '0: skip')
     ap.add_argument('--mmd-sweep', type=int, default=1,
-                    help='1: SURVEY 8d MMD microbench grid; 2: two configs; 0: skip')
+                    help='1: SURVEY 8d MMD microbench grid; 2: four configs; 0: skip')
     args = ap.parse_args()
     global BATCH
     BATCH = args.batch
@@ -268,123 +450,161 @@ def main():
     torch.backends.cudnn.benchmark = bool(args.miopen_find)
 
     from gan.core.smmd import SMMD
-    cfg = imagenet_config()
+    cfg = imagenet_config(BATCH)
     torch.manual_seed(2 + rank)
     model = SMMD(cfg, device=dev, process_group=dist.group.WORLD if world > 1 else None,
                  dp_mode=args.dp_mode, channels_last=bool(args.channels_last))
     gen = torch.Generator(device=dev).manual_seed(0 + rank)
     images = [torch.rand(BATCH, 3, 64, 64, device=dev, generator=gen) for _ in range(4)]
-    model.step = 21          # steady-state 5D+1G schedule (model.py:474-475)
+    log = (lambda *a: print('[bench]', *a, file=sys.stderr, flush=True)) if rank == 0 else \
+        (lambda *a: None)
 
-    from gan.core import _lib
-
+    # 1. prime every autograd graph (and its MIOpen kernels) once, untimed
     tw = time.perf_counter()
+    for sched in ('lean', 'reference'):
+        model.schedule = sched
+        model.d_step(images[0])
+        model.g_step(images[1])
+    model.schedule = 'lean'
+    sync(world)
+    log('primed D and G steps of both schedules in %.1f s' % (time.perf_counter() - tw))
+
+    # 2. warmup, then align to the start of a 5 D + 1 G cycle
+    model.step = 21          # steady state: 5 critic updates per generator update
     for i in range(args.warmup):
         model.train_step(images[i % len(images)])
         if rank == 0:
             torch.cuda.synchronize()
-            print('[bench] warmup step %d/%d done at %.1f s' % (i + 1, args.warmup,
-                  time.perf_counter() - tw), file=sys.stderr, flush=True)
+            log('warmup step %d/%d done at %.1f s' % (i + 1, args.warmup,
+                                                     time.perf_counter() - tw))
     model.check_finite()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    _lib.reset_timing()
-    _lib.enable_timing(True)
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        model.train_step(images[i % len(images)])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    _lib.enable_timing(False)
-    tm = _lib.timing_ms()            # before the extra runs below reset the records
-    tb = _lib.timing_bytes()
-    g_loss, d_loss = model.check_finite()
-    if world > 1:
-        t = torch.tensor([dt], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t)
+    model.d_counter = model.g_counter = 0
+    sync(world)
 
-    # the reference-schedule variant (both gradient sets every step)
+    # 3. the timed region: exactly K steps, nothing instrumented
+    counts = {'D': 0, 'G': 0}
+    t0 = time.perf_counter()
+    run_steps(model, images, args.steps, counts)
+    sync(world)
+    dt = max_over_ranks(time.perf_counter() - t0, world, dev)
+    g_loss, d_loss = model.check_finite()
+    log('timed %d steps: %.2f ms/step' % (args.steps, dt / args.steps * 1e3))
+
+    # 4. the reference schedule (both gradient sets every step, model.py:514)
     ref_sched = None
     if args.ref_schedule_steps > 0:
         model.schedule = 'reference'
-        for i in range(6):                        # covers one generator step
-            model.train_step(images[i % len(images)])
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
+        model.d_counter = model.g_counter = 0
+        run_steps(model, images, 6)                       # one cycle
+        sync(world)
+        model.d_counter = model.g_counter = 0
+        rc = {'D': 0, 'G': 0}
         t0 = time.perf_counter()
-        for i in range(args.ref_schedule_steps):
-            model.train_step(images[i % len(images)])
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        dtr = time.perf_counter() - t0
-        if world > 1:
-            t = torch.tensor([dtr], device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            dtr = float(t)
+        run_steps(model, images, args.ref_schedule_steps, rc)
+        sync(world)
+        dtr = max_over_ranks(time.perf_counter() - t0, world, dev)
         model.schedule = 'lean'
         ref_sched = {'value': round(world * BATCH * args.ref_schedule_steps / dtr, 2),
                      'unit': 'images/s', 'steps': args.ref_schedule_steps, 'warmup': 6,
+                     'd_steps': rc['D'], 'g_steps': rc['G'],
                      'ms_per_step': round(dtr / args.ref_schedule_steps * 1e3, 3),
                      'note': 'every step also computes the other network\'s gradient set '
                              'and discards it, as each sess.run of the reference does '
                              '(model.py:514); value above is the lean schedule'}
+        log('reference schedule: %.2f ms/step' % (dtr / args.ref_schedule_steps * 1e3))
+
+    # 5. instrumented pass (separate from the headline)
+    kernels, step_ms, roofline, hot = {}, {}, None, {}
+    if args.instrument_cycles > 0:
+        tm, tb, step_ms, n_inst = instrumented_pass(model, images, args.instrument_cycles,
+                                                    world, dev)
+        m_all = BATCH * world
+        sn_kn = sum(e.N * e.K for e in model.sn_D.entries)
+        per_img = 3 * 64 * 64
+        alg = {
+            # sqsum pass reads g; update pass reads g, p, m, v and writes p, m, v
+            'smmd_adam_flat[D]': model.d_optim.numel * 4 * 8,
+            'smmd_adam_flat[G]': model.g_optim.numel * 4 * 8,
+            # the same update with the SN weights' first power-iteration pass
+            # folded in (its column-partial writes are < 0.1 % of these bytes)
+            'smmd_adam_flat_sn[D]': model.d_optim.numel * 4 * 8,
+            'smmd_adam_flat_sn[G]': model.g_optim.numel * 4 * 8,
+            # one read of W + one write of W_eff (2 K N 4 B per iteration)
+            'smmd_sn_power_iter': sn_kn * 4 * 2,
+            # one read of G and W, one write of gW
+            'smmd_sn_weight_bwd': sn_kn * 4 * 3,
+            # X, Y rows read, unit gradients written, sums
+            'smmd_mmd2_fwd': 2 * m_all * 4 + 2 * BATCH * 4 + 8 * 4,
+            'smmd_scaled_loss_fwd': BATCH * per_img * 4,
+            # ConvMeanPool filter fold / adjoint: 9 floats read + 16 written (or
+            # back) per filter, every ConvMeanPool layer of the critic per call
+            'smmd_fold_pool_weights': sum(m.conv.weight.shape[0] * m.conv.weight.shape[1]
+                                          for m in model.discriminator.modules()
+                                          if isinstance(m, architecture._ConvMeanPool)) * 25 * 4,
+            'smmd_scaled_loss_bwd': 2 * BATCH * per_img * 4,
+        }
+        alg.update({k: int(v) for k, v in tb.items()})
+        for name, (calls, ms) in tm.items():
+            b = alg.get(name)
+            row = {'calls': calls, 'avg_ms': round(ms, 5),
+                   'ms_per_step': round(ms * calls / n_inst, 5), 'hot_path': name in HOT_PATH}
+            if b:
+                row.update(bytes=b, GB_s=round(b / (ms * 1e-3) / 1e9, 1),
+                           frac=round(b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
+            kernels[name] = row
+        # the roofline kernel: the SURVEY 8(a) entry point with the most time
+        # per step among the HBM-bound ones (the MMD launch is latency / VALU
+        # bound at D = 1 and is reported in roofline_hot_path)
+        cands = [k for k in kernels if k in HOT_PATH and 'GB_s' in kernels[k]
+                 and k != 'smmd_mmd2_fwd']
+        if cands:
+            dom = max(cands, key=lambda k: kernels[k]['ms_per_step'])
+            traffic, src = pmc_traffic(dom)
+            roofline = {'bound': 'hbm', 'kernel': dom, 'achieved': kernels[dom]['GB_s'],
+                        'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': kernels[dom]['frac'],
+                        'traffic': traffic, 'traffic_source': src,
+                        'avg_ms': kernels[dom]['avg_ms'],
+                        'algorithmic_bytes': kernels[dom]['bytes']}
+        for k in ('smmd_sn_power_iter', 'smmd_sn_weight_bwd', 'smmd_adam_flat_sn[D]',
+                  'smmd_scaled_loss_fwd', 'smmd_scaled_loss_bwd', 'smmd_fold_pool_weights'):
+            if k in kernels and 'bytes' in kernels[k]:
+                traffic, src = pmc_traffic(k)
+                hot[k] = {'avg_ms': kernels[k]['avg_ms'], 'algorithmic_bytes': kernels[k]['bytes'],
+                          'GB_s': kernels[k]['GB_s'], 'hbm_frac': kernels[k]['frac'],
+                          'pmc_traffic': traffic,
+                          'pmc_over_algorithmic': (round(traffic / kernels[k]['bytes'], 3)
+                                                   if traffic else None),
+                          'pmc_source': src}
+        if 'smmd_mmd2_fwd' in kernels:
+            mk = kernels['smmd_mmd2_fwd']
+            P = 3 * m_all * m_all
+            ops = mmd_valu_ops_per_pair('rbf', 1) * P
+            hot['smmd_mmd2_fwd'] = {
+                'avg_ms': mk['avg_ms'], 'N_per_side': m_all, 'pairs': P,
+                'valu_frac': round(ops / (mk['avg_ms'] * 1e-3) / VALU_LANE_OPS, 5),
+                'bound': 'latency at D = 1 (one launch per critic step)'}
+        log('instrumented pass: %d steps' % n_inst)
+
+    fl = step_flops(model, images[0])
+    ms_step = dt / args.steps * 1e3
+    # the timed region's own mix of D and G steps
+    fl_timed = (counts['D'] * fl['flops_per_D_step'] + counts['G'] * fl['flops_per_G_step']) \
+        / max(counts['D'] + counts['G'], 1)
+    tfs = fl_timed / (ms_step * 1e-3) / 1e12
+    hot['step'] = dict(fl, flops_per_timed_step=fl_timed, tflops=round(tfs, 2),
+                       fp32_peak_tflops=FP32_PEAK_TFS, frac=round(tfs / FP32_PEAK_TFS, 4),
+                       note='algorithmic = the reference\'s literal conv layers (no fold, '
+                            'direct-conv MAC count); the product runs Winograd and folded '
+                            'stride-2 convs, which execute fewer MACs, so this is a '
+                            'work-rate against the fp32 peak, not a utilisation counter')
+
     sweep = None
     if args.mmd_sweep:
         sweep = mmd_sweep(world, rank, dev, dist.group.WORLD if world > 1 else None,
                           quick=args.mmd_sweep == 2)
-
-    # every libsmmd_hip entry point of the timed region: HIP-event time on the
-    # compute stream and its algorithmic HBM bytes per call
-    m_all = BATCH * world
-    sn_kn = sum(e.N * e.K for e in model.sn_D.entries)
-    per_img = 3 * 64 * 64
-    alg = {
-        # sqsum pass reads g; update pass reads g, p, m, v and writes p, m, v
-        'smmd_adam_flat[D]': model.d_optim.numel * 4 * 8,
-        'smmd_adam_flat[G]': model.g_optim.numel * 4 * 8,
-        # the same update with the SN weights' first power-iteration pass folded
-        # in (its column-partial writes are < 0.1 % of these bytes)
-        'smmd_adam_flat_sn[D]': model.d_optim.numel * 4 * 8,
-        'smmd_adam_flat_sn[G]': model.g_optim.numel * 4 * 8,
-        # one read of W + one write of W_eff (2 K N 4 B per iteration)
-        'smmd_sn_power_iter': sn_kn * 4 * 2,
-        # one read of G and W, one write of gW
-        'smmd_sn_weight_bwd': sn_kn * 4 * 3,
-        # X, Y rows read, unit gradients written, sums
-        'smmd_mmd2_fwd': 2 * m_all * 4 + 2 * BATCH * 4 + 8 * 4,
-        'smmd_scaled_loss_fwd': BATCH * per_img * 4,
-        # ConvMeanPool filter fold / adjoint: 9 floats read + 16 written (or
-        # back) per filter, every ConvMeanPool layer of the critic per call
-        'smmd_fold_pool_weights': sum(m.conv.weight.shape[0] * m.conv.weight.shape[1]
-                                      for m in model.discriminator.modules()
-                                      if isinstance(m, architecture._ConvMeanPool)) * 25 * 4,
-        'smmd_scaled_loss_bwd': 2 * BATCH * per_img * 4,
-    }
-    # entry points whose size varies per call: mean algorithmic bytes per call
-    # (the conv bias gradient: 4 B per element of gy + 4 B per channel)
-    alg.update({k: int(v) for k, v in tb.items()})
-    kernels = {}
-    for name, (calls, ms) in tm.items():
-        b = alg.get(name)
-        row = {'calls': calls, 'avg_ms': round(ms, 5), 'ms_per_step': round(ms * calls /
-                                                                           args.steps, 5)}
-        if b:
-            row.update(bytes=b, GB_s=round(b / (ms * 1e-3) / 1e9, 1),
-                       frac=round(b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
-        kernels[name] = row
-    dom = max((k for k in kernels if 'GB_s' in kernels[k] and k != 'smmd_mmd2_fwd'),
-              key=lambda k: kernels[k]['ms_per_step'])
-    mk = kernels.get('smmd_mmd2_fwd', {})
-    pairs = (2 * m_all) * (2 * m_all)                     # rows x columns swept per critic step
+        hot['mmd_sweep_valu'] = [{'kernel': r['kernel'], 'N': r['N'], 'kernel_ms': r['kernel_ms'],
+                                  'valu_frac': r['valu_frac']}
+                                 for r in sweep if r['D'] == 1 and r['N'] in (64, 512, 2048)]
 
     result = {
         'metric': 'images/sec/step (64x64 SMMD, batch 64) + MMD-kernel GB/s at 1/2/4/8 GPU',
@@ -393,7 +613,10 @@ def main():
         'n_gpus': world,
         'steps': args.steps,
         'warmup': args.warmup,
-        'ms_per_step': round(dt / args.steps * 1e3, 3),
+        'prime_steps': 4,
+        'd_steps': counts['D'],
+        'g_steps': counts['G'],
+        'ms_per_step': round(ms_step, 3),
         'higher_is_better': True,
         'scaling': 'weak',
         'vs_baseline': None,
@@ -409,24 +632,20 @@ def main():
                    'conv_mean_pool': ('folded 4x4 stride-2 conv' if architecture.FOLD_POOL
                                       else 'conv3x3 + mean pool'),
                    'miopen_db': os.environ.get('MIOPEN_USER_DB_PATH')},
-        'roofline': {'bound': 'hbm', 'kernel': dom, 'achieved': kernels[dom]['GB_s'],
-                     'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': kernels[dom]['frac'],
-                     'traffic': pmc_traffic(dom), 'avg_ms': kernels[dom]['avg_ms'],
-                     'algorithmic_bytes': kernels[dom]['bytes']},
-        'mmd_kernel': {'kernel': 'smmd_mmd2_fwd (mmd2_fused_kernel<1,RBF>)',
-                       'avg_ms': mk.get('avg_ms'), 'GB_s': mk.get('GB_s'),
-                       'pair_evals_per_s': round(pairs / (mk['avg_ms'] * 1e-3), 1) if mk else None,
-                       'bound': 'latency (D=1: %s B algorithmic per call)' % mk.get('bytes')},
+        'roofline': roofline,
+        'roofline_hot_path': hot,
+        'step_ms_by_kind': {k: round(v, 3) for k, v in step_ms.items()},
         'hip_kernels': kernels,
         'schedule_reference': ref_sched,
         'mmd_sweep': sweep,
         'losses': {'g_loss': g_loss, 'd_loss': d_loss},
     }
+    if step_ms.get('D') and step_ms.get('G'):
+        result['cycle_value'] = round(world * BATCH * 6 / ((5 * step_ms['D'] + step_ms['G'])
+                                                           * 1e-3), 2)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            result['cpu_baseline'] = cpu_baseline(cfg, args.cpu_seconds)
-            result['cpu_baseline']['components'] = cpu_components(
-                cfg, result['cpu_baseline']['cores'])
+            result['cpu_baseline'] = cpu_baseline(args.cpu_seconds)
         except Exception as e:   # report, never hide the GPU number
             result['cpu_baseline'] = {'error': repr(e)}
     if rank == 0:

@@ -129,12 +129,71 @@ class TFMirrorStep:
     def step(self, images, z=None):
         d_loss, grads = self.grads(images, z)
         self.t += 1
-        lr_t = self.lr * math.sqrt(1 - self.b2 ** self.t) / (1 - self.b1 ** self.t)
-        with torch.no_grad():
-            for p, gr, m, v in zip(self.params, grads, self.m, self.v):
-                inv = torch.rsqrt(torch.sum(gr * gr))
-                gr = gr * 1.0 * torch.clamp(inv, max=1.0)       # tf.clip_by_norm(g, 1.)
-                m += (gr - m) * (1 - self.b1)
-                v += (gr * gr - v) * (1 - self.b2)
-                p -= lr_t * m / (torch.sqrt(v) + 1e-8)
+        tf_adam_(self.params, grads, self.m, self.v, self.t, self.lr, self.b1, self.b2)
         return float(d_loss.detach())
+
+
+def tf_adam_(params, grads, ms, vs, t, lr, b1, b2, eps=1e-8, clip=1.0):
+    """Per-variable tf.clip_by_norm(g, 1.) (model.py:449, :455) then
+    tf.train.AdamOptimizer's update (model.py:410-411, :458-468)."""
+    lr_t = lr * math.sqrt(1 - b2 ** t) / (1 - b1 ** t)
+    with torch.no_grad():
+        for p, gr, m, v in zip(params, grads, ms, vs):
+            if clip:
+                inv = torch.rsqrt(torch.sum(gr * gr))
+                gr = gr * torch.clamp(inv * clip, max=1.0)     # t c / max(|t|, c)
+            m += (gr - m) * (1 - b1)
+            v += (gr * gr - v) * (1 - b2)
+            p -= lr_t * m / (torch.sqrt(v) + eps)
+
+
+class TFMirrorTrainer:
+    """The reference's training loop on the CPU mirror: set_counters' 5 D + 1 G
+    schedule (model.py:470-478) and, as every ``sess.run`` of train_step does
+    (model.py:514, :522-533), BOTH gradient sets computed each step with one
+    of them applied.  The CPU baseline of bench.py."""
+
+    def __init__(self, G, D, sn_layers, lr=2e-4, beta1=0.5, beta2=0.9, sc=10.0, z_dim=128,
+                 dsteps=5, start_dsteps=10, gsteps=1):
+        self.critic = TFMirrorStep(G, D, sn_layers, lr, beta1, beta2, sc, z_dim)
+        self.g_params = [p for p in G.parameters() if p.requires_grad]
+        self.gm = [torch.zeros_like(p) for p in self.g_params]
+        self.gv = [torch.zeros_like(p) for p in self.g_params]
+        self.gt = 0
+        self.dsteps, self.start_dsteps, self.gsteps = dsteps, start_dsteps, gsteps
+        self.step_no, self.d_counter, self.g_counter = 0, 0, 0
+
+    def set_counters(self):
+        if self.g_counter == 0:
+            d = self.start_dsteps if (self.step_no % 500 == 0 or self.step_no < 20) \
+                else self.dsteps
+            self.d_counter = (self.d_counter + 1) % (d + 1)
+        if self.d_counter == 0:
+            self.g_counter = (self.g_counter + 1) % self.gsteps
+
+    def train_step(self, images):
+        """One sess.run: returns 'D' or 'G' (the update applied)."""
+        with stock_torch_ops():
+            c = self.critic
+            self.set_counters()
+            c._sn()
+            z = torch.empty(images.shape[0], c.z_dim).uniform_(-1, 1)
+            fake = c.G(z)
+            x = images.detach().requires_grad_(True)
+            d_images = c.D(x)
+            d_G = c.D(fake)
+            mmd2 = rbf_mmd2_tf(d_G, d_images)
+            g, = torch.autograd.grad(d_images[:, 0].sum(), x, create_graph=True)
+            J = torch.sum(g * g, dim=(1, 2, 3)).mean()
+            g_loss = mmd2 * (1.0 / (c.sc * J + 1.0))
+            d_loss = -g_loss
+            d_grads = torch.autograd.grad(d_loss, c.params, retain_graph=True)
+            g_grads = torch.autograd.grad(g_loss, self.g_params)
+            if self.d_counter == 0:
+                self.gt += 1
+                self.step_no += 1
+                tf_adam_(self.g_params, g_grads, self.gm, self.gv, self.gt, c.lr, c.b1, c.b2)
+                return 'G'
+            c.t += 1
+            tf_adam_(c.params, d_grads, c.m, c.v, c.t, c.lr, c.b1, c.b2)
+            return 'D'

@@ -18,6 +18,7 @@ a ROCm device and the library must be built (see ``_lib``).
 """
 from __future__ import annotations
 
+import threading
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -312,6 +313,44 @@ def get_kernel(name):
     return fn
 
 
+for _name in KERNEL_NAMES:              # lets spec_of map a kernel callable back
+    globals()['_%s_kernel' % _name].kernel_name = _name
+
+
+def spec_of(kernel):
+    """KernelSpec of one of this module's ``_<kind>_kernel`` callables (with
+    their default parameters), or None for any other callable."""
+    name = getattr(kernel, 'kernel_name', None)
+    return get_kernel_spec(name) if name is not None else None
+
+
+# ---------------------------------------------------------------------------
+# the batch a loss spans: in the all-gather data-parallel mode, mmd2 of a
+# kernel value evaluated inside ``loss_group(group)`` is the estimator of the
+# GLOBAL batch (every rank's rows), as model.set_tower_loss arranges around
+# set_loss -- so a subclass's ``mmd.mmd2(kernel(G, images))`` needs no change
+# ---------------------------------------------------------------------------
+_scope = threading.local()
+
+
+class loss_group:
+    def __init__(self, group):
+        self.group = group if (group is not None and dist.get_world_size(group) > 1) else None
+
+    def __enter__(self):
+        self.prev = getattr(_scope, 'group', None)
+        _scope.group = self.group
+        return self
+
+    def __exit__(self, *a):
+        _scope.group = self.prev
+        return False
+
+
+def current_loss_group():
+    return getattr(_scope, 'group', None)
+
+
 # ---------------------------------------------------------------------------
 # estimator
 # ---------------------------------------------------------------------------
@@ -319,7 +358,7 @@ def mmd2(K, biased=False):
     """gan/core/mmd.py:194-196.  A KernelMatrices argument takes the fused
     path; an explicit 4-tuple of matrices is reduced as given."""
     if isinstance(K, KernelMatrices):
-        return mmd2_fused(K.X, K.Y, K.spec, biased)
+        return mmd2_fused(K.X, K.Y, K.spec, biased, process_group=current_loss_group())
     K_XX, K_XY, K_YY, const_diagonal = K
     return _mmd2(K_XX, K_XY, K_YY, const_diagonal, biased)
 

@@ -151,64 +151,149 @@ class MMD_GAN:
         return torch.empty(n, self.z_dim, device=self.device).uniform_(-1.0, 1.0)  # model.py:271
 
     # ------------------------------------------------------------------
-    # losses (overridden by SMMD / SWGAN)
+    # the reference's loss hooks (model.py:268-403; SMMD / SWGAN override
+    # set_loss and apply_scaling, smmd.py:10-42).  They work on the same
+    # attributes the reference uses: self.images / self.G (critic inputs),
+    # self.d_images / self.d_G (critic outputs, 'hF'), self.d_images_layers /
+    # self.d_G_layers, and set self.g_loss / self.d_loss / self.optim_name.
     # ------------------------------------------------------------------
-    def base_loss(self, d_G, d_images):
-        """mmd2 of the configured kernel (model.py:314-318)."""
-        grp = self._dist_group() if self.dp_mode == 'global' else None
-        return mmd.mmd2_fused(d_G, d_images, self.spec, process_group=grp)
+    def _loss_group(self):
+        """The group the loss spans: all ranks in the all-gather mode."""
+        return self._dist_group() if self.dp_mode == 'global' else None
 
-    def apply_scaling(self, base, jac, d_images):
-        return ops.scaled_loss(base, jac, d_images, sc=self.sc, variant=self.config.scaling_variant,
-                               sqrt_scale=False,
-                               process_group=self._dist_group() if self.dp_mode == 'global'
-                               else None)
-
-    def uses_scaling(self):
-        return False
-
-    # ------------------------------------------------------------------
-    def _critic_losses(self, images, fake, need_critic_grad):
-        """Returns (g_loss, d_loss, aux).  need_critic_grad: build the graph
-        for d_loss w.r.t. the critic (including the Jacobian double backward)."""
+    def set_tower_loss(self, images, fake, need_critic_grad):
+        """The loss half of model.py:268-311: the critic on the real and the
+        generated batch, then ``set_loss(self.d_G, self.d_images)``.
+        ``need_critic_grad``: build the graph for d_loss w.r.t. the critic
+        (the Jacobian's double backward, the penalties).  Returns
+        (g_loss, d_loss, aux)."""
         D = self.discriminator
-        scaling = self.uses_scaling()
+        c = self.config
         if images.dim() == 4:
             images = images.contiguous(memory_format=self.memory_format)
-        if scaling:
-            images = images.detach().requires_grad_(True)
-        self._last_images = images
-        d_images = D(images)
-        d_G = D(fake)
-        base = self.base_loss(d_G, d_images)
-        aux = None
-        if scaling:
-            jac = ops.jacobian_columns(d_images, images, create_graph=need_critic_grad)
-            if not need_critic_grad:
-                jac = jac.detach()
-            g_loss, aux = self.apply_scaling(base, jac, d_images)
+        if getattr(c, 'with_scaling', False) and not getattr(c, 'use_gaussian_noise', False):
+            images = images.detach().requires_grad_(True)    # x_hat_data of add_scaling
+        self.images = self._last_images = images
+        self.G = fake
+        self._need_critic_grad = need_critic_grad
+        self.aux = None
+        if getattr(c, "L2_discriminator_penalty", 0) > 0:
+            self.d_images_layers = D(images, return_layers=True)
+            self.d_G_layers = D(fake, return_layers=True)
+            self.d_images = self.d_images_layers['hF']
+            self.d_G = self.d_G_layers['hF']
         else:
-            g_loss = base
-        d_loss = -g_loss
-        if need_critic_grad and self.gp > 0:
-            d_loss = d_loss + self.gp * self.gradient_penalty(images, fake, d_images, d_G)
-        if need_critic_grad and self.config.L2_discriminator_penalty > 0:
-            raise NotImplementedError('L2_discriminator_penalty is outside this build')
-        return g_loss, d_loss, aux
+            self.d_images_layers = self.d_G_layers = None
+            self.d_images = D(images)
+            self.d_G = D(fake)
+        # mmd.mmd2 inside set_loss spans the global batch in the all-gather mode
+        with mmd.loss_group(self._loss_group()):
+            self.set_loss(self.d_G, self.d_images)
+        return self.g_loss, self.d_loss, self.aux
 
-    def gradient_penalty(self, images, fake, d_images, d_G):
-        """Witness GP (model.py:327-350): x_hat = (1-a) real + a fake; the
-        witness gradient at the critic output comes from the HIP witness op
-        (with its own second-order backward); the input gradient and the
-        penalty (norm over the CHANNEL axis only, model.py:341) are PyTorch."""
+    def set_loss(self, G, images):
+        """model.py:313-325: mmd2 of the configured kernel, then the witness
+        gradient penalty and the L2 critic penalty."""
+        kernel = mmd.get_kernel(self.config.kernel)
+        self.g_loss = mmd.mmd2(kernel(G, images))
+        self.d_loss = -self.g_loss
+        self.optim_name = 'kernel_loss'
+        self.add_gradient_penalty(kernel, G, images)
+        self.add_l2_penalty()
+
+    def add_gradient_penalty(self, kernel, fake, real):
+        """Witness GP (model.py:327-350): x_hat = (1-a) real + a fake images;
+        witness_i = mean_j K(D(x_hat)_i, real_j) - mean_j K(D(x_hat)_i, fake_j)
+        on the critic features; penalty = mean((||d sum(witness)/d x_hat||_C -
+        1)^2), the norm over the CHANNEL axis only (model.py:341).  For the
+        library's kernels the witness gradient at the critic output is the HIP
+        witness op (with its own second-order backward); any other kernel
+        callable runs through its K_XY_only matrices."""
+        if self.config.gradient_penalty <= 0 or not self._need_critic_grad:
+            return
         bs = min(self.batch_size, self.real_batch_size)
+        real, fake = real[:bs], fake[:bs]
         alpha = torch.rand(bs, 1, 1, 1, device=self.device)
-        x_hat = ((1.0 - alpha) * images[:bs].detach() + alpha * fake[:bs].detach())
-        x_hat.requires_grad_(True)
-        h = self.discriminator(x_hat)
-        dH, _ = mmd.witness_and_grad(h, d_images[:bs], d_G[:bs], self.spec)
-        g, = torch.autograd.grad(h, x_hat, grad_outputs=dH, create_graph=True)
-        return torch.mean((ops.safer_norm(g, axis=1) - 1.0) ** 2)
+        x_hat_data = ((1.0 - alpha) * self.images[:bs].detach()
+                      + alpha * self.G[:bs].detach()).requires_grad_(True)
+        x_hat = self.discriminator(x_hat_data)                    # NO_OPS (model.py:335)
+        spec = mmd.spec_of(kernel)
+        if spec is not None:
+            dH, _ = mmd.witness_and_grad(x_hat, real, fake, spec)
+            g, = torch.autograd.grad(x_hat, x_hat_data, grad_outputs=dH, create_graph=True)
+        else:
+            witness = (kernel(x_hat, real, K_XY_only=True).mean(1)
+                       - kernel(x_hat, fake, K_XY_only=True).mean(1))
+            g, = torch.autograd.grad(witness.sum(), x_hat_data, create_graph=True)
+        penalty = torch.mean((ops.safer_norm(g, axis=1) - 1.0) ** 2)
+        self.d_loss = self.d_loss + penalty * self.gp
+        self.optim_name += '_(gp %.1f)' % self.config.gradient_penalty
+
+    def add_l2_penalty(self):
+        """model.py:352-364: L2 * mean over the batch of the per-sample mean
+        square of every critic layer output (real and generated calls)."""
+        coeff = self.config.L2_discriminator_penalty
+        if coeff <= 0 or not self._need_critic_grad:
+            return
+        penalty = 0.0
+        for layers in (self.d_G_layers, self.d_images_layers):
+            for layer in layers.values():
+                penalty = penalty + (layer * layer).reshape(layer.shape[0], -1).mean(1)
+        self.d_L2_penalty = coeff * torch.mean(penalty)
+        self.d_loss = self.d_loss + self.d_L2_penalty
+        self.optim_name += ' (L2 dp %.6f)' % coeff
+        self.optim_name = self.optim_name.replace(') (', ', ')
+
+    def add_scaling(self):
+        """model.py:366-403: scale = 1 / (sc E||d D(x)/dx||^2 + 1) ('grad') or
+        1 / (sc (E||dD/dx||^2 + E D(x)^2) + 1) ('value_and_grad'), x the real
+        batch or, with use_gaussian_noise, N(0, 10^2) noise of its shape through
+        one more critic call; then ``self.apply_scaling(scale)``.
+
+        The Jacobian is PyTorch autograd (create_graph in a critic update); J,
+        the scale and its backward are one HIP pass each over the Jacobian.
+        When apply_scaling is the class's own (not overridden), scale and
+        product run fused in the same launch (ops.scaled_loss)."""
+        c = self.config
+        if not c.with_scaling:          # the reference builds scale for summaries only
+            return
+        if c.scaling_variant not in ('grad', 'value_and_grad'):
+            raise ValueError('scaling_variant must be grad or value_and_grad (model.py:387-390)')
+        if getattr(c, "use_gaussian_noise", False):
+            x_hat_data = (torch.randn(self.images.shape, device=self.device) * 10.0) \
+                .contiguous(memory_format=self.memory_format).requires_grad_(True)
+            x_hat = self.discriminator(x_hat_data)                # NO_OPS (model.py:370)
+        else:
+            x_hat_data, x_hat = self.images, self.d_images
+        need = self._need_critic_grad
+        jac = ops.jacobian_columns(x_hat, x_hat_data, create_graph=need)
+        if not need:
+            jac = jac.detach()
+        feat = x_hat if need else x_hat.detach()
+        fused = self._fused_scaling()
+        if fused is not None:
+            self.g_loss, self.aux = ops.scaled_loss(
+                self.g_loss, jac, feat, sc=self.sc, variant=c.scaling_variant,
+                sqrt_scale=(fused == 'sqrt'), process_group=self._loss_group())
+            self.d_loss = -self.g_loss
+        else:
+            scale, self.aux = ops.scaling_factor(jac, feat, sc=self.sc,
+                                                 variant=c.scaling_variant,
+                                                 process_group=self._loss_group())
+            self.apply_scaling(scale)
+
+    def _fused_scaling(self):
+        """'mul' / 'sqrt' when apply_scaling is SMMD's / SWGAN's own (the
+        scale and the product then run in one HIP launch), else None."""
+        return None
+
+    def apply_scaling(self, scale):
+        raise NotImplementedError('apply_scaling is defined by SMMD / SWGAN (smmd.py:21-23, '
+                                  ':40-42)')
+
+    # kept for callers of the round-1 API
+    def _critic_losses(self, images, fake, need_critic_grad):
+        return self.set_tower_loss(images, fake, need_critic_grad)
 
     # ------------------------------------------------------------------
     def _exchange(self, opt):
@@ -235,7 +320,7 @@ class MMD_GAN:
         for p in self.d_vars:
             p.requires_grad_(True)
         self.d_optim.zero_grad()
-        g_loss, d_loss, aux = self._critic_losses(images, fake, need_critic_grad=True)
+        g_loss, d_loss, aux = self.set_tower_loss(images, fake, need_critic_grad=True)
         if ref:       # the generator's gradient set, computed and discarded
             torch.autograd.grad(g_loss, self.g_vars, retain_graph=True)
             d_loss.backward(inputs=self.d_vars)
@@ -262,7 +347,7 @@ class MMD_GAN:
                 self.sn_G.refresh(update_u=True)
             self.g_optim.zero_grad()
             fake = self.generator(self.sample_z(self.batch_size))
-            g_loss, d_loss, aux = self._critic_losses(images, fake, need_critic_grad=ref)
+            g_loss, d_loss, aux = self.set_tower_loss(images, fake, need_critic_grad=ref)
             if ref:   # the critic's gradient set, computed and discarded
                 torch.autograd.grad(d_loss, self.d_vars, retain_graph=True)
             g_loss.backward(inputs=self.g_vars)

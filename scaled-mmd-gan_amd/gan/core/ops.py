@@ -133,6 +133,76 @@ def scaled_loss(base, jac, feat=None, sc=10.0, variant='grad', sqrt_scale=False,
     return g, out
 
 
+class _ScaleFactor(torch.autograd.Function):
+    """scale = 1 / (sc * Q + 1) alone (model.py:387-390), for an overridden
+    apply_scaling: the same HIP pass as _ScaledLoss without a base loss.  The
+    backward reuses smmd_scaled_loss_bwd with base := 1 and f = id, whose
+    dL/dQ = go * base * (-sc scale^2) is then exactly d scale / dQ * go."""
+
+    @staticmethod
+    def forward(ctx, jac, feat, sc, variant, b_total, group):
+        _lib.require_cuda(jac, feat)
+        jac = jac.contiguous()
+        n_cols, b = jac.shape[0], jac.shape[1]
+        per = jac[0, 0].numel()
+        dev = jac.device
+        L = _lib.lib()
+        feat_c = feat.contiguous() if feat is not None else None
+        dof = feat_c.shape[1] if feat_c is not None else 0
+        out = torch.empty(8, device=dev, dtype=torch.float32)
+        per_sample = torch.empty(b, device=dev, dtype=torch.float32)
+        ws = _lib.workspace('scaled_loss', L.smmd_scaled_loss_workspace_bytes(n_cols * b, per),
+                            dev)
+        s = _lib.stream_handle(dev)
+        with _lib.timed('smmd_scaled_loss_fwd'):
+            st = L.smmd_scaled_loss_fwd(_lib.ptr(jac), n_cols, b, b_total, per, _lib.ptr(feat_c),
+                                        dof, None, float(sc), variant, 0, _lib.ptr(out),
+                                        _lib.ptr(per_sample), _lib.ptr(ws), ws.numel(), s)
+        _lib.check(st, 'smmd_scaled_loss_fwd')
+        if group is not None:
+            all_reduce_(out[3:5], group)
+            _lib.check(L.smmd_scaled_loss_finalize(_lib.ptr(out), float(sc), variant, 0, s),
+                       'smmd_scaled_loss_finalize')
+        ctx.save_for_backward(jac, feat_c, out)
+        ctx.cfg = (n_cols, b, b_total, per, dof, float(sc), variant)
+        ctx.mark_non_differentiable(out)
+        return out[2].clone().view(()), out
+
+    @staticmethod
+    def backward(ctx, g_scale, g_out):
+        jac, feat, out = ctx.saved_tensors
+        n_cols, b, b_total, per, dof, sc, variant = ctx.cfg
+        unit = out.clone()
+        unit[5] = 1.0                      # base := 1, so dL/dQ = g_scale d scale / dQ
+        go = g_scale.reshape(1).contiguous().to(torch.float32)
+        gjac = torch.empty_like(jac)
+        gfeat = torch.empty_like(feat) if (feat is not None and variant == 1) else None
+        with _lib.timed('smmd_scaled_loss_bwd'):
+            st = _lib.lib().smmd_scaled_loss_bwd(
+                _lib.ptr(jac), n_cols, b, b_total, per, _lib.ptr(feat), dof, _lib.ptr(unit), sc,
+                variant, 0, _lib.ptr(go), None, _lib.ptr(gjac), _lib.ptr(gfeat),
+                _lib.stream_handle(jac.device))
+        _lib.check(st, 'smmd_scaled_loss_bwd')
+        if feat is not None and gfeat is None:
+            gfeat = torch.zeros_like(feat)
+        return gjac, gfeat, None, None, None, None
+
+
+def scaling_factor(jac, feat=None, sc=10.0, variant='grad', process_group=None):
+    """scale of MMD_GAN.add_scaling (model.py:382-390) as a differentiable
+    0-dim tensor, for an ``apply_scaling(scale)`` override.  Returns (scale,
+    aux) with aux as in ``scaled_loss`` (g_loss, d_loss and base unset)."""
+    v = {'grad': 0, 'value_and_grad': 1}[variant]
+    if v == 1 and feat is None:
+        raise ValueError("scaling_variant 'value_and_grad' needs the critic output")
+    b = jac.shape[1]
+    group = process_group if (process_group is not None and
+                              dist.get_world_size(process_group) > 1) else None
+    b_total = b * (dist.get_world_size(group) if group is not None else 1)
+    scale, out = _ScaleFactor.apply(jac, feat if v == 1 else None, sc, v, b_total, group)
+    return scale, out
+
+
 class _SqNormJac(torch.autograd.Function):
     @staticmethod
     def forward(ctx, jac):
