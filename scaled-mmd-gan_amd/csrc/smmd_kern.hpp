@@ -118,4 +118,35 @@ struct GramArgs {
 size_t gram_ws_bytes(int m, int n, int d);
 smmd_status gram_mmd2_launch(const GramArgs &g, void *ws_body, hipStream_t s);
 
+// 2-D tiled row x column-chunk path (smmd_mmd_tile.hip) for d <= 8
+struct TileArgs {
+    const float *X;
+    const float *Y;
+    int m, n, d;
+    int nrows, nxr, x_begin, y_begin;
+    int tanh_in, trace_mode, need_grad, biased, has_const;
+    double const_diag;
+    float gw_same_x, gw_same_y, gw_cross;
+    float *grad_x;
+    float *grad_y;
+    float *out_sums;
+    float *out_mmd2;
+    KParams kp;
+    // filled by tile_mmd2_launch
+    int n_rt, n_ch, cpw, rows_pad;
+    float *part;          // [n_ch][d + 1][rows_pad] per-chunk row partials
+    double *blk_sums;     // [n_rt * n_ch][8], one record per workgroup
+    unsigned *rt_counter; // [n_rt], in the workspace header
+    unsigned *g_counter;
+};
+
+// Every smmd_mmd2_fwd path keeps its arrival counters in the first
+// MMD_WS_HEADER bytes of the caller's workspace (zero at rest: each path
+// resets what it used), its data after it, so one workspace serves all paths.
+constexpr size_t MMD_WS_HEADER = 16384;
+constexpr int TILE_MAX_RT = (int)(MMD_WS_HEADER / sizeof(unsigned)) - 64;
+bool tile_supported(int d);
+size_t tile_ws_bytes(int rows, int cols, int d);      // body bytes (after the header)
+smmd_status tile_mmd2_launch(TileArgs a, int kind, void *ws, hipStream_t s);
+
 }  // namespace smmd

@@ -695,10 +695,26 @@ static bool use_gram(int m, int n, int d) {
     return (d >= 16 && rows >= 1024) || (d >= 32 && rows >= 512);
 }
 
+// d <= 8 (every config: d = 1): the 2-D tiled kernel (smmd_mmd_tile.hip)
+// unless SMMD_MMD_TILE=0 selects the row sweep below (A/B, parity tests)
+static bool use_tile(int m, int n, int d) {
+    if (!tile_supported(d) || use_gram(m, n, d)) return false;
+    const char *e = getenv("SMMD_MMD_TILE");
+    if (e && e[0] == '0') return false;
+    const long rows = (long)(m > 0 ? m : 0) + (n > 0 ? n : 0);
+    return rows <= (long)TILE_MAX_RT * 64;
+}
+
 size_t smmd_mmd2_workspace_bytes(int m, int n, int d) {
-    if (use_gram(m, n, d)) return 256 + gram_ws_bytes(m, n, d);
     const int rows = (m > 0 ? m : 0) + (n > 0 ? n : 0);
-    return 256 + align_up((size_t)mmd2_grid(rows, pick_dt(d)) * 8 * sizeof(double), 256);
+    if (use_gram(m, n, d)) return MMD_WS_HEADER + gram_ws_bytes(m, n, d);
+    size_t b = align_up((size_t)mmd2_grid(rows, pick_dt(d)) * 8 * sizeof(double), 256);
+    // the tile path at any row split of this (m, n): at most m + n local rows
+    if (tile_supported(d)) {
+        const size_t t = tile_ws_bytes(rows, rows, d);
+        if (t > b) b = t;
+    }
+    return MMD_WS_HEADER + b;
 }
 
 smmd_status smmd_mmd2_fwd(const smmd_kernel_desc *desc, const float *X, int m, const float *Y,
@@ -740,7 +756,26 @@ smmd_status smmd_mmd2_fwd(const smmd_kernel_desc *desc, const float *X, int m, c
         g.out_sums = out_sums; g.out_mmd2 = out_mmd2;
         g.grad_x = grad_x; g.grad_y = grad_y;
         g.kp = kp;
-        return gram_mmd2_launch(g, (char *)ws + 256, (hipStream_t)stream);
+        return gram_mmd2_launch(g, (char *)ws + MMD_WS_HEADER, (hipStream_t)stream);
+    }
+    if (use_tile(m, n, d)) {
+        TileArgs t;
+        memset(&t, 0, sizeof(t));
+        t.X = X; t.Y = Y; t.m = m; t.n = n; t.d = d;
+        t.nrows = rows; t.nxr = x_end - x_begin; t.x_begin = x_begin; t.y_begin = y_begin;
+        t.tanh_in = desc->tanh_inputs ? 1 : 0;
+        t.biased = is_biased;
+        t.has_const = desc->has_const_diag ? 1 : 0;
+        t.const_diag = desc->const_diag;
+        t.trace_mode = (!is_biased && !t.has_const) ? 1 : 0;
+        t.need_grad = need_grad;
+        t.gw_same_x = (float)(2.0 * wxx);
+        t.gw_same_y = (float)(2.0 * wyy);
+        t.gw_cross = (float)(-2.0 / (md * nd));
+        t.grad_x = grad_x; t.grad_y = grad_y;
+        t.out_sums = out_sums; t.out_mmd2 = out_mmd2;
+        t.kp = kp;
+        return tile_mmd2_launch(t, desc->kind, ws, (hipStream_t)stream);
     }
     const int grid = mmd2_grid(rows, dt);
 
@@ -767,7 +802,7 @@ smmd_status smmd_mmd2_fwd(const smmd_kernel_desc *desc, const float *X, int m, c
     a.grad_x = grad_x;
     a.grad_y = grad_y;
     a.counter = (unsigned *)ws;
-    a.partials = (double *)((char *)ws + 256);
+    a.partials = (double *)((char *)ws + MMD_WS_HEADER);
     a.out_sums = out_sums;
     a.out_mmd2 = out_mmd2;
     a.kp = kp;

@@ -200,6 +200,144 @@ def test_mmd2_deterministic(dev):
     assert len(set(a)) == 1
 
 
+# ---------------------------------------------------------------------------
+# The 2-D tiled path (csrc/smmd_mmd_tile.hip, d <= 8): the configs' global
+# batch sizes (C4: 8 GPUs x 64 = 512 rows per side; C5: 8 x 256 = 2048) and
+# ragged shapes (partial row tiles, chunks straddling the X | Y boundary).
+# ---------------------------------------------------------------------------
+TILE_NAMES = ['rbf', 'mix_rbf', 'mix_rq_dot', 'distance', 'dot', 'tanh_mix_rq']
+
+
+@pytest.mark.parametrize('name', TILE_NAMES)
+@pytest.mark.parametrize('shape', [(512, 512, 1), (2048, 2048, 1), (1000, 777, 3),
+                                   (65, 4100, 2), (129, 64, 8)])
+def test_mmd2_tile_large_vs_oracle(dev, name, shape):
+    from gan.core import mmd
+    m, n, d = shape
+    X, Y = _feats(m, n, d, seed=zlib.crc32(repr(('tile', name, shape)).encode()))
+    spec = O.kernel_spec(name)
+    g32 = spec.kind == 'distance'          # see test_mmd2_fused_vs_oracle
+    Xt = torch.tensor(X, device=dev, requires_grad=True)
+    Yt = torch.tensor(Y, device=dev, requires_grad=True)
+    val, sums = mmd.mmd2_fused(Xt, Yt, name, return_sums=True)
+    val.backward()
+    _close(val.item(), O.mmd2(spec, X, Y, gram32=g32), 1e-5, 1e-4, 'mmd2 %s %s' % (name, shape))
+    _close(sums[:5].cpu().numpy(), O.mmd2_sums(spec, X, Y, gram32=g32), 1e-4 * max(m, n) / 64,
+           1e-4, 'sums')
+    rdx, rdy = O.mmd2_grad(spec, X, Y, gram32=g32)
+    _grad_close(Xt.grad.cpu().numpy(), rdx, 'dX %s %s' % (name, shape))
+    _grad_close(Yt.grad.cpu().numpy(), rdy, 'dY %s %s' % (name, shape))
+
+
+def _abi_mmd2_rows(dev, spec_name, X, Y, xb, xe, yb, ye, ws):
+    """One smmd_mmd2_fwd call through the C ABI on the row slices
+    [xb, xe) of X and [yb, ye) of Y against all columns: (sums[8], dX rows,
+    dY rows)."""
+    from gan.core import _lib, mmd
+    L = _lib.lib()
+    m, d = X.shape
+    n = Y.shape[0]
+    sums = torch.empty(8, device=dev)
+    out = torch.empty(1, device=dev)
+    gx = torch.empty(max(xe - xb, 1), d, device=dev)
+    gy = torch.empty(max(ye - yb, 1), d, device=dev)
+    _lib.check(L.smmd_mmd2_fwd(mmd.get_kernel_spec(spec_name).desc(), _lib.ptr(X), m, _lib.ptr(Y),
+                               n, d, 0, xb, xe, yb, ye, _lib.ptr(sums), _lib.ptr(out),
+                               _lib.ptr(gx), _lib.ptr(gy), _lib.ptr(ws), ws.numel(),
+                               _lib.stream_handle(dev)), 'smmd_mmd2_fwd')
+    return sums, gx[:xe - xb], gy[:ye - yb]
+
+
+@pytest.mark.parametrize('name', ['rbf', 'mix_rq', 'distance'])
+@pytest.mark.parametrize('per_rank', [64, 256])
+def test_mmd2_row_sharded_8way(dev, name, per_rank):
+    """The all-gather mode of 8 ranks emulated on one device:
+    8 calls on rank r's row slices of X and Y against all 8 * per_rank
+    columns, the 8 sums vectors added, then smmd_mmd2_combine -- equal to the
+    one-process oracle on the concatenated batch (C4: 8 x 64, C5: 8 x 256),
+    and each call's row gradients equal that process's rows."""
+    from gan.core import _lib, mmd
+    world = 8
+    N = world * per_rank
+    X, Y = _feats(N, N, 1, seed=zlib.crc32(repr(('shard', name, per_rank)).encode()))
+    spec = O.kernel_spec(name)
+    g32 = spec.kind == 'distance'
+    Xd, Yd = torch.tensor(X, device=dev), torch.tensor(Y, device=dev)
+    L = _lib.lib()
+    ws = torch.zeros(L.smmd_mmd2_workspace_bytes(N, N, 1), dtype=torch.uint8, device=dev)
+    total = torch.zeros(8, device=dev, dtype=torch.float64)
+    gxs, gys = [], []
+    for r in range(world):
+        s, gx, gy = _abi_mmd2_rows(dev, name, Xd, Yd, r * per_rank, (r + 1) * per_rank,
+                                   r * per_rank, (r + 1) * per_rank, ws)
+        total += s.double()
+        gxs.append(gx.cpu().numpy())
+        gys.append(gy.cpu().numpy())
+    out = torch.empty(1, device=dev)
+    _lib.check(L.smmd_mmd2_combine(mmd.get_kernel_spec(name).desc(),
+                                   _lib.ptr(total.float().contiguous()), N, N, 0, _lib.ptr(out),
+                                   _lib.stream_handle(dev)), 'smmd_mmd2_combine')
+    _close(out.item(), O.mmd2(spec, X, Y, gram32=g32), 1e-5, 1e-4, 'sharded mmd2')
+    rdx, rdy = O.mmd2_grad(spec, X, Y, gram32=g32)
+    _grad_close(np.concatenate(gxs), rdx, 'sharded dX')
+    _grad_close(np.concatenate(gys), rdy, 'sharded dY')
+
+
+@pytest.mark.parametrize('name', ['rbf', 'mix_rq_dot', 'distance', 'dot', 'tanh_mix_rq'])
+@pytest.mark.parametrize('shape', [(64, 64, 1), (300, 200, 2), (2048, 2048, 1)])
+def test_mmd2_tile_matches_row_sweep(dev, monkeypatch, name, shape):
+    """SMMD_MMD_TILE=0 selects the round-1 row sweep: both paths agree to the
+    order of their sums."""
+    from gan.core import mmd
+    m, n, d = shape
+    X, Y = _feats(m, n, d, seed=zlib.crc32(repr(('t-vs-s', name, shape)).encode()))
+    out = {}
+    for path in ('0', '1'):
+        monkeypatch.setenv('SMMD_MMD_TILE', path)
+        Xt = torch.tensor(X, device=dev, requires_grad=True)
+        Yt = torch.tensor(Y, device=dev, requires_grad=True)
+        val, sums = mmd.mmd2_fused(Xt, Yt, name, return_sums=True)
+        val.backward()
+        out[path] = (val.item(), sums[:6].cpu().numpy(), Xt.grad.cpu().numpy(),
+                     Yt.grad.cpu().numpy())
+    a, b = out['1'], out['0']
+    _close(a[0], b[0], 1e-6, 1e-5, 'mmd2 tile vs sweep')
+    _close(a[1], b[1], 1e-4 * max(m, n) / 64, 1e-5, 'sums tile vs sweep')
+    for ga, gb, what in ((a[2], b[2], 'dX'), (a[3], b[3], 'dY')):
+        _grad_close(ga, gb, what + ' tile vs sweep')
+
+
+def test_mmd2_tile_deterministic_and_shared_workspace(dev, monkeypatch):
+    """Bit-identical repeats, and one workspace shared by the three paths in
+    turn (Gram, tiled, row sweep): every path leaves the counter header at
+    rest for the next."""
+    from gan.core import mmd
+    X, Y = _feats(2048, 2048, 1, seed=5)
+    Xt, Yt = torch.tensor(X, device=dev), torch.tensor(Y, device=dev)
+    first = mmd.mmd2_fused(Xt, Yt, 'rbf').item()
+    ref = O.mmd2(O.kernel_spec('rbf'), X, Y)
+    Xw, Yw = _gfeats(300, 300, 64, seed=6)
+    Xw, Yw = torch.tensor(Xw, device=dev), torch.tensor(Yw, device=dev)
+    for k in range(6):
+        if k % 3 == 1:
+            mmd.mmd2_fused(Xw, Yw, 'rbf').item()                 # Gram path
+        if k % 3 == 2:
+            monkeypatch.setenv('SMMD_MMD_TILE', '0')              # row sweep
+            v = mmd.mmd2_fused(Xt, Yt, 'rbf').item()
+            _close(v, ref, 1e-5, 1e-4, 'row sweep after tile')
+            monkeypatch.delenv('SMMD_MMD_TILE')
+        assert mmd.mmd2_fused(Xt, Yt, 'rbf').item() == first
+        # every arrival counter back at rest (forward-only and gradient calls)
+        from gan.core import _lib
+        hdr = _lib.workspace('mmd2', 0, dev)[:16384]
+        assert int(hdr.count_nonzero()) == 0
+    Xg, Yg = Xt.clone().requires_grad_(True), Yt.clone().requires_grad_(True)
+    v = mmd.mmd2_fused(Xg, Yg, 'rbf')
+    v.backward()
+    from gan.core import _lib
+    assert int(_lib.workspace('mmd2', 0, dev)[:16384].count_nonzero()) == 0
+
+
 @pytest.mark.parametrize('name', ['rbf', 'mix_rq_dot', 'distance', 'dot', 'tanh_mix_rq'])
 def test_kernel_matrix_backward(dev, name):
     from gan.core import mmd
