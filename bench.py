@@ -102,14 +102,14 @@ def _pct(xs, q):
 
 def _mirror_trainer(cfg, batch, seed=2):
     from gan.core.architecture import get_networks
-    from gan.core.snops import sn_modules
     from oracle.tf_mirror import TFMirrorTrainer
     torch.manual_seed(seed)
     G_cls, D_cls = get_networks(cfg.architecture)
     G = G_cls(cfg.gf_dim, 3, cfg.output_size, cfg.batch_norm, z_dim=cfg.z_dim)
-    D = D_cls(cfg.df_dim, cfg.dof_dim, False, with_sn=True, with_learnable_sn_scale=True,
-              input_size=cfg.output_size)
-    tr = TFMirrorTrainer(G, D, sn_modules(D), lr=cfg.learning_rate, sc=cfg.scaling_coeff)
+    dbn = bool(cfg.batch_norm) and cfg.gradient_penalty <= 0
+    D = D_cls(cfg.df_dim, cfg.dof_dim, dbn, with_sn=cfg.with_sn,
+              with_learnable_sn_scale=cfg.with_learnable_sn_scale, input_size=cfg.output_size)
+    tr = TFMirrorTrainer(cfg, G, D)     # the mirror's own nets (oracle/ref_nets.py), these weights
     tr.step_no = 21              # steady-state 5 D + 1 G (model.py:474-475)
     g = torch.Generator().manual_seed(0)
     imgs = torch.rand(batch, 3, cfg.output_size, cfg.output_size, generator=g)

@@ -7,7 +7,8 @@
 // An HBM stream: every element of gy read once (4 B), 4 B written per channel.
 //
 // Stage 1: block (c, s) sums its contiguous chunk of rows n of channel c (each
-// row is HW contiguous floats, float4 loads when HW % 4 == 0) into one float,
+// row is HW contiguous floats, float4 loads when HW % 4 == 0 and the base is
+// 16-B aligned) into one float,
 // fixed order (per-thread sums, then the fixed wave/block tree).  Rows shorter
 // than the block are packed several per step so every lane loads.
 // Stage 2: one thread per channel adds its S partials in order.  S is chosen
@@ -21,12 +22,12 @@ constexpr int CS_T = 256;
 
 __global__ __launch_bounds__(CS_T) void chan_sum_partial_kernel(const float *__restrict__ gy,
                                                                 int N, int C, int HW, int S,
-                                                                float *__restrict__ part) {
+                                                                int vec, float *__restrict__ part) {
     const int c = blockIdx.x, s = blockIdx.y;
     const int R = (N + S - 1) / S;                      // rows n in [n0, n1) of this block
     const int n0 = s * R, n1 = min(N, n0 + R);
     float acc = 0.f;
-    const bool v4 = (HW & 3) == 0;
+    const bool v4 = vec != 0;                           // HW % 4 == 0 and gy 16-B aligned
     const int w = v4 ? (HW >> 2) : HW;                  // row width in load units
     if (w >= CS_T) {
         for (int n = n0; n < n1; ++n) {
@@ -112,16 +113,18 @@ extern "C" smmd_status smmd_channel_sum(const float *gy, int N, int C, int HW, f
         return SMMD_OK;
     }
     if (!gy) return SMMD_EINVAL;
-    if ((HW & 3) == 0 && (reinterpret_cast<uintptr_t>(gy) & 15) != 0) return SMMD_EINVAL;
+    // float4 rows need HW % 4 == 0 and a 16-B aligned base (a contiguous view
+    // with a storage offset may not be): otherwise the scalar-load path
+    const int vec = ((HW & 3) == 0 && (reinterpret_cast<uintptr_t>(gy) & 15) == 0) ? 1 : 0;
     const int S = chan_sum_split(N, C);
     if (!ws || ws_bytes < (size_t)C * S * sizeof(float)) return SMMD_EWORKSPACE;
     if (S > 65535) return SMMD_EINVAL;
     if (S == 1) {                  // each block owns a whole channel: write the result
-        chan_sum_partial_kernel<<<dim3(C, 1), dim3(CS_T), 0, st>>>(gy, N, C, HW, 1, out);
+        chan_sum_partial_kernel<<<dim3(C, 1), dim3(CS_T), 0, st>>>(gy, N, C, HW, 1, vec, out);
         return last_launch_status();
     }
     float *part = static_cast<float *>(ws);
-    chan_sum_partial_kernel<<<dim3(C, S), dim3(CS_T), 0, st>>>(gy, N, C, HW, S, part);
+    chan_sum_partial_kernel<<<dim3(C, S), dim3(CS_T), 0, st>>>(gy, N, C, HW, S, vec, part);
     smmd_status e = last_launch_status();
     if (e != SMMD_OK) return e;
     chan_sum_final_kernel<<<dim3((C + 255) / 256), dim3(256), 0, st>>>(part, C, S, out);

@@ -55,11 +55,16 @@ class _Up(nn.Module):
         self._kcache = None
 
     def _folded(self, w):
-        """fold_up_weight(w), contiguous, reused while w is the same unmodified
-        tensor under the same grad mode and no FlatAdam step ran (the
-        generator's weights change once per 5 + 1 steps; its forward runs in
-        every critic step)."""
-        key = (torch.is_grad_enabled(), _optim.param_epoch(w), w._version, w.requires_grad)
+        """fold_up_weight(w), contiguous.  Under no_grad (the generator's
+        forward in every critic step) it is reused while w is the same
+        unmodified tensor and no FlatAdam step ran: the generator's weights
+        change once per 5 + 1 steps.  With grad enabled it is rebuilt every
+        call: a cached K would carry an autograd graph that a non-retaining
+        backward frees."""
+        if torch.is_grad_enabled():
+            self._kcache = None
+            return fold_up_weight(w).contiguous()
+        key = (_optim.param_epoch(w), w._version)
         c = self._kcache
         if c is not None and c[0] == key and c[1] is w:
             return c[2]

@@ -377,6 +377,27 @@ class MMD_GAN:
         assert not np.isnan(d), 'NaN d_loss'
         return g, d
 
+    @torch.no_grad()
+    def get_samples(self, n):
+        """n generator samples [n, c, h, w] on the device, batch by batch
+        (model.py:663-694, the NO_OPS sampler graph; BN in training mode as
+        the reference's)."""
+        out, have = [], 0
+        while have < n:
+            out.append(self.generator(self.sample_z(self.batch_size)))
+            have += out[-1].shape[0]
+        return torch.cat(out)[:n]
+
+    def set_lr_sc(self, lr, sc):
+        """Set the learning rate (both optimizers, model.py:410-411) and the
+        scaling coefficient, e.g. after another rank's decay_ops."""
+        c = self.config
+        self.lr = lr
+        self.g_optim.lr = lr
+        self.d_optim.lr = lr * c.learning_rate_D / c.learning_rate
+        if self.sc is not None and sc is not None:
+            self.sc = sc
+
     def decay_ops(self):
         """lr *= decay_rate (min 1e-6) and sc *= sc_decay_rate (model.py:162, :173, :493-496)."""
         c = self.config

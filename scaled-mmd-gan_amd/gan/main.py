@@ -65,6 +65,9 @@ _FLAGS = [
     ('use_gaussian_noise', False, str2bool),
     # this build: data-parallel mode of the all-gather extension
     ('dp_mode', 'tower', str),
+    # this build: scorer features ('inception' is the reference's and is
+    # unavailable offline; 'random' = seeded random features, gan/utils/featurizer.py)
+    ('featurizer', 'inception', str),
 ]
 _DOUBLE_DASH = [('use-incomplete-cho', True, str2bool), ('incho-eta', 1e-3, float),
                 ('incho-max-steps', 1000, int)]
@@ -122,6 +125,41 @@ def output_size_for(flags):
 
 
 CHECKPOINT_FREQ = 2000                   # model.py:609
+SCORE_SIZE = 25000                       # gan/utils/scorer.py:27
+
+
+def make_scorer(flags, pipe, dev, size):
+    """Scorer + featurizer when -compute_scores (model.py:95-96), or
+    (None, None) when scoring is off or no featurizer is available (the
+    Inception graph: a warning says so).  Train codes: loaded from
+    <data_dir>/<dataset>-codes[-size]-<featurizer>.npy when present, else
+    featurized from SCORE_SIZE pipeline images and saved there
+    (gan/utils/scorer.py:37-64)."""
+    if not flags.compute_scores:
+        return None, None
+    import numpy as np
+    import torch
+    from gan.utils.featurizer import get_featurizer
+    from gan.utils.scorer import Scorer
+    feat = get_featurizer(flags.featurizer, dev)
+    if feat is None:
+        return None, None
+    suffix = '' if size <= 32 else '-%d' % size
+    path = os.path.join(flags.data_dir, '%s-codes%s-%s.npy' % (flags.dataset, suffix, feat.name))
+    if os.path.exists(path):
+        codes = np.load(path)                                   # allow_pickle=False
+    else:
+        ims, n = [], 0
+        while n < SCORE_SIZE:
+            b = pipe.next()
+            ims.append(feat(b))
+            n += b.shape[0]
+        codes = torch.cat(ims)[:SCORE_SIZE].cpu().numpy()
+        try:
+            np.save(path, codes)
+        except OSError:
+            pass
+    return Scorer(codes, lr_scheduler=flags.MMD_lr_scheduler), feat
 
 
 def make_pipeline(flags, size, c_dim, dev, rank=0, world=1):
@@ -174,6 +212,13 @@ def main(argv=None):
         else:
             print(' [!] Load failed...')
         step = gan.step
+        scorer, feat = make_scorer(flags, pipe, dev, size) if rank == 0 else (None, None)
+        if world > 1:       # every rank must apply the same learning-rate decays
+            flag = torch.tensor([1.0 if scorer is not None else 0.0], device=dev)
+            dist.broadcast(flag, 0)
+            scoring = bool(flag.item())
+        else:
+            scoring = scorer is not None
         try:
             while step <= flags.max_iteration:
                 _, _, step = gan.train_step(pipe.next())
@@ -183,10 +228,22 @@ def main(argv=None):
                         gan.timer(step, '%s, G: %.8f, D: %.8f' % (gan.optim_name, g, d))
                 if gan.d_counter == 0 and step % CHECKPOINT_FREQ == 0 and rank == 0:
                     gan.save_checkpoint(ckpt_dir, step)          # model.py:608-612
+                if scoring and gan.d_counter == 0 and step % flags.MMD_sdlr_freq == 0:
+                    # model.py:544-545 -> scorer.py:66-175 (rank 0), the decayed
+                    # lr / sc then broadcast so every replica applies them
+                    if rank == 0:
+                        scorer.compute(gan, step, feat(gan.get_samples(SCORE_SIZE)),
+                                       save_checkpoint=lambda: gan.save_checkpoint(ckpt_dir))
+                    if world > 1:
+                        ls = torch.tensor([gan.lr, gan.sc if gan.sc is not None else 0.0],
+                                          device=dev, dtype=torch.float64)
+                        dist.broadcast(ls, 0)
+                        gan.set_lr_sc(float(ls[0]), float(ls[1]) if gan.sc is not None else None)
         finally:
             pipe.stop()
     if world > 1:
         dist.destroy_process_group()
+    return gan
 
 
 if __name__ == '__main__':

@@ -187,3 +187,34 @@ def test_fold_caches_follow_flat_adam_updates():
                 architecture.FOLD_POOL, architecture.FOLD_UP = saved
         assert torch.allclose(d_c, d_l, rtol=1e-4, atol=1e-5 * float(d_l.abs().max()) + 1e-6)
         assert torch.allclose(u_c, u_l, rtol=1e-4, atol=1e-5 * float(u_l.abs().max()) + 1e-6)
+
+
+@pytest.mark.parametrize('offset', [1, 2, 3])
+def test_channel_sum_misaligned_base(offset):
+    """A contiguous view with a storage offset (not 16-B aligned, e.g. a
+    narrow/split backward) takes the kernel's scalar-load path: same sums."""
+    from gan.core.convops import bias_grad
+    shape = (8, 16, 8, 8)
+    rng = np.random.default_rng(offset)
+    flat = rng.standard_normal(int(np.prod(shape)) + offset).astype(np.float32)
+    base = torch.tensor(flat, device='cuda:0')
+    gy = base[offset:].view(shape)
+    assert gy.is_contiguous() and gy.data_ptr() % 16 != 0
+    with torch.no_grad():
+        out = bias_grad(gy)
+    ref = flat[offset:].reshape(shape).astype(np.float64).sum(axis=(0, 2, 3))
+    np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=0, atol=1e-4)
+
+
+def test_upsample_fold_two_backwards_without_step():
+    """Two generator backwards with grad enabled and no optimizer step in
+    between: the folded UpsampleConv filter is not reused across graphs
+    (a cached K would back through a freed graph)."""
+    from gan.core import architecture
+    dev = torch.device('cuda:0')
+    torch.manual_seed(4)
+    up = architecture._Up(8, 4, 3, False).to(dev)
+    z = torch.randn(2, 8, 4, 4, device=dev)
+    for _ in range(2):
+        up(z).square().sum().backward()
+    assert up.conv.weight.grad is not None and torch.isfinite(up.conv.weight.grad).all()

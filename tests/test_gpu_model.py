@@ -8,7 +8,6 @@ fp32 convs, same graph): d_loss rtol 1e-3; per-tensor gradients
 |d| <= max(2e-3 max|ref|, 1e-5 max over all tensors) + 2e-3 |ref|.
 """
 import argparse
-import copy
 
 import numpy as np
 import pytest
@@ -29,32 +28,30 @@ def _cfg(**kw):
 
 
 def _mirror_from(model):
-    from gan.core.snops import sn_modules
+    """The oracle's TF-graph mirror on its own networks (oracle/ref_nets.py),
+    started from the model's weights and u vectors."""
     from oracle.tf_mirror import TFMirrorStep
-    G = copy.deepcopy(model.generator).cpu()
-    D = copy.deepcopy(model.discriminator).cpu()
-    for m in sn_modules(D):
-        m.w_eff = None
-    st = TFMirrorStep(G, D, sn_modules(D), lr=model.config.learning_rate, sc=model.sc)
-    st.us = [e.u.detach().cpu().view(1, -1).clone() for e in model.sn_D.entries]
+    st = TFMirrorStep(model.config, model.generator, model.discriminator, sc=model.sc)
+    by_weight = {id(st.prod[k]): k.rsplit('/', 1)[0] for k in st.prod}
+    for e in model.sn_D.entries:
+        st.us[by_weight[id(e.module.weight)]] = e.u.detach().cpu().view(1, -1).clone()
     return st
 
 
-@pytest.mark.parametrize('arch,size,cl', [('sngan', 32, False), ('snresnet', 64, False),
-                                           ('snresnet', 64, True)])
-def test_critic_step_matches_tf_mirror(dev, arch, size, cl):
+@pytest.mark.parametrize('arch,size,dim,batch,cl', [
+    ('sngan', 32, 64, 8, False), ('snresnet', 64, 16, 8, False), ('snresnet', 64, 16, 8, True),
+    ('g-resnet5', 64, 16, 8, False),
+    ('snresnet', 64, 64, 64, False)])         # imagenet_smmd.yml's widths and batch, once
+def test_critic_step_matches_tf_mirror(dev, arch, size, dim, batch, cl):
     from gan.core.smmd import SMMD
     torch.manual_seed(0)
-    cfg = _cfg(architecture=arch, output_size=size, df_dim=16 if arch == 'snresnet' else 64,
-               gf_dim=16 if arch == 'snresnet' else 64)
+    cfg = _cfg(architecture=arch, output_size=size, df_dim=dim, gf_dim=dim, batch_size=batch,
+               batch_norm=arch != 'g-resnet5')         # celebA_smmd.yml: batch_norm False
     model = SMMD(cfg, device=dev, channels_last=cl)
     mirror = _mirror_from(model)
-    if cl:      # the mirror runs the default layout
-        mirror.G.to(memory_format=torch.contiguous_format)
-        mirror.D.to(memory_format=torch.contiguous_format)
     g = torch.Generator().manual_seed(1)
-    images = torch.rand(8, 3, size, size, generator=g)
-    z = torch.empty(8, 128).uniform_(-1, 1, generator=g)
+    images = torch.rand(batch, 3, size, size, generator=g)
+    z = torch.empty(batch, 128).uniform_(-1, 1, generator=g)
     ref_loss, ref_grads = mirror.grads(images, z)
 
     model.sample_z = lambda n: z.to(dev)
@@ -70,19 +67,24 @@ def test_critic_step_matches_tf_mirror(dev, arch, size, cl):
     _, d_loss, aux = model.d_step(images.to(dev))
     assert float(d_loss.detach()) == pytest.approx(float(ref_loss), rel=1e-3, abs=1e-6)
     flat = captured['g']
-    gmax = max(float(rg.abs().max()) for rg in ref_grads)
-    for i, (p, rg) in enumerate(zip(model.d_vars, ref_grads)):
-        o, n = model.d_optim.offsets[i], p.numel()
-        got = torch.as_strided(flat, p.shape, p.stride(), o).contiguous().view_as(rg)
+    gmax = max(float(rg.abs().max()) for rg in ref_grads.values())
+    index = {id(p): i for i, p in enumerate(model.d_vars)}
+    assert sorted(index) == sorted(id(mirror.prod[n]) for n in ref_grads)
+    for name, rg in ref_grads.items():
+        p = mirror.prod[name]
+        i = index[id(p)]
+        got = torch.as_strided(flat, p.shape, p.stride(), model.d_optim.offsets[i]).contiguous()
         got = got.numpy().astype(np.float64)
-        ref = rg.numpy().astype(np.float64)
+        ref = mirror.to_product(name, rg).numpy().astype(np.float64)
         # exact zeros (e.g. the output bias: RBF-MMD is translation invariant) are
         # rounding noise in both: absolute floor 1e-5 of the largest gradient
         tol = max(2e-3 * np.abs(ref).max(), 1e-5 * gmax) + 2e-3 * np.abs(ref)
-        assert (np.abs(got - ref) <= tol + 1e-12).all(), (p.shape, np.abs(got - ref).max(),
+        assert (np.abs(got - ref) <= tol + 1e-12).all(), (name, np.abs(got - ref).max(),
                                                            np.abs(ref).max())
     # u advanced exactly as the reference's u.assign(u') (sn.py:39-46)
-    for e, u in zip(model.sn_D.entries, mirror.us):
+    by_weight = {id(mirror.prod[k]): k.rsplit('/', 1)[0] for k in mirror.prod}
+    for e in model.sn_D.entries:
+        u = mirror.us[by_weight[id(e.module.weight)]]
         np.testing.assert_allclose(e.u.cpu().numpy(), u.numpy()[0], rtol=1e-4, atol=1e-6)
 
 
@@ -250,3 +252,33 @@ def test_main_cli_trains_on_cifar_files_and_checkpoints(dev, tmp_path):
     assert (ck / 'run' / 'MMDGAN.model-0.pt').exists()
     M.main(argv)                                       # resumes at step 1 from the save
     assert open(ck / 'run' / 'checkpoint').read().strip() == 'MMDGAN.model-0'
+
+
+def test_main_cli_scorer_drives_lr_schedule(dev, tmp_path, monkeypatch):
+    """-compute_scores with -featurizer random: the scorer runs after
+    generator updates every MMD_sdlr_freq steps (model.py:544-545), featurizes
+    the training images once (codes cached in -data_dir, scorer.py:37-64) and
+    keeps KID / 3-sample state; with the reference's default 'inception'
+    featurizer (unavailable offline) it warns and stays off."""
+    import warnings
+    from gan import main as M
+    monkeypatch.setattr(M, 'SCORE_SIZE', 2048)
+    rng = np.random.default_rng(4)
+    for name in ['data_batch_%d' % b for b in range(1, 6)] + ['test_batch']:
+        x = rng.integers(0, 256, (20, 3073), dtype=np.uint8)
+        x[:, 0] %= 10
+        x.tofile(str(tmp_path / (name + '.bin')))
+    base = ['-dataset', 'cifar10', '-data_dir', str(tmp_path), '-architecture', 'sngan',
+            '-model', 'smmd', '-kernel', 'rbf', '-batch_size', '64', '-with_sn', 'true',
+            '-with_learnable_sn_scale', 'true', '-with_scaling', 'true', '-batch_norm', 'true',
+            '-max_iteration', '1', '-checkpoint_dir', str(tmp_path / 'ck'), '-name', 'run',
+            '-MMD_sdlr_freq', '1', '-MMD_sdlr_past_sample', '1', '-MMD_sdlr_num_test', '1']
+    gan = M.main(base + ['-featurizer', 'random'])
+    assert (tmp_path / 'cifar10-codes-random.npy').exists()
+    codes = np.load(tmp_path / 'cifar10-codes-random.npy')
+    assert codes.shape == (2048, 2048) and np.isfinite(codes).all()
+    assert gan.step >= 1
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter('always')
+        M.main(base + ['-name', 'run2'])
+    assert any('Inception featurizer' in str(x.message) for x in w)

@@ -101,17 +101,27 @@ def test_counters_match_oracle():
 
 
 def test_cpu_mirror_step_runs():
+    import argparse
     from gan.core.architecture import get_networks
-    from gan.core.snops import sn_modules
-    from oracle.tf_mirror import TFMirrorStep, rbf_mmd2_tf
+    from gan.main import default_flags
+    from oracle.tf_mirror import TFMirrorStep, TFMirrorTrainer, rbf_mmd2_tf
     from oracle import smmd_oracle as O
     torch.manual_seed(0)
+    cfg = argparse.Namespace(**default_flags())
+    cfg.__dict__.update(architecture='sngan', gf_dim=16, df_dim=16, output_size=32,
+                        batch_norm=True, with_sn=True, with_learnable_sn_scale=True, dof_dim=1)
     G_cls, D_cls = get_networks('sngan')
     G = G_cls(16, 3, 32, True)
     D = D_cls(16, 1, False, with_sn=True, with_learnable_sn_scale=True, input_size=32)
-    st = TFMirrorStep(G, D, sn_modules(D))
+    st = TFMirrorStep(cfg, G, D)
+    before = {n: p.clone() for n, p in zip(st.d_names, st.params)}
     loss = st.step(torch.rand(4, 3, 32, 32))
     assert np.isfinite(loss)
+    assert all(not torch.equal(before[n], p) for n, p in zip(st.d_names, st.params)
+               if not n.endswith('d_l4/bias'))
+    tr = TFMirrorTrainer(cfg, G, D)
+    kinds = ''.join(tr.train_step(torch.rand(4, 3, 32, 32)) for _ in range(12))
+    assert kinds == 'D' * 10 + 'GD'          # start_dsteps 10 while step < 20
     X, Y = torch.randn(9, 1, dtype=torch.float64), torch.randn(7, 1, dtype=torch.float64)
     assert float(rbf_mmd2_tf(X, Y)) == pytest.approx(O.mmd2(O.kernel_spec('rbf'), X.numpy(),
                                                             Y.numpy()), rel=1e-10)
