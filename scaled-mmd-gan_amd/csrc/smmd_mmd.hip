@@ -364,35 +364,80 @@ __global__ __launch_bounds__(256) void witness_fwd_kernel(WitArgs a) {
     }
 }
 
-// Second-order term for the radial kernels (RBF / RQ incl. add_dot):
-//   L = sum_i <g_i, dH_i>,  dH_i = sum_j c_j [al h_i + be_ij (h_i - z_j)],
-//   be_ij = 2 f'(R_ij) [raw >= 0] - add_dot,  al = add_dot.
-//   dL/dh_i = sum_j c_j (al + be_ij) g_i + e_ij (h_i - z_j)
-//   dL/dz_j = sum_i -c_j be_ij g_i - e_ij (h_i - z_j)
-//   e_ij = 4 c_j f''(R_ij) [raw >= 0] <g_i, h_i - z_j>
-template <int KIND>
-__device__ __forceinline__ void radial_d2(const KParams &p, float raw, float &be, float &f2) {
-    const float R = fmaxf(raw, 0.f);
-    float d1 = 0.f, d2 = 0.f;
-    if (KIND == SMMD_KIND_RBF) {
-        for (int t = 0; t < p.n_terms; ++t) {
-            const float e = p.wt[t] * expf(p.c1[t] * R);
-            d1 += p.c1[t] * e;
-            d2 += p.c1[t] * p.c1[t] * e;
-        }
+// Second order of the witness gradient, for every kernel of the family.
+// With h = tanh(x) for the tanh kernels (else h = x), the forward gives
+//   dX_i = T_i * G_i,  G_i = sum_j c_j [al_i h_i + be_ij (h_i - z_j)],
+//   T_i = 1 - h_i^2 (tanh) or 1,
+// where al depends on |h_i|^2 only (grad_h al = a1 h_i) and be on the pair
+// distance raw_ij only (grad_h be = b1 (h_i - z_j) = -grad_z be).  For
+// L = sum_i <g_i, dX_i> and gt_i = g_i * T_i:
+//   dL/dh_i = (sum_j c_j (al + be_ij)) gt_i + a1 <gt_i, h_i> (sum_j c_j) h_i
+//             + sum_j c_j b1_ij <gt_i, d_ij> d_ij  [- 2 h_i g_i G_i  (tanh)]
+//   dL/dz_j = sum_i -c_j be_ij gt_i - c_j b1_ij <gt_i, d_ij> d_ij,
+// d_ij = h_i - z_j, each then times (1 - h^2) / (1 - z^2) for tanh inputs.
+//   rbf / rq:  be = 2 f'(R) [raw >= 0] - add_dot, b1 = 4 f''(R) [raw >= 0],
+//              al = add_dot, a1 = 0                      (mmd.py:55-188)
+//   distance:  be = -2 s'(raw), b1 = -4 s''(raw), al = 2 s'(|h|^2),
+//              a1 = 4 s''(|h|^2), s(x) = sqrt(max(x + 1e-5, 0))  (mmd.py:12-37)
+//   dot:       al = 1, be = -1, a1 = b1 = 0              (mmd.py:44-52)
+__device__ __forceinline__ void mysqrt_d12(float x, float &d1, float &d2) {
+    const float xe = x + 1.0e-5f;
+    if (xe >= 0.f) {            // tf.maximum: ties pass the gradient
+        const float r = 1.f / sqrtf(xe);
+        d1 = 0.5f * r;
+        d2 = -0.25f * r * r * r;
     } else {
-        for (int t = 0; t < p.n_terms; ++t) {
-            const float q = 1.f + R / p.c1[t];
-            const float e = p.wt[t] * expf(p.c2[t] * logf(q));
-            const float dq = 1.f / p.c1[t];
-            const float g1 = e * p.c2[t] / q * dq;                     // de/dR
-            d1 += g1;
-            d2 += g1 * (p.c2[t] - 1.f) / q * dq;                       // d2e/dR2
-        }
+        d1 = 0.f;
+        d2 = 0.f;
     }
-    const bool pass = raw >= 0.f;
-    be = (pass ? 2.f * d1 : 0.f) - (KIND == SMMD_KIND_RQ ? p.add_dot : 0.f);
-    f2 = pass ? d2 : 0.f;
+}
+
+template <int KIND>
+__device__ __forceinline__ void pair_d2(const KParams &p, float raw, float &be, float &b1) {
+    if (KIND == SMMD_KIND_DISTANCE) {
+        float d1, d2;
+        mysqrt_d12(raw, d1, d2);
+        be = -2.f * d1;
+        b1 = -4.f * d2;
+    } else if (KIND == SMMD_KIND_DOT) {
+        be = -1.f;
+        b1 = 0.f;
+    } else {
+        const float R = fmaxf(raw, 0.f);
+        float d1 = 0.f, d2 = 0.f;
+        if (KIND == SMMD_KIND_RBF) {
+            for (int t = 0; t < p.n_terms; ++t) {
+                const float e = p.wt[t] * expf(p.c1[t] * R);
+                d1 += p.c1[t] * e;
+                d2 += p.c1[t] * p.c1[t] * e;
+            }
+        } else {
+            for (int t = 0; t < p.n_terms; ++t) {
+                const float q = 1.f + R / p.c1[t];
+                const float e = p.wt[t] * expf(p.c2[t] * logf(q));
+                const float dq = 1.f / p.c1[t];
+                const float g1 = e * p.c2[t] / q * dq;                     // de/dR
+                d1 += g1;
+                d2 += g1 * (p.c2[t] - 1.f) / q * dq;                       // d2e/dR2
+            }
+        }
+        const bool pass = raw >= 0.f;
+        be = (pass ? 2.f * d1 : 0.f) - (KIND == SMMD_KIND_RQ ? p.add_dot : 0.f);
+        b1 = pass ? 4.f * d2 : 0.f;
+    }
+}
+
+template <int KIND>
+__device__ __forceinline__ void row_d2(const KParams &p, float sqi, float &al, float &a1) {
+    if (KIND == SMMD_KIND_DISTANCE) {
+        float d1, d2;
+        mysqrt_d12(sqi, d1, d2);
+        al = 2.f * d1;
+        a1 = 4.f * d2;
+    } else {
+        al = KIND == SMMD_KIND_DOT ? 1.f : (KIND == SMMD_KIND_RQ ? p.add_dot : 0.f);
+        a1 = 0.f;
+    }
 }
 
 struct WitBwdArgs {
@@ -401,6 +446,7 @@ struct WitBwdArgs {
     const float *F;
     const float *gdH;
     int b, nr, nf, d;
+    int tanh_in;
     float *gH;
     float *gR;
     float *gF;
@@ -412,15 +458,21 @@ template <int DT, int KIND>
 __global__ __launch_bounds__(256) void witness_bwd_h_kernel(WitBwdArgs a) {
     const int lane = threadIdx.x & 63;
     const int nwaves = gridDim.x * 4;
-    const float al = (KIND == SMMD_KIND_RQ) ? a.kp.add_dot : 0.f;
+    const bool tanh_in = a.tanh_in != 0;
     for (int i = blockIdx.x * 4 + (threadIdx.x >> 6); i < a.b; i += nwaves) {
-        float hi[DT], gi[DT], acc[DT];
-        load_feat<DT>(a.H + (size_t)i * a.d, a.d, false, hi);
+        float hi[DT], gi[DT], gt[DT], acc[DT], gb[DT];
+        load_feat<DT>(a.H + (size_t)i * a.d, a.d, tanh_in, hi);
         load_feat<DT>(a.gdH + (size_t)i * a.d, a.d, false, gi);
-        const float sqi = dotk<DT>(hi, hi);
 #pragma unroll
-        for (int k = 0; k < DT; ++k) acc[k] = 0.f;
-        float gcoef = 0.f;
+        for (int k = 0; k < DT; ++k) {
+            gt[k] = tanh_in ? gi[k] * (1.f - hi[k] * hi[k]) : gi[k];
+            acc[k] = 0.f;
+            gb[k] = 0.f;
+        }
+        const float sqi = dotk<DT>(hi, hi);
+        float al, a1;
+        row_d2<KIND>(a.kp, sqi, al, a1);
+        float cbe = 0.f, csum = 0.f;
 #pragma unroll
         for (int set = 0; set < 2; ++set) {
             const float *S = set == 0 ? a.R : a.F;
@@ -428,25 +480,43 @@ __global__ __launch_bounds__(256) void witness_bwd_h_kernel(WitBwdArgs a) {
             const float c = (set == 0 ? 1.f : -1.f) / (float)ns;
             for (int j = lane; j < ns; j += 64) {
                 float zc[DT], df[DT];
-                load_feat<DT>(S + (size_t)j * a.d, a.d, false, zc);
+                load_feat<DT>(S + (size_t)j * a.d, a.d, tanh_in, zc);
                 const float raw = (-2.f * dotk<DT>(hi, zc) + sqi) + dotk<DT>(zc, zc);
-                float be, f2;
-                radial_d2<KIND>(a.kp, raw, be, f2);
+                float be, b1;
+                pair_d2<KIND>(a.kp, raw, be, b1);
 #pragma unroll
                 for (int k = 0; k < DT; ++k) df[k] = hi[k] - zc[k];
-                const float e = 4.f * c * f2 * dotk<DT>(gi, df);
-                gcoef = fmaf(c, al + be, gcoef);
+                const float e = c * b1 * dotk<DT>(gt, df);
+                csum += c;
+                cbe = fmaf(c, be, cbe);
 #pragma unroll
-                for (int k = 0; k < DT; ++k) acc[k] = fmaf(e, df[k], acc[k]);
+                for (int k = 0; k < DT; ++k) {
+                    acc[k] = fmaf(e, df[k], acc[k]);
+                    if (tanh_in) gb[k] = fmaf(c * be, df[k], gb[k]);
+                }
             }
         }
-        gcoef = wave_sum(gcoef);
+        cbe = wave_sum(cbe);
+        csum = wave_sum(csum);
 #pragma unroll
-        for (int k = 0; k < DT; ++k) acc[k] = wave_sum(acc[k]);
+        for (int k = 0; k < DT; ++k) {
+            acc[k] = wave_sum(acc[k]);
+            if (tanh_in) gb[k] = wave_sum(gb[k]);
+        }
         if (lane == 0) {
+            const float gcoef = fmaf(al, csum, cbe);
+            const float hcoef = a1 * csum * dotk<DT>(gt, hi);
 #pragma unroll
             for (int k = 0; k < DT; ++k)
-                if (k < a.d) a.gH[(size_t)i * a.d + k] = fmaf(gcoef, gi[k], acc[k]);
+                if (k < a.d) {
+                    float v = fmaf(gcoef, gt[k], fmaf(hcoef, hi[k], acc[k]));
+                    if (tanh_in) {
+                        const float G = fmaf(al * csum, hi[k], gb[k]);
+                        v = fmaf(-2.f * hi[k] * gi[k], G, v);
+                        v *= 1.f - hi[k] * hi[k];
+                    }
+                    a.gH[(size_t)i * a.d + k] = v;
+                }
         }
     }
 }
@@ -457,28 +527,33 @@ __global__ __launch_bounds__(256) void witness_bwd_z_kernel(WitBwdArgs a) {
     const int lane = threadIdx.x & 63;
     const int nwaves = gridDim.x * 4;
     const int nz = a.nr + a.nf;
+    const bool tanh_in = a.tanh_in != 0;
     for (int r = blockIdx.x * 4 + (threadIdx.x >> 6); r < nz; r += nwaves) {
         const bool isr = r < a.nr;
         const int j = isr ? r : r - a.nr;
         const float c = (isr ? 1.f : -1.f) / (float)(isr ? a.nr : a.nf);
         float zj[DT], acc[DT];
-        load_feat<DT>((isr ? a.R : a.F) + (size_t)j * a.d, a.d, false, zj);
+        load_feat<DT>((isr ? a.R : a.F) + (size_t)j * a.d, a.d, tanh_in, zj);
         const float sqj = dotk<DT>(zj, zj);
 #pragma unroll
         for (int k = 0; k < DT; ++k) acc[k] = 0.f;
         for (int i = lane; i < a.b; i += 64) {
-            float hi[DT], gi[DT], df[DT];
-            load_feat<DT>(a.H + (size_t)i * a.d, a.d, false, hi);
-            load_feat<DT>(a.gdH + (size_t)i * a.d, a.d, false, gi);
+            float hi[DT], gt[DT], df[DT];
+            load_feat<DT>(a.H + (size_t)i * a.d, a.d, tanh_in, hi);
+            load_feat<DT>(a.gdH + (size_t)i * a.d, a.d, false, gt);
+            if (tanh_in) {
+#pragma unroll
+                for (int k = 0; k < DT; ++k) gt[k] *= 1.f - hi[k] * hi[k];
+            }
             // raw in the forward's order: row = h_i, column = z_j
             const float raw = (-2.f * dotk<DT>(hi, zj) + dotk<DT>(hi, hi)) + sqj;
-            float be, f2;
-            radial_d2<KIND>(a.kp, raw, be, f2);
+            float be, b1;
+            pair_d2<KIND>(a.kp, raw, be, b1);
 #pragma unroll
             for (int k = 0; k < DT; ++k) df[k] = hi[k] - zj[k];
-            const float e = 4.f * c * f2 * dotk<DT>(gi, df);
+            const float e = c * b1 * dotk<DT>(gt, df);
 #pragma unroll
-            for (int k = 0; k < DT; ++k) acc[k] = acc[k] - c * be * gi[k] - e * df[k];
+            for (int k = 0; k < DT; ++k) acc[k] = acc[k] - c * be * gt[k] - e * df[k];
         }
 #pragma unroll
         for (int k = 0; k < DT; ++k) acc[k] = wave_sum(acc[k]);
@@ -486,7 +561,8 @@ __global__ __launch_bounds__(256) void witness_bwd_z_kernel(WitBwdArgs a) {
             float *out = isr ? a.gR : a.gF;
 #pragma unroll
             for (int k = 0; k < DT; ++k)
-                if (k < a.d) out[(size_t)j * a.d + k] = acc[k];
+                if (k < a.d) out[(size_t)j * a.d + k] = tanh_in ? acc[k] * (1.f - zj[k] * zj[k])
+                                                                 : acc[k];
         }
     }
 }
@@ -868,31 +944,33 @@ smmd_status smmd_witness_bwd(const smmd_kernel_desc *desc, const float *H, int b
     if (b < 1 || nr < 1 || nf < 1 || d < 1) return SMMD_EINVAL;
     KParams kp;
     if (!make_kparams(desc, kp)) return SMMD_EINVAL;
-    // second derivatives implemented for the radial families on raw inputs
-    if (desc->tanh_inputs) return SMMD_EUNSUPPORTED;
-    if (desc->kind != SMMD_KIND_RBF && desc->kind != SMMD_KIND_RQ) return SMMD_EUNSUPPORTED;
     const int dt = pick_dt(d);
     if (dt == 0) return SMMD_EUNSUPPORTED;
     WitBwdArgs a;
     memset(&a, 0, sizeof(a));
     a.H = H; a.R = R; a.F = F; a.gdH = gdH; a.b = b; a.nr = nr; a.nf = nf; a.d = d;
+    a.tanh_in = desc->tanh_inputs ? 1 : 0;
     a.gH = gH; a.gR = gR; a.gF = gF; a.kp = kp;
     hipStream_t s = (hipStream_t)stream;
     const int gh = wave_grid(b), gz = wave_grid(nr + nf);
+#define SMMD_WB_K(DT_, K_)                                                                     \
+    hipLaunchKernelGGL((witness_bwd_h_kernel<DT_, K_>), dim3(gh), dim3(256), 0, s, a);         \
+    hipLaunchKernelGGL((witness_bwd_z_kernel<DT_, K_>), dim3(gz), dim3(256), 0, s, a);
 #define SMMD_WB(DT_)                                                                           \
     case DT_:                                                                                  \
-        if (desc->kind == SMMD_KIND_RBF) {                                                     \
-            hipLaunchKernelGGL((witness_bwd_h_kernel<DT_, SMMD_KIND_RBF>), dim3(gh), dim3(256), 0, s, a); \
-            hipLaunchKernelGGL((witness_bwd_z_kernel<DT_, SMMD_KIND_RBF>), dim3(gz), dim3(256), 0, s, a); \
-        } else {                                                                               \
-            hipLaunchKernelGGL((witness_bwd_h_kernel<DT_, SMMD_KIND_RQ>), dim3(gh), dim3(256), 0, s, a); \
-            hipLaunchKernelGGL((witness_bwd_z_kernel<DT_, SMMD_KIND_RQ>), dim3(gz), dim3(256), 0, s, a); \
+        switch (desc->kind) {                                                                  \
+            case SMMD_KIND_RBF: SMMD_WB_K(DT_, SMMD_KIND_RBF) break;                           \
+            case SMMD_KIND_RQ: SMMD_WB_K(DT_, SMMD_KIND_RQ) break;                             \
+            case SMMD_KIND_DISTANCE: SMMD_WB_K(DT_, SMMD_KIND_DISTANCE) break;                 \
+            case SMMD_KIND_DOT: SMMD_WB_K(DT_, SMMD_KIND_DOT) break;                           \
+            default: return SMMD_EINVAL;                                                        \
         }                                                                                      \
         break;
     switch (dt) {
         SMMD_WB(1) SMMD_WB(2) SMMD_WB(4) SMMD_WB(8) SMMD_WB(16) SMMD_WB(32)
         default: return SMMD_EUNSUPPORTED;
     }
+#undef SMMD_WB_K
 #undef SMMD_WB
     return last_launch_status();
 }

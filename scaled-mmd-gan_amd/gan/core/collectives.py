@@ -39,3 +39,148 @@ def all_reduce_(t, group):
         return t
     dist.all_reduce(t, group=group)
     return t
+
+
+def all_reduce_async(t, group):
+    """SUM in place, returning the pending work (None when it completed
+    synchronously: the host-staged gloo path)."""
+    if _host_staged(t, group):
+        all_reduce_(t, group)
+        return None
+    return dist.all_reduce(t, group=group, async_op=True)
+
+
+# ---------------------------------------------------------------------------
+# one latency-bound collective per loss evaluation (the all-gather mode)
+# ---------------------------------------------------------------------------
+class StepExchange:
+    """The small messages of one loss evaluation in the all-gather ('global')
+    mode packed into ONE ``all_gather_into_tensor``: each rank's critic
+    feature rows [X; Y] (d floats per row) and, when the scaling regulariser
+    is on, its partial statistics (J and nD summed over its rows, already
+    divided by the global batch).  Afterwards every rank holds the global
+    batch -- mmd2 then runs over all rows, needing no all-reduce of partial
+    sums -- and the global J / nD as the fixed rank-order sum of the gathered
+    partials (the same bits on every rank).  Without an exchange (a custom
+    set_loss, the gaussian-noise variant) the ops fall back to their own
+    all-reduces."""
+
+    def __init__(self, group):
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.jac = None           # the Jacobian columns computed ahead of set_loss
+        self.feat = None
+        self.stats = None         # local partials [2] (J, nD), set ahead of gather
+        self.stats_total = None   # global [2] after gather
+        self.used = False
+
+    def gather(self, X, Y):
+        """[X; Y; stats] of every rank -> (X_all, Y_all) in rank order."""
+        if self.used:
+            raise RuntimeError('StepExchange.gather runs once per loss evaluation')
+        self.used = True
+        ml, nl, d = X.shape[0], Y.shape[0], X.shape[1]
+        parts = [X.reshape(-1), Y.reshape(-1)]
+        if self.stats is not None:
+            parts.append(self.stats.reshape(-1).to(X.dtype))
+        packed = torch.cat(parts).view(1, -1)
+        allp = gather_rows(packed, self.group).view(self.world, -1)
+        Xa = allp[:, :ml * d].reshape(self.world * ml, d)
+        Ya = allp[:, ml * d:(ml + nl) * d].reshape(self.world * nl, d)
+        if self.stats is not None:
+            tot = allp[0, (ml + nl) * d:].clone()
+            for r in range(1, self.world):      # fixed rank order
+                tot += allp[r, (ml + nl) * d:]
+            self.stats_total = tot
+        return Xa, Ya
+
+
+# ---------------------------------------------------------------------------
+# bucketed gradient all-reduce, issued from autograd hooks during backward
+# ---------------------------------------------------------------------------
+def _bucket_bytes():
+    import os
+    return int(float(os.environ.get('SMMD_BUCKET_MB', '16')) * (1 << 20))
+
+
+class GradBuckets:
+    """All-reduce (SUM) of a FlatAdam's flat gradient in contiguous buckets of
+    about ``bucket_bytes``, formed from the last tensor backwards (the order
+    the backward produces them).  A bucket's all-reduce is issued, async, from
+    the post-accumulate-grad hook of its last tensor to receive a gradient,
+    so it overlaps the rest of the backward; ``finish`` issues the buckets no
+    hook completed (tensors without a gradient this step contribute their
+    zeros) and waits for all of them.  ``clip_norm`` > 0 clips every tensor of
+    a bucket before its all-reduce (the reference's per-tower clip_by_norm,
+    model.py:449-455)."""
+
+    def __init__(self, opt, group, bucket_bytes=None, clip_norm=0.0):
+        self.opt, self.group = opt, group
+        self.clip_norm = float(clip_norm)
+        cap = _bucket_bytes() if bucket_bytes is None else int(bucket_bytes)
+        offs = [int(o) for o in opt.offsets]
+        n = len(opt.params)
+        self.buckets = []
+        hi = n
+        while hi > 0:
+            lo = hi - 1
+            while lo > 0 and (offs[hi] - offs[lo - 1]) * 4 <= cap:
+                lo -= 1
+            self.buckets.append((lo, hi))
+            hi = lo
+        self.bucket_of = [0] * n
+        for b, (lo, hi) in enumerate(self.buckets):
+            for i in range(lo, hi):
+                self.bucket_of[i] = b
+        self._offs = offs
+        self.armed = False
+        self.left, self.works, self.launched = [], [], []
+        self._hooks = [p.register_post_accumulate_grad_hook(self._hook(i))
+                       for i, p in enumerate(opt.params)]
+        self.launch_log = []      # bucket ids in issue order of the last step (tests)
+
+    def arm(self):
+        """Call before the backward whose gradients this step exchanges."""
+        self.armed = True
+        self.left = [hi - lo for lo, hi in self.buckets]
+        self.launched = [False] * len(self.buckets)
+        self.works = []
+        self.launch_log = []
+
+    def _hook(self, i):
+        def fn(_p):
+            if not self.armed:
+                return
+            b = self.bucket_of[i]
+            self.left[b] -= 1
+            if self.left[b] == 0 and not self.launched[b]:
+                self._launch(b)
+        return fn
+
+    def _launch(self, b):
+        lo, hi = self.buckets[b]
+        self.launched[b] = True
+        self.launch_log.append(b)
+        if self.clip_norm > 0:
+            self.opt.clip_range_(lo, hi, self.clip_norm)
+        w = all_reduce_async(self.opt.flat_grad[self._offs[lo]:self._offs[hi]], self.group)
+        if w is not None:
+            self.works.append(w)
+
+    def finish(self):
+        """Issue what the hooks did not, then wait for every bucket."""
+        if not self.armed:          # no backward was armed: exchange everything now
+            self.arm()
+        for b in range(len(self.buckets)):
+            if not self.launched[b]:
+                self._launch(b)
+        for w in self.works:
+            w.wait()
+        self.works = []
+        self.armed = False
+
+    def remove(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []

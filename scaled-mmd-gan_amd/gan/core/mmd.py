@@ -18,6 +18,7 @@ a ROCm device and the library must be built (see ``_lib``).
 """
 from __future__ import annotations
 
+import os
 import threading
 from dataclasses import dataclass, field
 
@@ -117,9 +118,16 @@ def _features(t):
 # ---------------------------------------------------------------------------
 # fused MMD^2 (forward + unit gradient in one launch)
 # ---------------------------------------------------------------------------
+# In the all-gather mode a global batch of at most this many rows per side is
+# evaluated whole on every rank (one more launch-bound sweep, no all-reduce of
+# partial sums); larger ones are row-sharded, each rank its own rows against
+# all columns, with the 8 partial sums all-reduced.
+FULL_ROWS = int(os.environ.get('SMMD_GLOBAL_FULL_ROWS', '4096'))
+
+
 class _MMD2Fused(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, X, Y, spec, biased, group):
+    def forward(ctx, X, Y, spec, biased, group, exchange):
         X = _features(X)
         Y = _features(Y)
         if X.shape[1] != Y.shape[1]:
@@ -128,24 +136,31 @@ class _MMD2Fused(torch.autograd.Function):
         L = _lib.lib()
         need_grad = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
         d = X.shape[1]
+        ml, nl = X.shape[0], Y.shape[0]
+        shard = False
         if group is not None and dist.get_world_size(group) > 1:
             world, rank = dist.get_world_size(group), dist.get_rank(group)
-            ml, nl = X.shape[0], Y.shape[0]
-            # ONE all-gather of the packed local rows [X; Y] (latency-bound:
-            # 2 x 256 B per rank at batch 64), then each side's rows in rank order
-            Za = gather_rows(torch.cat([X, Y], 0), group).view(world, ml + nl, d)
-            Xa = Za[:, :ml].reshape(world * ml, d)
-            Ya = Za[:, ml:].reshape(world * nl, d)
-            rows = (rank * ml, (rank + 1) * ml, rank * nl, (rank + 1) * nl)
+            if exchange is not None and exchange.group is group and not exchange.used:
+                Xa, Ya = exchange.gather(X, Y)     # the step's one packed all-gather
+            else:
+                # ONE all-gather of the packed local rows [X; Y] (latency-bound:
+                # 2 x 256 B per rank at batch 64), then each side's rows in rank order
+                Za = gather_rows(torch.cat([X, Y], 0), group).view(world, ml + nl, d)
+                Xa = Za[:, :ml].reshape(world * ml, d)
+                Ya = Za[:, ml:].reshape(world * nl, d)
+            shard = max(Xa.shape[0], Ya.shape[0]) > FULL_ROWS
+            own = (rank * ml, (rank + 1) * ml, rank * nl, (rank + 1) * nl)
         else:
             group = None
             Xa, Ya = X, Y
-            rows = (0, X.shape[0], 0, Y.shape[0])
         m, n = Xa.shape[0], Ya.shape[0]
+        rows = own if shard else (0, m, 0, n)
         sums = torch.empty(8, device=dev, dtype=torch.float32)
         out = torch.empty(1, device=dev, dtype=torch.float32)
-        gx = torch.empty_like(X) if need_grad else None
-        gy = torch.empty_like(Y) if need_grad else None
+        gx = gy = None
+        if need_grad:
+            gx = torch.empty((rows[1] - rows[0], d), device=dev, dtype=torch.float32)
+            gy = torch.empty((rows[3] - rows[2], d), device=dev, dtype=torch.float32)
         nbytes = L.smmd_mmd2_workspace_bytes(m, n, d)
         ws = _lib.workspace('mmd2', nbytes, dev)
         desc = spec.desc()
@@ -155,11 +170,15 @@ class _MMD2Fused(torch.autograd.Function):
         with _lib.timed('smmd_mmd2_fwd'):
             st = L.smmd_mmd2_fwd(*args)
         _lib.check(st, 'smmd_mmd2_fwd')
-        if group is not None:
+        if group is not None and shard:
             all_reduce_(sums, group)
             _lib.check(L.smmd_mmd2_combine(desc, _lib.ptr(sums), m, n, 1 if biased else 0,
                                            _lib.ptr(out), _lib.stream_handle(dev)),
                        'smmd_mmd2_combine')
+        elif group is not None and need_grad:
+            # the whole batch was evaluated: this rank's rows of the gradient
+            gx = gx[own[0]:own[1]]
+            gy = gy[own[2]:own[3]]
         ctx.save_for_backward(gx, gy)
         ctx.mark_non_differentiable(sums)
         return out.view(()), sums
@@ -171,18 +190,22 @@ class _MMD2Fused(torch.autograd.Function):
         if gx is not None:
             dX = gx * g_mmd2
             dY = gy * g_mmd2
-        return dX, dY, None, None, None
+        return dX, dY, None, None, None, None
 
 
-def mmd2_fused(X, Y, kernel='rbf', biased=False, process_group=None, return_sums=False, **kw):
+def mmd2_fused(X, Y, kernel='rbf', biased=False, process_group=None, return_sums=False,
+               exchange=None, **kw):
     """mmd.mmd2(mmd._<kernel>_kernel(X, Y), biased) as one HIP launch.
 
     ``process_group`` (a torch.distributed group with >1 ranks) selects the
     all-gather mode: every rank contributes its local rows of X and Y, sees
     the full (world * batch) pairwise kernel, and gets the same estimator
-    (one all_gather per input + one all_reduce of 8 floats)."""
+    and the gradient of its own rows.  Messages: one all-gather of the packed
+    rows (carried by ``exchange``, a collectives.StepExchange, when given),
+    plus one all-reduce of 8 floats only when the global batch exceeds
+    FULL_ROWS per side and the sweep is row-sharded."""
     spec = _as_spec(kernel, **kw)
-    val, sums = _MMD2Fused.apply(X, Y, spec, bool(biased), process_group)
+    val, sums = _MMD2Fused.apply(X, Y, spec, bool(biased), process_group, exchange)
     return (val, sums) if return_sums else val
 
 
@@ -334,21 +357,30 @@ _scope = threading.local()
 
 
 class loss_group:
-    def __init__(self, group):
+    """``with loss_group(group, exchange):`` -- mmd2 inside spans ``group``'s
+    global batch; ``exchange`` (collectives.StepExchange) carries its
+    all-gather together with the step's other small messages."""
+
+    def __init__(self, group, exchange=None):
         self.group = group if (group is not None and dist.get_world_size(group) > 1) else None
+        self.exchange = exchange if self.group is not None else None
 
     def __enter__(self):
-        self.prev = getattr(_scope, 'group', None)
-        _scope.group = self.group
+        self.prev = (getattr(_scope, 'group', None), getattr(_scope, 'exchange', None))
+        _scope.group, _scope.exchange = self.group, self.exchange
         return self
 
     def __exit__(self, *a):
-        _scope.group = self.prev
+        _scope.group, _scope.exchange = self.prev
         return False
 
 
 def current_loss_group():
     return getattr(_scope, 'group', None)
+
+
+def current_exchange():
+    return getattr(_scope, 'exchange', None)
 
 
 # ---------------------------------------------------------------------------
@@ -358,7 +390,8 @@ def mmd2(K, biased=False):
     """gan/core/mmd.py:194-196.  A KernelMatrices argument takes the fused
     path; an explicit 4-tuple of matrices is reduced as given."""
     if isinstance(K, KernelMatrices):
-        return mmd2_fused(K.X, K.Y, K.spec, biased, process_group=current_loss_group())
+        return mmd2_fused(K.X, K.Y, K.spec, biased, process_group=current_loss_group(),
+                          exchange=current_exchange())
     K_XX, K_XY, K_YY, const_diagonal = K
     return _mmd2(K_XX, K_XY, K_YY, const_diagonal, biased)
 

@@ -7,17 +7,22 @@ One process per GPU.  A training step (one optimizer update, model.py:507-546):
            -> fused MMD^2 (1 HIP launch, gradient in the same sweep)
            -> jac = d critic(real) / d real   (PyTorch, create_graph)
            -> scaled loss (HIP) -> backward (PyTorch double backward + HIP ops)
-           -> [RCCL all_reduce of one flat gradient buffer]
+           -> [RCCL all_reduce of the flat gradient in ~16 MB buckets, each
+               issued from autograd hooks as its tensors' gradients land]
            -> clip_by_norm + TF-Adam over all critic tensors (1 HIP launch set)
   G step:  same forward with G in the graph; the scale is a constant for G
            (it depends on the critic only), so no double backward.
 
 Data-parallel modes:
   'tower'  -- the reference's towers (model.py:187-266): local MMD^2 and scale
-              per rank, per-rank clip_by_norm, all_reduce(SUM)/world, Adam.
-  'global' -- the north-star mode: critic features all-gathered so each rank
-              evaluates the full (world*batch) pairwise kernel; one scalar
-              all_reduce; parameter gradients all_reduce(SUM); clip; Adam.
+              per rank, per-rank clip_by_norm (inside each gradient bucket),
+              bucketed all_reduce(SUM)/world, Adam.
+  'global' -- the north-star mode: ONE all-gather per loss evaluation carries
+              every rank's critic features and its J / nD partials
+              (collectives.StepExchange), so each rank evaluates the full
+              (world*batch) pairwise kernel and the global scale with no
+              further small collective; parameter gradients bucketed
+              all_reduce(SUM); clip; Adam.
 """
 from __future__ import annotations
 
@@ -29,7 +34,7 @@ import torch.distributed as dist
 
 from . import convops, mmd, ops
 from .architecture import get_networks
-from .collectives import all_reduce_
+from .collectives import GradBuckets, StepExchange
 from .optim import FlatAdam
 from .sn import SpectralNormBank
 from .snops import sn_modules
@@ -122,8 +127,12 @@ class MMD_GAN:
         self.g_counter = 0
         self.optim_name = 'kernel_loss'
         self.last = {}
+        self._ex = None
+        self._buckets = {}
         if self.world > 1:
             self._broadcast_params()
+            for opt in (self.d_optim, self.g_optim):
+                self._bucket_for(opt)
 
     # ------------------------------------------------------------------
     def _dist_group(self):
@@ -186,10 +195,32 @@ class MMD_GAN:
             self.d_images_layers = self.d_G_layers = None
             self.d_images = D(images)
             self.d_G = D(fake)
-        # mmd.mmd2 inside set_loss spans the global batch in the all-gather mode
-        with mmd.loss_group(self._loss_group()):
-            self.set_loss(self.d_G, self.d_images)
+        # mmd.mmd2 inside set_loss spans the global batch in the all-gather
+        # mode, and one all-gather carries the features and the scale's partials
+        grp = self._loss_group()
+        self._ex = self._prepare_exchange(grp) if grp is not None else None
+        try:
+            with mmd.loss_group(grp, self._ex):
+                self.set_loss(self.d_G, self.d_images)
+        finally:
+            self._ex = None
         return self.g_loss, self.d_loss, self.aux
+
+    def _prepare_exchange(self, grp):
+        """The all-gather mode's StepExchange: with the scaling regulariser on
+        the real batch (the configs' case) the Jacobian and this rank's J / nD
+        partials are computed BEFORE set_loss, so they ride in mmd2's feature
+        all-gather and add_scaling needs no collective."""
+        ex = StepExchange(grp)
+        c = self.config
+        if (getattr(c, 'with_scaling', False) and not getattr(c, 'use_gaussian_noise', False)
+                and c.scaling_variant in ('grad', 'value_and_grad')):
+            need = self._need_critic_grad
+            jac = ops.jacobian_columns(self.d_images, self.images, create_graph=need)
+            ex.jac = jac if need else jac.detach()
+            ex.feat = self.d_images if need else self.d_images.detach()
+            ex.stats = ops.scaling_partials(ex.jac, ex.feat, c.scaling_variant, grp)
+        return ex
 
     def set_loss(self, G, images):
         """model.py:313-325: mmd2 of the configured kernel, then the witness
@@ -259,27 +290,32 @@ class MMD_GAN:
             return
         if c.scaling_variant not in ('grad', 'value_and_grad'):
             raise ValueError('scaling_variant must be grad or value_and_grad (model.py:387-390)')
-        if getattr(c, "use_gaussian_noise", False):
-            x_hat_data = (torch.randn(self.images.shape, device=self.device) * 10.0) \
-                .contiguous(memory_format=self.memory_format).requires_grad_(True)
-            x_hat = self.discriminator(x_hat_data)                # NO_OPS (model.py:370)
-        else:
-            x_hat_data, x_hat = self.images, self.d_images
         need = self._need_critic_grad
-        jac = ops.jacobian_columns(x_hat, x_hat_data, create_graph=need)
-        if not need:
-            jac = jac.detach()
-        feat = x_hat if need else x_hat.detach()
+        ex, pre = getattr(self, '_ex', None), None
+        if ex is not None and ex.jac is not None:
+            jac, feat = ex.jac, ex.feat            # computed ahead (_prepare_exchange)
+            pre = ex.stats_total                    # None if no mmd2 gathered them
+        else:
+            if getattr(c, "use_gaussian_noise", False):
+                x_hat_data = (torch.randn(self.images.shape, device=self.device) * 10.0) \
+                    .contiguous(memory_format=self.memory_format).requires_grad_(True)
+                x_hat = self.discriminator(x_hat_data)            # NO_OPS (model.py:370)
+            else:
+                x_hat_data, x_hat = self.images, self.d_images
+            jac = ops.jacobian_columns(x_hat, x_hat_data, create_graph=need)
+            if not need:
+                jac = jac.detach()
+            feat = x_hat if need else x_hat.detach()
         fused = self._fused_scaling()
         if fused is not None:
             self.g_loss, self.aux = ops.scaled_loss(
                 self.g_loss, jac, feat, sc=self.sc, variant=c.scaling_variant,
-                sqrt_scale=(fused == 'sqrt'), process_group=self._loss_group())
+                sqrt_scale=(fused == 'sqrt'), process_group=self._loss_group(), pre=pre)
             self.d_loss = -self.g_loss
         else:
             scale, self.aux = ops.scaling_factor(jac, feat, sc=self.sc,
                                                  variant=c.scaling_variant,
-                                                 process_group=self._loss_group())
+                                                 process_group=self._loss_group(), pre=pre)
             self.apply_scaling(scale)
 
     def _fused_scaling(self):
@@ -296,18 +332,32 @@ class MMD_GAN:
         return self.set_tower_loss(images, fake, need_critic_grad)
 
     # ------------------------------------------------------------------
+    def _bucket_for(self, opt):
+        """The GradBuckets of ``opt`` (created on first use): tower mode clips
+        each tensor inside its bucket before the all-reduce (model.py:449,
+        :455), global mode sums raw gradients and clips after."""
+        bk = getattr(self, '_buckets', None)
+        if bk is None:
+            bk = self._buckets = {}
+        if id(opt) not in bk:
+            clip = opt.clip_norm if self.dp_mode == 'tower' else 0.0
+            bk[id(opt)] = GradBuckets(opt, self.group, clip_norm=clip)
+        return bk[id(opt)]
+
+    def _arm(self, opt):
+        if self.world > 1:
+            self._bucket_for(opt).arm()
+
     def _exchange(self, opt):
         if self.world == 1:
             opt.step()
             return
+        # buckets not already issued from the backward's hooks go now; wait all
+        self._bucket_for(opt).finish()
         if self.dp_mode == 'tower':
-            # per-tower clip (model.py:449,455), then the tower mean (:257-258)
-            if opt.clip_norm > 0:
-                opt.clip_()
-            all_reduce_(opt.flat_grad, self.group)
+            # per-tower clip done per bucket; the tower mean (model.py:257-258)
             opt.step(grad_scale=1.0 / self.world, clip=False)
         else:
-            all_reduce_(opt.flat_grad, self.group)
             opt.step()
 
     def d_step(self, images):
@@ -321,6 +371,7 @@ class MMD_GAN:
             p.requires_grad_(True)
         self.d_optim.zero_grad()
         g_loss, d_loss, aux = self.set_tower_loss(images, fake, need_critic_grad=True)
+        self._arm(self.d_optim)
         if ref:       # the generator's gradient set, computed and discarded
             torch.autograd.grad(g_loss, self.g_vars, retain_graph=True)
             d_loss.backward(inputs=self.d_vars)
@@ -350,6 +401,7 @@ class MMD_GAN:
             g_loss, d_loss, aux = self.set_tower_loss(images, fake, need_critic_grad=ref)
             if ref:   # the critic's gradient set, computed and discarded
                 torch.autograd.grad(d_loss, self.d_vars, retain_graph=True)
+            self._arm(self.g_optim)
             g_loss.backward(inputs=self.g_vars)
             self._exchange(self.g_optim)
         finally:

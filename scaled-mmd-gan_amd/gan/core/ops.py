@@ -62,7 +62,7 @@ class _ScaledLoss(torch.autograd.Function):
     f = id (SMMD) or sqrt (SWGAN)."""
 
     @staticmethod
-    def forward(ctx, base, jac, feat, sc, variant, sqrt_scale, b_total, group):
+    def forward(ctx, base, jac, feat, sc, variant, sqrt_scale, b_total, group, pre):
         _lib.require_cuda(base, jac, feat)
         jac = jac.contiguous()
         n_cols, b = jac.shape[0], jac.shape[1]
@@ -72,17 +72,27 @@ class _ScaledLoss(torch.autograd.Function):
         base = base.reshape(1).contiguous()
         feat_c = feat.contiguous() if feat is not None else None
         dof = feat_c.shape[1] if feat_c is not None else 0
-        out = torch.empty(8, device=dev, dtype=torch.float32)
-        per_sample = torch.empty(b, device=dev, dtype=torch.float32)
-        nbytes = L.smmd_scaled_loss_workspace_bytes(n_cols * b, per)
-        ws = _lib.workspace('scaled_loss', nbytes, dev)
         s = _lib.stream_handle(dev)
-        args = (_lib.ptr(jac), n_cols, b, b_total, per, _lib.ptr(feat_c), dof, _lib.ptr(base),
-                float(sc), variant, sqrt_scale, _lib.ptr(out), _lib.ptr(per_sample), _lib.ptr(ws),
-                ws.numel(), s)
-        with _lib.timed('smmd_scaled_loss_fwd'):
-            st = L.smmd_scaled_loss_fwd(*args)
-        _lib.check(st, 'smmd_scaled_loss_fwd')
+        per_sample = torch.empty(b, device=dev, dtype=torch.float32)
+        if pre is not None:
+            # global J / nD already known (gathered with the step's features):
+            # only the single-thread finalize runs
+            out = torch.zeros(8, device=dev, dtype=torch.float32)
+            out[3:5] = pre
+            out[5:6] = base.detach()
+            _lib.check(L.smmd_scaled_loss_finalize(_lib.ptr(out), float(sc), variant,
+                                                   sqrt_scale, s), 'smmd_scaled_loss_finalize')
+            group = None
+        else:
+            out = torch.empty(8, device=dev, dtype=torch.float32)
+            nbytes = L.smmd_scaled_loss_workspace_bytes(n_cols * b, per)
+            ws = _lib.workspace('scaled_loss', nbytes, dev)
+            args = (_lib.ptr(jac), n_cols, b, b_total, per, _lib.ptr(feat_c), dof,
+                    _lib.ptr(base), float(sc), variant, sqrt_scale, _lib.ptr(out),
+                    _lib.ptr(per_sample), _lib.ptr(ws), ws.numel(), s)
+            with _lib.timed('smmd_scaled_loss_fwd'):
+                st = L.smmd_scaled_loss_fwd(*args)
+            _lib.check(st, 'smmd_scaled_loss_fwd')
         if group is not None:
             # J and nD are partial means over the global batch: sum them
             all_reduce_(out[3:5], group)
@@ -110,26 +120,53 @@ class _ScaledLoss(torch.autograd.Function):
         _lib.check(st, 'smmd_scaled_loss_bwd')
         if feat is not None and gfeat is None:
             gfeat = torch.zeros_like(feat)
-        return d_base.view(()), gjac, gfeat, None, None, None, None, None
+        return d_base.view(()), gjac, gfeat, None, None, None, None, None, None
+
+
+def _b_total(jac, process_group):
+    group = process_group if (process_group is not None and
+                              dist.get_world_size(process_group) > 1) else None
+    return group, jac.shape[1] * (dist.get_world_size(group) if group is not None else 1)
+
+
+def scaling_partials(jac, feat=None, variant='grad', process_group=None):
+    """This rank's share of (J, nD) over the global batch -- sum over its rows
+    divided by the global batch size -- as a detached [2] tensor: the partials
+    a collectives.StepExchange gathers with the critic features so the scale
+    needs no all-reduce of its own (``scaled_loss(..., pre=sum of them)``)."""
+    v = {'grad': 0, 'value_and_grad': 1}[variant]
+    _, b_total = _b_total(jac, process_group)
+    jac = jac.detach().contiguous()
+    n_cols, b, per = jac.shape[0], jac.shape[1], jac[0, 0].numel()
+    feat_c = feat.detach().contiguous() if (feat is not None and v == 1) else None
+    dof = feat_c.shape[1] if feat_c is not None else 0
+    dev = jac.device
+    L = _lib.lib()
+    out = torch.empty(8, device=dev, dtype=torch.float32)
+    ws = _lib.workspace('scaled_loss', L.smmd_scaled_loss_workspace_bytes(n_cols * b, per), dev)
+    with _lib.timed('smmd_scaled_loss_fwd'):
+        st = L.smmd_scaled_loss_fwd(_lib.ptr(jac), n_cols, b, b_total, per, _lib.ptr(feat_c), dof,
+                                    None, 0.0, v, 0, _lib.ptr(out), None, _lib.ptr(ws),
+                                    ws.numel(), _lib.stream_handle(dev))
+    _lib.check(st, 'smmd_scaled_loss_fwd')
+    return out[3:5]
 
 
 def scaled_loss(base, jac, feat=None, sc=10.0, variant='grad', sqrt_scale=False,
-                process_group=None):
+                process_group=None, pre=None):
     """Apply the scaling regulariser to ``base`` (mmd2 for SMMD, the critic
     mean difference for SWGAN).  ``jac`` = jacobian_columns(d_images, images).
 
     Returns (g_loss, aux) with aux a detached 8-vector
     [g_loss, d_loss, scale, J, norm_discriminator, base, 0, 0] and, in the
-    all-gather mode, J / nD over the global batch."""
+    all-gather mode, J / nD over the global batch: all-reduced here, or
+    ``pre`` = their global values already gathered (collectives.StepExchange)."""
     v = {'grad': 0, 'value_and_grad': 1}[variant]
     if v == 1 and feat is None:
         raise ValueError("scaling_variant 'value_and_grad' needs the critic output")
-    b = jac.shape[1]
-    group = process_group if (process_group is not None and
-                              dist.get_world_size(process_group) > 1) else None
-    b_total = b * (dist.get_world_size(group) if group is not None else 1)
+    group, b_total = _b_total(jac, process_group)
     g, out, _ = _ScaledLoss.apply(base, jac, feat if v == 1 else None, sc, v,
-                                  1 if sqrt_scale else 0, b_total, group)
+                                  1 if sqrt_scale else 0, b_total, group, pre)
     return g, out
 
 
@@ -140,7 +177,7 @@ class _ScaleFactor(torch.autograd.Function):
     dL/dQ = go * base * (-sc scale^2) is then exactly d scale / dQ * go."""
 
     @staticmethod
-    def forward(ctx, jac, feat, sc, variant, b_total, group):
+    def forward(ctx, jac, feat, sc, variant, b_total, group, pre):
         _lib.require_cuda(jac, feat)
         jac = jac.contiguous()
         n_cols, b = jac.shape[0], jac.shape[1]
@@ -149,16 +186,24 @@ class _ScaleFactor(torch.autograd.Function):
         L = _lib.lib()
         feat_c = feat.contiguous() if feat is not None else None
         dof = feat_c.shape[1] if feat_c is not None else 0
-        out = torch.empty(8, device=dev, dtype=torch.float32)
-        per_sample = torch.empty(b, device=dev, dtype=torch.float32)
-        ws = _lib.workspace('scaled_loss', L.smmd_scaled_loss_workspace_bytes(n_cols * b, per),
-                            dev)
         s = _lib.stream_handle(dev)
-        with _lib.timed('smmd_scaled_loss_fwd'):
-            st = L.smmd_scaled_loss_fwd(_lib.ptr(jac), n_cols, b, b_total, per, _lib.ptr(feat_c),
-                                        dof, None, float(sc), variant, 0, _lib.ptr(out),
-                                        _lib.ptr(per_sample), _lib.ptr(ws), ws.numel(), s)
-        _lib.check(st, 'smmd_scaled_loss_fwd')
+        if pre is not None:
+            out = torch.zeros(8, device=dev, dtype=torch.float32)
+            out[3:5] = pre
+            _lib.check(L.smmd_scaled_loss_finalize(_lib.ptr(out), float(sc), variant, 0, s),
+                       'smmd_scaled_loss_finalize')
+            group = None
+        else:
+            out = torch.empty(8, device=dev, dtype=torch.float32)
+            per_sample = torch.empty(b, device=dev, dtype=torch.float32)
+            ws = _lib.workspace('scaled_loss',
+                                L.smmd_scaled_loss_workspace_bytes(n_cols * b, per), dev)
+            with _lib.timed('smmd_scaled_loss_fwd'):
+                st = L.smmd_scaled_loss_fwd(_lib.ptr(jac), n_cols, b, b_total, per,
+                                            _lib.ptr(feat_c), dof, None, float(sc), variant, 0,
+                                            _lib.ptr(out), _lib.ptr(per_sample), _lib.ptr(ws),
+                                            ws.numel(), s)
+            _lib.check(st, 'smmd_scaled_loss_fwd')
         if group is not None:
             all_reduce_(out[3:5], group)
             _lib.check(L.smmd_scaled_loss_finalize(_lib.ptr(out), float(sc), variant, 0, s),
@@ -185,21 +230,18 @@ class _ScaleFactor(torch.autograd.Function):
         _lib.check(st, 'smmd_scaled_loss_bwd')
         if feat is not None and gfeat is None:
             gfeat = torch.zeros_like(feat)
-        return gjac, gfeat, None, None, None, None
+        return gjac, gfeat, None, None, None, None, None
 
 
-def scaling_factor(jac, feat=None, sc=10.0, variant='grad', process_group=None):
+def scaling_factor(jac, feat=None, sc=10.0, variant='grad', process_group=None, pre=None):
     """scale of MMD_GAN.add_scaling (model.py:382-390) as a differentiable
     0-dim tensor, for an ``apply_scaling(scale)`` override.  Returns (scale,
     aux) with aux as in ``scaled_loss`` (g_loss, d_loss and base unset)."""
     v = {'grad': 0, 'value_and_grad': 1}[variant]
     if v == 1 and feat is None:
         raise ValueError("scaling_variant 'value_and_grad' needs the critic output")
-    b = jac.shape[1]
-    group = process_group if (process_group is not None and
-                              dist.get_world_size(process_group) > 1) else None
-    b_total = b * (dist.get_world_size(group) if group is not None else 1)
-    scale, out = _ScaleFactor.apply(jac, feat if v == 1 else None, sc, v, b_total, group)
+    group, b_total = _b_total(jac, process_group)
+    scale, out = _ScaleFactor.apply(jac, feat if v == 1 else None, sc, v, b_total, group, pre)
     return scale, out
 
 

@@ -98,6 +98,14 @@ class FlatAdam:
             _lib.ptr(self.ws), self.ws.numel(), _lib.stream_handle(self.flat_grad.device)),
             'smmd_clip_by_norm_flat')
 
+    def clip_range_(self, lo, hi, clip_norm=None):
+        """clip_by_norm of tensors [lo, hi) in place (one gradient bucket)."""
+        c = self.clip_norm if clip_norm is None else clip_norm
+        sub = ctypes.cast(ctypes.byref(self.offsets, 8 * lo), ctypes.POINTER(ctypes.c_int64))
+        _lib.check(_lib.lib().smmd_clip_by_norm_flat(
+            _lib.ptr(self.flat_grad), sub, hi - lo, float(c), _lib.ptr(self.ws), self.ws.numel(),
+            _lib.stream_handle(self.flat_grad.device)), 'smmd_clip_by_norm_flat')
+
     def attach_sn(self, bank):
         """Fuse the first power-iteration pass of ``bank`` (a
         SpectralNormBank whose weights are parameters of this optimizer) into

@@ -1,11 +1,14 @@
-"""world_size-2 gloo tests (CPU) of the data-parallel paths:
+"""gloo tests (CPU, world sizes 2, 4 and 8) of the data-parallel paths:
 
 * all-gather ('global') MMD^2: each rank holds half of X and Y, sees the full
   pairwise kernel, gets the same estimator as one process on the
   concatenated batch, and row-local gradients equal that process's rows;
 * the scaled loss over the global batch (J all-reduced);
 * gradient exchange: 'tower' = per-rank clip, SUM/world, Adam (reference
-  model.py:233-266, :444-456); 'global' = SUM, clip, Adam.
+  model.py:233-266, :444-456); 'global' = SUM, clip, Adam -- both through
+  the bucketed all-reduce issued from autograd hooks during a real backward;
+* the step exchange: ONE all-gather carries the features and the J
+  partials, after which mmd2 and the scale need no collective.
 
 The HIP library is replaced by tests/fake_lib.py (oracle on CPU memory) so
 only the plumbing is under test here; the kernels' parity is tested on the GPU.
@@ -80,14 +83,18 @@ def _run(target, *args, world=2):
     return sorted(out, key=lambda t: t[0])
 
 
+WORLDS = [2, 4, 8]
+
+
+@pytest.mark.parametrize('world', WORLDS)
 @pytest.mark.parametrize('kernel', ['rbf', 'mix_rq_dot', 'distance'])
-def test_global_mmd2_matches_single_process(kernel):
+def test_global_mmd2_matches_single_process(kernel, world):
     X, Y = _data()
     spec = O.kernel_spec(kernel)
     ref = O.mmd2(spec, X, Y)
     dX, dY = O.mmd2_grad(spec, X, Y)
-    res = _run(_worker_mmd, kernel)
-    n = X.shape[0] // 2
+    res = _run(_worker_mmd, kernel, world=world)
+    n = X.shape[0] // world
     for rank, val, gx, gy in res:
         assert val == pytest.approx(ref, rel=1e-5, abs=1e-7)
         np.testing.assert_allclose(gx, dX[rank * n:(rank + 1) * n], rtol=1e-5, atol=1e-7)
@@ -98,8 +105,9 @@ def _worker_scaled(rank, world, port, q):
     _init(rank, world, port)
     from gan.core import ops
     rng = np.random.default_rng(3)
-    jac = rng.standard_normal((1, 2 * 4, 3, 2, 2)).astype(np.float32)
-    jl = torch.tensor(jac[:, rank * 4:(rank + 1) * 4], requires_grad=True)
+    jac = rng.standard_normal((1, 8, 3, 2, 2)).astype(np.float32)
+    k = 8 // world
+    jl = torch.tensor(jac[:, rank * k:(rank + 1) * k], requires_grad=True)
     base = torch.tensor(0.5, requires_grad=True)
     g, aux = ops.scaled_loss(base, jl, None, sc=10.0, process_group=dist.group.WORLD)
     g.backward()
@@ -108,54 +116,155 @@ def _worker_scaled(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_global_scaled_loss_uses_global_batch():
+@pytest.mark.parametrize('world', WORLDS)
+def test_global_scaled_loss_uses_global_batch(world):
     rng = np.random.default_rng(3)
-    jac = rng.standard_normal((1, 8, 3, 2, 2)).astype(np.float64)
+    jac = rng.standard_normal((1, 8, 3, 2, 2)).astype(np.float32).astype(np.float64)
     J = np.mean(O.squared_norm_per_sample(jac[0]))
     scale = O.scale_factor(J, 10.0)
-    res = _run(_worker_scaled)
+    res = _run(_worker_scaled, world=world)
     cq = 0.5 * (-10.0 * scale ** 2)
+    k = 8 // world
     for rank, g, Jg, gj in res:
         assert Jg == pytest.approx(J, rel=1e-6)
         assert g == pytest.approx(0.5 * scale, rel=1e-6)
-        np.testing.assert_allclose(gj, cq * 2.0 / 8 * jac[:, rank * 4:(rank + 1) * 4], rtol=1e-5)
+        np.testing.assert_allclose(gj, cq * 2.0 / 8 * jac[:, rank * k:(rank + 1) * k], rtol=1e-5)
 
 
-def _worker_exchange(rank, world, port, mode, q):
+class _Count:
+    """Counts the collectives a worker issues (wrapping torch.distributed)."""
+
+    def __init__(self):
+        self.n = {'all_gather_into_tensor': 0, 'all_reduce': 0}
+        self._orig = {k: getattr(dist, k) for k in self.n}
+        for k in self.n:
+            setattr(dist, k, self._wrap(k))
+
+    def _wrap(self, k):
+        def f(*a, **kw):
+            self.n[k] += 1
+            return self._orig[k](*a, **kw)
+        return f
+
+
+def _net():
+    torch.manual_seed(7)
+    return torch.nn.Sequential(torch.nn.Linear(6, 5), torch.nn.Tanh(), torch.nn.Linear(5, 4),
+                               torch.nn.Tanh(), torch.nn.Linear(4, 1))
+
+
+def _local_grads(rank):
+    """Parameter gradients of rank ``rank``'s loss on its own data."""
+    net = _net()
+    x = torch.tensor(np.random.default_rng(200 + rank).standard_normal((3, 6)),
+                     dtype=torch.float32)
+    (net(x) ** 2).sum().mul(3.0).backward()
+    return [p.grad.detach().numpy().astype(np.float64).ravel() for p in net.parameters()], \
+        [p.detach().numpy().astype(np.float64).ravel() for p in net.parameters()]
+
+
+def _worker_exchange(rank, world, port, mode, bucket_bytes, q):
     _init(rank, world, port)
+    from gan.core.collectives import GradBuckets
     from gan.core.model import MMD_GAN
     from gan.core.optim import FlatAdam
-    rng = np.random.default_rng(10)
-    p0 = rng.standard_normal(5).astype(np.float32)
-    p1 = rng.standard_normal(3).astype(np.float32)
-    params = [torch.nn.Parameter(torch.tensor(p0)), torch.nn.Parameter(torch.tensor(p1))]
-    opt = FlatAdam(params, lr=1e-3, clip_norm=1.0)
-    g = np.random.default_rng(100 + rank).standard_normal(8).astype(np.float32) * 2
-    params[0].grad.copy_(torch.tensor(g[:5]))
-    params[1].grad.copy_(torch.tensor(g[5:]))
+    net = _net()
+    opt = FlatAdam(list(net.parameters()), lr=1e-3, clip_norm=1.0)
     m = MMD_GAN.__new__(MMD_GAN)
     m.world, m.group, m.dp_mode = world, dist.group.WORLD, mode
+    m._buckets = {id(opt): GradBuckets(opt, m.group, bucket_bytes=bucket_bytes,
+                                       clip_norm=opt.clip_norm if mode == 'tower' else 0.0)}
+    cnt = _Count()
+    opt.zero_grad()
+    m._arm(opt)
+    x = torch.tensor(np.random.default_rng(200 + rank).standard_normal((3, 6)),
+                     dtype=torch.float32)
+    (net(x) ** 2).sum().mul(3.0).backward()
+    bk = m._buckets[id(opt)]
+    issued_in_backward = len(bk.launch_log)
     m._exchange(opt)
-    q.put((rank, np.concatenate([p.detach().numpy().ravel() for p in params])))
+    q.put((rank, np.concatenate([p.detach().numpy().ravel() for p in net.parameters()]),
+           issued_in_backward, len(bk.buckets), cnt.n['all_reduce']))
     dist.barrier()
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize('world', WORLDS)
 @pytest.mark.parametrize('mode', ['tower', 'global'])
-def test_gradient_exchange_semantics(mode):
-    rng = np.random.default_rng(10)
-    p = [rng.standard_normal(5), rng.standard_normal(3)]
-    grads = [np.random.default_rng(100 + r).standard_normal(8).astype(np.float32).astype(
-        np.float64) * 2 for r in range(2)]
-    sl = [slice(0, 5), slice(5, 8)]
+def test_gradient_exchange_semantics(mode, world):
+    """Bucketed, hook-issued all-reduce inside a real backward equals the
+    reference semantics: tower = per-rank clip_by_norm, mean, Adam
+    (model.py:449-455, :257-258); global = sum, clip, Adam."""
+    per_rank = [_local_grads(r) for r in range(world)]
+    params = per_rank[0][1]
     expect = []
-    for i in range(2):
-        if mode == 'tower':      # clip per tower, then mean (model.py:449-455, :257-258)
-            g = np.mean([O.clip_by_norm(gr[sl[i]], 1.0) for gr in grads], axis=0)
-        else:                    # global loss: sum, then clip
-            g = O.clip_by_norm(sum(gr[sl[i]] for gr in grads), 1.0)
-        expect.append(O.adam_step(p[i].astype(np.float32).astype(np.float64), 0, 0, g, 1,
-                                  1e-3)[0])
-    res = _run(_worker_exchange, mode)
-    for rank, flat in res:
+    for i in range(len(params)):
+        gs = [pr[0][i] for pr in per_rank]
+        if mode == 'tower':
+            g = np.mean([O.clip_by_norm(gr, 1.0) for gr in gs], axis=0)
+        else:
+            g = O.clip_by_norm(sum(gs), 1.0)
+        expect.append(O.adam_step(params[i], 0, 0, g, 1, 1e-3)[0])
+    res = _run(_worker_exchange, mode, 64, world=world)     # 64-byte buckets: several
+    for rank, flat, issued, nb, n_ar in res:
+        assert nb >= 3
+        assert issued == nb          # every bucket went out from a hook, inside backward
+        assert n_ar == nb            # one all-reduce per bucket, nothing else
         np.testing.assert_allclose(flat, np.concatenate(expect), rtol=1e-5, atol=1e-7)
+
+
+def _worker_step_exchange(rank, world, port, variant, q):
+    _init(rank, world, port)
+    from gan.core import mmd, ops
+    from gan.core.collectives import StepExchange
+    X, Y = _data()
+    n = X.shape[0] // world
+    rng = np.random.default_rng(3)
+    jac = rng.standard_normal((1, X.shape[0], 3, 2, 2)).astype(np.float32)
+    Xl = torch.tensor(X[rank * n:(rank + 1) * n], requires_grad=True)
+    Yl = torch.tensor(Y[rank * n:(rank + 1) * n], requires_grad=True)
+    jl = torch.tensor(jac[:, rank * n:(rank + 1) * n], requires_grad=True)
+    grp = dist.group.WORLD
+    cnt = _Count()
+    ex = StepExchange(grp)
+    feat = Xl[:, :1]
+    ex.stats = ops.scaling_partials(jl, feat, variant, grp)
+    with mmd.loss_group(grp, ex):
+        val = mmd.mmd2(mmd._rbf_kernel(Xl, Yl))
+    g, aux = ops.scaled_loss(val, jl, feat, sc=10.0, variant=variant, process_group=grp,
+                             pre=ex.stats_total)
+    g.backward()
+    q.put((rank, float(g), float(aux[3]), Xl.grad.numpy().copy(), jl.grad.numpy().copy(),
+           dict(cnt.n)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world', WORLDS)
+@pytest.mark.parametrize('variant', ['grad', 'value_and_grad'])
+def test_step_exchange_one_collective(world, variant):
+    """The all-gather mode's loss with one packed all-gather and no
+    all-reduce equals one process on the concatenated batch."""
+    X, Y = _data()
+    spec = O.kernel_spec('rbf')
+    rng = np.random.default_rng(3)
+    jac = rng.standard_normal((1, X.shape[0], 3, 2, 2)).astype(np.float32).astype(np.float64)
+    J = np.mean(O.squared_norm_per_sample(jac[0]))
+    nD = np.mean(X[:, :1].astype(np.float64) ** 2) if variant == 'value_and_grad' else 0.0
+    scale = O.scale_factor(J + nD, 10.0)
+    mm = O.mmd2(spec, X, Y)
+    dX, _ = O.mmd2_grad(spec, X, Y)
+    res = _run(_worker_step_exchange, variant, world=world)
+    n = X.shape[0] // world
+    cq = mm * (-10.0 * scale ** 2)
+    for rank, g, Jg, gx, gj, counts in res:
+        assert counts == {'all_gather_into_tensor': 1, 'all_reduce': 0}
+        assert Jg == pytest.approx(J, rel=1e-5)
+        assert g == pytest.approx(mm * scale, rel=1e-5)
+        np.testing.assert_allclose(gj, cq * 2.0 / X.shape[0] * jac[:, rank * n:(rank + 1) * n],
+                                   rtol=1e-4, atol=1e-8)
+        gx_ref = scale * dX[rank * n:(rank + 1) * n]
+        if variant == 'value_and_grad':      # d nD / d feat through X[:, :1]
+            gx_ref = gx_ref.copy()
+            gx_ref[:, :1] += cq * 2.0 / X.shape[0] * X[rank * n:(rank + 1) * n, :1]
+        np.testing.assert_allclose(gx, gx_ref, rtol=1e-4, atol=1e-7)

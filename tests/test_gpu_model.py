@@ -5,7 +5,9 @@ scaled loss -> double backward -> HIP SN backward) is compared with the
 oracle's CPU op-by-op mirror of the TF graph (oracle/tf_mirror.py) from the
 same weights, u vectors, images and z.  Tolerances (MIOpen fp32 convs vs CPU
 fp32 convs, same graph): d_loss rtol 1e-3; per-tensor gradients
-|d| <= max(2e-3 max|ref|, 1e-5 max over all tensors) + 2e-3 |ref|.
+|d| <= max(t max|ref|, 1e-5 max over all tensors) + t |ref| with t = 2e-3, and
+t = 5e-3 at the configs' full widths and batch 64 (64x longer fp32 reductions
+over the batch in a different order: MIOpen's vs the CPU's).
 """
 import argparse
 
@@ -41,6 +43,7 @@ def _mirror_from(model):
 @pytest.mark.parametrize('arch,size,dim,batch,cl', [
     ('sngan', 32, 64, 8, False), ('snresnet', 64, 16, 8, False), ('snresnet', 64, 16, 8, True),
     ('g-resnet5', 64, 16, 8, False),
+    ('g-resnet5', 64, 64, 64, False),         # celebA_smmd.yml's widths and batch at 64x64 (C3)
     ('snresnet', 64, 64, 64, False)])         # imagenet_smmd.yml's widths and batch, once
 def test_critic_step_matches_tf_mirror(dev, arch, size, dim, batch, cl):
     from gan.core.smmd import SMMD
@@ -78,7 +81,8 @@ def test_critic_step_matches_tf_mirror(dev, arch, size, dim, batch, cl):
         ref = mirror.to_product(name, rg).numpy().astype(np.float64)
         # exact zeros (e.g. the output bias: RBF-MMD is translation invariant) are
         # rounding noise in both: absolute floor 1e-5 of the largest gradient
-        tol = max(2e-3 * np.abs(ref).max(), 1e-5 * gmax) + 2e-3 * np.abs(ref)
+        t = 5e-3 if batch == 64 else 2e-3
+        tol = max(t * np.abs(ref).max(), 1e-5 * gmax) + t * np.abs(ref)
         assert (np.abs(got - ref) <= tol + 1e-12).all(), (name, np.abs(got - ref).max(),
                                                            np.abs(ref).max())
     # u advanced exactly as the reference's u.assign(u') (sn.py:39-46)

@@ -377,9 +377,10 @@ def test_witness_forward(dev, name):
     _grad_close(dH.cpu().numpy(), O.witness_grad_H(spec, H, R, F, g32), 'dH')
 
 
-@pytest.mark.parametrize('name', ['rbf', 'mix_rbf', 'mix_rq', 'mix_rq_dot'])
+@pytest.mark.parametrize('name', O.KERNEL_NAMES)
 def test_witness_second_order(dev, name):
-    """d <g, dH>/d(H, R, F) against central differences of the float64 oracle."""
+    """d <g, dH>/d(H, R, F) against central differences of the float64 oracle,
+    for every kernel (incl. distance / dot and the tanh-input ones)."""
     from gan.core import mmd
     rng = np.random.default_rng(4)
     H = rng.standard_normal((12, 2))
