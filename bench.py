@@ -165,9 +165,15 @@ def cpu_baseline(seconds_budget=20.0):
 
 
 def mmd_path(rows, d):
-    """The implementation smmd_mmd2_fwd picks (csrc/smmd_mmd.hip use_gram)."""
+    """The implementation smmd_mmd2_fwd picks (csrc/smmd_mmd.hip use_gram /
+    use_tile; env overrides aside): MFMA Gram for wide features, the 2-D
+    tiled sweep for d <= 8 (up to TILE_MAX_RT row tiles), else the row sweep."""
     gram = d > 32 or (d >= 16 and rows >= 1024) or (d >= 32 and rows >= 512)
-    return 'mfma-gram' if gram else 'row-sweep'
+    if gram:
+        return 'mfma-gram'
+    if d <= 8 and rows <= (16384 // 4 - 64) * 64:
+        return 'tile-2d'
+    return 'row-sweep'
 
 
 def mmd_valu_ops_per_pair(kernel, D):
@@ -520,6 +526,9 @@ def main():
                                                     world, dev)
         m_all = BATCH * world
         sn_kn = sum(e.N * e.K for e in model.sn_D.entries)
+        # the SN output per layer: W_eff [N, K], or for a ConvMeanPool conv the
+        # pool-folded 4 x 4 filter the bank writes directly (16 floats per 9)
+        sn_out = sum(e.N * e.K * 16 // 9 if e.fold else e.N * e.K for e in model.sn_D.entries)
         per_img = 3 * 64 * 64
         alg = {
             # sqsum pass reads g; update pass reads g, p, m, v and writes p, m, v
@@ -529,10 +538,11 @@ def main():
             # folded in (its column-partial writes are < 0.1 % of these bytes)
             'smmd_adam_flat_sn[D]': model.d_optim.numel * 4 * 8,
             'smmd_adam_flat_sn[G]': model.g_optim.numel * 4 * 8,
-            # one read of W + one write of W_eff (2 K N 4 B per iteration)
-            'smmd_sn_power_iter': sn_kn * 4 * 2,
-            # one read of G and W, one write of gW
-            'smmd_sn_weight_bwd': sn_kn * 4 * 3,
+            # one read of W + one write of W_eff (2 K N 4 B per
+            # iteration; the folded filters' 16 / 9 larger output for ConvMeanPool)
+            'smmd_sn_power_iter': (sn_kn + sn_out) * 4,
+            # one read of G (W_eff's shape) and W, one write of gW
+            'smmd_sn_weight_bwd': (sn_out + 2 * sn_kn) * 4,
             # X, Y rows read, unit gradients written, sums
             'smmd_mmd2_fwd': 2 * m_all * 4 + 2 * BATCH * 4 + 8 * 4,
             'smmd_scaled_loss_fwd': BATCH * per_img * 4,

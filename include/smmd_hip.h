@@ -57,7 +57,8 @@ typedef struct {
 } smmd_kernel_desc;
 
 const char *smmd_status_string(smmd_status s);
-int smmd_abi_version(void);         /* bumped on any ABI change (2: Gram/poly) */
+int smmd_abi_version(void);         /* bumped on any ABI change (2: Gram/poly,
+                                       3: smmd_sn_layer.fold) */
 
 /* ---------------------------------------------------------------------------
  * Fused pairwise MMD^2 (forward + unit gradient).
@@ -181,16 +182,25 @@ smmd_status smmd_scaled_loss_bwd(const float *jac, int n_cols, int b, int b_tota
 
 typedef struct {
     const float *W;      /* [N, K]                                            */
-    float *W_eff;        /* [N, K] out: s * W / sigma (NULL: not written)     */
+    float *W_eff;        /* [N, K] out: s * W / sigma (NULL: not written);    */
+                         /* fold = 1: [N, K/9, 4, 4], see below               */
     float *u;            /* [N] in: current u ; out: u' when update_u         */
     float *v;            /* [K] out: v (normalised)                           */
     float *sigma;        /* [1] out                                           */
     const float *s;      /* [1] SN scale (NULL -> 1.0), snops.py:82           */
-    const float *G;      /* bwd: [N, K] dL/dW_eff                             */
+    const float *G;      /* bwd: dL/dW_eff, W_eff's shape                     */
     float *gW;           /* bwd: [N, K] out dL/dW                             */
     float *gs;           /* bwd: [1] out dL/ds (NULL: not written)            */
     int32_t N;
     int32_t K;
+    /* fold = 1: the layer is the 3x3 stride-1 conv of a ConvMeanPool
+     * (gan/core/resnet/block.py:63-66), W [N, C, 3, 3] (K = 9 C, 16-byte
+     * aligned).  W_eff is then written directly as the pool-folded filter
+     * W'[n, c] (4 x 4) = 1/4 sum_{a,b in {0,1}} W_bar[n, c][. - a, . - b],
+     * W_bar = s W / sigma, so conv(x, W', stride 2) = meanpool2(conv(x, W_bar));
+     * the backward's G is dL/dW' and its adjoint is applied on the fly.
+     * fold = 0: W_eff = s W / sigma as is. */
+    int32_t fold;
 } smmd_sn_layer;
 
 size_t smmd_sn_workspace_bytes(const smmd_sn_layer *layers, int n_layers);
@@ -198,11 +208,8 @@ size_t smmd_sn_workspace_bytes(const smmd_sn_layer *layers, int n_layers);
 /* update_u = 1 mirrors update_collection=None (u.assign(u'), sn.py:39-46);
  * 0 mirrors "NO_OPS" (u left untouched). layers[] is a HOST array read during
  * the call; the pointers in it are device pointers. n_layers <= SMMD_SN_MAX_LAYERS.
- * ws: zero-filled at allocation and then reused as is; its first 16 bytes are
- * the grid barrier of the single-launch (cooperative) path.  That path is
- * opt-in (env SMMD_SN_RESIDENT=1) and runs only when n_layers <= 16 and the
- * weights fit the registers of the co-resident grid; the default is a
- * multi-launch path. */
+ * ws: zero-filled at allocation and then reused as is (its first 256 bytes
+ * are reserved). */
 smmd_status smmd_sn_power_iter(const smmd_sn_layer *layers, int n_layers,
                                int num_iters, float eps, int update_u,
                                void *ws, size_t ws_bytes, smmd_stream_t stream);
@@ -211,7 +218,7 @@ smmd_status smmd_sn_power_iter(const smmd_sn_layer *layers, int n_layers,
  * per 32-row tile) are already in ws, written by smmd_adam_flat_sn from the
  * current W and u; the call skips that pass (one read of every W).  The
  * caller guarantees neither W nor u changed since.  flags = 0 is
- * smmd_sn_power_iter.  The resident path ignores the flag. */
+ * smmd_sn_power_iter. */
 #define SMMD_SN_P1_READY 1
 smmd_status smmd_sn_power_iter_ex(const smmd_sn_layer *layers, int n_layers,
                                   int num_iters, float eps, int update_u, int flags,

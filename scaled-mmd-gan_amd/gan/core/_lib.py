@@ -24,7 +24,7 @@ SMMD_SN_MAX_LAYERS = 32
 SN_P1_READY = 1            # smmd_sn_power_iter_ex flag
 OPT_MAX_FUSED = 96         # tensors smmd_adam_flat_sn takes in one call
 SN_MAX_FUSED = 16          # SN layers smmd_adam_flat_sn takes in one call
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 KIND_RBF, KIND_RQ, KIND_DISTANCE, KIND_DOT = 0, 1, 2, 3
 
@@ -59,7 +59,8 @@ class SnLayer(ctypes.Structure):
                 ('gW', ctypes.c_void_p),
                 ('gs', ctypes.c_void_p),
                 ('N', ctypes.c_int32),
-                ('K', ctypes.c_int32)]
+                ('K', ctypes.c_int32),
+                ('fold', ctypes.c_int32)]
 
 
 class PolySums(ctypes.Structure):

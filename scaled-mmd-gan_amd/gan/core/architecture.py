@@ -91,6 +91,8 @@ class _ConvMeanPool(nn.Module):
     def __init__(self, cin, cout, k, bias, **sn):
         super().__init__()
         self.conv = Conv2d(cin, cout, k, 1, bias=bias, init='glorot_uniform', **sn)
+        # the SN bank may write this conv's pool-folded filter directly
+        self.conv.sn_fold = self.foldable()
 
     _w4 = None      # set by prefolded(): this call's folded weight
 
@@ -127,6 +129,12 @@ class prefolded:
         self.mods = [m for m in net.modules() if isinstance(m, _ConvMeanPool) and m.foldable()]
 
     def __enter__(self):
+        if self.mods and all(m.conv.with_sn and m.conv.w_eff is None and
+                             m.conv.w_fold is not None for m in self.mods):
+            # the SN bank already wrote every folded filter (smmd_sn_layer.fold)
+            for m in self.mods:
+                m._w4 = m.conv.w_fold
+            return self
         if self.mods:
             ws = [m.conv.effective_weight() for m in self.mods]
             key = (torch.is_grad_enabled(),

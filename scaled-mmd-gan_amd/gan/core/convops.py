@@ -266,6 +266,28 @@ def fold_pool_weight(w):
     return fold_pool_weights([w])[0]
 
 
+def unfold_pool_weight(w4):
+    """Inverse of fold_pool_weight on its image: W [cout, cin, 3, 3] from
+    W' = fold(W) by back-substitution, W[s, t] = 4 W'[s, t] - W[s-1, t] -
+    W[s, t-1] - W[s-1, t-1] (differentiable torch ops; the fallback for a
+    ConvMeanPool whose bank wrote only the folded filter but whose input has
+    odd spatial size)."""
+    rows = []
+    for s_ in range(3):
+        row = []
+        for t_ in range(3):
+            v = 4.0 * w4[:, :, s_, t_]
+            if s_ > 0:
+                v = v - rows[s_ - 1][t_]
+            if t_ > 0:
+                v = v - row[t_ - 1]
+            if s_ > 0 and t_ > 0:
+                v = v - rows[s_ - 1][t_ - 1]
+            row.append(v)
+        rows.append(row)
+    return torch.stack([torch.stack(r, -1) for r in rows], -2)
+
+
 def fold_up_weight(w):
     """W [cout, cin, 3, 3] -> K [cin, cout, 4, 4] with
     conv(upsample_nearest2(x), W, stride 1, pad 1) == conv_transpose(x, K, stride 2, pad 1):

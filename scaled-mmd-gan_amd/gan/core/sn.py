@@ -13,6 +13,7 @@ permutation of K, which leaves sigma and u unchanged (v is permuted).
 """
 from __future__ import annotations
 
+import os
 import warnings
 
 import torch
@@ -21,6 +22,14 @@ from . import _lib
 
 NO_OPS = 'NO_OPS'         # gan/core/sn.py:9
 SN_EPS = 1e-12            # gan/core/sn.py:12
+# SMMD_SN_FOLD=0: ConvMeanPool SN layers get W_eff and a separate fold launch
+SN_FOLD = os.environ.get('SMMD_SN_FOLD', '1') != '0'
+
+
+def _folds(e, W):
+    """This call writes the layer's pool-folded filter (smmd_sn_layer.fold)."""
+    return (e.fold and W.dim() == 4 and tuple(W.shape[2:]) == (3, 3) and W.is_contiguous()
+            and W.data_ptr() % 16 == 0)
 
 
 def truncated_normal_(t, std=1.0):
@@ -43,9 +52,12 @@ class _SNBatch(torch.autograd.Function):
             # order of K, see the module docstring)
             if _memfmt(W) is None:
                 raise ValueError('SN weight %d is neither contiguous nor channels_last' % i)
-            W_eff = torch.empty_like(W)
+            fold = _folds(e, W)
+            W_eff = (torch.empty(W.shape[0], W.shape[1], 4, 4, device=W.device,
+                                 dtype=torch.float32) if fold else torch.empty_like(W))
             outs.append(W_eff)
             L = arr[i]
+            L.fold = 1 if fold else 0
             L.W = W.data_ptr()
             L.W_eff = W_eff.data_ptr()
             L.u = e.u.data_ptr()
@@ -61,6 +73,7 @@ class _SNBatch(torch.autograd.Function):
             st = lib.smmd_sn_power_iter_ex(*args)
         _lib.check(st, 'smmd_sn_power_iter_ex')
         ctx.bank = bank
+        ctx.folds = [bool(a.fold) for a in arr]
         ctx.save_for_backward(*Ws, *ss)
         return tuple(outs)
 
@@ -73,9 +86,11 @@ class _SNBatch(torch.autograd.Function):
         arr = (_lib.SnLayer * n)()
         gWs, gss, keep = [], [], []
         for i, (e, W, s, G) in enumerate(zip(bank.entries, Ws, ss, grads)):
+            fold = ctx.folds[i]
             if G is None:
-                G = torch.zeros_like(W)
-            G = G.contiguous(memory_format=_memfmt(W))
+                G = (torch.zeros(W.shape[0], W.shape[1], 4, 4, device=W.device,
+                                 dtype=torch.float32) if fold else torch.zeros_like(W))
+            G = G.contiguous() if fold else G.contiguous(memory_format=_memfmt(W))
             keep.append(G)
             gW = torch.empty_like(W)
             gs = torch.empty(1, device=W.device, dtype=torch.float32)
@@ -91,6 +106,7 @@ class _SNBatch(torch.autograd.Function):
             L.gW = gW.data_ptr()
             L.gs = gs.data_ptr()
             L.N, L.K = e.N, e.K
+            L.fold = 1 if fold else 0
         args = (arr, n, _lib.ptr(bank.ws), bank.ws.numel(), _lib.stream_handle(Ws[0].device))
         with _lib.timed('smmd_sn_weight_bwd'):
             st = _lib.lib().smmd_sn_weight_bwd(*args)
@@ -127,6 +143,8 @@ class SNEntry:
         self.u = truncated_normal_(torch.empty(self.N, device=dev, dtype=torch.float32))
         self.v = torch.zeros(self.K, device=dev, dtype=torch.float32)
         self.sigma = torch.ones(1, device=dev, dtype=torch.float32)
+        # a ConvMeanPool conv: the bank writes its pool-folded filter
+        self.fold = SN_FOLD and bool(getattr(module, 'sn_fold', False))
 
     @property
     def weight(self):
@@ -199,7 +217,10 @@ class SpectralNormBank:
         self._p1_token = None
         outs = _SNBatch.apply(self, bool(update_u), _lib.SN_P1_READY if ready else 0, *Ws, *ss)
         for e, w in zip(self.entries, outs):
-            e.module.w_eff = w
+            if w.shape != e.weight.shape:        # the pool-folded 4 x 4 filter
+                e.module.w_eff, e.module.w_fold = None, w
+            else:
+                e.module.w_eff, e.module.w_fold = w, None
         return list(outs)
 
     def sigmas(self):
@@ -234,7 +255,7 @@ def spectral_normed_weight(W, u=None, num_iters=1, update_collection=None, with_
     bank = SpectralNormBank.__new__(SpectralNormBank)
     e = SNEntry.__new__(SNEntry)
     e.module, e.weight_name, e.scale_name = holder, 'weight', 'sn_scale'
-    e.N, e.K = N, Wt.shape[1]
+    e.N, e.K, e.fold = N, Wt.shape[1], False
     e.u = u.reshape(N).detach().clone().contiguous()
     e.v = torch.zeros(e.K, device=W.device, dtype=torch.float32)
     e.sigma = torch.ones(1, device=W.device, dtype=torch.float32)

@@ -37,7 +37,12 @@ def _glorot_uniform_(t, fan_in, fan_out):
 
 class _SNMixin:
     """with_sn: forward uses self.w_eff (set by the bank); with_learnable_sn_scale
-    makes ``sn_scale`` trainable (snops.py:82)."""
+    makes ``sn_scale`` trainable (snops.py:82).  A ConvMeanPool conv
+    (``sn_fold``) may instead receive its pool-folded 4 x 4 filter straight
+    from the bank (``w_fold``); ``effective_weight`` then unfolds it, for the
+    rare call that needs the 3 x 3 filter (odd spatial sizes)."""
+
+    sn_fold = False
 
     def _init_sn(self, with_sn, with_learnable_sn_scale, scale):
         self.with_sn = with_sn
@@ -45,11 +50,16 @@ class _SNMixin:
             self.sn_scale = nn.Parameter(torch.full((1,), float(scale)),
                                          requires_grad=with_learnable_sn_scale)
         self.w_eff = None
+        self.w_fold = None
 
     def effective_weight(self):
         if not self.with_sn:
             return self.weight
         if self.w_eff is None:
+            if getattr(self, 'w_fold', None) is not None:
+                from .convops import unfold_pool_weight
+                self.w_eff = unfold_pool_weight(self.w_fold)
+                return self.w_eff
             raise RuntimeError('SN layer used before its SpectralNormBank.refresh()')
         return self.w_eff
 

@@ -191,7 +191,8 @@ def test_reference_schedule_applies_the_lean_update(dev):
         caps.append(cap)
     for step, name in (('d_step', 'D'), ('g_step', 'G')):
         outs = [getattr(mdl, step)(images) for mdl in (lean, ref)]
-        np.testing.assert_allclose(outs[1][1].item(), outs[0][1].item(), rtol=1e-5, atol=1e-7)
+        # the loss value too goes through solver-dependent convs (see below)
+        np.testing.assert_allclose(outs[1][1].item(), outs[0][1].item(), rtol=1e-3, atol=1e-7)
         ga, gb = caps[0][name], caps[1][name]
         scale = float(ga.abs().max())
         # The two schedules run different autograd graphs, so MIOpen picks other

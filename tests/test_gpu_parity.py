@@ -413,63 +413,98 @@ def test_witness_second_order(dev, name):
 
 SN_SHAPES = [(64, 27), (128, 576), (256, 1152), (1, 1024), (1024, 4608), (7, 13), (130, 300)]
 
-# smmd_sn_power_iter / smmd_sn_weight_bwd have two implementations: the
-# resident cooperative kernel (one launch, W held in registers) and the
-# multi-pass launch set it falls back to; SMMD_SN_RESIDENT=0 forces the latter.
-SN_PATHS = ['resident', 'multipass']
-
-
-def _sn_path(monkeypatch, path):
-    monkeypatch.setenv('SMMD_SN_RESIDENT', '1' if path == 'resident' else '0')
-
-
-def _sn_bank(dev, shapes, seed, num_iters=1):
+def _sn_bank(dev, shapes, seed, num_iters=1, fold=()):
+    """SN bank over plain modules; shapes (N, K), or (N, C, 3, 3) for a conv,
+    with fold[i] marking a ConvMeanPool conv (the bank then writes its
+    pool-folded 4 x 4 filter, smmd_sn_layer.fold)."""
     from gan.core import sn
     rng = np.random.default_rng(seed)
     mods = []
-    for N, K in shapes:
+    for i, shp in enumerate(shapes):
         m = torch.nn.Module()
-        m.weight = torch.nn.Parameter(torch.tensor(rng.standard_normal((N, K)) * 0.05,
+        m.weight = torch.nn.Parameter(torch.tensor(rng.standard_normal(shp) * 0.05,
                                                    dtype=torch.float32, device=dev))
         m.sn_scale = torch.nn.Parameter(torch.tensor([1.3], device=dev))
+        m.sn_fold = bool(fold[i]) if i < len(fold) else False
         mods.append(m)
     return mods, sn.SpectralNormBank(mods, num_iters=num_iters), rng
 
 
 def _check_sn(mods, bank, u0, outs, Gs, num_iters=1):
     for i, (m, e) in enumerate(zip(mods, bank.entries)):
-        W = m.weight.detach().cpu().numpy().astype(np.float64)
+        W4d = m.weight.detach().cpu().numpy().astype(np.float64)
+        W = W4d.reshape(W4d.shape[0], -1)
         sigma, u1, v1 = O.spectral_norm_rows(W, u0[i], num_iters)
         _close(e.sigma.item(), sigma, 0, 1e-4, 'sigma %d' % i)
         _close(e.u.cpu().numpy(), u1, 1e-6, 1e-4, 'u %d' % i)
         _close(e.v.cpu().numpy(), v1, 1e-6, 1e-4, 'v %d' % i)
-        weff = W / sigma * 1.3
+        weff = W4d / sigma * 1.3
+        if e.fold:
+            weff = O.fold_pool_weight(weff)
         _close(outs[i].detach().cpu().numpy(), weff, 1e-6 * np.abs(weff).max(), 1e-4, 'Weff')
         if Gs is None:
             continue
-        gW, gs = O.sn_weight_backward(W, 1.3, sigma, u1, v1, Gs[i])
-        _close(m.weight.grad.cpu().numpy(), gW, 1e-4 * np.abs(gW).max(), 1e-3, 'gW %d' % i)
+        G = O.fold_pool_weight_adjoint(Gs[i]) if e.fold else Gs[i]
+        gW, gs = O.sn_weight_backward(W, 1.3, sigma, u1, v1, G.reshape(W.shape))
+        _close(m.weight.grad.cpu().numpy().reshape(W.shape), gW, 1e-4 * np.abs(gW).max(), 1e-3,
+               'gW %d' % i)
         _close(m.sn_scale.grad.item(), gs, 1e-4 * abs(gs), 1e-3, 'gs %d' % i)
 
 
-@pytest.mark.parametrize('path', SN_PATHS)
-def test_sn_bank_vs_oracle(dev, monkeypatch, path):
-    _sn_path(monkeypatch, path)
-    mods, bank, rng = _sn_bank(dev, SN_SHAPES, 2)
+def _sn_roundtrip(dev, shapes, seed, fold=()):
+    mods, bank, rng = _sn_bank(dev, shapes, seed, fold=fold)
     u0 = [e.u.cpu().numpy().astype(np.float64) for e in bank.entries]
     outs = bank.refresh(update_u=True)
-    Gs = [rng.standard_normal((N, K)) for N, K in SN_SHAPES]
+    Gs = [rng.standard_normal(tuple(o.shape)) for o in outs]
     loss = sum((o * torch.tensor(G, device=dev, dtype=torch.float32)).sum()
                for o, G in zip(outs, Gs))
     loss.backward()
     _check_sn(mods, bank, u0, outs, Gs)
+    return mods, bank, outs
 
 
-@pytest.mark.parametrize('path', SN_PATHS)
-def test_sn_num_iters(dev, monkeypatch, path):
-    """num_iters > 1 (sn.py:24-35): the resident kernel loops its phases with
-    W still in registers."""
-    _sn_path(monkeypatch, path)
+def test_sn_bank_vs_oracle(dev):
+    _sn_roundtrip(dev, SN_SHAPES, 2)
+
+
+SN_FOLD_SHAPES = [(128, 64, 3, 3), (256, 128, 3, 3), (64, 3, 3, 3), (7, 5, 3, 3),
+                  (130, 300), (1024, 512, 3, 3)]
+
+
+def test_sn_bank_fold_layers_vs_oracle(dev):
+    """ConvMeanPool layers (fold = 1): the bank writes the pool-folded filter
+    of s W / sigma directly and its backward takes dL/dW' (the fold's
+    adjoint applied in the same pass), mixed with plain layers in one call."""
+    mods, bank, outs = _sn_roundtrip(dev, SN_FOLD_SHAPES, 3, fold=(1, 1, 0, 1, 0, 1))
+    assert [tuple(o.shape) for o in outs] == [(128, 64, 4, 4), (256, 128, 4, 4), (64, 3, 3, 3),
+                                             (7, 5, 4, 4), (130, 300), (1024, 512, 4, 4)]
+
+
+def test_sn_fold_matches_separate_fold_launch(dev, monkeypatch):
+    """The fused path equals W_eff followed by smmd_fold_pool_weights (the
+    SMMD_SN_FOLD=0 path): the same arithmetic in the same order."""
+    from gan.core import convops, sn
+    res = {}
+    for fused in (True, False):
+        monkeypatch.setattr(sn, 'SN_FOLD', fused)
+        torch.manual_seed(0)
+        mods, bank, rng = _sn_bank(dev, SN_FOLD_SHAPES[:2], 5, fold=(1, 1))
+        outs = bank.refresh(update_u=True)
+        if not fused:
+            outs = convops.fold_pool_weights(outs)
+        G = [torch.tensor(rng.standard_normal(tuple(o.shape)), device=dev, dtype=torch.float32)
+             for o in outs]
+        torch.autograd.backward(outs, G)
+        res[fused] = ([o.detach().cpu().numpy() for o in outs],
+                      [m.weight.grad.cpu().numpy() for m in mods])
+    for a, b in zip(res[True][0], res[False][0]):
+        np.testing.assert_array_equal(a, b)
+    for a, b in zip(res[True][1], res[False][1]):
+        _close(a, b, 1e-6 * np.abs(b).max(), 1e-5, 'gW fused vs separate')
+
+
+def test_sn_num_iters(dev):
+    """num_iters > 1 (sn.py:24-35)."""
     shapes = [(64, 27), (256, 1152), (33, 70)]
     mods, bank, rng = _sn_bank(dev, shapes, 5, num_iters=3)
     u0 = [e.u.cpu().numpy().astype(np.float64) for e in bank.entries]
@@ -477,48 +512,34 @@ def test_sn_num_iters(dev, monkeypatch, path):
     _check_sn(mods, bank, u0, outs, None, num_iters=3)
 
 
-def test_sn_paths_agree_and_barrier_state(dev, monkeypatch):
-    """Both implementations give the same sigma/W_eff to fp32 rounding on the
-    SNResNet-64 critic shapes; after many resident launches the grid barrier
-    in the workspace header is back at rest (count 0, no timeout flag) with
-    exactly 4 barriers per power iteration and 1 per backward."""
+def test_sn_snresnet64_critic_layers(dev):
+    """the SNResNet-64 critic (df_dim 64) has exactly 14 SN
+    layers, 10,099,392 SN weights, in the reference's layer order and shapes
+    (architecture.py:410-434); its 4 ConvMeanPool convs take the fused fold.
+    The whole bank runs forward + backward against the oracle."""
     from gan.core.architecture import SNResNetDiscriminator
     from gan.core.snops import sn_modules
     D = SNResNetDiscriminator(64, 1, False, with_sn=True, with_learnable_sn_scale=True)
-    shapes = [(m.weight.shape[0], m.weight[0].numel()) for m in sn_modules(D)]
-    assert sum(N * K for N, K in shapes) > 10_000_000          # SURVEY 8a a7: 10.10 M
-    res = {}
-    for path in SN_PATHS:
-        _sn_path(monkeypatch, path)
-        torch.manual_seed(0)                   # same initial u for both banks
-        mods, bank, rng = _sn_bank(dev, shapes, 11)
-        hdr0 = bank.ws[:16].view(torch.int32).clone()
-        calls = 20
-        for _ in range(calls):
-            outs = bank.refresh(update_u=False)
-            G = [torch.ones_like(o) for o in outs]
-            torch.autograd.backward(outs, G)
-        torch.cuda.synchronize()
-        hdr = bank.ws[:16].view(torch.int32).cpu().tolist()
-        if path == 'resident':
-            assert hdr[0] == 0, hdr            # count back at rest
-            assert hdr[2] == 0, hdr            # no barrier timed out
-            assert hdr[1] - int(hdr0[1]) == calls * (4 + 1), hdr
-        res[path] = (bank.sigmas().cpu().numpy(), [o.detach().cpu().numpy() for o in outs],
-                     [m.weight.grad.cpu().numpy() for m in mods])
-    a, b = res['resident'], res['multipass']
-    _close(a[0], b[0], 0, 2e-6, 'sigma resident vs multipass')
-    for i in range(len(shapes)):
-        _close(a[1][i], b[1][i], 1e-7 * np.abs(b[1][i]).max(), 2e-6, 'Weff %d' % i)
-        _close(a[2][i], b[2][i], 1e-6 * np.abs(b[2][i]).max(), 1e-5, 'gW %d' % i)
+    layers = sn_modules(D)
+    shapes = [tuple(m.weight.shape) for m in layers]
+    assert len(shapes) == 14
+    assert sum(int(np.prod(s)) for s in shapes) == 10_099_392
+    expect = [(64, 3, 3, 3)]                          # d_h0_conv
+    for ci, co in ((64, 128), (128, 256), (256, 512), (512, 1024)):
+        # d_res{i}: .Conv1, .Conv2 (ConvMeanPool), .Shortcut (1 x 1, MeanPoolConv)
+        expect += [(ci, ci, 3, 3), (co, ci, 3, 3), (co, ci, 1, 1)]
+    expect.append((1, 1024))                          # d_h5_lin
+    assert shapes == expect
+    folds = [bool(getattr(m, 'sn_fold', False)) for m in layers]
+    assert folds == [False] + [False, True, False] * 4 + [False]
+    _sn_roundtrip(dev, shapes, 11, fold=folds)
 
 
-def test_sn_repeated_calls_track_weights(dev, monkeypatch):
+def test_sn_repeated_calls_track_weights(dev):
     """Workspace state carried between calls (slabs, u') never leaks into the
     next call: new weights each call, checked against the oracle from the u
     the previous call left."""
-    _sn_path(monkeypatch, 'multipass')
-    shapes = [(1024, 4608), (64, 27), (1, 1024), (130, 300)]
+    shapes = [(1024, 4608), (64, 27), (1, 1024), (130, 300), (2048, 9216)]
     mods, bank, rng = _sn_bank(dev, shapes, 21)
     for _ in range(4):
         with torch.no_grad():
@@ -527,17 +548,6 @@ def test_sn_repeated_calls_track_weights(dev, monkeypatch):
         u0 = [e.u.cpu().numpy().astype(np.float64) for e in bank.entries]
         outs = bank.refresh(update_u=True)
         _check_sn(mods, bank, u0, outs, None)
-
-
-def test_sn_over_resident_capacity(dev, monkeypatch):
-    """More tiles than the co-resident grid holds in registers: the call falls
-    back to the multi-pass launch set and stays correct."""
-    _sn_path(monkeypatch, 'resident')
-    shapes = [(2048, 9216), (64, 27)]          # 2 * 64 * 36 + 1 tiles of 32 x 256 > 8 * 256
-    mods, bank, rng = _sn_bank(dev, shapes, 4)
-    u0 = [e.u.cpu().numpy().astype(np.float64) for e in bank.entries]
-    outs = bank.refresh(update_u=True)
-    _check_sn(mods, bank, u0, outs, None)
 
 
 def test_sn_reference_layout(dev):

@@ -51,7 +51,6 @@ def _grads(opt, seed):
 @pytest.mark.parametrize('num_iters', [1, 2])
 @pytest.mark.parametrize('groups', ['1', '2', '4'])
 def test_fused_step_same_bits_as_unfused(dev, monkeypatch, clip, num_iters, groups):
-    monkeypatch.setenv('SMMD_SN_RESIDENT', '0')
     monkeypatch.setenv('SMMD_SN_ADAM_H', groups)      # row groups of the fused tile
     _, bank_a, opt_a = _net(dev, 5, num_iters)
     _, bank_b, opt_b = _net(dev, 5, num_iters)
@@ -79,7 +78,6 @@ def test_fused_step_same_bits_as_unfused(dev, monkeypatch, clip, num_iters, grou
 def test_fused_refresh_vs_oracle(dev, monkeypatch):
     """After fused steps the refresh is still the oracle's power iteration on
     the updated weights from the u the previous refresh left."""
-    monkeypatch.setenv('SMMD_SN_RESIDENT', '0')
     mods, bank, opt = _net(dev, 8, 1)
     assert opt.attach_sn(bank)
     bank.refresh(update_u=True)
@@ -103,7 +101,6 @@ def test_torch_write_between_step_and_refresh(dev, monkeypatch):
     """A weight or u written through torch after the fused step (a checkpoint
     load, a manual edit) bumps its version: the refresh recomputes the pass
     instead of using the partials of the old weights."""
-    monkeypatch.setenv('SMMD_SN_RESIDENT', '0')
     mods, bank, opt = _net(dev, 11, 1)
     assert opt.attach_sn(bank)
     bank.refresh(update_u=True)

@@ -14,12 +14,11 @@ import sys
 from collections import defaultdict
 
 GROUPS = {
-    'smmd_sn_power_iter': ('sn_p1_kernel', 'sn_p2_kernel', 'sn_r2_kernel', 'sn_p3_kernel',
-                           'sn_resident_kernel'),
-    'smmd_sn_weight_bwd': ('sn_bwd_a_kernel', 'sn_bwd_b_kernel', 'sn_resident_bwd_kernel'),
+    'smmd_sn_power_iter': ('sn_p1_kernel', 'sn_p2_kernel', 'sn_r2_kernel', 'sn_p3_kernel'),
+    'smmd_sn_weight_bwd': ('sn_bwd_a_kernel', 'sn_bwd_b_kernel'),
     'smmd_adam_flat': ('opt_sqsum_kernel', 'opt_adam_kernel'),
     'smmd_adam_flat_sn': ('opt_sqsum_kernel', 'opt_adam_sn_kernel'),
-    'smmd_mmd2_fwd': ('mmd2_fused_kernel',),
+    'smmd_mmd2_fwd': ('mmd2_fused_kernel', 'mmd2_tile_kernel'),
     'smmd_scaled_loss_fwd': ('sqnorm_partial_kernel', 'scaled_loss_final_kernel'),
     'smmd_scaled_loss_bwd': ('scaled_loss_bwd_kernel',),
     'smmd_fold_pool_weights': ('fold_fwd_kernel', 'fold_adj_kernel'),
