@@ -161,6 +161,50 @@ def cpu_baseline(seconds_budget=20.0):
         'schedule': ''.join(kinds),
         'step_s': {'median': round(_pct(times, .5), 4), 'p10': round(_pct(times, .1), 4),
                    'p90': round(_pct(times, .9), 4), 'mean': round(mean, 4)}}
+    out['components'] = cpu_components()
+    return out
+
+
+def _reps(fn, n=20, warm=3):
+    for _ in range(warm):
+        fn()
+    ts = []
+    for _ in range(n):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return {'median_ms': round(_pct(ts, .5) * 1e3, 3), 'p10_ms': round(_pct(ts, .1) * 1e3, 3),
+            'p90_ms': round(_pct(ts, .9) * 1e3, 3), 'reps': n}
+
+
+def cpu_components():
+    """SURVEY 8d CPU components on the mirror (median of 20 after 3 warm-ups):
+    (i) MMD^2 fwd + bwd per N (the three N x N matrices materialised, d = 1),
+    (ii) the SN power iteration of every SN layer of each BASELINE critic
+    (oracle/ref_nets.py variable shapes, reference layout)."""
+    from oracle import ref_nets as R
+    from oracle.tf_mirror import rbf_mmd2_tf, sn_weight_tf
+    g = torch.Generator().manual_seed(0)
+    out = {}
+    for N in (64, 512, 2048):
+        X = torch.randn(N, 1, generator=g).requires_grad_(True)
+        Y = torch.randn(N, 1, generator=g).requires_grad_(True)
+
+        def mmd_once():
+            torch.autograd.grad(rbf_mmd2_tf(X, Y), (X, Y))
+        out['mmd_fwd_bwd_N%d' % N] = dict(_reps(mmd_once), pairs=3 * N * N)
+    for arch, size in (('snresnet', 64), ('sngan', 32), ('g-resnet5', 160)):
+        vs = [v for v in R.critic_vars(arch, 64, 1, size, True, True) if v.sn]
+        Ws = [torch.randn(*v.shape, generator=g) * 0.02 for v in vs]
+        us = [torch.randn(1, v.shape[-1], generator=g) for v in vs]
+        s1 = torch.ones(1)
+
+        def sn_once():
+            with torch.no_grad():
+                for W, u in zip(Ws, us):
+                    sn_weight_tf(W, u, s1)
+        out['sn_power_iter_%s%d' % (arch, size)] = dict(
+            _reps(sn_once), layers=len(vs), weights=sum(int(W.numel()) for W in Ws))
     return out
 
 

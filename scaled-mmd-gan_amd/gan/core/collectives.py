@@ -107,11 +107,13 @@ def _bucket_bytes():
 class GradBuckets:
     """All-reduce (SUM) of a FlatAdam's flat gradient in contiguous buckets of
     about ``bucket_bytes``, formed from the last tensor backwards (the order
-    the backward produces them).  A bucket's all-reduce is issued, async, from
-    the post-accumulate-grad hook of its last tensor to receive a gradient,
-    so it overlaps the rest of the backward; ``finish`` issues the buckets no
-    hook completed (tensors without a gradient this step contribute their
-    zeros) and waits for all of them.  ``clip_norm`` > 0 clips every tensor of
+    the backward produces them).  Buckets are issued, async, from the
+    post-accumulate-grad hooks as they complete, strictly in bucket order (a
+    bucket that completes early waits for its predecessors), so every rank
+    issues the same collectives in the same order whatever order its
+    backward ran in; they overlap the rest of the backward.  ``finish``
+    issues what no hook did (tensors without a gradient this step contribute
+    their zeros) and waits for all.  ``clip_norm`` > 0 clips every tensor of
     a bucket before its all-reduce (the reference's per-tower clip_by_norm,
     model.py:449-455)."""
 
@@ -135,7 +137,7 @@ class GradBuckets:
                 self.bucket_of[i] = b
         self._offs = offs
         self.armed = False
-        self.left, self.works, self.launched = [], [], []
+        self.left, self.works, self.next = [], [], 0
         self._hooks = [p.register_post_accumulate_grad_hook(self._hook(i))
                        for i, p in enumerate(opt.params)]
         self.launch_log = []      # bucket ids in issue order of the last step (tests)
@@ -144,7 +146,7 @@ class GradBuckets:
         """Call before the backward whose gradients this step exchanges."""
         self.armed = True
         self.left = [hi - lo for lo, hi in self.buckets]
-        self.launched = [False] * len(self.buckets)
+        self.next = 0
         self.works = []
         self.launch_log = []
 
@@ -152,15 +154,14 @@ class GradBuckets:
         def fn(_p):
             if not self.armed:
                 return
-            b = self.bucket_of[i]
-            self.left[b] -= 1
-            if self.left[b] == 0 and not self.launched[b]:
-                self._launch(b)
+            self.left[self.bucket_of[i]] -= 1
+            while self.next < len(self.buckets) and self.left[self.next] <= 0:
+                self._launch(self.next)
         return fn
 
     def _launch(self, b):
         lo, hi = self.buckets[b]
-        self.launched[b] = True
+        self.next = b + 1
         self.launch_log.append(b)
         if self.clip_norm > 0:
             self.opt.clip_range_(lo, hi, self.clip_norm)
@@ -172,9 +173,8 @@ class GradBuckets:
         """Issue what the hooks did not, then wait for every bucket."""
         if not self.armed:          # no backward was armed: exchange everything now
             self.arm()
-        for b in range(len(self.buckets)):
-            if not self.launched[b]:
-                self._launch(b)
+        while self.next < len(self.buckets):
+            self._launch(self.next)
         for w in self.works:
             w.wait()
         self.works = []

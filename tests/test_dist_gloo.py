@@ -182,9 +182,10 @@ def _worker_exchange(rank, world, port, mode, bucket_bytes, q):
     (net(x) ** 2).sum().mul(3.0).backward()
     bk = m._buckets[id(opt)]
     issued_in_backward = len(bk.launch_log)
+    order = list(bk.launch_log)
     m._exchange(opt)
     q.put((rank, np.concatenate([p.detach().numpy().ravel() for p in net.parameters()]),
-           issued_in_backward, len(bk.buckets), cnt.n['all_reduce']))
+           issued_in_backward, len(bk.buckets), cnt.n['all_reduce'], order))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -206,9 +207,10 @@ def test_gradient_exchange_semantics(mode, world):
             g = O.clip_by_norm(sum(gs), 1.0)
         expect.append(O.adam_step(params[i], 0, 0, g, 1, 1e-3)[0])
     res = _run(_worker_exchange, mode, 64, world=world)     # 64-byte buckets: several
-    for rank, flat, issued, nb, n_ar in res:
+    for rank, flat, issued, nb, n_ar, order in res:
         assert nb >= 3
         assert issued == nb          # every bucket went out from a hook, inside backward
+        assert order == list(range(nb))      # in bucket order on every rank
         assert n_ar == nb            # one all-reduce per bucket, nothing else
         np.testing.assert_allclose(flat, np.concatenate(expect), rtol=1e-5, atol=1e-7)
 
@@ -268,3 +270,36 @@ def test_step_exchange_one_collective(world, variant):
             gx_ref = gx_ref.copy()
             gx_ref[:, :1] += cq * 2.0 / X.shape[0] * X[rank * n:(rank + 1) * n, :1]
         np.testing.assert_allclose(gx, gx_ref, rtol=1e-4, atol=1e-7)
+
+
+def test_buckets_issue_in_order_when_completed_out_of_order():
+    """A bucket whose tensors finish first still waits for its predecessors:
+    ranks whose backward ran in different orders issue identical sequences."""
+    from gan.core import collectives
+
+    class Opt:
+        def __init__(self, sizes):
+            self.params = [torch.nn.Parameter(torch.zeros(n)) for n in sizes]
+            offs = [0]
+            for n in sizes:
+                offs.append(offs[-1] + n)
+            self.offsets = offs
+            self.flat_grad = torch.zeros(offs[-1])
+
+    launched = []
+    orig = collectives.all_reduce_async
+    collectives.all_reduce_async = lambda t, g: launched.append(t.numel())
+    try:
+        opt = Opt([4, 4, 4, 4])
+        bk = collectives.GradBuckets(opt, None, bucket_bytes=16)    # one tensor per bucket
+        assert bk.buckets == [(3, 4), (2, 3), (1, 2), (0, 1)]
+        bk.arm()
+        for i in (0, 1, 3, 2):          # tensor 0 -> last bucket completes first
+            bk._hook(i)(opt.params[i])
+            if i == 0:
+                assert bk.launch_log == []
+        assert bk.launch_log == [0, 1, 2, 3]
+        bk.finish()
+        assert launched == [4, 4, 4, 4]
+    finally:
+        collectives.all_reduce_async = orig

@@ -16,8 +16,9 @@ from collections import defaultdict
 GROUPS = {
     'smmd_sn_power_iter': ('sn_p1_kernel', 'sn_p2_kernel', 'sn_r2_kernel', 'sn_p3_kernel'),
     'smmd_sn_weight_bwd': ('sn_bwd_a_kernel', 'sn_bwd_b_kernel'),
-    'smmd_adam_flat': ('opt_sqsum_kernel', 'opt_adam_kernel'),
-    'smmd_adam_flat_sn': ('opt_sqsum_kernel', 'opt_adam_sn_kernel'),
+    'smmd_adam_flat': ('opt_sqsum@opt_adam_kernel', 'opt_adam_kernel'),
+    'smmd_adam_flat_sn': ('opt_sqsum@opt_adam_sn_kernel', 'opt_adam_sn_kernel'),
+    'smmd_clip_by_norm_flat': ('opt_sqsum@opt_clip_kernel', 'opt_clip_kernel'),
     'smmd_mmd2_fwd': ('mmd2_fused_kernel', 'mmd2_tile_kernel'),
     'smmd_scaled_loss_fwd': ('sqnorm_partial_kernel', 'scaled_loss_final_kernel'),
     'smmd_scaled_loss_bwd': ('scaled_loss_bwd_kernel',),
@@ -30,12 +31,22 @@ SUM_CALLS = ('smmd_fold_pool_weights',)
 
 
 def per_kernel(path):
-    """kernel name -> (sum of the counter over its launches, launches)"""
+    """kernel name -> (sum of the counter over its launches, launches); the
+    norm pass (opt_sqsum) is attributed, launch by launch, to the update kernel
+    dispatched after it (the plain generator update and the SN-fused critic
+    update both start with one), under the pseudo-names 'opt_sqsum@<update>'."""
+    rows = [r for r in csv.DictReader(open(path)) if 'smmd::' in r['Kernel_Name']]
+    rows.sort(key=lambda r: int(r['Dispatch_Id']))
     acc = defaultdict(list)
-    for r in csv.DictReader(open(path)):
-        if 'smmd::' not in r['Kernel_Name']:
-            continue
-        acc[r['Kernel_Name']].append(float(r['Counter_Value']))
+    for i, r in enumerate(rows):
+        name = r['Kernel_Name']
+        if 'opt_sqsum_kernel' in name:
+            nxt = next((q['Kernel_Name'] for q in rows[i + 1:]
+                        if 'opt_adam' in q['Kernel_Name'] or 'opt_clip' in q['Kernel_Name']), '')
+            tag = ('opt_adam_sn_kernel' if 'opt_adam_sn' in nxt else
+                   'opt_adam_kernel' if 'opt_adam' in nxt else 'opt_clip_kernel')
+            name = 'opt_sqsum@' + tag
+        acc[name].append(float(r['Counter_Value']))
     return {k: (sum(v), len(v)) for k, v in acc.items()}
 
 
@@ -44,18 +55,16 @@ def main():
     write = per_kernel(sys.argv[2])
     out = {'_note': 'bytes per call; read = 2 * FETCH_SIZE(KB) * 1024 (gfx950 correction), '
                     'write = WRITE_SIZE(KB) * 1024'}
-    fused = any('opt_adam_sn_kernel' in k for k in fetch)
     for entry, kernels in GROUPS.items():
-        if entry == ('smmd_adam_flat' if fused else 'smmd_adam_flat_sn'):
-            continue        # the opt_* kernels belong to whichever entry the run used
         rd = wr = 0.0
         found = []
         calls = 0
         for kname in fetch:
             if any(k in kname for k in kernels):
                 rd += 2 * fetch[kname][0] * 1024
-                calls = (calls + fetch[kname][1] if entry in SUM_CALLS
-                         else max(calls, fetch[kname][1]))
+                if 'opt_sqsum@' not in kname:
+                    calls = (calls + fetch[kname][1] if entry in SUM_CALLS
+                             else max(calls, fetch[kname][1]))
                 found.append(kname.split('(')[0])
         for kname in write:
             if any(k in kname for k in kernels):
@@ -63,11 +72,12 @@ def main():
         # per call of the entry point = launches of its most frequent kernel
         # (the SN refresh skips P1 after a fused update: P1's bytes are spread
         # over the calls that did run it and those that did not)
-        if found:
+        if found and calls:
             rd /= calls
             wr /= calls
             out[entry] = {'read_bytes': round(rd), 'write_bytes': round(wr),
-                          'traffic_bytes': round(rd + wr), 'kernels': sorted(set(found))}
+                          'traffic_bytes': round(rd + wr), 'calls': calls,
+                          'kernels': sorted(set(found))}
     print(json.dumps(out, indent=1))
     if len(sys.argv) > 3:
         with open(sys.argv[3], 'w') as f:
