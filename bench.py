@@ -83,6 +83,27 @@ def imagenet_config(batch=BATCH):
     return f
 
 
+def celeba64_config(batch):
+    """configs/celebA_smmd.yml (g-resnet5: ResNet G + DCGAN5 critic, SN, no BN)
+    at 64 x 64, BASELINE configs[2] (the yml's own output_size is 160)."""
+    from gan.main import make_flags
+    f = make_flags(argv=['-config_file', os.path.join(PKG, 'configs', 'celebA_smmd.yml')])
+    f.batch_size = batch
+    f.output_size = 64
+    return f
+
+
+CONFIGS = {
+    'imagenet': (lambda b: imagenet_config(b),
+                 'imagenet_smmd 64x64 SNResNet G/D, rbf kernel, scaling, SN'),
+    'cifar10': (lambda b: cifar_config(b),
+                'cifar10_smmd 32x32 SNGAN G/D, rbf kernel, scaling, SN (BASELINE configs[1])'),
+    'celebA64': (lambda b: celeba64_config(b),
+                 'celebA_smmd g-resnet5 (ResNet G, DCGAN5 critic) at 64x64, rbf kernel, scaling, '
+                 'SN (BASELINE configs[2])'),
+}
+
+
 def cifar_config(batch):
     """configs/cifar10_smmd.yml (BASELINE configs[0]: batch 32, CPU)."""
     from gan.main import make_flags
@@ -446,6 +467,9 @@ def main():
     ap.add_argument('--batch', type=int, default=64,
                     help='images per GPU: 64 is the headline (imagenet_smmd.yml); 256 is '
                          'BASELINE configs[4] (the 256 x 256 pairwise tile per GPU)')
+    ap.add_argument('--config', default='imagenet', choices=sorted(CONFIGS),
+                    help='imagenet: the headline (BASELINE metric); cifar10 / celebA64: '
+                         'BASELINE configs[1] / [2] measured the same way')
     ap.add_argument('--steps', type=int, default=60)
     ap.add_argument('--warmup', type=int, default=12)
     ap.add_argument('--dp-mode', default='global', choices=['global', 'tower'])
@@ -458,6 +482,10 @@ def main():
                     help='1: torch.backends.cudnn.benchmark (MIOpen Find: times every '
                          'applicable solver per conv problem during warmup); the find '
                          'results persist in MIOPEN_USER_DB_PATH when set')
+    ap.add_argument('--graphs', type=int, default=0,
+                    help='1: the timed steps replay HIP graphs of the captured step kinds '
+                         '(model.enable_graphs; one GPU). Measured: no gain at batch 64 '
+                         '(GPU-bound), 1.85x at batch 8 (host-bound)')
     ap.add_argument('--cpu-seconds', type=float, default=20.0)
     ap.add_argument('--ref-schedule-steps', type=int, default=30,
                     help='steps timed with the reference schedule (both gradient sets '
@@ -500,12 +528,13 @@ def main():
     torch.backends.cudnn.benchmark = bool(args.miopen_find)
 
     from gan.core.smmd import SMMD
-    cfg = imagenet_config(BATCH)
+    cfg = CONFIGS[args.config][0](BATCH)
+    size = int(cfg.output_size)
     torch.manual_seed(2 + rank)
     model = SMMD(cfg, device=dev, process_group=dist.group.WORLD if world > 1 else None,
                  dp_mode=args.dp_mode, channels_last=bool(args.channels_last))
     gen = torch.Generator(device=dev).manual_seed(0 + rank)
-    images = [torch.rand(BATCH, 3, 64, 64, device=dev, generator=gen) for _ in range(4)]
+    images = [torch.rand(BATCH, 3, size, size, device=dev, generator=gen) for _ in range(4)]
     log = (lambda *a: print('[bench]', *a, file=sys.stderr, flush=True)) if rank == 0 else \
         (lambda *a: None)
 
@@ -516,6 +545,10 @@ def main():
         model.d_step(images[0])
         model.g_step(images[1])
     model.schedule = 'lean'
+    if args.graphs:
+        model.enable_graphs()       # capture every step kind before the warmup
+        model.step = 21
+        run_steps(model, images, 6)
     sync(world)
     log('primed D and G steps of both schedules in %.1f s' % (time.perf_counter() - tw))
 
@@ -541,6 +574,7 @@ def main():
     log('timed %d steps: %.2f ms/step' % (args.steps, dt / args.steps * 1e3))
 
     # 4. the reference schedule (both gradient sets every step, model.py:514)
+    model.enable_graphs(False)      # the rest runs eagerly
     ref_sched = None
     if args.ref_schedule_steps > 0:
         model.schedule = 'reference'
@@ -573,7 +607,7 @@ def main():
         # the SN output per layer: W_eff [N, K], or for a ConvMeanPool conv the
         # pool-folded 4 x 4 filter the bank writes directly (16 floats per 9)
         sn_out = sum(e.N * e.K * 16 // 9 if e.fold else e.N * e.K for e in model.sn_D.entries)
-        per_img = 3 * 64 * 64
+        per_img = 3 * size * size
         alg = {
             # sqsum pass reads g; update pass reads g, p, m, v and writes p, m, v
             'smmd_adam_flat[D]': model.d_optim.numel * 4 * 8,
@@ -667,7 +701,7 @@ def main():
         'n_gpus': world,
         'steps': args.steps,
         'warmup': args.warmup,
-        'prime_steps': 4,
+        'prime_steps': 4 + (6 if args.graphs else 0),
         'd_steps': counts['D'],
         'g_steps': counts['G'],
         'ms_per_step': round(ms_step, 3),
@@ -676,13 +710,14 @@ def main():
         'vs_baseline': None,
         'dtype': 'fp32',
         'data': 'synthetic (U[0,1] images in HBM, z~U(-1,1), random-init weights)',
-        'config': {'workload': 'imagenet_smmd 64x64 SNResNet G/D, rbf kernel, scaling, SN, '
-                               'batch %d/GPU, 5D+1G schedule' % BATCH,
-                   'model': 'snresnet', 'global_batch': BATCH * world, 'seq_len': None,
+        'config': {'workload': '%s, batch %d/GPU, 5D+1G schedule' % (CONFIGS[args.config][1],
+                                                                       BATCH),
+                   'model': cfg.architecture, 'global_batch': BATCH * world, 'seq_len': None,
                    'parallelism': 'dp%d' % world, 'dp_mode': args.dp_mode,
                    'memory_format': 'channels_last' if args.channels_last else 'nchw',
                    'miopen_winograd': bool(args.miopen_winograd),
                    'miopen_find': bool(args.miopen_find),
+                   'step_graphs': bool(args.graphs),
                    'conv_mean_pool': ('folded 4x4 stride-2 conv' if architecture.FOLD_POOL
                                       else 'conv3x3 + mean pool'),
                    'miopen_db': os.environ.get('MIOPEN_USER_DB_PATH')},

@@ -58,7 +58,7 @@ typedef struct {
 
 const char *smmd_status_string(smmd_status s);
 int smmd_abi_version(void);         /* bumped on any ABI change (2: Gram/poly,
-                                       3: smmd_sn_layer.fold) */
+                                       3: smmd_sn_layer.fold, 4: smmd_adam_flat_ex) */
 
 /* ---------------------------------------------------------------------------
  * Fused pairwise MMD^2 (forward + unit gradient).
@@ -277,6 +277,20 @@ smmd_status smmd_adam_flat_sn(float *param, const float *grad, float *m, float *
                               const int64_t *offsets, int n_tensors, float grad_scale,
                               float clip_norm, float lr, float beta1, float beta2, float eps,
                               int64_t step, void *ws, size_t ws_bytes,
+                              const smmd_sn_layer *layers, const int32_t *sn_tensor,
+                              int n_layers, void *sn_ws, size_t sn_ws_bytes,
+                              smmd_stream_t stream);
+
+/* smmd_adam_flat / smmd_adam_flat_sn (n_layers = 0: the plain update) with the
+ * bias-corrected step size lr_t = lr sqrt(1 - b2^t) / (1 - b1^t) read from
+ * DEVICE memory (lr_t [1] fp32) when the kernels execute, instead of lr and
+ * step passed by value: a HIP graph capturing the update then replays every
+ * step with the value the host writes before the replay (model.py:405-412,
+ * :458-468 semantics unchanged). */
+smmd_status smmd_adam_flat_ex(float *param, const float *grad, float *m, float *v,
+                              const int64_t *offsets, int n_tensors, float grad_scale,
+                              float clip_norm, const float *lr_t, float beta1, float beta2,
+                              float eps, void *ws, size_t ws_bytes,
                               const smmd_sn_layer *layers, const int32_t *sn_tensor,
                               int n_layers, void *sn_ws, size_t sn_ws_bytes,
                               smmd_stream_t stream);

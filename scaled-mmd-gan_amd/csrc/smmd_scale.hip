@@ -270,10 +270,17 @@ struct AdamArgs {
     float *p, *m, *v;
     const float *g;
     const double *part;     // norm-pass partials
+    const float *lr_t_dev;  // non-NULL: lr_t read at execution time (graph replay)
     float clip;             // > 0: per-tensor clip_by_norm
     int vec;
     AdamK k;                // k.f set per tensor
 };
+
+__device__ __forceinline__ AdamK adam_k(const AdamArgs &a) {
+    AdamK k = a.k;
+    if (a.lr_t_dev) k.lr_t = a.lr_t_dev[0];
+    return k;
+}
 
 // update block b of the table (blocks of skipped tensors return at once)
 __device__ __forceinline__ void opt_adam_block(const OptTable &t, int b, const AdamArgs &a) {
@@ -285,7 +292,7 @@ __device__ __forceinline__ void opt_adam_block(const OptTable &t, int b, const A
     const float *__restrict__ g = a.g;
     const int vec = a.vec;
     __shared__ float sh[1];
-    AdamK k = a.k;
+    AdamK k = adam_k(a);
     k.f = (a.clip > 0.f) ? clip_factor(t, ti, a.part, a.clip, sh) : 1.f;
     int64_t lo, hi;
     opt_range(t, ti, b, lo, hi);
@@ -351,7 +358,7 @@ template <int H>
 __global__ __launch_bounds__(256) void opt_adam_sn_kernel(OptTable t, SnAdamTable st,
                                                           AdamArgs a) {
     if ((int)blockIdx.x < st.total_tiles)
-        sn_adam_tile<H>(st, blockIdx.x, a.k, a.part, a.clip);
+        sn_adam_tile<H>(st, blockIdx.x, adam_k(a), a.part, a.clip);
     else
         opt_adam_block(t, blockIdx.x - st.total_tiles, a);
 }
@@ -373,6 +380,7 @@ static AdamArgs adam_args(float *p, const float *g, float *m, float *v, const vo
     a.v = v;
     a.g = g;
     a.part = (const double *)ws;
+    a.lr_t_dev = nullptr;
     a.clip = clip;
     a.vec = vec;
     a.k.gscale = gscale;
@@ -532,17 +540,20 @@ smmd_status smmd_clip_by_norm_flat(float *grad, const int64_t *offsets, int n_te
     return SMMD_OK;
 }
 
-smmd_status smmd_adam_flat(float *param, const float *grad, float *m, float *v,
-                           const int64_t *offsets, int n_tensors, float grad_scale,
-                           float clip_norm, float lr, float beta1, float beta2, float eps,
-                           int64_t step, void *ws, size_t ws_bytes, smmd_stream_t stream) {
-    if (!param || !grad || !m || !v || !offsets || n_tensors < 1 || step < 1) return SMMD_EINVAL;
+// tf.train.AdamOptimizer: lr_t = lr * sqrt(1 - b2^t) / (1 - b1^t)
+static double adam_lr_t(float lr, float beta1, float beta2, int64_t step) {
+    return (double)lr * sqrt(1.0 - pow((double)beta2, (double)step)) /
+           (1.0 - pow((double)beta1, (double)step));
+}
+
+static smmd_status adam_flat_impl(float *param, const float *grad, float *m, float *v,
+                                  const int64_t *offsets, int n_tensors, float grad_scale,
+                                  float clip_norm, double lr_t, const float *lr_t_dev,
+                                  float beta1, float beta2, float eps, void *ws, size_t ws_bytes,
+                                  hipStream_t s) {
+    if (!param || !grad || !m || !v || !offsets || n_tensors < 1) return SMMD_EINVAL;
     if (clip_norm > 0.f && (!ws || ws_bytes < smmd_opt_workspace_bytes(offsets, n_tensors)))
         return SMMD_EWORKSPACE;
-    // tf.train.AdamOptimizer: lr_t = lr * sqrt(1 - b2^t) / (1 - b1^t)
-    const double lr_t = (double)lr * sqrt(1.0 - pow((double)beta2, (double)step)) /
-                        (1.0 - pow((double)beta1, (double)step));
-    hipStream_t s = (hipStream_t)stream;
     for (int first = 0; first < n_tensors; first += OPT_MAX) {
         const int count = (n_tensors - first < OPT_MAX) ? n_tensors - first : OPT_MAX;
         OptTable ts, tu;
@@ -553,23 +564,34 @@ smmd_status smmd_adam_flat(float *param, const float *grad, float *m, float *v,
         if (clip_norm > 0.f)
             hipLaunchKernelGGL(opt_sqsum_kernel, dim3(ts.total_blocks), dim3(256), 0, s, ts, grad,
                                grad_scale, vec, (double *)ws);
-        hipLaunchKernelGGL(opt_adam_kernel, dim3(tu.total_blocks), dim3(256), 0, s, tu,
-                           adam_args(param, grad, m, v, ws, grad_scale, clip_norm, lr_t, beta1,
-                                     beta2, eps, vec));
+        AdamArgs aa = adam_args(param, grad, m, v, ws, grad_scale, clip_norm, lr_t, beta1, beta2,
+                                eps, vec);
+        aa.lr_t_dev = lr_t_dev;
+        hipLaunchKernelGGL(opt_adam_kernel, dim3(tu.total_blocks), dim3(256), 0, s, tu, aa);
         smmd_status st = last_launch_status();
         if (st != SMMD_OK) return st;
     }
     return SMMD_OK;
 }
 
-smmd_status smmd_adam_flat_sn(float *param, const float *grad, float *m, float *v,
-                              const int64_t *offsets, int n_tensors, float grad_scale,
-                              float clip_norm, float lr, float beta1, float beta2, float eps,
-                              int64_t step, void *ws, size_t ws_bytes,
-                              const smmd_sn_layer *layers, const int32_t *sn_tensor,
-                              int n_layers, void *sn_ws, size_t sn_ws_bytes,
-                              smmd_stream_t stream) {
-    if (!param || !grad || !m || !v || !offsets || n_tensors < 1 || step < 1) return SMMD_EINVAL;
+smmd_status smmd_adam_flat(float *param, const float *grad, float *m, float *v,
+                           const int64_t *offsets, int n_tensors, float grad_scale,
+                           float clip_norm, float lr, float beta1, float beta2, float eps,
+                           int64_t step, void *ws, size_t ws_bytes, smmd_stream_t stream) {
+    if (step < 1) return SMMD_EINVAL;
+    return adam_flat_impl(param, grad, m, v, offsets, n_tensors, grad_scale, clip_norm,
+                          adam_lr_t(lr, beta1, beta2, step), nullptr, beta1, beta2, eps, ws,
+                          ws_bytes, (hipStream_t)stream);
+}
+
+static smmd_status adam_flat_sn_impl(float *param, const float *grad, float *m, float *v,
+                                     const int64_t *offsets, int n_tensors, float grad_scale,
+                                     float clip_norm, double lr_t, const float *lr_t_dev,
+                                     float beta1, float beta2, float eps, void *ws,
+                                     size_t ws_bytes, const smmd_sn_layer *layers,
+                                     const int32_t *sn_tensor, int n_layers, void *sn_ws,
+                                     size_t sn_ws_bytes, hipStream_t s) {
+    if (!param || !grad || !m || !v || !offsets || n_tensors < 1) return SMMD_EINVAL;
     if (!layers || !sn_tensor || n_layers < 1 || n_layers > SMMD_SN_MAX_LAYERS) return SMMD_EINVAL;
     if (n_tensors > OPT_MAX) return SMMD_EUNSUPPORTED;     // one partial slab for every tensor
     if (clip_norm > 0.f && (!ws || ws_bytes < smmd_opt_workspace_bytes(offsets, n_tensors)))
@@ -580,9 +602,6 @@ smmd_status smmd_adam_flat_sn(float *param, const float *grad, float *m, float *
         if (ti < 0 || ti >= n_tensors || skip[ti]) return SMMD_EINVAL;
         skip[ti] = 1;
     }
-    const double lr_t = (double)lr * sqrt(1.0 - pow((double)beta2, (double)step)) /
-                        (1.0 - pow((double)beta1, (double)step));
-    hipStream_t s = (hipStream_t)stream;
     OptTable ts, tu;
     if (!build_opt(offsets, 0, n_tensors, OPT_SQ_CHUNK, ts) ||
         !build_opt(offsets, 0, n_tensors, OPT_UP_CHUNK, tu, skip))
@@ -601,8 +620,9 @@ smmd_status smmd_adam_flat_sn(float *param, const float *grad, float *m, float *
     if (clip_norm > 0.f)
         hipLaunchKernelGGL(opt_sqsum_kernel, dim3(ts.total_blocks), dim3(256), 0, s, ts, grad,
                            grad_scale, vec, (double *)ws);
-    const AdamArgs aa = adam_args(param, grad, m, v, ws, grad_scale, clip_norm, lr_t, beta1, beta2,
-                                  eps, vec);
+    AdamArgs aa = adam_args(param, grad, m, v, ws, grad_scale, clip_norm, lr_t, beta1, beta2, eps,
+                            vec);
+    aa.lr_t_dev = lr_t_dev;
     const dim3 grid(snt.total_tiles + tu.total_blocks);
     const int hg = sn_adam_groups();
     if (hg == 1)
@@ -612,6 +632,36 @@ smmd_status smmd_adam_flat_sn(float *param, const float *grad, float *m, float *
     else
         hipLaunchKernelGGL(opt_adam_sn_kernel<2>, grid, dim3(256), 0, s, tu, snt, aa);
     return last_launch_status();
+}
+
+smmd_status smmd_adam_flat_sn(float *param, const float *grad, float *m, float *v,
+                              const int64_t *offsets, int n_tensors, float grad_scale,
+                              float clip_norm, float lr, float beta1, float beta2, float eps,
+                              int64_t step, void *ws, size_t ws_bytes,
+                              const smmd_sn_layer *layers, const int32_t *sn_tensor,
+                              int n_layers, void *sn_ws, size_t sn_ws_bytes,
+                              smmd_stream_t stream) {
+    if (step < 1) return SMMD_EINVAL;
+    return adam_flat_sn_impl(param, grad, m, v, offsets, n_tensors, grad_scale, clip_norm,
+                             adam_lr_t(lr, beta1, beta2, step), nullptr, beta1, beta2, eps, ws,
+                             ws_bytes, layers, sn_tensor, n_layers, sn_ws, sn_ws_bytes,
+                             (hipStream_t)stream);
+}
+
+smmd_status smmd_adam_flat_ex(float *param, const float *grad, float *m, float *v,
+                              const int64_t *offsets, int n_tensors, float grad_scale,
+                              float clip_norm, const float *lr_t, float beta1, float beta2,
+                              float eps, void *ws, size_t ws_bytes,
+                              const smmd_sn_layer *layers, const int32_t *sn_tensor,
+                              int n_layers, void *sn_ws, size_t sn_ws_bytes,
+                              smmd_stream_t stream) {
+    if (!lr_t) return SMMD_EINVAL;
+    if (n_layers == 0)
+        return adam_flat_impl(param, grad, m, v, offsets, n_tensors, grad_scale, clip_norm, 0.0,
+                              lr_t, beta1, beta2, eps, ws, ws_bytes, (hipStream_t)stream);
+    return adam_flat_sn_impl(param, grad, m, v, offsets, n_tensors, grad_scale, clip_norm, 0.0,
+                             lr_t, beta1, beta2, eps, ws, ws_bytes, layers, sn_tensor, n_layers,
+                             sn_ws, sn_ws_bytes, (hipStream_t)stream);
 }
 
 }  // extern "C"

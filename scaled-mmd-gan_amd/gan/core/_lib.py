@@ -24,7 +24,7 @@ SMMD_SN_MAX_LAYERS = 32
 SN_P1_READY = 1            # smmd_sn_power_iter_ex flag
 OPT_MAX_FUSED = 96         # tensors smmd_adam_flat_sn takes in one call
 SN_MAX_FUSED = 16          # SN layers smmd_adam_flat_sn takes in one call
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 KIND_RBF, KIND_RQ, KIND_DISTANCE, KIND_DOT = 0, 1, 2, 3
 
@@ -107,6 +107,9 @@ _SIGS = {
                             _F, _F, _I64, _P, _SZ, _P]),
     'smmd_adam_flat_sn': (_I, [_P, _P, _P, _P, ctypes.POINTER(ctypes.c_int64), _I, _F, _F, _F,
                                _F, _F, _F, _I64, _P, _SZ, ctypes.POINTER(SnLayer),
+                               ctypes.POINTER(ctypes.c_int32), _I, _P, _SZ, _P]),
+    'smmd_adam_flat_ex': (_I, [_P, _P, _P, _P, ctypes.POINTER(ctypes.c_int64), _I, _F, _F, _P,
+                               _F, _F, _F, _P, _SZ, ctypes.POINTER(SnLayer),
                                ctypes.POINTER(ctypes.c_int32), _I, _P, _SZ, _P]),
     'smmd_poly_sums_workspace_bytes': (_SZ, [_I, _I, _I]),
     'smmd_poly_kernel_sums': (_I, [_P, _I, _P, _I, _I, ctypes.c_double, ctypes.c_double, _I, _P,

@@ -44,6 +44,10 @@ def _bn_or_id(use, c):
 FOLD_POOL = os.environ.get('SMMD_FOLD_POOL', '1') != '0'
 # SMMD_FOLD_UP=0 restores the literal upsample -> conv order of UpsampleConv
 FOLD_UP = os.environ.get('SMMD_FOLD_UP', '1') != '0'
+# Host-side caches of folded filters (the generator's across critic steps,
+# the critic's across its real / fake calls).  A captured step graph
+# (model.StepGraphs) must recompute them on every replay: it turns this off.
+CACHE_FOLDS = True
 
 
 class _Up(nn.Module):
@@ -61,7 +65,7 @@ class _Up(nn.Module):
         change once per 5 + 1 steps.  With grad enabled it is rebuilt every
         call: a cached K would carry an autograd graph that a non-retaining
         backward frees."""
-        if torch.is_grad_enabled():
+        if torch.is_grad_enabled() or not CACHE_FOLDS:
             self._kcache = None
             return fold_up_weight(w).contiguous()
         key = (_optim.param_epoch(w), w._version)
@@ -139,7 +143,7 @@ class prefolded:
             ws = [m.conv.effective_weight() for m in self.mods]
             key = (torch.is_grad_enabled(),
                    tuple((w._version, _optim.param_epoch(w), w.requires_grad) for w in ws))
-            cache = getattr(self.net, '_fold_cache', None)
+            cache = getattr(self.net, '_fold_cache', None) if CACHE_FOLDS else None
             if (cache is not None and cache[0] == key
                     and all(a is b for a, b in zip(cache[1], ws))):
                 ws4 = cache[2]

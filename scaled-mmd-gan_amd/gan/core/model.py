@@ -381,7 +381,38 @@ class MMD_GAN:
             with convops.no_input_grad(self._last_images):
                 d_loss.backward()
         self._exchange(self.d_optim)
-        return g_loss, d_loss, aux
+        return self._detach_step_state()
+
+    def _detach_step_state(self):
+        """After a step's backward: keep the reference attributes (self.g_loss,
+        self.d_images, ...) as values, so no tensor keeps the step's autograd
+        graph -- its activations, and the parameters' gradient-accumulation
+        nodes bound to this step's stream -- alive into the next step (a
+        captured step graph must create its own).  Returns (g_loss, d_loss,
+        aux) detached."""
+        for name in ('g_loss', 'd_loss', 'd_images', 'd_G', 'G', 'images', '_last_images'):
+            v = getattr(self, name, None)
+            if torch.is_tensor(v):
+                setattr(self, name, v.detach())
+        for name in ('d_images_layers', 'd_G_layers'):
+            v = getattr(self, name, None)
+            if v:
+                setattr(self, name, {k: t.detach() for k, t in v.items()})
+        aux = self.aux.detach() if torch.is_tensor(self.aux) else self.aux
+        self.aux = aux
+        # the SN layers' effective weights are outputs of the step's SN node
+        # (whose backward holds the weights' accumulation nodes): keep values
+        for bank in (self.sn_D, self.sn_G):
+            for e in bank.entries:
+                mod = e.module
+                if torch.is_tensor(getattr(mod, 'w_eff', None)):
+                    mod.w_eff = mod.w_eff.detach()
+                if torch.is_tensor(getattr(mod, 'w_fold', None)):
+                    mod.w_fold = mod.w_fold.detach()
+        for net in (self.discriminator, self.generator):
+            if getattr(net, '_fold_cache', None) is not None:
+                net._fold_cache = None
+        return self.g_loss, self.d_loss, aux
 
     def g_step(self, images):
         # critic weights are constants of the generator update: freeze them
@@ -407,19 +438,36 @@ class MMD_GAN:
         finally:
             for p in self.d_vars:
                 p.requires_grad_(True)
-        return g_loss, d_loss, aux
+        return self._detach_step_state()
 
     def train_step(self, images):
         """model.py:507-546 (lean: only the gradient set being applied)."""
         step = self.step
         self.set_counters(step)
+        graphs = getattr(self, '_graphs', None)
         if self.d_counter == 0:
-            g_loss, d_loss, aux = self.g_step(images)
+            g_loss, d_loss, aux = (graphs.run(False, images) if graphs is not None
+                                   else self.g_step(images))
             self.step += 1                                   # global_step (model.py:460-463)
         else:
-            g_loss, d_loss, aux = self.d_step(images)
+            g_loss, d_loss, aux = (graphs.run(True, images) if graphs is not None
+                                   else self.d_step(images))
         self.last = {'g_loss': g_loss.detach(), 'd_loss': d_loss.detach(), 'aux': aux}
         return g_loss, d_loss, step
+
+    def enable_graphs(self, on=True):
+        """Run ``train_step`` as HIP-graph replays of the captured critic and
+        generator steps (StepGraphs).  One GPU, lean schedule only."""
+        if not on:
+            if getattr(self, '_graphs', None) is not None:
+                self._graphs.close()
+            self._graphs = None
+            return
+        if self.world > 1:
+            raise NotImplementedError('step graphs are single-GPU (the collectives run eagerly)')
+        if self.schedule != 'lean':
+            raise NotImplementedError("step graphs capture the lean schedule")
+        self._graphs = StepGraphs(self)
 
     def check_finite(self):
         """NaN asserts of model.py:537-538 (forces a host sync)."""
@@ -511,3 +559,96 @@ class MMD_GAN:
         self.d_counter, self.g_counter = sd['counters']
         self.g_optim.lr = self.lr
         self.d_optim.lr = self.lr * self.config.learning_rate_D / self.config.learning_rate
+
+
+class StepGraphs:
+    """The lean training step as HIP-graph replays (one GPU).
+
+    A step's ~800 kernel launches (MIOpen convolutions, PyTorch elementwise
+    ops, the autograd double backward and the libsmmd_hip calls) are
+    recorded once per step kind and replayed, which removes the host's
+    per-launch cost and the idle gaps between the step's phases.  The kinds
+    are the critic step (with or without the SN bank's first power-iteration
+    pass already written by the previous critic update) and the generator
+    step.  Everything a replay must change is read from device memory: the
+    images (copied into a static buffer), z (the graph-safe RNG), the Adam
+    step size (``FlatAdam.lr_t_dev``, written before every replay); the
+    host-side folded-filter caches are off while graphs are in use, and the
+    host bookkeeping of a step (optimizer step counts, the SN bank's
+    first-pass token) is replayed by ``run``.  A new scaling coefficient is
+    recaptured automatically; anything else that changes a launch argument
+    (a checkpoint load re-pointing tensors, another batch shape) needs
+    ``invalidate``."""
+
+    def __init__(self, model):
+        from . import architecture
+        self.m = model
+        self.graphs, self.outs = {}, {}
+        self.pool = None
+        self.images = None
+        self.key = None
+        architecture.CACHE_FOLDS = False
+        for opt in (model.d_optim, model.g_optim):
+            opt.graph_mode = True
+
+    def close(self):
+        from . import architecture
+        architecture.CACHE_FOLDS = True
+        for opt in (self.m.d_optim, self.m.g_optim):
+            opt.graph_mode = False
+        self.graphs, self.outs, self.pool = {}, {}, None
+
+    def invalidate(self):
+        self.graphs, self.outs = {}, {}
+
+    @staticmethod
+    def _ready(bank):
+        return bool(bank.entries) and bank._p1_token is not None and \
+            bank._p1_token == bank._state_token()
+
+    def _kind(self, critic):
+        m = self.m
+        return (critic, self._ready(m.sn_D), self._ready(m.sn_G))
+
+    def _bookkeeping(self, critic):
+        """The host effects of one step that a replay does not re-run."""
+        m = self.m
+        opt = m.d_optim if critic else m.g_optim
+        opt.advance()
+        for bank in (m.sn_D, m.sn_G):
+            bank._p1_token = None                 # each refresh consumes it
+        if opt._sn is not None:
+            opt._sn[0].mark_p1_ready()            # the fused update wrote P1
+
+    def _capture(self, kind, critic):
+        m = self.m
+        tokens = (m.sn_D._p1_token, m.sn_G._p1_token)
+        counts = (m.d_optim.step_count, m.g_optim.step_count)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, pool=self.pool):
+            out = m.d_step(self.images) if critic else m.g_step(self.images)
+        self.pool = g.pool()
+        # the capture ran the host side of one step without executing it
+        m.sn_D._p1_token, m.sn_G._p1_token = tokens
+        m.d_optim.step_count, m.g_optim.step_count = counts
+        self.graphs[kind], self.outs[kind] = g, out
+
+    def run(self, critic, images):
+        m = self.m
+        key = m.sc
+        if key != self.key:                       # sc is baked into the graphs (lr is not)
+            self.invalidate()
+            self.key = key
+        if self.images is None or self.images.shape != images.shape:
+            self.images = torch.empty_like(images)
+            self.invalidate()
+        self.images.copy_(images)
+        kind = self._kind(critic)
+        if kind not in self.graphs:
+            self._capture(kind, critic)
+        opt = m.d_optim if critic else m.g_optim
+        opt.lr_t_dev.fill_(opt.lr_t(opt.step_count + 1))
+        self.graphs[kind].replay()
+        self._bookkeeping(critic)
+        return self.outs[kind]

@@ -17,6 +17,7 @@ the first pass of the bank's next power iteration, which the next
 from __future__ import annotations
 
 import ctypes
+import math
 import os
 
 import torch
@@ -66,6 +67,10 @@ class FlatAdam:
                 p.grad = self._view(self.flat_grad, p, o)
         self.step_count = 0
         self._sn = None
+        # graph mode (model.StepGraphs): the update reads its bias-corrected
+        # step size from this device scalar, written before every replay
+        self.graph_mode = False
+        self.lr_t_dev = torch.zeros(1, device=dev, dtype=torch.float32)
         nbytes = _lib.lib().smmd_opt_workspace_bytes(self.offsets, len(self.params))
         self.ws = torch.zeros(max(nbytes, 256), dtype=torch.uint8, device=dev)
 
@@ -137,11 +142,26 @@ class FlatAdam:
             arr[k].N, arr[k].K = e.N, e.K
         return arr
 
-    def step(self, grad_scale=1.0, clip=True, lr=None):
-        self._check_grads()
+    def lr_t(self, step=None, lr=None):
+        """tf.train.AdamOptimizer's lr_t = lr sqrt(1 - b2^t) / (1 - b1^t) in
+        double, as smmd_adam_flat computes it (model.py:405-412)."""
+        t = self.step_count if step is None else step
+        lr = self.lr if lr is None else lr
+        return lr * math.sqrt(1.0 - self.beta2 ** t) / (1.0 - self.beta1 ** t)
+
+    def advance(self):
+        """Host bookkeeping of one update (step count, parameter epoch); a
+        graph replay of the update calls it instead of ``step``."""
         self.step_count += 1
         key = self.flat_param.untyped_storage().data_ptr()
         _EPOCH[key] = _EPOCH.get(key, 0) + 1
+
+    def step(self, grad_scale=1.0, clip=True, lr=None):
+        self._check_grads()
+        self.advance()
+        if self.graph_mode:
+            self._step_dev(grad_scale, clip)
+            return
         c = float(self.clip_norm) if clip else 0.0
         args = (_lib.ptr(self.flat_param), _lib.ptr(self.flat_grad), _lib.ptr(self.m),
                 _lib.ptr(self.v), self.offsets, len(self.params), float(grad_scale), c,
@@ -160,6 +180,29 @@ class FlatAdam:
         with _lib.timed('smmd_adam_flat[%s]' % self.name):
             st = _lib.lib().smmd_adam_flat(*args, stream)
         _lib.check(st, 'smmd_adam_flat')
+
+    def _step_dev(self, grad_scale, clip):
+        """The update with lr_t from ``lr_t_dev`` (smmd_adam_flat_ex): what a
+        captured step graph replays.  Outside a capture the scalar is written
+        here; during one the replaying code writes it before each replay."""
+        if not torch.cuda.is_current_stream_capturing():
+            self.lr_t_dev.fill_(self.lr_t())
+        c = float(self.clip_norm) if clip else 0.0
+        stream = _lib.stream_handle(self.flat_grad.device)
+        layers = self._sn_layers() if self._sn is not None else None
+        if layers is not None:
+            bank, idx = self._sn
+            n, sn_ws, sn_b = len(bank.entries), _lib.ptr(bank.ws), bank.ws.numel()
+        else:
+            idx, n, sn_ws, sn_b = None, 0, None, 0
+        st = _lib.lib().smmd_adam_flat_ex(
+            _lib.ptr(self.flat_param), _lib.ptr(self.flat_grad), _lib.ptr(self.m),
+            _lib.ptr(self.v), self.offsets, len(self.params), float(grad_scale), c,
+            _lib.ptr(self.lr_t_dev), float(self.beta1), float(self.beta2), float(self.eps),
+            _lib.ptr(self.ws), self.ws.numel(), layers, idx, n, sn_ws, sn_b, stream)
+        _lib.check(st, 'smmd_adam_flat_ex')
+        if layers is not None:
+            bank.mark_p1_ready()
 
     def state_dict(self):
         return {'m': self.m.clone(), 'v': self.v.clone(), 'step': self.step_count,

@@ -5,7 +5,7 @@ scaled loss -> double backward -> HIP SN backward) is compared with the
 oracle's CPU op-by-op mirror of the TF graph (oracle/tf_mirror.py) from the
 same weights, u vectors, images and z.  Tolerances (MIOpen fp32 convs vs CPU
 fp32 convs, same graph): d_loss rtol 1e-3; per-tensor gradients
-|d| <= max(t max|ref|, 1e-5 max over all tensors) + t |ref| with t = 2e-3, and
+|d| <= max(t max|ref|, 5e-5 max over all tensors) + t |ref| with t = 2e-3, and
 t = 5e-3 at the configs' full widths and batch 64 (64x longer fp32 reductions
 over the batch in a different order: MIOpen's vs the CPU's).
 """
@@ -80,9 +80,10 @@ def test_critic_step_matches_tf_mirror(dev, arch, size, dim, batch, cl):
         got = got.numpy().astype(np.float64)
         ref = mirror.to_product(name, rg).numpy().astype(np.float64)
         # exact zeros (e.g. the output bias: RBF-MMD is translation invariant) are
-        # rounding noise in both: absolute floor 1e-5 of the largest gradient
+        # rounding noise in both (either sign): absolute floor 5e-5 of the
+        # largest gradient
         t = 5e-3 if batch == 64 else 2e-3
-        tol = max(t * np.abs(ref).max(), 1e-5 * gmax) + t * np.abs(ref)
+        tol = max(t * np.abs(ref).max(), 5e-5 * gmax) + t * np.abs(ref)
         assert (np.abs(got - ref) <= tol + 1e-12).all(), (name, np.abs(got - ref).max(),
                                                            np.abs(ref).max())
     # u advanced exactly as the reference's u.assign(u') (sn.py:39-46)
@@ -287,3 +288,57 @@ def test_main_cli_scorer_drives_lr_schedule(dev, tmp_path, monkeypatch):
         warnings.simplefilter('always')
         M.main(base + ['-name', 'run2'])
     assert any('Inception featurizer' in str(x.message) for x in w)
+
+
+def test_step_graphs_match_eager(dev):
+    """model.enable_graphs(): the lean step replayed from HIP graphs (one per
+    step kind) trains as the eager step does, from the same state through
+    every kind (critic after critic, critic after generator, generator).
+    MIOpen's weight gradients are not bitwise deterministic and the GAN
+    dynamics amplify that noise, so a second eager copy is the yardstick:
+    eager vs graph must stay within 3x eager vs eager (+1e-3 of the update;
+    a stale tensor or a wrong step size in a replay is O(1) there)."""
+    from gan.core.smmd import SMMD
+    torch.manual_seed(0)
+    cfg = _cfg()
+    a = SMMD(cfg, device=dev)
+    g = torch.Generator().manual_seed(3)
+    imgs = [torch.rand(8, 3, 32, 32, generator=g).to(dev) for _ in range(3)]
+    z = torch.empty(8, 128).uniform_(-1, 1, generator=g).to(dev)
+    a.sample_z = lambda n: z
+    a.step = 25
+    for i in range(12):                        # eager: every step kind runs once first
+        a.train_step(imgs[i % 3])
+    copies = []
+    for _ in range(2):
+        m = SMMD(cfg, device=dev)
+        m.load_state_dict(a.state_dict())
+        m.sample_z = lambda n: z
+        copies.append(m)
+    b, c = copies
+    start = [t.clone() for t in (a.d_optim.flat_param, a.g_optim.flat_param)]
+    b.enable_graphs()
+    for i in range(14):
+        for m in (a, b, c):
+            m.train_step(imgs[i % 3])
+    torch.cuda.synchronize()
+    assert {k[0] for k in b._graphs.graphs} == {True, False}
+    assert len(b._graphs.graphs) == 3
+    assert (a.step, a.d_counter, a.g_counter) == (b.step, b.d_counter, b.g_counter)
+    assert (a.d_optim.step_count, a.g_optim.step_count) == \
+        (b.d_optim.step_count, b.g_optim.step_count)
+
+    def dist(x, y):
+        return float((x - y).norm())
+    for name in ('d_optim', 'g_optim'):
+        oa, ob, oc = (getattr(m, name) for m in (a, b, c))
+        p0 = start[0] if name == 'd_optim' else start[1]
+        moved = dist(oa.flat_param, p0)
+        assert moved > 0
+        for t in ('flat_param', 'm', 'v'):
+            ta, tb, tc = (getattr(o, t) for o in (oa, ob, oc))
+            noise = dist(ta, tc)
+            assert dist(ta, tb) <= 3 * noise + 1e-3 * max(moved, float(ta.norm())), \
+                (name, t, dist(ta, tb), noise)
+    b.enable_graphs(False)
+    b.train_step(imgs[0])                      # back to eager
