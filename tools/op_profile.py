@@ -34,7 +34,8 @@ def main():
         model.train_step(images)
     torch.cuda.synchronize()
     from torch.profiler import ProfilerActivity, profile
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA],
+                 record_shapes=True) as prof:
         for _ in range(args.steps):
             model.train_step(images)
         torch.cuda.synchronize()
@@ -43,6 +44,14 @@ def main():
     os.makedirs(os.path.dirname(args.out) or '.', exist_ok=True)
     with open(args.out, 'w') as f:
         f.write(tab)
+    # the elementwise ops by input shape (which tensors the adds accumulate)
+    shp = prof.key_averages(group_by_input_shape=True)
+    rows = [e for e in shp if e.key in ('aten::add_', 'aten::add', 'aten::mul', 'aten::fill_')]
+    rows.sort(key=lambda e: -e.self_device_time_total)
+    with open(args.out.replace('.txt', '_shapes.txt'), 'w') as f:
+        for e in rows[:60]:
+            f.write('%-12s %10.1f us total %5d calls  %s\n' % (
+                e.key, e.self_device_time_total, e.count, str(e.input_shapes)[:160]))
     print(tab[:6000])
 
 
