@@ -295,12 +295,15 @@ def test_step_graphs_match_eager(dev):
     step kind) trains as the eager step does, from the same state through
     every kind (critic after critic, critic after generator, generator).
     MIOpen's weight gradients are not bitwise deterministic and the GAN
-    dynamics amplify that noise, so a second eager copy is the yardstick:
-    eager vs graph must stay within 3x eager vs eager (+1e-3 of the update;
-    a stale tensor or a wrong step size in a replay is O(1) there)."""
+    dynamics amplify that noise over steps, so the run uses a tiny learning
+    rate (the states stay equal to far below the gradients' rounding, so the
+    moments compare tightly) and a second eager copy calibrates the rest:
+    parameters within 5 % of the update they made (+3x the eager-vs-eager
+    spread), moments within 1e-3 (+3x); a stale tensor or a wrong step size
+    in a replay is O(1) there."""
     from gan.core.smmd import SMMD
     torch.manual_seed(0)
-    cfg = _cfg()
+    cfg = _cfg(learning_rate=1e-8)
     a = SMMD(cfg, device=dev)
     g = torch.Generator().manual_seed(3)
     imgs = [torch.rand(8, 3, 32, 32, generator=g).to(dev) for _ in range(3)]
@@ -338,7 +341,7 @@ def test_step_graphs_match_eager(dev):
         for t in ('flat_param', 'm', 'v'):
             ta, tb, tc = (getattr(o, t) for o in (oa, ob, oc))
             noise = dist(ta, tc)
-            assert dist(ta, tb) <= 3 * noise + 1e-3 * max(moved, float(ta.norm())), \
-                (name, t, dist(ta, tb), noise)
+            lim = 0.05 * moved if t == 'flat_param' else 1e-3 * float(ta.norm())
+            assert dist(ta, tb) <= 3 * noise + lim, (name, t, dist(ta, tb), noise, lim)
     b.enable_graphs(False)
     b.train_step(imgs[0])                      # back to eager
