@@ -46,6 +46,15 @@ def main():
         f.write(tab)
     # the elementwise ops by input shape (which tensors the adds accumulate)
     shp = prof.key_averages(group_by_input_shape=True)
+    conv = [e for e in shp if e.key in ('aten::miopen_convolution', 'aten::convolution_backward',
+                                        'aten::miopen_convolution_transpose',
+                                        'aten::cudnn_convolution', 'aten::convolution')]
+    conv.sort(key=lambda e: -e.self_device_time_total)
+    with open(args.out.replace('.txt', '_convs.txt'), 'w') as f:
+        for e in conv[:80]:
+            f.write('%-36s %10.1f us total %5d calls %8.1f us/call  %s\n' % (
+                e.key, e.self_device_time_total, e.count, e.self_device_time_total / e.count,
+                str(e.input_shapes)[:200]))
     rows = [e for e in shp if e.key in ('aten::add_', 'aten::add', 'aten::mul', 'aten::fill_')]
     rows.sort(key=lambda e: -e.self_device_time_total)
     with open(args.out.replace('.txt', '_shapes.txt'), 'w') as f:
