@@ -58,7 +58,8 @@ typedef struct {
 
 const char *smmd_status_string(smmd_status s);
 int smmd_abi_version(void);         /* bumped on any ABI change (2: Gram/poly,
-                                       3: smmd_sn_layer.fold, 4: smmd_adam_flat_ex) */
+                                       3: smmd_sn_layer.fold, 4: smmd_adam_flat_ex,
+                                       5: smmd_conv3x3_thin*) */
 
 /* ---------------------------------------------------------------------------
  * Fused pairwise MMD^2 (forward + unit gradient).
@@ -361,12 +362,45 @@ smmd_status smmd_fold_pool_weights(const float *const *src, float *const *dst,
  * tensor [N, C, HW] (TF's BiasAddGrad of the bias_add in snops.conv2d,
  * gan/core/snops.py:79-80, and resnet Conv2D, gan/core/resnet/ops/conv2d.py:34-35).
  * Fixed-order two-stage sum; workspace from smmd_channel_sum_workspace_bytes.
- * gy must be 16-byte aligned when HW % 4 == 0.
+ * float4 loads when HW % 4 == 0 and gy is 16-byte aligned, scalar otherwise.
  * ------------------------------------------------------------------------- */
 size_t smmd_channel_sum_workspace_bytes(int N, int C);
 
 smmd_status smmd_channel_sum(const float *gy, int N, int C, int HW, float *out, void *ws,
                              size_t ws_bytes, smmd_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * Thin 3x3 convolutions: stride 1, zero padding 1 (TF SAME at stride 1), NCHW
+ * fp32, one side with <= 4 channels.  They serve the critics' first layer
+ * (3 -> dim: snops.conv2d / resnet Conv2D, gan/core/snops.py:76-80,
+ * gan/core/resnet/ops/conv2d.py:29-35, as used at architecture.py:395-407 and
+ * :410-434) and the generators' last (dim -> 3: snops.deconv2d at stride 1,
+ * gan/core/snops.py:109-121, architecture.py:178-208, :211-230), with their
+ * input and weight gradients (the TF autodiff of those ops, to second order
+ * through the scaling regulariser's Jacobian).
+ *
+ * Tap t = 3 kh + kw reads the input at (h + kh - 1, w + kw - 1), zero outside.
+ * smmd_conv3x3_thin: y[n][o][p] = bias[o] + sum_{i, t} A[o][i][t] x[n][i][p + d(t)]
+ *   x [n, ci, h, w_img], y [n, co, h, w_img], bias [co] or NULL;
+ *   mode 0: A[o][i][t] = w[o][i][t],     w [co, ci, 3, 3] (the convolution);
+ *   mode 1: A[o][i][t] = w[i][o][8 - t], w [ci, co, 3, 3] (the input gradient
+ *           of a convolution with weight w; also a stride-1 SAME conv2d_transpose).
+ *   Needs ci <= 4, or co <= 4 and w_img <= 64; otherwise SMMD_EUNSUPPORTED.
+ * smmd_conv3x3_thin_wgrad: gw[o][i][t] = sum_{n, p} gy[n][o][p] x[n][i][p + d(t)]
+ *   gy [n, co, h, w_img], x [n, ci, h, w_img], gw [co, ci, 3, 3]; needs
+ *   min(ci, co) <= 4 and w_img <= 64.  Workspace from
+ *   smmd_conv3x3_thin_wgrad_workspace_bytes (per-image partials, added over
+ *   the images in order).
+ * ------------------------------------------------------------------------- */
+smmd_status smmd_conv3x3_thin(const float *x, const float *w, const float *bias, float *y,
+                              int n, int ci, int co, int h, int w_img, int mode,
+                              smmd_stream_t stream);
+
+size_t smmd_conv3x3_thin_wgrad_workspace_bytes(int n, int ci, int co, int h, int w_img);
+
+smmd_status smmd_conv3x3_thin_wgrad(const float *gy, const float *x, float *gw, int n, int ci,
+                                    int co, int h, int w_img, void *ws, size_t ws_bytes,
+                                    smmd_stream_t stream);
 
 #ifdef __cplusplus
 }

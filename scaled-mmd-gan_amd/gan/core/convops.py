@@ -15,9 +15,14 @@ with the three standard primitives on the layer's own shapes:
     d/dw  = Dw(ggx, gy)
     d/dx  = Dx(gy, ggw)
 
-so it uses MIOpen's forward, backward-data and backward-weights kernels.
+so it uses MIOpen's forward, backward-data and backward-weights kernels --
+except for the thin 3x3 layers (a critic's 3-channel input conv, a
+generator's 3-channel output layer), whose three primitives run on the
+library's `smmd_conv3x3_thin*` kernels (csrc/smmd_thin.hip).
 """
 from __future__ import annotations
+
+import os
 
 import torch
 import torch.nn.functional as F
@@ -59,8 +64,85 @@ class no_input_grad:
         _no_dx.discard(self.key)
 
 
+# ---------------------------------------------------------------------------
+# thin 3x3 convolutions on the library (SMMD_THIN_CONV=0: MIOpen for them too)
+# ---------------------------------------------------------------------------
+THIN = os.environ.get('SMMD_THIN_CONV', '1') != '0'
+THIN_MAX_W = 64          # the library's cross-lane column tiling (smmd_thin.hip)
+
+
+def thin_applicable(x, cin, cout, k, stride, padding):
+    """True when conv(x, [cout, cin, k, k], stride, padding) -- and its input
+    and weight gradients -- run on the library's thin kernels: an NCHW fp32
+    device tensor, 3 x 3 at stride 1 with padding 1, one side <= 4 channels,
+    width <= 64."""
+    s = tuple(stride) if isinstance(stride, (list, tuple)) else (stride, stride)
+    p = tuple(padding) if isinstance(padding, (list, tuple)) else (padding, padding)
+    return (THIN and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
+            and x.is_contiguous() and k == 3 and s == (1, 1) and p == (1, 1)
+            and min(cin, cout) <= 4 and x.shape[1] == cin and x.shape[3] <= THIN_MAX_W)
+
+
+def _thin_conv(x, w, b, mode):
+    """smmd_conv3x3_thin: mode 0 conv(x, w) + b (w [co, ci, 3, 3]); mode 1 the
+    input gradient of a conv with weight w [ci', co', 3, 3] at upstream x."""
+    from . import _lib
+    x = x.contiguous()
+    w = w.contiguous()
+    if b is not None:
+        b = b.contiguous()
+    _lib.require_cuda(x, w)
+    N, ci, H, W = x.shape
+    co = w.shape[0] if mode == 0 else w.shape[1]
+    y = torch.empty((N, co, H, W), dtype=x.dtype, device=x.device)
+    _lib.add_bytes('smmd_conv3x3_thin', (x.numel() + y.numel()) * 4)
+    with _lib.timed('smmd_conv3x3_thin'):
+        st = _lib.lib().smmd_conv3x3_thin(_lib.ptr(x), _lib.ptr(w),
+                                          _lib.ptr(b) if b is not None else None, _lib.ptr(y),
+                                          N, ci, co, H, W, int(mode),
+                                          _lib.stream_handle(x.device))
+    _lib.check(st, 'smmd_conv3x3_thin')
+    return y
+
+
+def _thin_wgrad(gy, x):
+    """smmd_conv3x3_thin_wgrad: gw[o][i][t] = sum gy[n, o, p] x[n, i, p + d(t)]."""
+    from . import _lib
+    gy = gy.contiguous()
+    x = x.contiguous()
+    _lib.require_cuda(gy, x)
+    N, co, H, W = gy.shape
+    ci = x.shape[1]
+    L = _lib.lib()
+    nbytes = L.smmd_conv3x3_thin_wgrad_workspace_bytes(N, ci, co, H, W)
+    ws = _lib.workspace('thin_wgrad', nbytes, gy.device)
+    gw = torch.empty((co, ci, 3, 3), dtype=gy.dtype, device=gy.device)
+    _lib.add_bytes('smmd_conv3x3_thin_wgrad', (gy.numel() + x.numel()) * 4)
+    with _lib.timed('smmd_conv3x3_thin_wgrad'):
+        st = L.smmd_conv3x3_thin_wgrad(_lib.ptr(gy), _lib.ptr(x), _lib.ptr(gw), N, ci, co, H, W,
+                                       _lib.ptr(ws), ws.numel(), _lib.stream_handle(gy.device))
+    _lib.check(st, 'smmd_conv3x3_thin_wgrad')
+    return gw
+
+
+def _is_thin(x, w, stride, padding):
+    return thin_applicable(x, w.shape[1], w.shape[0], w.shape[2], stride, padding) \
+        and w.shape[2] == w.shape[3]
+
+
+def _fwd(x, w, b, stride, padding):
+    """conv(x, w) + b: the library's thin kernel or MIOpen."""
+    if _is_thin(x, w, stride, padding):
+        return _thin_conv(x, w, b, 0)
+    return F.conv2d(x, w, b, stride, padding)
+
+
 def _bwd(gy, x, w, stride, padding, mask):
     """(Dx, Dw) of conv(x, w) at upstream gy via the native backward kernels."""
+    if _is_thin(x, w, stride, padding):
+        gx = _thin_conv(gy, w, None, 1) if mask[0] else None
+        gw = _thin_wgrad(gy, x) if mask[1] else None
+        return gx, gw
     gx, gw, _ = _aten.convolution_backward(gy, x, w, None, stride, padding, [1, 1], False,
                                            [0, 0], 1, [mask[0], mask[1], False])
     return gx, gw
@@ -93,12 +175,12 @@ class _ConvBackward(torch.autograd.Function):
         if ggx is not None:
             ggx = ggx.contiguous(memory_format=_fmt(x))
             if need_gy:
-                g_gy = F.conv2d(ggx, w, None, stride, padding)
+                g_gy = _fwd(ggx, w, None, stride, padding)
             if need_w:
                 _, g_w = _bwd(gy, ggx, w, stride, padding, (False, True))
         if ggw is not None:
             if need_gy:
-                t = F.conv2d(x, ggw, None, stride, padding)
+                t = _fwd(x, ggw, None, stride, padding)
                 g_gy = t if g_gy is None else g_gy + t
             if need_x:
                 g_x, _ = _bwd(gy, x, ggw, stride, padding, (True, False))
@@ -117,7 +199,7 @@ class _Conv2d(torch.autograd.Function):
     def forward(ctx, x, w, b, stride, padding):
         ctx.save_for_backward(x, w)
         ctx.cfg = (stride, padding, b is not None)
-        return F.conv2d(x, w, b, stride, padding)
+        return _fwd(x, w, b, stride, padding)
 
     @staticmethod
     def backward(ctx, gy):

@@ -16,7 +16,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .convops import conv2d
+from .convops import conv2d, thin_applicable
 
 
 def same_pad(n_in, k, s):
@@ -110,6 +110,12 @@ class Deconv2d(nn.Module, _SNMixin):
         w = self.effective_weight()
         h, wd = x.shape[2] * self.stride, x.shape[3] * self.stride
         before, _ = same_pad(h, self.k, self.stride)
+        if self.stride == 1 and before == 1 and thin_applicable(x, self.cin, self.cout, self.k,
+                                                                1, 1):
+            # a stride-1 SAME transposed conv is the conv with the flipped,
+            # transposed filter: the generator's dim -> 3 output layer then runs
+            # on the library's thin kernels (csrc/smmd_thin.hip)
+            return conv2d(x, w.flip(2, 3).transpose(0, 1), self.bias, 1, 1)
         y = F.conv_transpose2d(x, w, self.bias, self.stride, before)
         if y.shape[2] != h or y.shape[3] != wd:
             y = y[:, :, :h, :wd]
