@@ -360,7 +360,7 @@ smmd_status smmd_fold_pool_weights(const float *const *src, float *const *dst,
 /* ---------------------------------------------------------------------------
  * Convolution bias gradient: out[c] = sum_{n, hw} gy[n, c, hw] over an NCHW
  * tensor [N, C, HW] (TF's BiasAddGrad of the bias_add in snops.conv2d,
- * gan/core/snops.py:79-80, and resnet Conv2D, gan/core/resnet/ops/conv2d.py:34-35).
+ * gan/core/snops.py:89-90, and resnet Conv2D, gan/core/resnet/ops/conv2d.py:37-39).
  * Fixed-order two-stage sum; workspace from smmd_channel_sum_workspace_bytes.
  * float4 loads when HW % 4 == 0 and gy is 16-byte aligned, scalar otherwise.
  * ------------------------------------------------------------------------- */
@@ -372,10 +372,10 @@ smmd_status smmd_channel_sum(const float *gy, int N, int C, int HW, float *out, 
 /* ---------------------------------------------------------------------------
  * Thin 3x3 convolutions: stride 1, zero padding 1 (TF SAME at stride 1), NCHW
  * fp32, one side with <= 4 channels.  They serve the critics' first layer
- * (3 -> dim: snops.conv2d / resnet Conv2D, gan/core/snops.py:76-80,
- * gan/core/resnet/ops/conv2d.py:29-35, as used at architecture.py:395-407 and
+ * (3 -> dim: snops.conv2d / resnet Conv2D, gan/core/snops.py:69-90,
+ * gan/core/resnet/ops/conv2d.py:16-39, as used at architecture.py:395-407 and
  * :410-434) and the generators' last (dim -> 3: snops.deconv2d at stride 1,
- * gan/core/snops.py:109-121, architecture.py:178-208, :211-230), with their
+ * gan/core/snops.py:104-126, architecture.py:178-208, :211-230), with their
  * input and weight gradients (the TF autodiff of those ops, to second order
  * through the scaling regulariser's Jacobian).
  *

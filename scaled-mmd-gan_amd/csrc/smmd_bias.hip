@@ -2,7 +2,7 @@
 // (gfx950 / MI355X).
 //
 // Reference: the TF autodiff of tf.nn.bias_add in snops.conv2d / resnet
-// Conv2D (gan/core/snops.py:79-80, gan/core/resnet/ops/conv2d.py:34-35), i.e.
+// Conv2D (gan/core/snops.py:89-90, gan/core/resnet/ops/conv2d.py:37-39), i.e.
 // BiasAddGrad over NHWC; here over the NCHW tensor the MIOpen convolutions use.
 // An HBM stream: every element of gy read once (4 B), 4 B written per channel.
 //

@@ -3,9 +3,9 @@
 // generator's last (dim -> 3), with their input and weight gradients.
 //
 // Reference layers: snops.conv2d / resnet Conv2D at stride 1 SAME
-// (gan/core/snops.py:76-80, gan/core/resnet/ops/conv2d.py:29-35; the critics'
+// (gan/core/snops.py:69-90, gan/core/resnet/ops/conv2d.py:16-39; the critics'
 // first conv, gan/core/architecture.py:395-407, :410-434) and snops.deconv2d
-// at stride 1 SAME (gan/core/snops.py:109-121; the generators' last layer,
+// at stride 1 SAME (gan/core/snops.py:104-126; the generators' last layer,
 // architecture.py:178-208, :211-230).
 //
 // MIOpen runs these at 3-6x their HBM time on MI355X (its implicit-GEMM

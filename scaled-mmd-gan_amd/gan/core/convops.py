@@ -223,7 +223,7 @@ class _Conv2d(torch.autograd.Function):
 
 def bias_grad(gy):
     """sum of gy over (N, H, W): the conv bias gradient (TF BiasAddGrad,
-    snops.py:79-80).  An NCHW device tensor outside a create_graph pass runs
+    snops.py:89-90).  An NCHW device tensor outside a create_graph pass runs
     `smmd_channel_sum` (csrc/smmd_bias.hip, fixed-order two-stage sum); a
     gradient that must itself be differentiable (create_graph, e.g. the
     witness penalty), channels_last or host tensors use torch's reduction."""

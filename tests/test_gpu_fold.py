@@ -137,7 +137,7 @@ def test_folded_upsample_conv_on_device(k, bias):
 @pytest.mark.parametrize('shape', [(64, 64, 64, 64), (64, 128, 32, 32), (64, 1024, 4, 4),
                                    (3, 5, 3, 3), (7, 1, 1, 1), (2, 2000, 2, 2), (0, 4, 2, 2)])
 def test_channel_sum_matches_oracle(shape):
-    """smmd_channel_sum (conv bias gradient, BiasAddGrad of snops.py:79-80)
+    """smmd_channel_sum (conv bias gradient, BiasAddGrad of snops.py:89-90)
     against a float64 sum over (N, H, W); odd HW takes the scalar path."""
     from gan.core.convops import bias_grad
     rng = np.random.default_rng(sum(shape))

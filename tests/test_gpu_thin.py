@@ -1,6 +1,6 @@
 """Thin 3x3 convolutions on the GPU (`smmd_conv3x3_thin*`, csrc/smmd_thin.hip):
 the critics' 3-channel input conv and the generators' 3-channel output layer
-(snops.conv2d / snops.deconv2d at stride 1 SAME, gan/core/snops.py:76-80,
+(snops.conv2d / snops.deconv2d at stride 1 SAME, gan/core/snops.py:69-90,
 :109-121), their input gradient (mode 1) and weight gradient, against the
 oracle's TF-SAME ops (oracle/ref_nets.py conv2d_same / deconv2d_same) and
 torch's float64 conv gradients on the same fp32 inputs; then through

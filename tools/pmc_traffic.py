@@ -24,10 +24,14 @@ GROUPS = {
     'smmd_scaled_loss_bwd': ('scaled_loss_bwd_kernel',),
     'smmd_fold_pool_weights': ('fold_fwd_kernel', 'fold_adj_kernel'),
     'smmd_channel_sum': ('chan_sum_partial_kernel', 'chan_sum_final_kernel'),
+    'smmd_conv3x3_thin': ('thin_in_kernel', 'thin_out_kernel'),
+    'smmd_conv3x3_thin_wgrad': ('thin_wgrad_mfma_kernel', 'thin_wgrad_kernel',
+                                'thin_wgrad_final_kernel'),
 }
-# entry points whose calls each run ONE of their kernels (fold or adjoint):
+# entry points whose calls each run ONE of their kernels (fold or adjoint;
+# thin_in or thin_out):
 # calls = the sum of the kernels' launches, not the most frequent one's
-SUM_CALLS = ('smmd_fold_pool_weights',)
+SUM_CALLS = ('smmd_fold_pool_weights', 'smmd_conv3x3_thin')
 
 
 def per_kernel(path):
