@@ -109,14 +109,37 @@ struct AdamK {
     }
 };
 
+// One lane's share of a fixed-order strided sum: s = sum over j ascending of
+// x[i0 + j * stride] for i0 + j * stride < i1, accumulated in double.  The
+// loads of each batch of 16 are all issued before the first add, so a slab
+// just written by another XCD costs one memory round trip per 16 terms instead
+// of one per term (the sum, and so the bits, are those of the plain loop).
+template <typename T>
+__device__ __forceinline__ double strided_sum(const T *__restrict__ x, int i0, int i1,
+                                              int stride) {
+    constexpr int B = 16;
+    double s = 0.0;
+    for (int base = i0; base < i1; base += B * stride) {
+        T t[B];
+#pragma unroll
+        for (int j = 0; j < B; ++j) {
+            const int i = base + j * stride;
+            t[j] = (i < i1) ? x[i] : T(0);
+        }
+#pragma unroll
+        for (int j = 0; j < B; ++j)
+            if (base + j * stride < i1) s += (double)t[j];
+    }
+    return s;
+}
+
 // clip factor of tf.clip_by_norm (TF 1.x form): clip * min(rsqrt(ss), 1/clip),
 // ss = the norm pass's double partials [b0, b1) summed by wave 0 in a fixed
 // order; every thread of the block gets it (sh: one float of LDS)
 __device__ __forceinline__ float clip_factor_slab(const double *part, int b0, int b1, float clip,
                                                   float *sh) {
     if (threadIdx.x < 64) {
-        double s = 0.0;
-        for (int b = b0 + (int)threadIdx.x; b < b1; b += 64) s += part[b];
+        double s = strided_sum(part, b0 + (int)threadIdx.x, b1, 64);
         s = wave_sum(s);
         if (threadIdx.x == 0) {
             const float ss = (float)s;

@@ -307,8 +307,8 @@ __device__ __forceinline__ void opt_adam_block(const OptTable &t, int b, const A
         for (int j = 0; j < OPT_UP_IT; ++j) {
             gg[j] = g4[j * 256];
             pp[j] = p4[j * 256];
-            mm[j] = m4[j * 256];
-            vv[j] = v4[j * 256];
+            mm[j] = ld_nt(m4 + j * 256);
+            vv[j] = ld_nt(v4 + j * 256);
         }
 #pragma unroll
         for (int j = 0; j < OPT_UP_IT; ++j) {
@@ -317,8 +317,8 @@ __device__ __forceinline__ void opt_adam_block(const OptTable &t, int b, const A
             k.upd(pp[j].z, gg[j].z, mm[j].z, vv[j].z);
             k.upd(pp[j].w, gg[j].w, mm[j].w, vv[j].w);
             p4[j * 256] = pp[j];
-            m4[j * 256] = mm[j];
-            v4[j * 256] = vv[j];
+            st_nt(m4 + j * 256, mm[j]);
+            st_nt(v4 + j * 256, vv[j]);
         }
     } else if (vec) {
         float4 *p4 = reinterpret_cast<float4 *>(p);

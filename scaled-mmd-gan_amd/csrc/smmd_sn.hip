@@ -222,26 +222,35 @@ __device__ __forceinline__ void snf_bwd_a(const SnLayerDev &L, int unit, int lu)
 }
 
 // backward B of a fold layer: gW = (s adj(G')) / sigma - coef u'_n v_k
-__device__ __forceinline__ void snf_bwd_b(const SnLayerDev &L, int unit, float d) {
+__device__ __forceinline__ float layer_dot(const SnLayerDev &L, float *sh);
+
+__device__ __forceinline__ void snf_bwd_b(const SnLayerDev &L, int unit, float *sh_d) {
     __shared__ float s9[SNF_T * 9];
     __shared__ float s16[16 * SNF_S16];
     const int64_t nf = (int64_t)L.N * L.nfc;
     const int64_t q0 = (int64_t)unit * SNF_T;
     const int nb = (int)min<int64_t>(SNF_T, nf - q0);
     snf_load16(L.G + q0 * 16, s16, nb);
-    __syncthreads();
+    const int f = threadIdx.x;
+    float un = 0.f, vk[9];                       // in flight with G' and the dot
+    {
+        const int64_t q = q0 + (f < nb ? f : 0);
+        const int n = (int)(q / L.nfc), c = (int)(q - (int64_t)n * L.nfc);
+        un = L.ucur[n];
+#pragma unroll
+        for (int j = 0; j < 9; ++j) vk[j] = L.v[c * 9 + j];
+    }
     const float sigma = L.sigma[0];
     const float s = L.s ? L.s[0] : 1.f;
+    const float d = layer_dot(L, sh_d);          // its barrier also publishes s16
+    if (unit == 0 && threadIdx.x == 0 && L.gs) L.gs[0] = d / sigma;
     const float coef = (s * d) / (sigma * sigma);
-    const int f = threadIdx.x;
     if (f < nb) {
-        const int64_t q = q0 + f;
-        const int n = (int)(q / L.nfc), c = (int)(q - (int64_t)n * L.nfc);
-        const float cu = coef * L.ucur[n];
+        const float cu = coef * un;
         float g[9];
         snf_adjoint(s16, f, g);
 #pragma unroll
-        for (int j = 0; j < 9; ++j) s9[f * 9 + j] = (s * g[j]) / sigma - cu * L.v[c * 9 + j];
+        for (int j = 0; j < 9; ++j) s9[f * 9 + j] = (s * g[j]) / sigma - cu * vk[j];
     }
     __syncthreads();
     snf_store9(L.gW + q0 * 9, s9, nb * 9);
@@ -273,14 +282,24 @@ __global__ __launch_bounds__(256) void sn_p2_kernel(SnTable t) {
     float4 wt[SN_RPW];
     load_tile(L.W, L.N, L.K, L.vec, r0, c0, wt);   // issue the tile loads first
 
-    // v_raw for this tile's columns: fixed-order sum over row tiles of P1
+    // v_raw for this tile's columns: fixed-order sum over row tiles of P1.  The
+    // slab was just written by other XCDs, so each batch of 16 loads is issued
+    // before its adds (one memory round trip per 16 row tiles, not per 4)
     __shared__ float vr[SN_TC];
     {
         const int c = ct * SN_TC + threadIdx.x;
         float s = 0.f;
         if (c < L.K) {
-#pragma unroll 4
-            for (int r = 0; r < L.nrt; ++r) s += L.p1[(size_t)r * L.K + c];
+            const float *col = L.p1 + c;
+            for (int r0 = 0; r0 < L.nrt; r0 += 16) {
+                float t[16];
+#pragma unroll
+                for (int j = 0; j < 16; ++j)
+                    t[j] = (r0 + j < L.nrt) ? col[(size_t)(r0 + j) * L.K] : 0.f;
+#pragma unroll
+                for (int j = 0; j < 16; ++j)
+                    if (r0 + j < L.nrt) s += t[j];
+            }
         }
         vr[threadIdx.x] = s;
         if (rt == 0 && c < L.K) L.vraw[c] = s;
@@ -484,27 +503,29 @@ __device__ __forceinline__ int layer_units(const SnLayerDev &L) {
     return L.fold ? (int)(((int64_t)L.N * L.nfc + SNF_T - 1) / SNF_T) : L.nrt * L.nct;
 }
 
+// <G, W> of the unit's layer: wave 0 sums the layer's A partials in a fixed
+// order; every thread gets it.  Called after the unit's G loads are issued, so
+// the two memory round trips overlap.
+__device__ __forceinline__ float layer_dot(const SnLayerDev &L, float *sh) {
+    const int lane = threadIdx.x & 63;
+    if (threadIdx.x < 64) {
+        double d = strided_sum(L.dotp, lane, layer_units(L), 64);
+        d = wave_sum(d);
+        if (lane == 0) sh[0] = (float)d;
+    }
+    __syncthreads();
+    return sh[0];
+}
+
 // backward B: gW = (s G)/sigma - (s <G,W> / sigma^2) u' v^T ; gs = <G,W>/sigma
 __global__ __launch_bounds__(256) void sn_bwd_b_kernel(SnTable t) {
     const int unit = blockIdx.x;
     const SnLayerDev L = t.L[find_unit_layer(t, unit)];
     const int lt = unit - L.unit_begin;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    __shared__ float sh_d;
-    if (w == 0) {
-        const int nt = layer_units(L);
-        double d = 0.0;
-        for (int i = lane; i < nt; i += 64) d += (double)L.dotp[i];
-        d = wave_sum(d);
-        if (lane == 0) sh_d = (float)d;
-    }
-    __syncthreads();
-    const float d = sh_d;                         // <G, W>
-    const float sigma = L.sigma[0];
-    const float s = L.s ? L.s[0] : 1.f;
-    if (lt == 0 && threadIdx.x == 0 && L.gs) L.gs[0] = d / sigma;
+    __shared__ float sh_d[1];
     if (L.fold) {
-        snf_bwd_b(L, lt, d);
+        snf_bwd_b(L, lt, sh_d);
         return;
     }
     const int rt = lt / L.nct, ct = lt % L.nct;
@@ -512,16 +533,22 @@ __global__ __launch_bounds__(256) void sn_bwd_b_kernel(SnTable t) {
     const int c0 = ct * SN_TC + lane * 4;
     float4 gt[SN_RPW];
     load_tile(L.G, L.N, L.K, L.vec, r0, c0, gt);
-    const float coef = (s * d) / (sigma * sigma);  // -dsigma factor
-    float vv[4];
+    float vv[4], uc[SN_RPW];                       // in flight with G and the dot
 #pragma unroll
     for (int k = 0; k < 4; ++k) vv[k] = (c0 + k < L.K) ? L.v[c0 + k] : 0.f;
+#pragma unroll
+    for (int i = 0; i < SN_RPW; ++i) uc[i] = (r0 + i < L.N) ? L.ucur[r0 + i] : 0.f;
+    const float sigma = L.sigma[0];
+    const float s = L.s ? L.s[0] : 1.f;
+    const float d = layer_dot(L, sh_d);            // <G, W>
+    if (lt == 0 && threadIdx.x == 0 && L.gs) L.gs[0] = d / sigma;
+    const float coef = (s * d) / (sigma * sigma);  // -dsigma factor
     const bool full_cols = (c0 + 3 < L.K);
 #pragma unroll
     for (int i = 0; i < SN_RPW; ++i) {
         const int r = r0 + i;
         if (r >= L.N) break;
-        const float cu = coef * L.ucur[r];
+        const float cu = coef * uc[i];
         float4 o;
         o.x = (s * gt[i].x) / sigma - cu * vv[0];
         o.y = (s * gt[i].y) / sigma - cu * vv[1];

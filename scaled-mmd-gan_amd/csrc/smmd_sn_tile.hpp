@@ -14,17 +14,30 @@ constexpr int SN_TC = 256;     // tile cols (64 lanes x 4)
 constexpr int SN_RPW = SN_TR / 4;   // rows per wave
 constexpr int SN_CHUNK = 16;   // layers per launch set
 
+// float4 loads / stores with the non-temporal hint (streamed once per step:
+// the Adam moments), so they do not displace the weights the next power
+// iteration reads from the Infinity Cache
+typedef float smmd_f4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ld_nt(const float4 *p) {
+    const smmd_f4v v = __builtin_nontemporal_load(reinterpret_cast<const smmd_f4v *>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st_nt(float4 *p, float4 x) {
+    const smmd_f4v v = {x.x, x.y, x.z, x.w};
+    __builtin_nontemporal_store(v, reinterpret_cast<smmd_f4v *>(p));
+}
+
 // load the NR rows x 4 cols this thread owns from row r0 (zero outside the
 // matrix).  Interior tiles of 16-B aligned layers take one branch-free path:
 // NR independent float4 loads issued back to back.
-template <int NR>
+template <int NR, bool NT = false>
 __device__ __forceinline__ void load_tile(const float *__restrict__ base, int N, int K, int vec,
                                           int r0, int c0, float4 (&w)[NR]) {
     if (vec && r0 + NR <= N && c0 + 3 < K) {
         const float4 *p = reinterpret_cast<const float4 *>(base + (size_t)r0 * K + c0);
         const int stride4 = K / 4;
 #pragma unroll
-        for (int i = 0; i < NR; ++i) w[i] = p[(size_t)i * stride4];
+        for (int i = 0; i < NR; ++i) w[i] = NT ? ld_nt(p + (size_t)i * stride4) : p[(size_t)i * stride4];
         return;
     }
 #pragma unroll
@@ -43,14 +56,17 @@ __device__ __forceinline__ void load_tile(const float *__restrict__ base, int N,
 }
 
 // masked / vector store of NR rows x 4 cols (load_tile's inverse)
-template <int NR>
+template <int NR, bool NT = false>
 __device__ __forceinline__ void store_tile(float *__restrict__ base, int N, int K, int vec, int r0,
                                            int c0, const float4 (&w)[NR]) {
     if (vec && r0 + NR <= N && c0 + 3 < K) {
         float4 *p = reinterpret_cast<float4 *>(base + (size_t)r0 * K + c0);
         const int stride4 = K / 4;
 #pragma unroll
-        for (int i = 0; i < NR; ++i) p[(size_t)i * stride4] = w[i];
+        for (int i = 0; i < NR; ++i) {
+            if (NT) st_nt(p + (size_t)i * stride4, w[i]);
+            else p[(size_t)i * stride4] = w[i];
+        }
         return;
     }
 #pragma unroll
@@ -155,8 +171,8 @@ __device__ __forceinline__ void sn_adam_tile(const SnAdamTable &t, int tile, Ada
         float4 pp[NR], gg[NR], mm[NR], vv[NR];
         load_tile(L.g, L.N, L.K, L.vec, r0, c0, gg);
         load_tile(L.p, L.N, L.K, L.vec, r0, c0, pp);
-        load_tile(L.m, L.N, L.K, L.vec, r0, c0, mm);
-        load_tile(L.v, L.N, L.K, L.vec, r0, c0, vv);
+        load_tile<NR, true>(L.m, L.N, L.K, L.vec, r0, c0, mm);
+        load_tile<NR, true>(L.v, L.N, L.K, L.vec, r0, c0, vv);
         if (h == 0) k.f = (clip > 0.f) ? clip_factor_slab(part, L.sb0, L.sb1, clip, sh) : 1.f;
 #pragma unroll
         for (int i = 0; i < NR; ++i) {
@@ -166,8 +182,8 @@ __device__ __forceinline__ void sn_adam_tile(const SnAdamTable &t, int tile, Ada
             k.upd(pp[i].w, gg[i].w, mm[i].w, vv[i].w);
         }
         store_tile(L.p, L.N, L.K, L.vec, r0, c0, pp);
-        store_tile(L.m, L.N, L.K, L.vec, r0, c0, mm);
-        store_tile(L.v, L.N, L.K, L.vec, r0, c0, vv);
+        store_tile<NR, true>(L.m, L.N, L.K, L.vec, r0, c0, mm);
+        store_tile<NR, true>(L.v, L.N, L.K, L.vec, r0, c0, vv);
         p1_accum(L.u, L.N, r0, pp, acc);
     }
     p1_store(acc, L.p1, L.K, rt, c0);

@@ -155,6 +155,28 @@ def test_channel_sum_matches_oracle(shape):
         assert torch.equal(out, b2)           # fixed order: bit-identical
 
 
+def test_channel_sum_shape_sequence_shared_workspace():
+    """Calls of different channel counts back to back through the one cached
+    workspace (C < 512 takes the two-stage path, C >= 512 the direct one; wide
+    and short rows, batched loads): every result against float64, and repeated
+    calls give the same bits."""
+    from gan.core.convops import bias_grad
+    rng = np.random.default_rng(7)
+    shapes = [(64, 64, 16, 16), (64, 256, 8, 8), (64, 3, 8, 8), (64, 1024, 4, 4),
+              (32, 128, 4, 4), (64, 64, 16, 16)]
+    xs = [torch.tensor(rng.standard_normal(sh).astype(np.float32), device='cuda:0')
+          for sh in shapes]
+    with torch.no_grad():
+        first = [bias_grad(x) for x in xs]
+        second = [bias_grad(x) for x in reversed(xs)][::-1]
+    torch.cuda.synchronize()
+    for sh, x, a, b in zip(shapes, xs, first, second):
+        ref = x.cpu().numpy().astype(np.float64).sum(axis=(0, 2, 3))
+        tol = 1e-5 * np.sqrt(sh[0] * sh[2] * sh[3] + 1) + 1e-6
+        np.testing.assert_allclose(a.cpu().numpy(), ref, rtol=0, atol=tol)
+        assert torch.equal(a, b)
+
+
 def test_fold_caches_follow_flat_adam_updates():
     """The prefold (critic) and folded-UpsampleConv (generator) caches must
     miss after a FlatAdam step: the library writes the parameters without

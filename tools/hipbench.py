@@ -44,7 +44,8 @@ def main():
     opt = FlatAdam([p for p in D.parameters() if p.requires_grad], 2e-4, name='D')
     if not args.no_fuse:     # as MMD_GAN: the critic step of the bench's 5 D + 1 G schedule
         assert opt.attach_sn(bank)
-    Gs = [torch.randn_like(e.weight) for e in bank.entries]
+    with torch.no_grad():      # the refresh outputs (pool-folded 4x4 filters for ConvMeanPool)
+        Gs = [torch.randn_like(o) for o in bank.refresh(update_u=False)]
     B = args.batch
     X = torch.randn(B, 1, device=dev, requires_grad=True)
     Y = torch.randn(B, 1, device=dev, requires_grad=True)
