@@ -59,7 +59,8 @@ typedef struct {
 const char *smmd_status_string(smmd_status s);
 int smmd_abi_version(void);         /* bumped on any ABI change (2: Gram/poly,
                                        3: smmd_sn_layer.fold, 4: smmd_adam_flat_ex,
-                                       5: smmd_conv3x3_thin*) */
+                                       5: smmd_conv3x3_thin*,
+                                       6: smmd_mask_pool2*) */
 
 /* ---------------------------------------------------------------------------
  * Fused pairwise MMD^2 (forward + unit gradient).
@@ -368,6 +369,29 @@ size_t smmd_channel_sum_workspace_bytes(int N, int C);
 
 smmd_status smmd_channel_sum(const float *gy, int N, int C, int HW, float *out, void *ws,
                              size_t ws_bytes, smmd_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * The input of a critic down block feeds two ops: the main path's ReLU
+ * (gan/core/resnet/block.py:44, norm off in the critic) and the shortcut's 2x2
+ * mean pool (MeanPoolConv, block.py:69-71); the block output is their paths'
+ * sum (block.py:50).  These two entry points read it once forward and write
+ * its gradient in one pass backward.  Planes [planes, H, W] NCHW fp32, H even,
+ * W % 4 == 0, 16-byte aligned full-size tensors, 8-byte aligned pooled ones.
+ * smmd_mask_pool2:     out_masked = x * [m > 0]  (m = x: the ReLU; NULL: skip),
+ *                      out_pool[i][j] = (((x[2i][2j] + x[2i][2j+1]) + x[2i+1][2j])
+ *                                        + x[2i+1][2j+1]) / 4   (NULL: skip)
+ * smmd_mask_pool2_adj: out = a * [m > 0] + nearest_up(b / 4)  (a or b NULL: that
+ *                      term absent) -- the adjoint of smmd_mask_pool2 in x, so each
+ *                      is the other's backward (linear in x / (a, b), m constant).
+ * The select, the pooling order and the one add are those of torch's relu /
+ * avg_pool2d / threshold_backward / nearest upsample and autograd's gradient
+ * sum, so results are bit-identical to that composition.
+ * ------------------------------------------------------------------------- */
+smmd_status smmd_mask_pool2(const float *x, const float *m, int64_t planes, int H, int W,
+                            float *out_masked, float *out_pool, smmd_stream_t stream);
+
+smmd_status smmd_mask_pool2_adj(const float *a, const float *b, const float *m, int64_t planes,
+                                int H, int W, float *out, smmd_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * Thin 3x3 convolutions: stride 1, zero padding 1 (TF SAME at stride 1), NCHW

@@ -24,7 +24,7 @@ SMMD_SN_MAX_LAYERS = 32
 SN_P1_READY = 1            # smmd_sn_power_iter_ex flag
 OPT_MAX_FUSED = 96         # tensors smmd_adam_flat_sn takes in one call
 SN_MAX_FUSED = 16          # SN layers smmd_adam_flat_sn takes in one call
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 KIND_RBF, KIND_RQ, KIND_DISTANCE, KIND_DOT = 0, 1, 2, 3
 
@@ -121,6 +121,8 @@ _SIGS = {
     'smmd_channel_sum_workspace_bytes': (_SZ, [_I, _I]),
     'smmd_channel_sum': (_I, [_P, _I, _I, _I, _P, _P, _SZ, _P]),
     'smmd_conv3x3_thin': (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
+    'smmd_mask_pool2': (_I, [_P, _P, _I64, _I, _I, _P, _P, _P]),
+    'smmd_mask_pool2_adj': (_I, [_P, _P, _P, _I64, _I, _I, _P, _P]),
     'smmd_conv3x3_thin_wgrad_workspace_bytes': (_SZ, [_I, _I, _I, _I, _I]),
     'smmd_conv3x3_thin_wgrad': (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P, _SZ, _P]),
     'smmd_poly_diff_ratio': (_I, [ctypes.POINTER(PolySums), ctypes.POINTER(PolySums),

@@ -15,6 +15,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import convops
 from . import optim as _optim
 from .convops import conv2d, fold_pool_weight, fold_pool_weights, fold_up_weight, mean_pool2
 from .snops import Conv2d, Deconv2d, Linear, batch_norm, lrelu
@@ -204,8 +205,17 @@ class ResidualBlock(nn.Module):
         use_bn = mode == 'batchnorm'                     # Normalize, block.py:76-86
         self.bn1 = _bn_or_id(use_bn, n1)
         self.bn2 = _bn_or_id(use_bn, n2)
+        # a critic down block: relu(x) (main path) and the shortcut's mean pool
+        # of x read the input in one pass (convops.relu_pool)
+        self._relu_pool = resample == 'down' and not use_bn
 
     def forward(self, x):
+        if self._relu_pool and convops.relu_pool_applicable(x):
+            r, p = convops.relu_pool(x)
+            s = self.shortcut.conv(p)                    # _MeanPoolConv on the pooled x
+            h = self.conv_1(r)
+            h = self.conv_2(F.relu(self.bn2(h)))
+            return s + h
         s = x if self.shortcut is None else self.shortcut(x)
         h = self.conv_1(F.relu(self.bn1(x)))
         h = self.conv_2(F.relu(self.bn2(h)))

@@ -389,3 +389,142 @@ def mean_pool2(x):
         return (x[:, :, ::2, ::2] + x[:, :, 1::2, ::2] + x[:, :, ::2, 1::2]
                 + x[:, :, 1::2, 1::2]) / 4.
     return _MeanPool2.apply(x)
+
+
+# ---------------------------------------------------------------------------
+# a critic down block's input: the main path's ReLU and the shortcut's mean
+# pool in one read, their gradients in one write (csrc/smmd_relupool.hip;
+# SMMD_RELU_POOL=0: relu + mean_pool2 as separate torch ops)
+# ---------------------------------------------------------------------------
+RELU_POOL = os.environ.get('SMMD_RELU_POOL', '1') != '0'
+
+
+def relu_pool_applicable(x):
+    """An NCHW fp32 device tensor with even height and width % 4 == 0."""
+    return (RELU_POOL and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
+            and x.is_contiguous() and x.shape[2] % 2 == 0 and x.shape[3] % 4 == 0)
+
+
+def _mask_pool(x, m, masked=True, pooled=True):
+    """smmd_mask_pool2: (x [m > 0], 2x2 mean pool of x); either may be skipped."""
+    from . import _lib
+    x = x.contiguous()
+    m = x if m is None else m.contiguous()
+    _lib.require_cuda(x, m)
+    N, C, H, W = x.shape
+    out_m = torch.empty_like(x) if masked else None
+    out_p = torch.empty((N, C, H // 2, W // 2), dtype=x.dtype, device=x.device) if pooled else None
+    nb = x.numel() * (1 + (masked and m is not x) + masked) + (out_p.numel() if pooled else 0)
+    _lib.add_bytes('smmd_mask_pool2', nb * 4)
+    with _lib.timed('smmd_mask_pool2'):
+        st = _lib.lib().smmd_mask_pool2(_lib.ptr(x), _lib.ptr(m), N * C, H, W, _lib.ptr(out_m),
+                                        _lib.ptr(out_p), _lib.stream_handle(x.device))
+    _lib.check(st, 'smmd_mask_pool2')
+    return out_m, out_p
+
+
+def _mask_pool_adj(a, b, m):
+    """smmd_mask_pool2_adj: a [m > 0] + nearest_up(b / 4) (a or b None: absent)."""
+    from . import _lib
+    m = m.contiguous()
+    a = a.contiguous() if a is not None else None
+    b = b.contiguous() if b is not None else None
+    _lib.require_cuda(m, *[t for t in (a, b) if t is not None])
+    N, C, H, W = m.shape
+    out = torch.empty_like(m)
+    nb = out.numel() * (1 + 2 * (a is not None)) + (b.numel() if b is not None else 0)
+    _lib.add_bytes('smmd_mask_pool2_adj', nb * 4)
+    with _lib.timed('smmd_mask_pool2_adj'):
+        st = _lib.lib().smmd_mask_pool2_adj(_lib.ptr(a), _lib.ptr(b), _lib.ptr(m), N * C, H, W,
+                                            _lib.ptr(out), _lib.stream_handle(m.device))
+    _lib.check(st, 'smmd_mask_pool2_adj')
+    return out
+
+
+class _MaskPool(torch.autograd.Function):
+    """(x; m) -> (x [m > 0], pool(x)), linear in x with the mask m constant."""
+
+    @staticmethod
+    def forward(ctx, x, m):
+        ctx.save_for_backward(m)
+        ctx.set_materialize_grads(False)
+        return _mask_pool(x, m)
+
+    @staticmethod
+    def backward(ctx, ga, gb):
+        if ga is None and gb is None:
+            return None, None
+        m, = ctx.saved_tensors
+        return _MaskPoolAdj.apply(ga, gb, m), None
+
+
+class _MaskPoolAdj(torch.autograd.Function):
+    """(a, b; m) -> a [m > 0] + up(b) / 4: the adjoint of _MaskPool, and its
+    backward (and the other way round), so every order of differentiation
+    stays on the two kernels."""
+
+    @staticmethod
+    def forward(ctx, a, b, m):
+        ctx.save_for_backward(m)
+        ctx.set_materialize_grads(False)
+        return _mask_pool_adj(a, b, m)
+
+    @staticmethod
+    def backward(ctx, g):
+        if g is None:
+            return None, None, None
+        m, = ctx.saved_tensors
+        need_a, need_b = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        if not (need_a or need_b):
+            return None, None, None
+        ga, gb = _mask_pool_torch_or_lib(g, m, need_a, need_b)
+        return ga, gb, None
+
+
+def _mask_pool_torch_or_lib(g, m, need_a, need_b):
+    if need_a and need_b:
+        return _MaskPool.apply(g, m)
+    # one output only: a single-output Function keeps the graph exact
+    if need_a:
+        return _MaskOnly.apply(g, m), None
+    return None, mean_pool2(g)
+
+
+class _MaskOnly(torch.autograd.Function):
+    """g -> g [m > 0] (self-adjoint)."""
+
+    @staticmethod
+    def forward(ctx, g, m):
+        ctx.save_for_backward(m)
+        return _mask_pool(g, m, pooled=False)[0]
+
+    @staticmethod
+    def backward(ctx, gg):
+        m, = ctx.saved_tensors
+        return _MaskOnly.apply(gg, m), None
+
+
+class _ReluPool(torch.autograd.Function):
+    """x -> (relu(x), pool(x)); the ReLU output is the backward's mask."""
+
+    @staticmethod
+    def forward(ctx, x):
+        r, p = _mask_pool(x, None)
+        ctx.save_for_backward(r)
+        ctx.set_materialize_grads(False)
+        return r, p
+
+    @staticmethod
+    def backward(ctx, gr, gp):
+        if gr is None and gp is None:
+            return None
+        r, = ctx.saved_tensors
+        return _MaskPoolAdj.apply(gr, gp, r)
+
+
+def relu_pool(x):
+    """(relu(x), mean_pool2(x)) of a critic down block's input (block.py:44,
+    :69-71): one HIP pass each way on device tensors, torch ops otherwise."""
+    if relu_pool_applicable(x):
+        return _ReluPool.apply(x)
+    return F.relu(x), mean_pool2(x)

@@ -160,8 +160,11 @@ def test_tower_and_global_agree_on_one_gpu(dev):
         images = torch.rand(8, 3, 32, 32, device=dev)
         model.train_step(images)
         outs.append(cap['g'])
+    # two runs of the same mode differ by up to ~1e-5 of the largest entry
+    # (MIOpen's nondeterministic reductions; tools/dbg_towerglobal.py), so
+    # the bound sits above that noise
     scale = float(outs[0].abs().max())
-    assert torch.allclose(outs[0], outs[1], rtol=1e-4, atol=1e-5 * scale)
+    assert torch.allclose(outs[0], outs[1], rtol=1e-4, atol=1e-4 * scale)
 
 
 def test_reference_schedule_applies_the_lean_update(dev):

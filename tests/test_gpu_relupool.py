@@ -1,0 +1,143 @@
+"""GPU parity of the fused input ops of a critic down block (csrc/smmd_relupool.hip,
+convops.relu_pool): relu(x) of the main path (gan/core/resnet/block.py:44) and
+the shortcut's 2x2 mean pool (block.py:69-71), forward, backward and double
+backward, against the torch composition they replace.  The kernels keep that
+composition's operation order, so values and gradients are compared for
+equality (not a tolerance)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = 'cuda:0'
+
+
+def _ref(x):
+    from gan.core.convops import mean_pool2
+    return F.relu(x), mean_pool2(x)
+
+
+@pytest.fixture
+def relu_pool_off():
+    from gan.core import convops
+    saved = convops.RELU_POOL
+    yield convops
+    convops.RELU_POOL = saved
+
+
+@pytest.mark.parametrize('shape', [(64, 64, 64, 64), (4, 128, 32, 32), (3, 5, 8, 4), (2, 1, 2, 4)])
+def test_relu_pool_forward_equals_torch(shape):
+    from gan.core import convops
+    g = torch.Generator(device=DEV).manual_seed(sum(shape))
+    x = torch.randn(shape, device=DEV, generator=g)
+    assert convops.relu_pool_applicable(x)
+    r, p = convops.relu_pool(x)
+    rr, pr = _ref(x)
+    assert torch.equal(r, rr) and torch.equal(p, pr)
+
+
+@pytest.mark.parametrize('use', ['both', 'relu', 'pool'])
+def test_relu_pool_backward_equals_torch(use):
+    """The input gradient when the block uses both outputs (their sum), or
+    only one (the other arrives as None)."""
+    from gan.core import convops
+    g = torch.Generator(device=DEV).manual_seed(5)
+    x = torch.randn(8, 16, 16, 16, device=DEV, generator=g)
+    A = torch.randn(8, 16, 16, 16, device=DEV, generator=g)
+    B = torch.randn(8, 16, 8, 8, device=DEV, generator=g)
+    grads = []
+    for fn in (convops.relu_pool, _ref):
+        xx = x.clone().requires_grad_(True)
+        r, p = fn(xx)
+        L = {'both': (r * A).sum() + (p * B).sum(), 'relu': (r * A).sum(),
+             'pool': (p * B).sum()}[use]
+        gx, = torch.autograd.grad(L, xx)
+        grads.append(gx)
+    assert torch.equal(grads[0], grads[1])
+
+
+def _tiny_critic(x, w1, w2, w3, fn):
+    """x -> (relu, pool) -> 3x3 conv of the relu branch + 1x1 conv of the
+    pooled branch (a down block's two paths), reduced to one feature per image."""
+    r, p = fn(x)
+    h = F.conv2d(r, w1, padding=1)
+    h = F.avg_pool2d(F.relu(h), 2)
+    s = F.conv2d(p, w2)
+    out = F.conv2d(F.relu(h + s), w3)
+    return out.mean(dim=(1, 2, 3))
+
+
+def test_relu_pool_double_backward_matches_torch():
+    """The scaling regulariser's pattern: the Jacobian of the features with
+    respect to the input (create_graph), then the gradient of its squared
+    norm with respect to the weights, through the fused ops."""
+    from gan.core import convops
+    g = torch.Generator(device=DEV).manual_seed(11)
+    x = torch.randn(4, 8, 16, 16, device=DEV, generator=g)
+    w1 = torch.randn(8, 8, 3, 3, device=DEV, generator=g) * 0.2
+    w2 = torch.randn(8, 8, 1, 1, device=DEV, generator=g) * 0.2
+    w3 = torch.randn(1, 8, 1, 1, device=DEV, generator=g) * 0.2
+    res = []
+    for fn in (convops.relu_pool, _ref):
+        xx = x.clone().requires_grad_(True)
+        ws = [w.clone().requires_grad_(True) for w in (w1, w2, w3)]
+        feat = _tiny_critic(xx, *ws, fn)
+        jac, = torch.autograd.grad(feat.sum(), xx, create_graph=True)
+        J = (jac * jac).sum()
+        gws = torch.autograd.grad(J + feat.sum(), ws)
+        res.append([jac.detach()] + list(gws))
+    for a, b in zip(*res):
+        tol = 1e-5 * float(b.abs().max()) + 1e-7
+        assert float((a - b).abs().max()) <= tol
+
+
+def test_relu_pool_third_order_runs():
+    """Each kernel's backward is the other one: a third differentiation (the
+    witness penalty's second order through a critic Jacobian) stays defined."""
+    from gan.core import convops
+    x = torch.randn(2, 4, 8, 8, device=DEV, requires_grad=True)
+    A = torch.randn(2, 4, 8, 8, device=DEV)
+    r, p = convops.relu_pool(x)
+    L = (r * A).sum() + (p * p).sum()
+    gx, = torch.autograd.grad(L, x, create_graph=True)
+    ggx, = torch.autograd.grad((gx * gx).sum(), x, create_graph=True)
+    assert torch.isfinite(ggx).all()
+
+
+def test_residual_down_block_fused_equals_unfused(relu_pool_off):
+    """An SNResNet critic down block (block.py:9-50, resample 'down') with the
+    fused input ops against the same block on relu + mean_pool2: output, the
+    input gradient and the parameter gradients of a scaled Jacobian loss."""
+    convops = relu_pool_off
+    from gan.core.architecture import ResidualBlock
+    torch.manual_seed(3)
+    blk = ResidualBlock(16, 32, 3, 'down').to(DEV)
+    x0 = torch.randn(8, 16, 32, 32, device=DEV)
+    out = []
+    for on in (True, False):
+        convops.RELU_POOL = on
+        x = x0.clone().requires_grad_(True)
+        y = blk(x)
+        feat = y.mean(dim=(1, 2, 3))
+        jac, = torch.autograd.grad(feat.sum(), x, create_graph=True)
+        L = feat.sum() + 10.0 * (jac * jac).sum()
+        gp = torch.autograd.grad(L, list(blk.parameters()))
+        out.append([y.detach(), jac.detach()] + [t.detach() for t in gp])
+    for a, b in zip(*out):
+        tol = 1e-5 * float(b.abs().max()) + 1e-7
+        assert float((a - b).abs().max()) <= tol
+
+
+def test_mask_pool_abi_rejects_bad_shapes():
+    from gan.core import _lib
+    L = _lib.lib()
+    x = torch.zeros(1, 1, 4, 6, device=DEV)
+    o = torch.empty_like(x)
+    s = _lib.stream_handle(x.device)
+    assert L.smmd_mask_pool2(_lib.ptr(x), _lib.ptr(x), 1, 4, 6, _lib.ptr(o), None, s) != 0
+    assert L.smmd_mask_pool2(_lib.ptr(x), _lib.ptr(x), 1, 3, 4, _lib.ptr(o), None, s) != 0
+    assert L.smmd_mask_pool2_adj(None, None, _lib.ptr(x), 1, 4, 4, _lib.ptr(o), s) != 0
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(o.shape, x.shape)
