@@ -374,24 +374,32 @@ smmd_status smmd_channel_sum(const float *gy, int N, int C, int HW, float *out, 
  * The input of a critic down block feeds two ops: the main path's ReLU
  * (gan/core/resnet/block.py:44, norm off in the critic) and the shortcut's 2x2
  * mean pool (MeanPoolConv, block.py:69-71); the block output is their paths'
- * sum (block.py:50).  These two entry points read it once forward and write
+ * sum (block.py:50).  These two entry points read it once forward (from the
+ * previous block's two paths, or the first conv's pre-activation) and write
  * its gradient in one pass backward.  Planes [planes, H, W] NCHW fp32, H even,
  * W % 4 == 0, 16-byte aligned full-size tensors, 8-byte aligned pooled ones.
- * smmd_mask_pool2:     out_masked = x * [m > 0]  (m = x: the ReLU; NULL: skip),
- *                      out_pool[i][j] = (((x[2i][2j] + x[2i][2j+1]) + x[2i+1][2j])
- *                                        + x[2i+1][2j+1]) / 4   (NULL: skip)
- * smmd_mask_pool2_adj: out = a * [m > 0] + nearest_up(b / 4)  (a or b NULL: that
- *                      term absent) -- the adjoint of smmd_mask_pool2 in x, so each
- *                      is the other's backward (linear in x / (a, b), m constant).
- * The select, the pooling order and the one add are those of torch's relu /
- * avg_pool2d / threshold_backward / nearest upsample and autograd's gradient
- * sum, so results are bit-identical to that composition.
+ * With s(m) = 1 where m > 0, else the slope, and u = x (+ y if y != NULL):
+ * smmd_mask_pool2:     out_masked = u * s_m(m)   (slope_m 0: the ReLU; NULL: skip),
+ *                      out_pool[i][j] = (((v[2i][2j] + v[2i][2j+1]) + v[2i+1][2j])
+ *                                        + v[2i+1][2j+1]) / 4,  v = u * s_p(m)
+ *                      (NULL: skip); m NULL: the mask source is u itself.
+ *                      slope_p 1 pools u; 0.2 pools lrelu(u) (the first block's
+ *                      input, architecture.py:393, never written); y is the
+ *                      previous block's second path (block.py:50's add, fused).
+ * smmd_mask_pool2_adj: out = a * s_m(m) + s_p(m) * nearest_up(b / 4)  (a or b
+ *                      NULL: that term absent) -- the adjoint of smmd_mask_pool2 in
+ *                      u, so each is the other's backward (linear, m constant).
+ * The selects, the pooling order and the one add are those of torch's relu /
+ * leaky_relu / avg_pool2d / their backward / nearest upsample and autograd's
+ * gradient sum, so results are bit-identical to that composition.
  * ------------------------------------------------------------------------- */
-smmd_status smmd_mask_pool2(const float *x, const float *m, int64_t planes, int H, int W,
-                            float *out_masked, float *out_pool, smmd_stream_t stream);
+smmd_status smmd_mask_pool2(const float *x, const float *y, const float *m, float slope_m,
+                            float slope_p, int64_t planes, int H, int W, float *out_masked,
+                            float *out_pool, smmd_stream_t stream);
 
-smmd_status smmd_mask_pool2_adj(const float *a, const float *b, const float *m, int64_t planes,
-                                int H, int W, float *out, smmd_stream_t stream);
+smmd_status smmd_mask_pool2_adj(const float *a, const float *b, const float *m, float slope_m,
+                                float slope_p, int64_t planes, int H, int W, float *out,
+                                smmd_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * Thin 3x3 convolutions: stride 1, zero padding 1 (TF SAME at stride 1), NCHW

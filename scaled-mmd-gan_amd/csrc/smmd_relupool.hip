@@ -7,8 +7,13 @@
 // slices / 4, then the 1x1 conv), :50 (shortcut + output, so the input's
 // gradient is the sum of the two paths' gradients).
 //
-//   mask_pool     (x; m) -> (x [m > 0], pool(x))        forward, m = x: (relu, pool)
-//   mask_pool_adj (a, b; m) -> a [m > 0] + up(b) / 4    its adjoint (the backward)
+//   mask_pool     (u; m) -> (u s_m(m), pool(u s_p(m)))     u = x (+ y)
+//   mask_pool_adj (a, b; m) -> a s_m(m) + s_p(m) up(b) / 4  its adjoint (the backward)
+// with s(m) = 1 where m > 0, else the slope (s_m: 0, the ReLU; s_p: 1, or the
+// leaky ReLU's 0.2 when the block input is lrelu of the first conv's output,
+// architecture.py:393 -- then relu(lrelu(h)) = relu(h) and the block's input
+// is never written).  y: the previous block's two paths, added here instead
+// of in a separate pass (block.py:50 feeding the next block).
 //
 // Each is linear in its first arguments with m a constant, and each is the
 // other's backward, so every order of the double backward is these two
@@ -25,10 +30,24 @@ namespace smmd {
 
 constexpr int RP_T = 256;
 
-__device__ __forceinline__ float msel(float m, float x) { return m > 0.f ? x : 0.f; }
+// x s(m): x where m > 0, else x * slope (0 for the ReLU; 1: x unchanged)
+__device__ __forceinline__ float msel(float m, float x, float slope) {
+    return m > 0.f ? x : (slope == 0.f ? 0.f : (slope == 1.f ? x : x * slope));
+}
+
+__device__ __forceinline__ float4 msel4(float4 m, float4 x, float slope) {
+    return make_float4(msel(m.x, x.x, slope), msel(m.y, x.y, slope), msel(m.z, x.z, slope),
+                       msel(m.w, x.w, slope));
+}
+
+__device__ __forceinline__ float4 add4(float4 a, float4 b) {
+    return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
 
 __global__ __launch_bounds__(RP_T) void mask_pool_kernel(const float *__restrict__ x,
+                                                         const float *__restrict__ y,
                                                          const float *__restrict__ m,
+                                                         float slope_m, float slope_p,
                                                          int64_t patches, int H, int W,
                                                          float *__restrict__ out_m,
                                                          float *__restrict__ out_p) {
@@ -40,23 +59,26 @@ __global__ __launch_bounds__(RP_T) void mask_pool_kernel(const float *__restrict
     const int i = (int)(r % hh);
     const int64_t plane = r / hh;
     const size_t o0 = ((size_t)plane * H + 2 * i) * W + 4 * j;
-    const float4 x0 = *reinterpret_cast<const float4 *>(x + o0);
-    const float4 x1 = *reinterpret_cast<const float4 *>(x + o0 + W);
+    float4 x0 = *reinterpret_cast<const float4 *>(x + o0);
+    float4 x1 = *reinterpret_cast<const float4 *>(x + o0 + W);
+    if (y) {                                  // the residual sum, x + y
+        x0 = add4(x0, *reinterpret_cast<const float4 *>(y + o0));
+        x1 = add4(x1, *reinterpret_cast<const float4 *>(y + o0 + W));
+    }
+    float4 m0 = x0, m1 = x1;                  // m NULL: the mask is the input itself
+    if (m) {
+        m0 = *reinterpret_cast<const float4 *>(m + o0);
+        m1 = *reinterpret_cast<const float4 *>(m + o0 + W);
+    }
     if (out_m) {
-        float4 m0 = x0, m1 = x1;
-        if (m != x) {
-            m0 = *reinterpret_cast<const float4 *>(m + o0);
-            m1 = *reinterpret_cast<const float4 *>(m + o0 + W);
-        }
-        *reinterpret_cast<float4 *>(out_m + o0) =
-            make_float4(msel(m0.x, x0.x), msel(m0.y, x0.y), msel(m0.z, x0.z), msel(m0.w, x0.w));
-        *reinterpret_cast<float4 *>(out_m + o0 + W) =
-            make_float4(msel(m1.x, x1.x), msel(m1.y, x1.y), msel(m1.z, x1.z), msel(m1.w, x1.w));
+        *reinterpret_cast<float4 *>(out_m + o0) = msel4(m0, x0, slope_m);
+        *reinterpret_cast<float4 *>(out_m + o0 + W) = msel4(m1, x1, slope_m);
     }
     if (out_p) {
 #pragma clang fp contract(off)
-        const float p0 = (((x0.x + x0.y) + x1.x) + x1.y) / 4.f;   // block.py:71 mean
-        const float p1 = (((x0.z + x0.w) + x1.z) + x1.w) / 4.f;
+        const float4 q0 = msel4(m0, x0, slope_p), q1 = msel4(m1, x1, slope_p);
+        const float p0 = (((q0.x + q0.y) + q1.x) + q1.y) / 4.f;   // block.py:71 mean
+        const float p1 = (((q0.z + q0.w) + q1.z) + q1.w) / 4.f;
         const size_t op = ((size_t)plane * hh + i) * (W >> 1) + 2 * j;
         *reinterpret_cast<float2 *>(out_p + op) = make_float2(p0, p1);
     }
@@ -65,6 +87,7 @@ __global__ __launch_bounds__(RP_T) void mask_pool_kernel(const float *__restrict
 __global__ __launch_bounds__(RP_T) void mask_pool_adj_kernel(const float *__restrict__ a,
                                                              const float *__restrict__ b,
                                                              const float *__restrict__ m,
+                                                             float slope_m, float slope_p,
                                                              int64_t patches, int H, int W,
                                                              float *__restrict__ out) {
     const int64_t t = (int64_t)blockIdx.x * RP_T + threadIdx.x;
@@ -75,26 +98,21 @@ __global__ __launch_bounds__(RP_T) void mask_pool_adj_kernel(const float *__rest
     const int i = (int)(r % hh);
     const int64_t plane = r / hh;
     const size_t o0 = ((size_t)plane * H + 2 * i) * W + 4 * j;
+    const float4 m0 = *reinterpret_cast<const float4 *>(m + o0);
+    const float4 m1 = *reinterpret_cast<const float4 *>(m + o0 + W);
     float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0;
     if (a) {
-        const float4 a0 = *reinterpret_cast<const float4 *>(a + o0);
-        const float4 a1 = *reinterpret_cast<const float4 *>(a + o0 + W);
-        const float4 m0 = *reinterpret_cast<const float4 *>(m + o0);
-        const float4 m1 = *reinterpret_cast<const float4 *>(m + o0 + W);
-        s0 = make_float4(msel(m0.x, a0.x), msel(m0.y, a0.y), msel(m0.z, a0.z), msel(m0.w, a0.w));
-        s1 = make_float4(msel(m1.x, a1.x), msel(m1.y, a1.y), msel(m1.z, a1.z), msel(m1.w, a1.w));
+        s0 = msel4(m0, *reinterpret_cast<const float4 *>(a + o0), slope_m);
+        s1 = msel4(m1, *reinterpret_cast<const float4 *>(a + o0 + W), slope_m);
     }
     if (b) {
         const size_t op = ((size_t)plane * hh + i) * (W >> 1) + 2 * j;
         const float2 bb = *reinterpret_cast<const float2 *>(b + op);
         const float q0 = bb.x * 0.25f, q1 = bb.y * 0.25f;   // up(b / 4): block.py:71 adjoint
-        if (a) {
-            s0.x += q0; s0.y += q0; s0.z += q1; s0.w += q1;
-            s1.x += q0; s1.y += q0; s1.z += q1; s1.w += q1;
-        } else {
-            s0 = make_float4(q0, q0, q1, q1);
-            s1 = s0;
-        }
+        const float4 u0 = msel4(m0, make_float4(q0, q0, q1, q1), slope_p);
+        const float4 u1 = msel4(m1, make_float4(q0, q0, q1, q1), slope_p);
+        s0 = a ? add4(s0, u0) : u0;
+        s1 = a ? add4(s1, u1) : u1;
     }
     *reinterpret_cast<float4 *>(out + o0) = s0;
     *reinterpret_cast<float4 *>(out + o0 + W) = s1;
@@ -111,31 +129,32 @@ static bool al8(const void *p) { return p == nullptr || ((uintptr_t)p & 7) == 0;
 
 using namespace smmd;
 
-extern "C" smmd_status smmd_mask_pool2(const float *x, const float *m, int64_t planes, int H,
+extern "C" smmd_status smmd_mask_pool2(const float *x, const float *y, const float *m,
+                                       float slope_m, float slope_p, int64_t planes, int H,
                                        int W, float *out_masked, float *out_pool,
                                        smmd_stream_t stream) {
-    if (!rp_shape_ok(planes, H, W) || !x || (out_masked && !m) || (!out_masked && !out_pool))
-        return SMMD_EINVAL;
-    if (!al16(x) || !al16(m) || !al16(out_masked) || !al8(out_pool)) return SMMD_EINVAL;
+    if (!rp_shape_ok(planes, H, W) || !x || (!out_masked && !out_pool)) return SMMD_EINVAL;
+    if (!al16(x) || !al16(y) || !al16(m) || !al16(out_masked) || !al8(out_pool)) return SMMD_EINVAL;
     const int64_t patches = planes * (H / 2) * (W / 4);
     if (patches == 0) return SMMD_OK;
     const int64_t blocks = (patches + RP_T - 1) / RP_T;
     if (blocks > 0x7fffffff) return SMMD_EINVAL;
     hipLaunchKernelGGL(mask_pool_kernel, dim3((unsigned)blocks), dim3(RP_T), 0,
-                       (hipStream_t)stream, x, m, patches, H, W, out_masked, out_pool);
+                       (hipStream_t)stream, x, y, m, slope_m, slope_p, patches, H, W, out_masked,
+                       out_pool);
     return last_launch_status();
 }
 
 extern "C" smmd_status smmd_mask_pool2_adj(const float *a, const float *b, const float *m,
-                                           int64_t planes, int H, int W, float *out,
-                                           smmd_stream_t stream) {
-    if (!rp_shape_ok(planes, H, W) || !out || (!a && !b) || (a && !m)) return SMMD_EINVAL;
+                                           float slope_m, float slope_p, int64_t planes, int H,
+                                           int W, float *out, smmd_stream_t stream) {
+    if (!rp_shape_ok(planes, H, W) || !out || !m || (!a && !b)) return SMMD_EINVAL;
     if (!al16(a) || !al16(m) || !al16(out) || !al8(b)) return SMMD_EINVAL;
     const int64_t patches = planes * (H / 2) * (W / 4);
     if (patches == 0) return SMMD_OK;
     const int64_t blocks = (patches + RP_T - 1) / RP_T;
     if (blocks > 0x7fffffff) return SMMD_EINVAL;
     hipLaunchKernelGGL(mask_pool_adj_kernel, dim3((unsigned)blocks), dim3(RP_T), 0,
-                       (hipStream_t)stream, a, b, m, patches, H, W, out);
+                       (hipStream_t)stream, a, b, m, slope_m, slope_p, patches, H, W, out);
     return last_launch_status();
 }

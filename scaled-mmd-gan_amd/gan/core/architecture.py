@@ -209,12 +209,18 @@ class ResidualBlock(nn.Module):
         # of x read the input in one pass (convops.relu_pool)
         self._relu_pool = resample == 'down' and not use_bn
 
+    def down_parts(self, x, y=None, slope_p=1.0):
+        """(shortcut, main path) of a critic down block, not yet added, whose
+        input is u = x + y (y None: x), or lrelu(x) when slope_p is 0.2: the
+        input is never written (convops.relu_pool reads x and y once)."""
+        r, p = convops.relu_pool(x, y, slope_p)
+        s = self.shortcut.conv(p)                        # _MeanPoolConv on the pooled input
+        h = self.conv_2(F.relu(self.bn2(self.conv_1(r))))
+        return s, h
+
     def forward(self, x):
         if self._relu_pool and convops.relu_pool_applicable(x):
-            r, p = convops.relu_pool(x)
-            s = self.shortcut.conv(p)                    # _MeanPoolConv on the pooled x
-            h = self.conv_1(r)
-            h = self.conv_2(F.relu(self.bn2(h)))
+            s, h = self.down_parts(x)
             return s + h
         s = x if self.shortcut is None else self.shortcut(x)
         h = self.conv_1(F.relu(self.bn1(x)))
@@ -399,6 +405,8 @@ class SNResNetDiscriminator(nn.Module):
             return self._forward(x, return_layers)
 
     def _forward(self, x, return_layers):
+        if not return_layers:
+            return self._forward_chained(x)
         layers = {}
         h = lrelu(self.h0(x))
         layers['h0'] = h
@@ -409,6 +417,26 @@ class SNResNetDiscriminator(nn.Module):
         hF = self.h5_lin(h)
         layers['hF'] = hF
         return layers if return_layers else hF
+
+    def _forward_chained(self, x):
+        """The same network with each down block's input kept as the pieces
+        that make it -- the first conv's pre-activation (its lrelu fused into
+        the block's input ops), then the previous block's two paths (their
+        add fused) -- so no block input is written or read twice."""
+        u, v, slope = self.h0(x), None, 0.2
+        for b in self.res:
+            if b._relu_pool and convops.relu_pool_applicable(u, v):
+                u, v = b.down_parts(u, v, slope)
+                slope = 1.0
+                continue
+            h = u if v is None else u + v
+            if slope != 1.0:
+                h = lrelu(h, slope)
+            u, v, slope = b(h), None, 1.0
+        h = u if v is None else u + v
+        if slope != 1.0:
+            h = lrelu(h, slope)
+        return self.h5_lin(lrelu(h).sum(dim=(2, 3)))
 
 
 class ResNetDiscriminator(nn.Module):

@@ -394,37 +394,47 @@ def mean_pool2(x):
 # ---------------------------------------------------------------------------
 # a critic down block's input: the main path's ReLU and the shortcut's mean
 # pool in one read, their gradients in one write (csrc/smmd_relupool.hip;
-# SMMD_RELU_POOL=0: relu + mean_pool2 as separate torch ops)
+# SMMD_RELU_POOL=0: relu + mean_pool2 as separate torch ops).  The input may
+# arrive as the previous block's two paths (their add fused) or as the first
+# conv's pre-activation (its leaky ReLU fused: relu(lrelu(h)) = relu(h)).
 # ---------------------------------------------------------------------------
 RELU_POOL = os.environ.get('SMMD_RELU_POOL', '1') != '0'
 
 
-def relu_pool_applicable(x):
-    """An NCHW fp32 device tensor with even height and width % 4 == 0."""
-    return (RELU_POOL and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
-            and x.is_contiguous() and x.shape[2] % 2 == 0 and x.shape[3] % 4 == 0)
+def relu_pool_applicable(x, y=None):
+    """An NCHW fp32 device tensor with even height and width % 4 == 0 (and y,
+    if given, of the same shape and layout)."""
+    ok = (RELU_POOL and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
+          and x.is_contiguous() and x.shape[2] % 2 == 0 and x.shape[3] % 4 == 0)
+    if ok and y is not None:
+        ok = y.shape == x.shape and y.dtype == x.dtype and y.is_contiguous() and y.is_cuda
+    return ok
 
 
-def _mask_pool(x, m, masked=True, pooled=True):
-    """smmd_mask_pool2: (x [m > 0], 2x2 mean pool of x); either may be skipped."""
+def _mask_pool(x, y, m, slope_m, slope_p, masked=True, pooled=True):
+    """smmd_mask_pool2: with u = x (+ y), (u s_m(m), pool(u s_p(m))); m None:
+    the mask source is u; either output may be skipped."""
     from . import _lib
     x = x.contiguous()
-    m = x if m is None else m.contiguous()
-    _lib.require_cuda(x, m)
+    y = y.contiguous() if y is not None else None
+    m = m.contiguous() if m is not None else None
+    _lib.require_cuda(*[t for t in (x, y, m) if t is not None])
     N, C, H, W = x.shape
     out_m = torch.empty_like(x) if masked else None
     out_p = torch.empty((N, C, H // 2, W // 2), dtype=x.dtype, device=x.device) if pooled else None
-    nb = x.numel() * (1 + (masked and m is not x) + masked) + (out_p.numel() if pooled else 0)
+    nb = x.numel() * (1 + (y is not None) + (m is not None) + masked) + \
+        (out_p.numel() if pooled else 0)
     _lib.add_bytes('smmd_mask_pool2', nb * 4)
     with _lib.timed('smmd_mask_pool2'):
-        st = _lib.lib().smmd_mask_pool2(_lib.ptr(x), _lib.ptr(m), N * C, H, W, _lib.ptr(out_m),
+        st = _lib.lib().smmd_mask_pool2(_lib.ptr(x), _lib.ptr(y), _lib.ptr(m), float(slope_m),
+                                        float(slope_p), N * C, H, W, _lib.ptr(out_m),
                                         _lib.ptr(out_p), _lib.stream_handle(x.device))
     _lib.check(st, 'smmd_mask_pool2')
     return out_m, out_p
 
 
-def _mask_pool_adj(a, b, m):
-    """smmd_mask_pool2_adj: a [m > 0] + nearest_up(b / 4) (a or b None: absent)."""
+def _mask_pool_adj(a, b, m, slope_m, slope_p):
+    """smmd_mask_pool2_adj: a s_m(m) + s_p(m) nearest_up(b / 4) (a or b None: absent)."""
     from . import _lib
     m = m.contiguous()
     a = a.contiguous() if a is not None else None
@@ -432,99 +442,87 @@ def _mask_pool_adj(a, b, m):
     _lib.require_cuda(m, *[t for t in (a, b) if t is not None])
     N, C, H, W = m.shape
     out = torch.empty_like(m)
-    nb = out.numel() * (1 + 2 * (a is not None)) + (b.numel() if b is not None else 0)
+    nb = out.numel() * (2 + (a is not None)) + (b.numel() if b is not None else 0)
     _lib.add_bytes('smmd_mask_pool2_adj', nb * 4)
     with _lib.timed('smmd_mask_pool2_adj'):
-        st = _lib.lib().smmd_mask_pool2_adj(_lib.ptr(a), _lib.ptr(b), _lib.ptr(m), N * C, H, W,
-                                            _lib.ptr(out), _lib.stream_handle(m.device))
+        st = _lib.lib().smmd_mask_pool2_adj(_lib.ptr(a), _lib.ptr(b), _lib.ptr(m), float(slope_m),
+                                            float(slope_p), N * C, H, W, _lib.ptr(out),
+                                            _lib.stream_handle(m.device))
     _lib.check(st, 'smmd_mask_pool2_adj')
     return out
 
 
 class _MaskPool(torch.autograd.Function):
-    """(x; m) -> (x [m > 0], pool(x)), linear in x with the mask m constant."""
+    """(x; m) -> (x s_m(m), pool(x s_p(m))): linear in x, the mask m constant."""
 
     @staticmethod
-    def forward(ctx, x, m):
+    def forward(ctx, x, m, slope_m, slope_p):
         ctx.save_for_backward(m)
+        ctx.slopes = (slope_m, slope_p)
         ctx.set_materialize_grads(False)
-        return _mask_pool(x, m)
+        return _mask_pool(x, None, m, slope_m, slope_p)
 
     @staticmethod
     def backward(ctx, ga, gb):
         if ga is None and gb is None:
-            return None, None
+            return None, None, None, None
         m, = ctx.saved_tensors
-        return _MaskPoolAdj.apply(ga, gb, m), None
+        return _MaskPoolAdj.apply(ga, gb, m, *ctx.slopes), None, None, None
 
 
 class _MaskPoolAdj(torch.autograd.Function):
-    """(a, b; m) -> a [m > 0] + up(b) / 4: the adjoint of _MaskPool, and its
-    backward (and the other way round), so every order of differentiation
+    """(a, b; m) -> a s_m(m) + s_p(m) up(b) / 4: the adjoint of _MaskPool, and
+    its backward (and the other way round), so every order of differentiation
     stays on the two kernels."""
 
     @staticmethod
-    def forward(ctx, a, b, m):
+    def forward(ctx, a, b, m, slope_m, slope_p):
         ctx.save_for_backward(m)
-        ctx.set_materialize_grads(False)
-        return _mask_pool_adj(a, b, m)
+        ctx.slopes = (slope_m, slope_p)
+        return _mask_pool_adj(a, b, m, slope_m, slope_p)
 
     @staticmethod
     def backward(ctx, g):
-        if g is None:
-            return None, None, None
         m, = ctx.saved_tensors
         need_a, need_b = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         if not (need_a or need_b):
-            return None, None, None
-        ga, gb = _mask_pool_torch_or_lib(g, m, need_a, need_b)
-        return ga, gb, None
-
-
-def _mask_pool_torch_or_lib(g, m, need_a, need_b):
-    if need_a and need_b:
-        return _MaskPool.apply(g, m)
-    # one output only: a single-output Function keeps the graph exact
-    if need_a:
-        return _MaskOnly.apply(g, m), None
-    return None, mean_pool2(g)
-
-
-class _MaskOnly(torch.autograd.Function):
-    """g -> g [m > 0] (self-adjoint)."""
-
-    @staticmethod
-    def forward(ctx, g, m):
-        ctx.save_for_backward(m)
-        return _mask_pool(g, m, pooled=False)[0]
-
-    @staticmethod
-    def backward(ctx, gg):
-        m, = ctx.saved_tensors
-        return _MaskOnly.apply(gg, m), None
+            return None, None, None, None, None
+        ga, gb = _MaskPool.apply(g, m, *ctx.slopes)
+        return (ga if need_a else None), (gb if need_b else None), None, None, None
 
 
 class _ReluPool(torch.autograd.Function):
-    """x -> (relu(x), pool(x)); the ReLU output is the backward's mask."""
+    """(x, y) -> (relu(u), pool(u s_p(u))), u = x + y (y may be None): the
+    ReLU output is the backward's mask (its sign is u's); the gradient of u
+    goes to both x and y."""
 
     @staticmethod
-    def forward(ctx, x):
-        r, p = _mask_pool(x, None)
+    def forward(ctx, x, y, slope_p):
+        r, p = _mask_pool(x, y, None, 0.0, slope_p)
         ctx.save_for_backward(r)
+        ctx.slope_p = slope_p
+        ctx.has_y = y is not None
         ctx.set_materialize_grads(False)
         return r, p
 
     @staticmethod
     def backward(ctx, gr, gp):
         if gr is None and gp is None:
-            return None
+            return None, None, None
         r, = ctx.saved_tensors
-        return _MaskPoolAdj.apply(gr, gp, r)
+        gu = _MaskPoolAdj.apply(gr, gp, r, 0.0, ctx.slope_p)
+        return gu, (gu if ctx.has_y else None), None
 
 
-def relu_pool(x):
-    """(relu(x), mean_pool2(x)) of a critic down block's input (block.py:44,
-    :69-71): one HIP pass each way on device tensors, torch ops otherwise."""
-    if relu_pool_applicable(x):
-        return _ReluPool.apply(x)
-    return F.relu(x), mean_pool2(x)
+def relu_pool(x, y=None, slope_p=1.0):
+    """A critic down block's two input ops (block.py:44, :69-71) on u = x + y
+    (y None: u = x): (relu(u), mean_pool2(u)) with slope_p 1, or with slope_p
+    0.2 (relu(lrelu(u)), mean_pool2(lrelu(u))) -- u the first conv's output,
+    architecture.py:393.  One HIP pass each way on device tensors, the torch
+    composition otherwise."""
+    if relu_pool_applicable(x, y):
+        return _ReluPool.apply(x, y, float(slope_p))
+    u = x if y is None else x + y
+    if slope_p != 1.0:
+        u = F.leaky_relu(u, slope_p)
+    return F.relu(u), mean_pool2(u)

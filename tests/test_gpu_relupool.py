@@ -136,8 +136,89 @@ def test_mask_pool_abi_rejects_bad_shapes():
     x = torch.zeros(1, 1, 4, 6, device=DEV)
     o = torch.empty_like(x)
     s = _lib.stream_handle(x.device)
-    assert L.smmd_mask_pool2(_lib.ptr(x), _lib.ptr(x), 1, 4, 6, _lib.ptr(o), None, s) != 0
-    assert L.smmd_mask_pool2(_lib.ptr(x), _lib.ptr(x), 1, 3, 4, _lib.ptr(o), None, s) != 0
-    assert L.smmd_mask_pool2_adj(None, None, _lib.ptr(x), 1, 4, 4, _lib.ptr(o), s) != 0
+    P = _lib.ptr
+    assert L.smmd_mask_pool2(P(x), None, None, 0.0, 1.0, 1, 4, 6, P(o), None, s) != 0   # W % 4
+    assert L.smmd_mask_pool2(P(x), None, None, 0.0, 1.0, 1, 3, 4, P(o), None, s) != 0   # H odd
+    assert L.smmd_mask_pool2(P(x), None, None, 0.0, 1.0, 1, 4, 4, None, None, s) != 0   # no output
+    assert L.smmd_mask_pool2_adj(None, None, P(x), 0.0, 1.0, 1, 4, 4, P(o), s) != 0     # no term
+    assert L.smmd_mask_pool2_adj(P(x), None, None, 0.0, 1.0, 1, 4, 4, P(o), s) != 0     # no mask
     torch.cuda.synchronize()
     np.testing.assert_array_equal(o.shape, x.shape)
+
+
+def _ref_general(x, y, slope):
+    from gan.core.convops import mean_pool2
+    u = x if y is None else x + y
+    if slope != 1.0:
+        u = F.leaky_relu(u, slope)
+    return F.relu(u), mean_pool2(u)
+
+
+@pytest.mark.parametrize('variant', ['add', 'lrelu', 'add_lrelu'])
+def test_relu_pool_fused_add_and_lrelu_equal_torch(variant):
+    """The chained critic's block inputs: u = x + y (the previous block's two
+    paths, block.py:50) or lrelu(x) (the first conv's pre-activation,
+    architecture.py:393): outputs and the gradients of x and y, bit for bit."""
+    from gan.core import convops
+    g = torch.Generator(device=DEV).manual_seed(21)
+    x = torch.randn(8, 16, 16, 16, device=DEV, generator=g)
+    y = torch.randn(8, 16, 16, 16, device=DEV, generator=g) if 'add' in variant else None
+    slope = 0.2 if 'lrelu' in variant else 1.0
+    A = torch.randn(8, 16, 16, 16, device=DEV, generator=g)
+    B = torch.randn(8, 16, 8, 8, device=DEV, generator=g)
+    res = []
+    for fn in (convops.relu_pool, _ref_general):
+        xx = x.clone().requires_grad_(True)
+        yy = y.clone().requires_grad_(True) if y is not None else None
+        r, p = fn(xx, yy, slope)
+        ins = [xx] + ([yy] if yy is not None else [])
+        grads = torch.autograd.grad((r * A).sum() + (p * B).sum(), ins)
+        res.append([r.detach(), p.detach()] + list(grads))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+
+
+def test_relu_pool_lrelu_double_backward_matches_torch():
+    from gan.core import convops
+    g = torch.Generator(device=DEV).manual_seed(23)
+    x = torch.randn(4, 8, 16, 16, device=DEV, generator=g)
+    w1 = torch.randn(8, 8, 3, 3, device=DEV, generator=g) * 0.2
+    w2 = torch.randn(8, 8, 1, 1, device=DEV, generator=g) * 0.2
+    w3 = torch.randn(1, 8, 1, 1, device=DEV, generator=g) * 0.2
+    res = []
+    for fn in (lambda t: convops.relu_pool(t, None, 0.2), lambda t: _ref_general(t, None, 0.2)):
+        xx = x.clone().requires_grad_(True)
+        ws = [w.clone().requires_grad_(True) for w in (w1, w2, w3)]
+        feat = _tiny_critic(xx, *ws, fn)
+        jac, = torch.autograd.grad(feat.sum(), xx, create_graph=True)
+        gws = torch.autograd.grad((jac * jac).sum() + feat.sum(), ws)
+        res.append([jac.detach()] + list(gws))
+    for a, b in zip(*res):
+        tol = 1e-5 * float(b.abs().max()) + 1e-7
+        assert float((a - b).abs().max()) <= tol
+
+
+def test_snresnet_critic_chained_equals_layerwise(relu_pool_off):
+    """The SNResNet-64 critic (architecture.py:410-434) with its block inputs
+    chained through the fused ops against the same critic on the unfused
+    composition: features, the input Jacobian and the parameter gradients of
+    a scaling-regulariser loss."""
+    convops = relu_pool_off
+    from gan.core.architecture import SNResNetDiscriminator
+    torch.manual_seed(4)
+    D = SNResNetDiscriminator(16, 1, False, input_size=64).to(DEV)
+    x0 = torch.rand(8, 3, 64, 64, device=DEV)
+    out = []
+    for on in (True, False):
+        convops.RELU_POOL = on
+        x = x0.clone().requires_grad_(True)
+        feat = D(x)
+        jac, = torch.autograd.grad(feat.sum(), x, create_graph=True)
+        L = feat.sum() + 10.0 * (jac * jac).sum()
+        gp = torch.autograd.grad(L, list(D.parameters()))
+        out.append([feat.detach(), jac.detach()] + [t.detach() for t in gp])
+    # same ops in the same order, but MIOpen's convolutions are not bitwise
+    # reproducible run to run, so the comparison carries a tolerance
+    for a, b in zip(*out):
+        tol = 1e-5 * float(b.abs().max()) + 1e-7
+        assert float((a - b).abs().max()) <= tol
