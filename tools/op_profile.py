@@ -19,6 +19,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--steps', type=int, default=6)
     ap.add_argument('--out', default='gpurun_out/ops.txt')
+    ap.add_argument('--stack', action='store_true',
+                    help='also attribute small add_/fill_/add kernels to Python call sites')
     args = ap.parse_args()
     import bench
     from gan.core import miopen_db
@@ -35,7 +37,7 @@ def main():
     torch.cuda.synchronize()
     from torch.profiler import ProfilerActivity, profile
     with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA],
-                 record_shapes=True) as prof:
+                 record_shapes=True, with_stack=args.stack) as prof:
         for _ in range(args.steps):
             model.train_step(images)
         torch.cuda.synchronize()
@@ -61,6 +63,15 @@ def main():
         for e in rows[:60]:
             f.write('%-12s %10.1f us total %5d calls  %s\n' % (
                 e.key, e.self_device_time_total, e.count, str(e.input_shapes)[:160]))
+    if args.stack:
+        st = prof.key_averages(group_by_stack_n=6)
+        rows = [e for e in st if e.key in ('aten::add_', 'aten::add', 'aten::fill_', 'aten::zero_',
+                                           'aten::zeros', 'aten::zeros_like', 'aten::copy_')]
+        rows.sort(key=lambda e: -e.count)
+        with open(args.out.replace('.txt', '_stacks.txt'), 'w') as f:
+            for e in rows[:40]:
+                f.write('%-14s %5d calls %10.1f us\n    %s\n' % (
+                    e.key, e.count, e.self_device_time_total, '\n    '.join(e.stack[:6])))
     print(tab[:6000])
 
 
