@@ -378,7 +378,8 @@ smmd_status smmd_channel_sum(const float *gy, int N, int C, int HW, float *out, 
  * previous block's two paths, or the first conv's pre-activation) and write
  * its gradient in one pass backward.  Planes [planes, H, W] NCHW fp32, H even,
  * W % 4 == 0, 16-byte aligned full-size tensors, 8-byte aligned pooled ones.
- * With s(m) = 1 where m > 0, else the slope, and u = x (+ y if y != NULL):
+ * With s(m) = 1 where m > 0, else the slope, and u = (x + bx) (+ (y + by) if y
+ * != NULL), bx / by per-channel biases [C] of planes = N * C (NULL: none):
  * smmd_mask_pool2:     out_masked = u * s_m(m)   (slope_m 0: the ReLU; NULL: skip),
  *                      out_pool[i][j] = (((v[2i][2j] + v[2i][2j+1]) + v[2i+1][2j])
  *                                        + v[2i+1][2j+1]) / 4,  v = u * s_p(m)
@@ -393,9 +394,10 @@ smmd_status smmd_channel_sum(const float *gy, int N, int C, int HW, float *out, 
  * leaky_relu / avg_pool2d / their backward / nearest upsample and autograd's
  * gradient sum, so results are bit-identical to that composition.
  * ------------------------------------------------------------------------- */
-smmd_status smmd_mask_pool2(const float *x, const float *y, const float *m, float slope_m,
-                            float slope_p, int64_t planes, int H, int W, float *out_masked,
-                            float *out_pool, smmd_stream_t stream);
+smmd_status smmd_mask_pool2(const float *x, const float *y, const float *bx, const float *by,
+                            int C, const float *m, float slope_m, float slope_p, int64_t planes,
+                            int H, int W, float *out_masked, float *out_pool,
+                            smmd_stream_t stream);
 
 smmd_status smmd_mask_pool2_adj(const float *a, const float *b, const float *m, float slope_m,
                                 float slope_p, int64_t planes, int H, int W, float *out,

@@ -7,13 +7,14 @@
 // slices / 4, then the 1x1 conv), :50 (shortcut + output, so the input's
 // gradient is the sum of the two paths' gradients).
 //
-//   mask_pool     (u; m) -> (u s_m(m), pool(u s_p(m)))     u = x (+ y)
+//   mask_pool     (u; m) -> (u s_m(m), pool(u s_p(m)))     u = (x + bx) (+ (y + by))
 //   mask_pool_adj (a, b; m) -> a s_m(m) + s_p(m) up(b) / 4  its adjoint (the backward)
 // with s(m) = 1 where m > 0, else the slope (s_m: 0, the ReLU; s_p: 1, or the
 // leaky ReLU's 0.2 when the block input is lrelu of the first conv's output,
 // architecture.py:393 -- then relu(lrelu(h)) = relu(h) and the block's input
 // is never written).  y: the previous block's two paths, added here instead
-// of in a separate pass (block.py:50 feeding the next block).
+// of in a separate pass (block.py:50 feeding the next block); bx, by: their
+// convolutions' per-channel biases (snops.py:89-90), added here too.
 //
 // Each is linear in its first arguments with m a constant, and each is the
 // other's backward, so every order of the double backward is these two
@@ -44,8 +45,14 @@ __device__ __forceinline__ float4 add4(float4 a, float4 b) {
     return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
 }
 
+__device__ __forceinline__ float4 addb(float4 a, float b) {
+    return make_float4(a.x + b, a.y + b, a.z + b, a.w + b);
+}
+
 __global__ __launch_bounds__(RP_T) void mask_pool_kernel(const float *__restrict__ x,
                                                          const float *__restrict__ y,
+                                                         const float *__restrict__ bx,
+                                                         const float *__restrict__ by, int C,
                                                          const float *__restrict__ m,
                                                          float slope_m, float slope_p,
                                                          int64_t patches, int H, int W,
@@ -61,9 +68,22 @@ __global__ __launch_bounds__(RP_T) void mask_pool_kernel(const float *__restrict
     const size_t o0 = ((size_t)plane * H + 2 * i) * W + 4 * j;
     float4 x0 = *reinterpret_cast<const float4 *>(x + o0);
     float4 x1 = *reinterpret_cast<const float4 *>(x + o0 + W);
+    const int c = (bx || by) ? (int)(plane % C) : 0;
+    if (bx) {                                 // conv output + its bias
+        const float b = bx[c];
+        x0 = addb(x0, b);
+        x1 = addb(x1, b);
+    }
     if (y) {                                  // the residual sum, x + y
-        x0 = add4(x0, *reinterpret_cast<const float4 *>(y + o0));
-        x1 = add4(x1, *reinterpret_cast<const float4 *>(y + o0 + W));
+        float4 y0 = *reinterpret_cast<const float4 *>(y + o0);
+        float4 y1 = *reinterpret_cast<const float4 *>(y + o0 + W);
+        if (by) {
+            const float b = by[c];
+            y0 = addb(y0, b);
+            y1 = addb(y1, b);
+        }
+        x0 = add4(x0, y0);
+        x1 = add4(x1, y1);
     }
     float4 m0 = x0, m1 = x1;                  // m NULL: the mask is the input itself
     if (m) {
@@ -129,19 +149,21 @@ static bool al8(const void *p) { return p == nullptr || ((uintptr_t)p & 7) == 0;
 
 using namespace smmd;
 
-extern "C" smmd_status smmd_mask_pool2(const float *x, const float *y, const float *m,
-                                       float slope_m, float slope_p, int64_t planes, int H,
-                                       int W, float *out_masked, float *out_pool,
+extern "C" smmd_status smmd_mask_pool2(const float *x, const float *y, const float *bx,
+                                       const float *by, int C, const float *m, float slope_m,
+                                       float slope_p, int64_t planes, int H, int W,
+                                       float *out_masked, float *out_pool,
                                        smmd_stream_t stream) {
     if (!rp_shape_ok(planes, H, W) || !x || (!out_masked && !out_pool)) return SMMD_EINVAL;
+    if ((by && !y) || ((bx || by) && (C < 1 || planes % C != 0))) return SMMD_EINVAL;
     if (!al16(x) || !al16(y) || !al16(m) || !al16(out_masked) || !al8(out_pool)) return SMMD_EINVAL;
     const int64_t patches = planes * (H / 2) * (W / 4);
     if (patches == 0) return SMMD_OK;
     const int64_t blocks = (patches + RP_T - 1) / RP_T;
     if (blocks > 0x7fffffff) return SMMD_EINVAL;
     hipLaunchKernelGGL(mask_pool_kernel, dim3((unsigned)blocks), dim3(RP_T), 0,
-                       (hipStream_t)stream, x, y, m, slope_m, slope_p, patches, H, W, out_masked,
-                       out_pool);
+                       (hipStream_t)stream, x, y, bx, by, C, m, slope_m, slope_p, patches, H, W,
+                       out_masked, out_pool);
     return last_launch_status();
 }
 

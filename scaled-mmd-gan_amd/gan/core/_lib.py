@@ -121,7 +121,7 @@ _SIGS = {
     'smmd_channel_sum_workspace_bytes': (_SZ, [_I, _I]),
     'smmd_channel_sum': (_I, [_P, _I, _I, _I, _P, _P, _SZ, _P]),
     'smmd_conv3x3_thin': (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
-    'smmd_mask_pool2': (_I, [_P, _P, _P, _F, _F, _I64, _I, _I, _P, _P, _P]),
+    'smmd_mask_pool2': (_I, [_P, _P, _P, _P, _I, _P, _F, _F, _I64, _I, _I, _P, _P, _P]),
     'smmd_mask_pool2_adj': (_I, [_P, _P, _P, _F, _F, _I64, _I, _I, _P, _P]),
     'smmd_conv3x3_thin_wgrad_workspace_bytes': (_SZ, [_I, _I, _I, _I, _I]),
     'smmd_conv3x3_thin_wgrad': (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P, _SZ, _P]),

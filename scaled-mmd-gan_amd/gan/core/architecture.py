@@ -45,6 +45,9 @@ def _bn_or_id(use, c):
 FOLD_POOL = os.environ.get('SMMD_FOLD_POOL', '1') != '0'
 # SMMD_FOLD_UP=0 restores the literal upsample -> conv order of UpsampleConv
 FOLD_UP = os.environ.get('SMMD_FOLD_UP', '1') != '0'
+# SMMD_DEFER_BIAS=0: each critic block's two conv biases added by the convs
+# themselves instead of inside the next block's fused input pass (A/B)
+DEFER_BIAS = os.environ.get('SMMD_DEFER_BIAS', '1') != '0'
 # Host-side caches of folded filters (the generator's across critic steps,
 # the critic's across its real / fake calls).  A captured step graph
 # (model.StepGraphs) must recompute them on every replay: it turns this off.
@@ -104,8 +107,19 @@ class _ConvMeanPool(nn.Module):
     def foldable(self):
         return FOLD_POOL and self.conv.k == 3 and self.conv.stride == 1
 
-    def forward(self, x):
+    def bias_deferrable(self, x):
+        """The bias is a plain per-channel add after the folded conv (the
+        literal conv -> pool order would pool it)."""
+        return self.foldable() and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0
+
+    def forward(self, x, with_bias=True):
+        """with_bias False (the folded path only, see bias_deferrable): the
+        convolution alone, a consumer adds self.conv.bias."""
         c = self.conv
+        if not with_bias:
+            assert self.bias_deferrable(x)
+            w4 = self._w4 if self._w4 is not None else fold_pool_weight(c.effective_weight())
+            return conv2d(x, w4, None, 2, 1)
         if self.foldable() and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0:
             # meanpool2(conv3x3(x)) as ONE 4x4 stride-2 conv on the folded
             # weight: same value, a quarter of the output rows, no pool and no
@@ -209,18 +223,26 @@ class ResidualBlock(nn.Module):
         # of x read the input in one pass (convops.relu_pool)
         self._relu_pool = resample == 'down' and not use_bn
 
-    def down_parts(self, x, y=None, slope_p=1.0):
-        """(shortcut, main path) of a critic down block, not yet added, whose
-        input is u = x + y (y None: x), or lrelu(x) when slope_p is 0.2: the
-        input is never written (convops.relu_pool reads x and y once)."""
-        r, p = convops.relu_pool(x, y, slope_p)
-        s = self.shortcut.conv(p)                        # _MeanPoolConv on the pooled input
-        h = self.conv_2(F.relu(self.bn2(self.conv_1(r))))
-        return s, h
+    def down_parts(self, x, y=None, slope_p=1.0, bx=None, by=None, defer_bias=False):
+        """(shortcut, main path, their biases) of a critic down block, not yet
+        added, whose input is u = (x + bx) + (y + by) (None terms absent), or
+        lrelu(x) when slope_p is 0.2: the input is never written
+        (convops.relu_pool reads x and y once and adds the biases).  With
+        defer_bias the two convolutions leave their biases to the consumer
+        (the next block's relu_pool) and return them; otherwise (None, None)."""
+        r, p = convops.relu_pool(x, y, slope_p, bx, by)
+        h1 = F.relu(self.bn2(self.conv_1(r)))
+        sc = self.shortcut.conv
+        if defer_bias and self.conv_2.bias_deferrable(h1) and sc.bias is not None \
+                and self.conv_2.conv.bias is not None:
+            s = sc(p, with_bias=False)                   # _MeanPoolConv on the pooled input
+            h = self.conv_2(h1, with_bias=False)
+            return s, h, sc.bias, self.conv_2.conv.bias
+        return sc(p), self.conv_2(h1), None, None
 
     def forward(self, x):
         if self._relu_pool and convops.relu_pool_applicable(x):
-            s, h = self.down_parts(x)
+            s, h, _, _ = self.down_parts(x)
             return s + h
         s = x if self.shortcut is None else self.shortcut(x)
         h = self.conv_1(F.relu(self.bn1(x)))
@@ -421,22 +443,31 @@ class SNResNetDiscriminator(nn.Module):
     def _forward_chained(self, x):
         """The same network with each down block's input kept as the pieces
         that make it -- the first conv's pre-activation (its lrelu fused into
-        the block's input ops), then the previous block's two paths (their
-        add fused) -- so no block input is written or read twice."""
-        u, v, slope = self.h0(x), None, 0.2
-        for b in self.res:
+        the block's input ops), then the previous block's two paths and their
+        conv biases (the add and the bias adds fused) -- so no block input is
+        written or read twice."""
+        u, v, bu, bv, slope = self.h0(x), None, None, None, 0.2
+        n = len(self.res)
+        for i, b in enumerate(self.res):
             if b._relu_pool and convops.relu_pool_applicable(u, v):
-                u, v = b.down_parts(u, v, slope)
+                nxt = self.res[i + 1] if i + 1 < n else None
+                defer = DEFER_BIAS and nxt is not None and nxt._relu_pool and convops.RELU_POOL
+                u, v, bu, bv = b.down_parts(u, v, slope, bu, bv, defer_bias=defer)
                 slope = 1.0
                 continue
-            h = u if v is None else u + v
-            if slope != 1.0:
-                h = lrelu(h, slope)
-            u, v, slope = b(h), None, 1.0
-        h = u if v is None else u + v
-        if slope != 1.0:
-            h = lrelu(h, slope)
+            u, v, bu, bv, slope = b(self._join(u, v, bu, bv, slope)), None, None, None, 1.0
+        h = self._join(u, v, bu, bv, slope)
         return self.h5_lin(lrelu(h).sum(dim=(2, 3)))
+
+    @staticmethod
+    def _join(u, v, bu, bv, slope):
+        """(u + bu) + (v + bv), then lrelu unless slope is 1: the block
+        output exactly as the unfused ops form it."""
+        if bu is not None:
+            u = u + bu.view(1, -1, 1, 1)
+        if v is not None:
+            u = u + (v if bv is None else v + bv.view(1, -1, 1, 1))
+        return u if slope == 1.0 else lrelu(u, slope)
 
 
 class ResNetDiscriminator(nn.Module):

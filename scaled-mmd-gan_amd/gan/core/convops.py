@@ -411,14 +411,14 @@ def relu_pool_applicable(x, y=None):
     return ok
 
 
-def _mask_pool(x, y, m, slope_m, slope_p, masked=True, pooled=True):
-    """smmd_mask_pool2: with u = x (+ y), (u s_m(m), pool(u s_p(m))); m None:
-    the mask source is u; either output may be skipped."""
+def _mask_pool(x, y, m, slope_m, slope_p, masked=True, pooled=True, bx=None, by=None):
+    """smmd_mask_pool2: with u = (x + bx) (+ (y + by)), (u s_m(m), pool(u s_p(m)));
+    m None: the mask source is u; either output may be skipped."""
     from . import _lib
     x = x.contiguous()
     y = y.contiguous() if y is not None else None
     m = m.contiguous() if m is not None else None
-    _lib.require_cuda(*[t for t in (x, y, m) if t is not None])
+    _lib.require_cuda(*[t for t in (x, y, m, bx, by) if t is not None])
     N, C, H, W = x.shape
     out_m = torch.empty_like(x) if masked else None
     out_p = torch.empty((N, C, H // 2, W // 2), dtype=x.dtype, device=x.device) if pooled else None
@@ -426,9 +426,10 @@ def _mask_pool(x, y, m, slope_m, slope_p, masked=True, pooled=True):
         (out_p.numel() if pooled else 0)
     _lib.add_bytes('smmd_mask_pool2', nb * 4)
     with _lib.timed('smmd_mask_pool2'):
-        st = _lib.lib().smmd_mask_pool2(_lib.ptr(x), _lib.ptr(y), _lib.ptr(m), float(slope_m),
-                                        float(slope_p), N * C, H, W, _lib.ptr(out_m),
-                                        _lib.ptr(out_p), _lib.stream_handle(x.device))
+        st = _lib.lib().smmd_mask_pool2(_lib.ptr(x), _lib.ptr(y), _lib.ptr(bx), _lib.ptr(by), C,
+                                        _lib.ptr(m), float(slope_m), float(slope_p), N * C, H, W,
+                                        _lib.ptr(out_m), _lib.ptr(out_p),
+                                        _lib.stream_handle(x.device))
     _lib.check(st, 'smmd_mask_pool2')
     return out_m, out_p
 
@@ -492,37 +493,46 @@ class _MaskPoolAdj(torch.autograd.Function):
 
 
 class _ReluPool(torch.autograd.Function):
-    """(x, y) -> (relu(u), pool(u s_p(u))), u = x + y (y may be None): the
-    ReLU output is the backward's mask (its sign is u's); the gradient of u
-    goes to both x and y."""
+    """(x, y, bx, by) -> (relu(u), pool(u s_p(u))), u = (x + bx) + (y + by) (y,
+    bx, by may be None): the ReLU output is the backward's mask (its sign is
+    u's); the gradient of u goes to x and y, its channel sum to bx and by."""
 
     @staticmethod
-    def forward(ctx, x, y, slope_p):
-        r, p = _mask_pool(x, y, None, 0.0, slope_p)
+    def forward(ctx, x, y, bx, by, slope_p):
+        r, p = _mask_pool(x, y, None, 0.0, slope_p, bx=bx, by=by)
         ctx.save_for_backward(r)
         ctx.slope_p = slope_p
-        ctx.has_y = y is not None
+        ctx.has = (y is not None, bx is not None, by is not None)
         ctx.set_materialize_grads(False)
         return r, p
 
     @staticmethod
     def backward(ctx, gr, gp):
         if gr is None and gp is None:
-            return None, None, None
+            return None, None, None, None, None
         r, = ctx.saved_tensors
         gu = _MaskPoolAdj.apply(gr, gp, r, 0.0, ctx.slope_p)
-        return gu, (gu if ctx.has_y else None), None
+        has_y, has_bx, has_by = ctx.has
+        gb = None
+        if (has_bx and ctx.needs_input_grad[2]) or (has_by and ctx.needs_input_grad[3]):
+            if _input_only[0] == 0:         # not the Jacobian's input-only pass
+                gb = bias_grad(gu)
+        return (gu, (gu if has_y else None), (gb if has_bx else None), (gb if has_by else None),
+                None)
 
 
-def relu_pool(x, y=None, slope_p=1.0):
-    """A critic down block's two input ops (block.py:44, :69-71) on u = x + y
-    (y None: u = x): (relu(u), mean_pool2(u)) with slope_p 1, or with slope_p
-    0.2 (relu(lrelu(u)), mean_pool2(lrelu(u))) -- u the first conv's output,
-    architecture.py:393.  One HIP pass each way on device tensors, the torch
-    composition otherwise."""
+def relu_pool(x, y=None, slope_p=1.0, bx=None, by=None):
+    """A critic down block's two input ops (block.py:44, :69-71) on u = (x +
+    bx) + (y + by) (y None: u = x + bx; bx, by: the previous block's conv
+    biases, None when already applied): (relu(u), mean_pool2(u)) with slope_p
+    1, or with slope_p 0.2 (relu(lrelu(u)), mean_pool2(lrelu(u))) -- u the
+    first conv's output, architecture.py:393.  One HIP pass each way on
+    device tensors, the torch composition otherwise."""
     if relu_pool_applicable(x, y):
-        return _ReluPool.apply(x, y, float(slope_p))
-    u = x if y is None else x + y
+        return _ReluPool.apply(x, y, bx, by, float(slope_p))
+    u = x if bx is None else x + bx.view(1, -1, 1, 1)
+    if y is not None:
+        u = u + (y if by is None else y + by.view(1, -1, 1, 1))
     if slope_p != 1.0:
         u = F.leaky_relu(u, slope_p)
     return F.relu(u), mean_pool2(u)

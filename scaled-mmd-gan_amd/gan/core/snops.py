@@ -81,14 +81,16 @@ class Conv2d(nn.Module, _SNMixin):
         self.bias = nn.Parameter(torch.zeros(cout)) if bias else None
         self._init_sn(with_sn, with_learnable_sn_scale, scale)
 
-    def forward(self, x):
+    def forward(self, x, with_bias=True):
+        """with_bias False: the convolution alone (a consumer adds self.bias)."""
         w = self.effective_weight()
+        b = self.bias if with_bias else None
         ph = same_pad(x.shape[2], self.k, self.stride)
         pw = same_pad(x.shape[3], self.k, self.stride)
         if ph[0] == ph[1] and pw[0] == pw[1]:
-            return conv2d(x, w, self.bias, self.stride, (ph[0], pw[0]))
+            return conv2d(x, w, b, self.stride, (ph[0], pw[0]))
         x = F.pad(x, (pw[0], pw[1], ph[0], ph[1]))
-        return conv2d(x, w, self.bias, self.stride, 0)
+        return conv2d(x, w, b, self.stride, 0)
 
 
 class Deconv2d(nn.Module, _SNMixin):

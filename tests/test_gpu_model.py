@@ -302,8 +302,10 @@ def test_step_graphs_match_eager(dev):
     rate (the states stay equal to far below the gradients' rounding, so the
     moments compare tightly) and a second eager copy calibrates the rest:
     parameters within 5 % of the update they made (+3x the eager-vs-eager
-    spread), moments within 1e-3 (+3x); a stale tensor or a wrong step size
-    in a replay is O(1) there."""
+    spread), moments within 3e-3 (+3x: graph replays have come out up to
+    1.4e-3 from eager on MI355X while two eager copies agree to 1e-9, MIOpen
+    picking its kernels per capture); a stale tensor or a wrong step size in a
+    replay is O(1) there."""
     from gan.core.smmd import SMMD
     torch.manual_seed(0)
     cfg = _cfg(learning_rate=1e-8)
@@ -344,7 +346,7 @@ def test_step_graphs_match_eager(dev):
         for t in ('flat_param', 'm', 'v'):
             ta, tb, tc = (getattr(o, t) for o in (oa, ob, oc))
             noise = dist(ta, tc)
-            lim = 0.05 * moved if t == 'flat_param' else 1e-3 * float(ta.norm())
+            lim = 0.05 * moved if t == 'flat_param' else 3e-3 * float(ta.norm())
             assert dist(ta, tb) <= 3 * noise + lim, (name, t, dist(ta, tb), noise, lim)
     b.enable_graphs(False)
     b.train_step(imgs[0])                      # back to eager

@@ -137,9 +137,13 @@ def test_mask_pool_abi_rejects_bad_shapes():
     o = torch.empty_like(x)
     s = _lib.stream_handle(x.device)
     P = _lib.ptr
-    assert L.smmd_mask_pool2(P(x), None, None, 0.0, 1.0, 1, 4, 6, P(o), None, s) != 0   # W % 4
-    assert L.smmd_mask_pool2(P(x), None, None, 0.0, 1.0, 1, 3, 4, P(o), None, s) != 0   # H odd
-    assert L.smmd_mask_pool2(P(x), None, None, 0.0, 1.0, 1, 4, 4, None, None, s) != 0   # no output
+    b = torch.zeros(3, device=DEV)
+    args = lambda H, W, om, op, C=1, bx=None: (P(x), None, P(bx), None, C, None, 0.0, 1.0, 1,
+                                              H, W, om, op, s)
+    assert L.smmd_mask_pool2(*args(4, 6, P(o), None)) != 0          # W % 4
+    assert L.smmd_mask_pool2(*args(3, 4, P(o), None)) != 0          # H odd
+    assert L.smmd_mask_pool2(*args(4, 4, None, None)) != 0          # no output
+    assert L.smmd_mask_pool2(*args(4, 4, P(o), None, 3, b)) != 0    # planes % C
     assert L.smmd_mask_pool2_adj(None, None, P(x), 0.0, 1.0, 1, 4, 4, P(o), s) != 0     # no term
     assert L.smmd_mask_pool2_adj(P(x), None, None, 0.0, 1.0, 1, 4, 4, P(o), s) != 0     # no mask
     torch.cuda.synchronize()
@@ -176,6 +180,35 @@ def test_relu_pool_fused_add_and_lrelu_equal_torch(variant):
         res.append([r.detach(), p.detach()] + list(grads))
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+def test_relu_pool_with_deferred_biases_equals_torch():
+    """The previous block's two conv biases added inside the fused pass:
+    u = (x + bx) + (y + by); outputs and the gradients of x, y, bx, by against
+    the broadcast adds of the unfused convolutions, bit for bit."""
+    from gan.core import convops
+    g = torch.Generator(device=DEV).manual_seed(31)
+    x = torch.randn(8, 16, 16, 16, device=DEV, generator=g)
+    y = torch.randn(8, 16, 16, 16, device=DEV, generator=g)
+    bx = torch.randn(16, device=DEV, generator=g)
+    by = torch.randn(16, device=DEV, generator=g)
+    A = torch.randn(8, 16, 16, 16, device=DEV, generator=g)
+    B = torch.randn(8, 16, 8, 8, device=DEV, generator=g)
+
+    def ref(x, y, bx, by):
+        return _ref_general(x + bx.view(1, -1, 1, 1), y + by.view(1, -1, 1, 1), 1.0)
+
+    res = []
+    for fn in (lambda *a: convops.relu_pool(a[0], a[1], 1.0, a[2], a[3]), ref):
+        ins = [t.clone().requires_grad_(True) for t in (x, y, bx, by)]
+        r, p = fn(*ins)
+        grads = torch.autograd.grad((r * A).sum() + (p * B).sum(), ins)
+        res.append([r.detach(), p.detach()] + list(grads))
+    for a, b in zip(res[0][:4], res[1][:4]):
+        assert torch.equal(a, b)
+    for a, b in zip(res[0][4:], res[1][4:]):            # bias gradients: channel sums
+        tol = 1e-5 * float(b.abs().max()) + 1e-6
+        assert float((a - b).abs().max()) <= tol
 
 
 def test_relu_pool_lrelu_double_backward_matches_torch():
