@@ -403,6 +403,15 @@ smmd_status smmd_mask_pool2_adj(const float *a, const float *b, const float *m, 
                                 float slope_p, int64_t planes, int H, int W, float *out,
                                 smmd_stream_t stream);
 
+/* A generator up block's output (block.py:50; its UpsampleConv shortcut,
+ * block.py:53-60, runs the 1x1 conv before the nearest upsample):
+ *   out[n][c][i][j] = (s[n][c][i/2][j/2] + bs[c]) + (h[n][c][i][j] + bh[c])
+ * s [planes, H/2, W/2] (8-byte aligned), h and out [planes, H, W] (16-byte
+ * aligned), planes = N * C, bs / bh NULL: no bias; H even, W % 4 == 0.  The
+ * order of the unfused bias adds, upsample and add, so bit-identical to them. */
+smmd_status smmd_up_add(const float *s, const float *bs, const float *h, const float *bh, int C,
+                        int64_t planes, int H, int W, float *out, smmd_stream_t stream);
+
 /* ---------------------------------------------------------------------------
  * Thin 3x3 convolutions: stride 1, zero padding 1 (TF SAME at stride 1), NCHW
  * fp32, one side with <= 4 channels.  They serve the critics' first layer

@@ -138,6 +138,44 @@ __global__ __launch_bounds__(RP_T) void mask_pool_adj_kernel(const float *__rest
     *reinterpret_cast<float4 *>(out + o0 + W) = s1;
 }
 
+// a generator up block's output (block.py:50 with the UpsampleConv shortcut,
+// block.py:53-60, whose 1x1 conv runs before the nearest upsample):
+// out = up(s + bs) + (h + bh), s at half resolution.  The unfused ops' order:
+// bias adds, the upsample copy, then the one add.
+__global__ __launch_bounds__(RP_T) void up_add_kernel(const float *__restrict__ s,
+                                                      const float *__restrict__ bs,
+                                                      const float *__restrict__ h,
+                                                      const float *__restrict__ bh, int C,
+                                                      int64_t patches, int H, int W,
+                                                      float *__restrict__ out) {
+    const int64_t t = (int64_t)blockIdx.x * RP_T + threadIdx.x;
+    if (t >= patches) return;
+    const int wq = W >> 2, hh = H >> 1;
+    const int j = (int)(t % wq);
+    const int64_t r = t / wq;
+    const int i = (int)(r % hh);
+    const int64_t plane = r / hh;
+    const int c = (int)(plane % C);
+    const size_t o0 = ((size_t)plane * H + 2 * i) * W + 4 * j;
+    const size_t op = ((size_t)plane * hh + i) * (W >> 1) + 2 * j;
+    float2 ss = *reinterpret_cast<const float2 *>(s + op);
+    if (bs) {
+        const float b = bs[c];
+        ss.x += b;
+        ss.y += b;
+    }
+    float4 h0 = *reinterpret_cast<const float4 *>(h + o0);
+    float4 h1 = *reinterpret_cast<const float4 *>(h + o0 + W);
+    if (bh) {
+        const float b = bh[c];
+        h0 = addb(h0, b);
+        h1 = addb(h1, b);
+    }
+    const float4 u = make_float4(ss.x, ss.x, ss.y, ss.y);
+    *reinterpret_cast<float4 *>(out + o0) = add4(u, h0);
+    *reinterpret_cast<float4 *>(out + o0 + W) = add4(u, h1);
+}
+
 static bool rp_shape_ok(int64_t planes, int H, int W) {
     return planes >= 0 && H > 0 && W > 0 && (H % 2) == 0 && (W % 4) == 0;
 }
@@ -178,5 +216,20 @@ extern "C" smmd_status smmd_mask_pool2_adj(const float *a, const float *b, const
     if (blocks > 0x7fffffff) return SMMD_EINVAL;
     hipLaunchKernelGGL(mask_pool_adj_kernel, dim3((unsigned)blocks), dim3(RP_T), 0,
                        (hipStream_t)stream, a, b, m, slope_m, slope_p, patches, H, W, out);
+    return last_launch_status();
+}
+
+extern "C" smmd_status smmd_up_add(const float *s, const float *bs, const float *h,
+                                   const float *bh, int C, int64_t planes, int H, int W,
+                                   float *out, smmd_stream_t stream) {
+    if (!rp_shape_ok(planes, H, W) || !s || !h || !out || C < 1 || planes % C != 0)
+        return SMMD_EINVAL;
+    if (!al8(s) || !al16(h) || !al16(out)) return SMMD_EINVAL;
+    const int64_t patches = planes * (H / 2) * (W / 4);
+    if (patches == 0) return SMMD_OK;
+    const int64_t blocks = (patches + RP_T - 1) / RP_T;
+    if (blocks > 0x7fffffff) return SMMD_EINVAL;
+    hipLaunchKernelGGL(up_add_kernel, dim3((unsigned)blocks), dim3(RP_T), 0, (hipStream_t)stream,
+                       s, bs, h, bh, C, patches, H, W, out);
     return last_launch_status();
 }

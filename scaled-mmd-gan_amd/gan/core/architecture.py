@@ -222,6 +222,9 @@ class ResidualBlock(nn.Module):
         # a critic down block: relu(x) (main path) and the shortcut's mean pool
         # of x read the input in one pass (convops.relu_pool)
         self._relu_pool = resample == 'down' and not use_bn
+        # an up block: the shortcut's upsample, both conv biases and the sum
+        # in one pass (convops.up_add)
+        self._up_add = resample == 'up' and isinstance(self.shortcut, _Up)
 
     def down_parts(self, x, y=None, slope_p=1.0, bx=None, by=None, defer_bias=False):
         """(shortcut, main path, their biases) of a critic down block, not yet
@@ -244,6 +247,13 @@ class ResidualBlock(nn.Module):
         if self._relu_pool and convops.relu_pool_applicable(x):
             s, h, _, _ = self.down_parts(x)
             return s + h
+        if self._up_add and convops.UP_ADD and FOLD_UP and x.is_cuda and \
+                self.shortcut.conv.k == 1 and self.shortcut.conv.stride == 1:
+            sc = self.shortcut.conv
+            s = sc(x, with_bias=False)                   # 1x1 conv before the upsample
+            h = self.conv_1(F.relu(self.bn1(x)))
+            h = self.conv_2(F.relu(self.bn2(h)), with_bias=False)
+            return convops.up_add(s, sc.bias, h, self.conv_2.bias)
         s = x if self.shortcut is None else self.shortcut(x)
         h = self.conv_1(F.relu(self.bn1(x)))
         h = self.conv_2(F.relu(self.bn2(h)))

@@ -536,3 +536,59 @@ def relu_pool(x, y=None, slope_p=1.0, bx=None, by=None):
     if slope_p != 1.0:
         u = F.leaky_relu(u, slope_p)
     return F.relu(u), mean_pool2(u)
+
+
+# ---------------------------------------------------------------------------
+# a generator up block's output: up(s + bs) + (h + bh) in one pass
+# (csrc/smmd_relupool.hip smmd_up_add; SMMD_UP_ADD=0: the torch ops)
+# ---------------------------------------------------------------------------
+UP_ADD = os.environ.get('SMMD_UP_ADD', '1') != '0'
+
+
+def up_add_applicable(s, h):
+    """s [N, C, H/2, W/2] and h [N, C, H, W]: NCHW fp32 device tensors, H even,
+    W % 4 == 0."""
+    return (UP_ADD and h.is_cuda and s.is_cuda and h.dtype == torch.float32
+            and s.dtype == torch.float32 and h.dim() == 4 and h.is_contiguous()
+            and s.is_contiguous() and h.shape[2] % 2 == 0 and h.shape[3] % 4 == 0
+            and tuple(s.shape) == (h.shape[0], h.shape[1], h.shape[2] // 2, h.shape[3] // 2))
+
+
+class _UpAdd(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, s, bs, h, bh):
+        from . import _lib
+        _lib.require_cuda(s, h)
+        N, C, H, W = h.shape
+        out = torch.empty_like(h)
+        _lib.add_bytes('smmd_up_add', (2 * h.numel() + s.numel()) * 4)
+        with _lib.timed('smmd_up_add'):
+            st = _lib.lib().smmd_up_add(_lib.ptr(s), _lib.ptr(bs), _lib.ptr(h), _lib.ptr(bh), C,
+                                        N * C, H, W, _lib.ptr(out),
+                                        _lib.stream_handle(h.device))
+        _lib.check(st, 'smmd_up_add')
+        ctx.has = (bs is not None, bh is not None)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        # the nearest upsample's adjoint is the 2x2 window sum: avg_pool2d's
+        # ((g00 + g01) + g10) + g11, then / 4 * 4 (exact), the order of
+        # upsample_nearest2d's backward
+        g = g.contiguous()
+        gs = F.avg_pool2d(g, 2) * 4.0 if ctx.needs_input_grad[0] or ctx.has[0] else None
+        gbs = bias_grad(gs) if ctx.has[0] and ctx.needs_input_grad[1] else None
+        gbh = bias_grad(g) if ctx.has[1] and ctx.needs_input_grad[3] else None
+        return gs, gbs, g, gbh
+
+
+def up_add(s, bs, h, bh):
+    """up(s + bs) + (h + bh) (block.py:50 of an up block, biases per channel,
+    either may be None): one HIP pass on device tensors, torch ops otherwise."""
+    if up_add_applicable(s, h):
+        return _UpAdd.apply(s, bs, h, bh)
+    if bs is not None:
+        s = s + bs.view(1, -1, 1, 1)
+    if bh is not None:
+        h = h + bh.view(1, -1, 1, 1)
+    return F.interpolate(s, scale_factor=2, mode='nearest') + h

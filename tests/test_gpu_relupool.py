@@ -255,3 +255,60 @@ def test_snresnet_critic_chained_equals_layerwise(relu_pool_off):
     for a, b in zip(*out):
         tol = 1e-5 * float(b.abs().max()) + 1e-7
         assert float((a - b).abs().max()) <= tol
+
+
+def test_up_add_equals_torch():
+    """A generator up block's output up(s + bs) + (h + bh) (block.py:50,
+    :53-60): value and the gradients of s, bs, h, bh against the unfused
+    bias adds, nearest upsample and add."""
+    from gan.core import convops
+    g = torch.Generator(device=DEV).manual_seed(41)
+    s = torch.randn(8, 32, 8, 8, device=DEV, generator=g)
+    h = torch.randn(8, 32, 16, 16, device=DEV, generator=g)
+    bs = torch.randn(32, device=DEV, generator=g)
+    bh = torch.randn(32, device=DEV, generator=g)
+    A = torch.randn(8, 32, 16, 16, device=DEV, generator=g)
+
+    def ref(s, bs, h, bh):
+        return (F.interpolate(s + bs.view(1, -1, 1, 1), scale_factor=2, mode='nearest')
+                + (h + bh.view(1, -1, 1, 1)))
+
+    res = []
+    for fn in (convops.up_add, ref):
+        ins = [t.clone().requires_grad_(True) for t in (s, bs, h, bh)]
+        out = fn(*ins)
+        grads = torch.autograd.grad((out * A).sum(), ins)
+        res.append([out.detach()] + list(grads))
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][3], res[1][3])
+    for a, b in ((res[0][2], res[1][2]), (res[0][4], res[1][4])):   # bias grads
+        tol = 1e-5 * float(b.abs().max()) + 1e-6
+        assert float((a - b).abs().max()) <= tol
+
+
+def test_snresnet_generator_up_add_equals_unfused():
+    """The SNResNet-64 generator (architecture.py:178-208) with its up blocks'
+    outputs on smmd_up_add against SMMD_UP_ADD off: images and the parameter
+    gradients."""
+    from gan.core import convops
+    from gan.core.architecture import SNResNetGenerator
+    saved = convops.UP_ADD
+    torch.manual_seed(6)
+    G = SNResNetGenerator(16, 3, 64, True).to(DEV)
+    z = torch.rand(8, 128, device=DEV) * 2 - 1
+    out = []
+    try:
+        for on in (True, False):
+            convops.UP_ADD = on
+            img = G(z)
+            gp = torch.autograd.grad((img * img).sum(), list(G.parameters()))
+            out.append([img.detach()] + [t.detach() for t in gp])
+    finally:
+        convops.UP_ADD = saved
+    # conv biases in front of a batch norm have a zero gradient in exact
+    # arithmetic (rounding noise in both runs), so the bound is relative to
+    # the largest gradient of the network, not to each tensor's own
+    assert float((out[0][0] - out[1][0]).abs().max()) <= 1e-5 * float(out[1][0].abs().max())
+    scale = max(float(t.abs().max()) for t in out[1][1:])
+    for a, b in zip(out[0][1:], out[1][1:]):
+        assert float((a - b).abs().max()) <= 1e-5 * scale
