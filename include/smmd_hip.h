@@ -413,6 +413,25 @@ smmd_status smmd_up_add(const float *s, const float *bs, const float *h, const f
                         int64_t planes, int H, int W, float *out, smmd_stream_t stream);
 
 /* ---------------------------------------------------------------------------
+ * Training-mode batch norm + ReLU when no gradient is taken (the generator's
+ * forward in a critic step): tf.layers.batch_normalization(training=True,
+ * momentum 0.9, eps) + tf.nn.relu (gan/core/snops.py:31-40,
+ * resnet/ops/batchnorm.py:10-18, resnet/block.py:42-47, architecture.py:178-208).
+ *   y = relu(x * scale + shift), scale = gamma / sqrt(var + eps),
+ *   shift = beta - mean * scale, mean / biased var of x[:, c] over (N, HW),
+ *   running_mean / running_var (NULL: not kept) <- (1 - momentum) * old +
+ *   momentum * (mean / unbiased var).  x, y [N, C, HW] NCHW fp32, 16-byte
+ *   aligned, HW % 4 == 0; gamma / beta NULL: 1 / 0.  Statistics in double in
+ *   a fixed order; workspace from smmd_bn_relu_workspace_bytes.
+ * ------------------------------------------------------------------------- */
+size_t smmd_bn_relu_workspace_bytes(int N, int C);
+
+smmd_status smmd_bn_relu_fwd(const float *x, int N, int C, int HW, const float *gamma,
+                             const float *beta, float *running_mean, float *running_var,
+                             float momentum, float eps, float *y, void *ws, size_t ws_bytes,
+                             smmd_stream_t stream);
+
+/* ---------------------------------------------------------------------------
  * Thin 3x3 convolutions: stride 1, zero padding 1 (TF SAME at stride 1), NCHW
  * fp32, one side with <= 4 channels.  They serve the critics' first layer
  * (3 -> dim: snops.conv2d / resnet Conv2D, gan/core/snops.py:69-90,

@@ -1,0 +1,149 @@
+// smmd_bnrelu.hip -- training-mode batch norm + ReLU of the generator's
+// forward when no gradient is taken (every critic step runs G(z) that way),
+// gfx950 / MI355X.
+//
+// Reference: tf.layers.batch_normalization(training=True, momentum=0.9,
+// epsilon=1e-5) then tf.nn.relu (gan/core/snops.py:31-40 batch_norm,
+// resnet/ops/batchnorm.py:10-18, resnet/block.py:42-47 Normalize + relu,
+// architecture.py:178-208 bn4 + relu): y = relu((x - mean) / sqrt(var + eps)
+// * gamma + beta) with the batch's per-channel mean and biased variance over
+// (N, H, W), the moving averages updated with the unbiased variance (torch's
+// BatchNorm2d convention, momentum 0.1 = TF's 0.9 decay).
+//
+// Two launches over [N, C, HW] NCHW fp32, the grid (C, S) of the channel sum
+// (smmd_bias.hip): (1) block (c, s) sums and sums the squares of its rows of
+// channel c (float4 loads, per-thread float, block tree in double) into a
+// [S][C] double slab; (2) block (c, s) reduces channel c's S partials in a
+// fixed order (every block of the channel the same way), forms
+// scale = gamma / sqrt(var + eps), shift = beta - mean * scale, applies
+// relu(x * scale + shift) to its rows, and block (c, 0) updates the moving
+// averages.  HBM: one read for the statistics, one read + one write to apply.
+#include "smmd_common.hpp"
+
+namespace smmd {
+
+constexpr int BN_T = 256;
+
+__device__ __forceinline__ void bn_rows(int N, int S, int s, int &n0, int &n1) {
+    const int R = (N + S - 1) / S;
+    n0 = s * R;
+    n1 = min(N, n0 + R);
+}
+
+__global__ __launch_bounds__(BN_T) void bn_stats_kernel(const float *__restrict__ x, int N, int C,
+                                                        int HW, int S,
+                                                        double *__restrict__ part) {
+    const int c = blockIdx.x, s = blockIdx.y;
+    int n0, n1;
+    bn_rows(N, S, s, n0, n1);
+    const int w4 = HW >> 2;
+    float a = 0.f, q = 0.f;
+    for (int n = n0; n < n1; ++n) {
+        const float4 *row = reinterpret_cast<const float4 *>(x + ((size_t)n * C + c) * HW);
+        for (int i = threadIdx.x; i < w4; i += BN_T) {
+            const float4 v = row[i];
+            a += (v.x + v.y) + (v.z + v.w);
+            q = fmaf(v.x, v.x, q);
+            q = fmaf(v.y, v.y, q);
+            q = fmaf(v.z, v.z, q);
+            q = fmaf(v.w, v.w, q);
+        }
+    }
+    __shared__ double red[BN_T / SMMD_WAVE];
+    const double sa = block_sum<BN_T / SMMD_WAVE>((double)a, red);
+    const double sq = block_sum<BN_T / SMMD_WAVE>((double)q, red);
+    if (threadIdx.x == 0) {
+        part[((size_t)s * C + c) * 2 + 0] = sa;
+        part[((size_t)s * C + c) * 2 + 1] = sq;
+    }
+}
+
+__global__ __launch_bounds__(BN_T) void bn_apply_kernel(const float *__restrict__ x, int N, int C,
+                                                        int HW, int S,
+                                                        const double *__restrict__ part,
+                                                        const float *__restrict__ gamma,
+                                                        const float *__restrict__ beta,
+                                                        float *__restrict__ run_mean,
+                                                        float *__restrict__ run_var,
+                                                        float momentum, float eps,
+                                                        float *__restrict__ y) {
+    const int c = blockIdx.x, s = blockIdx.y;
+    __shared__ float sh[2];
+    if (threadIdx.x < SMMD_WAVE) {
+        // fixed order: lane-strided over the S partials, then the wave tree
+        double a = 0.0, q = 0.0;
+        for (int k = threadIdx.x; k < S; k += SMMD_WAVE) {
+            a += part[((size_t)k * C + c) * 2 + 0];
+            q += part[((size_t)k * C + c) * 2 + 1];
+        }
+        a = wave_sum(a);
+        q = wave_sum(q);
+        if (threadIdx.x == 0) {
+            const double cnt = (double)N * (double)HW;
+            const double mean = a / cnt;
+            double var = q / cnt - mean * mean;
+            if (var < 0.0) var = 0.0;
+            const double inv = 1.0 / sqrt(var + (double)eps);
+            const double g = gamma ? (double)gamma[c] : 1.0;
+            const double b = beta ? (double)beta[c] : 0.0;
+            sh[0] = (float)(g * inv);
+            sh[1] = (float)(b - mean * g * inv);
+            if (s == 0 && run_mean && run_var) {
+                const double unb = cnt > 1.0 ? var * cnt / (cnt - 1.0) : var;
+                run_mean[c] = (float)((1.0 - momentum) * (double)run_mean[c] + momentum * mean);
+                run_var[c] = (float)((1.0 - momentum) * (double)run_var[c] + momentum * unb);
+            }
+        }
+    }
+    __syncthreads();
+    const float sc = sh[0], sf = sh[1];
+    int n0, n1;
+    bn_rows(N, S, s, n0, n1);
+    const int w4 = HW >> 2;
+    for (int n = n0; n < n1; ++n) {
+        const size_t off = ((size_t)n * C + c) * HW;
+        const float4 *row = reinterpret_cast<const float4 *>(x + off);
+        float4 *out = reinterpret_cast<float4 *>(y + off);
+        for (int i = threadIdx.x; i < w4; i += BN_T) {
+            const float4 v = row[i];
+            out[i] = make_float4(fmaxf(fmaf(v.x, sc, sf), 0.f), fmaxf(fmaf(v.y, sc, sf), 0.f),
+                                 fmaxf(fmaf(v.z, sc, sf), 0.f), fmaxf(fmaf(v.w, sc, sf), 0.f));
+        }
+    }
+}
+
+inline int bn_split(int N, int C) {
+    if (C >= 512) return 1;
+    int S = (2048 + C - 1) / C;
+    if (S > N) S = N;
+    return S < 1 ? 1 : S;
+}
+
+}  // namespace smmd
+
+using namespace smmd;
+
+extern "C" size_t smmd_bn_relu_workspace_bytes(int N, int C) {
+    if (N <= 0 || C <= 0) return 0;
+    return (size_t)bn_split(N, C) * C * 2 * sizeof(double);
+}
+
+extern "C" smmd_status smmd_bn_relu_fwd(const float *x, int N, int C, int HW, const float *gamma,
+                                        const float *beta, float *running_mean,
+                                        float *running_var, float momentum, float eps, float *y,
+                                        void *ws, size_t ws_bytes, smmd_stream_t stream) {
+    if (!x || !y || N < 1 || C < 1 || HW < 4 || (HW & 3)) return SMMD_EINVAL;
+    if (((uintptr_t)x & 15) || ((uintptr_t)y & 15)) return SMMD_EINVAL;
+    const int S = bn_split(N, C);
+    if (S > 65535) return SMMD_EINVAL;
+    if (!ws || ws_bytes < smmd_bn_relu_workspace_bytes(N, C)) return SMMD_EWORKSPACE;
+    hipStream_t st = (hipStream_t)stream;
+    double *part = static_cast<double *>(ws);
+    hipLaunchKernelGGL(bn_stats_kernel, dim3(C, S), dim3(BN_T), 0, st, x, N, C, HW, S, part);
+    smmd_status e = last_launch_status();
+    if (e != SMMD_OK) return e;
+    hipLaunchKernelGGL(bn_apply_kernel, dim3(C, S), dim3(BN_T), 0, st, x, N, C, HW, S,
+                       (const double *)part, gamma, beta, running_mean, running_var, momentum,
+                       eps, y);
+    return last_launch_status();
+}

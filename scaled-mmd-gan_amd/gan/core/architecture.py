@@ -18,7 +18,7 @@ import torch.nn.functional as F
 from . import convops
 from . import optim as _optim
 from .convops import conv2d, fold_pool_weight, fold_pool_weights, fold_up_weight, mean_pool2
-from .snops import Conv2d, Deconv2d, Linear, batch_norm, lrelu
+from .snops import Conv2d, Deconv2d, Linear, batch_norm, bn_relu, lrelu
 
 
 def conv_sizes(size, layers, stride=2):
@@ -251,12 +251,12 @@ class ResidualBlock(nn.Module):
                 self.shortcut.conv.k == 1 and self.shortcut.conv.stride == 1:
             sc = self.shortcut.conv
             s = sc(x, with_bias=False)                   # 1x1 conv before the upsample
-            h = self.conv_1(F.relu(self.bn1(x)))
-            h = self.conv_2(F.relu(self.bn2(h)), with_bias=False)
+            h = self.conv_1(bn_relu(self.bn1, x))
+            h = self.conv_2(bn_relu(self.bn2, h), with_bias=False)
             return convops.up_add(s, sc.bias, h, self.conv_2.bias)
         s = x if self.shortcut is None else self.shortcut(x)
-        h = self.conv_1(F.relu(self.bn1(x)))
-        h = self.conv_2(F.relu(self.bn2(h)))
+        h = self.conv_1(bn_relu(self.bn1, x))
+        h = self.conv_2(bn_relu(self.bn2, h))
         return s + h
 
 
@@ -282,10 +282,10 @@ class SNGANGenerator(nn.Module):
 
     def forward(self, z):
         h = self.h0_lin(z).view(-1, self.dim * 8, self.s8, self.s8)
-        h = F.relu(self.bn0(h))
-        h = F.relu(self.bn1(self.h1(h)))
-        h = F.relu(self.bn2(self.h2(h)))
-        h = F.relu(self.bn3(self.h3(h)))
+        h = bn_relu(self.bn0, h)
+        h = bn_relu(self.bn1, self.h1(h))
+        h = bn_relu(self.bn2, self.h2(h))
+        h = bn_relu(self.bn3, self.h3(h))
         return torch.sigmoid(self.h4(h))
 
 
@@ -305,11 +305,11 @@ class DCGANGenerator(nn.Module):
                                  for i in range(layers - 1))
 
     def forward(self, z):
-        h = F.relu(self.bn0(self.h0_lin(z).view(-1, self.top, self.s0, self.s0)))
+        h = bn_relu(self.bn0, self.h0_lin(z).view(-1, self.top, self.s0, self.s0))
         for i, dc in enumerate(self.deconvs):
             h = dc(h)
             if i < len(self.bns):
-                h = F.relu(self.bns[i](h))
+                h = bn_relu(self.bns[i], h)
         return torch.sigmoid(h)
 
 
@@ -331,7 +331,7 @@ class ResNetGenerator(nn.Module):
 
     def forward(self, z):
         h = self.h0_lin(z).view(-1, self.dim * 16, self.s32, self.s32)
-        h = F.relu(self.bn4(self.res(h)))
+        h = bn_relu(self.bn4, self.res(h))
         return torch.sigmoid(self.h5(h))
 
 
@@ -357,7 +357,7 @@ class SNResNetGenerator(nn.Module):
 
     def forward(self, z):
         h = self.h0_lin(z).view(-1, self.dim * 16, self.s32, self.s32)
-        h = F.relu(self.bn4(self.res(h)))
+        h = bn_relu(self.bn4, self.res(h))
         return torch.sigmoid(self.h5(h))
 
 

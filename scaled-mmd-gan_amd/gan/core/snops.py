@@ -11,6 +11,7 @@ before the critic runs.  TF 'SAME' padding is reproduced exactly
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -144,6 +145,39 @@ def batch_norm(c):
     """tf.layers.batch_normalization(momentum=.9, eps=1e-5, training=True)
     (snops.py:31-40, resnet/ops/batchnorm.py:10-18)."""
     return nn.BatchNorm2d(c, eps=1e-5, momentum=0.1)
+
+
+# SMMD_BN_RELU=1: the library's batch norm + ReLU for the generator outside
+# autograd (default off until measured on MI355X)
+BN_RELU = os.environ.get('SMMD_BN_RELU', '0') != '0'
+
+
+def bn_relu(bn, x):
+    """relu(bn(x)) (resnet/block.py:42-47 Normalize then tf.nn.relu): when no
+    gradient is taken -- the generator's forward in every critic step -- a
+    training-mode nn.BatchNorm2d on an NCHW device tensor runs as the
+    library's two-pass smmd_bn_relu_fwd (batch statistics, moving averages,
+    normalise + ReLU in one write); otherwise the torch modules."""
+    if (BN_RELU and isinstance(bn, nn.BatchNorm2d) and bn.training and bn.track_running_stats
+            and bn.momentum is not None and not torch.is_grad_enabled() and x.is_cuda
+            and x.dtype == torch.float32 and x.dim() == 4 and x.is_contiguous()
+            and (x.shape[2] * x.shape[3]) % 4 == 0 and x.data_ptr() % 16 == 0):
+        from . import _lib
+        N, C, H, W = x.shape
+        L = _lib.lib()
+        ws = _lib.workspace('bn_relu', L.smmd_bn_relu_workspace_bytes(N, C), x.device)
+        y = torch.empty_like(x)
+        _lib.add_bytes('smmd_bn_relu_fwd', 3 * x.numel() * 4)
+        with _lib.timed('smmd_bn_relu_fwd'):
+            st = L.smmd_bn_relu_fwd(_lib.ptr(x), N, C, H * W, _lib.ptr(bn.weight),
+                                    _lib.ptr(bn.bias), _lib.ptr(bn.running_mean),
+                                    _lib.ptr(bn.running_var), float(bn.momentum), float(bn.eps),
+                                    _lib.ptr(y), _lib.ptr(ws), ws.numel(),
+                                    _lib.stream_handle(x.device))
+        _lib.check(st, 'smmd_bn_relu_fwd')
+        bn.num_batches_tracked.add_(1)
+        return y
+    return F.relu(bn(x))
 
 
 def lrelu(x, leak=0.2):

@@ -312,3 +312,30 @@ def test_snresnet_generator_up_add_equals_unfused():
     scale = max(float(t.abs().max()) for t in out[1][1:])
     for a, b in zip(out[0][1:], out[1][1:]):
         assert float((a - b).abs().max()) <= 1e-5 * scale
+
+
+@pytest.mark.parametrize('shape', [(64, 64, 64, 64), (64, 512, 8, 8), (8, 1024, 4, 4), (3, 7, 4, 4)])
+def test_bn_relu_no_grad_matches_torch(shape):
+    """smmd_bn_relu_fwd (the generator's batch norm + ReLU in a critic step,
+    resnet/block.py:42-47) against nn.BatchNorm2d in training mode + relu:
+    output and the updated moving averages, from the same module state."""
+    from gan.core import snops
+    from gan.core.snops import batch_norm, bn_relu
+    saved, snops.BN_RELU = snops.BN_RELU, True
+    g = torch.Generator(device=DEV).manual_seed(sum(shape))
+    x = torch.randn(shape, device=DEV, generator=g) * 3 + 1
+    bns = [batch_norm(shape[1]).to(DEV) for _ in range(2)]
+    with torch.no_grad():
+        for bn in bns:
+            bn.weight.copy_(torch.rand(shape[1], device=DEV, generator=g) + 0.5)
+            bn.bias.copy_(torch.randn(shape[1], device=DEV, generator=g))
+        bns[1].load_state_dict(bns[0].state_dict())
+        try:
+            y = bn_relu(bns[0], x)
+        finally:
+            snops.BN_RELU = saved
+        ref = torch.relu(bns[1](x))
+    assert float((y - ref).abs().max()) <= 2e-5 * float(ref.abs().max()) + 1e-6
+    for k in ('running_mean', 'running_var', 'num_batches_tracked'):
+        a, b = getattr(bns[0], k), getattr(bns[1], k)
+        assert float((a.double() - b.double()).abs().max()) <= 1e-5 * float(b.abs().max()) + 1e-7, k
