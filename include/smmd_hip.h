@@ -60,7 +60,8 @@ const char *smmd_status_string(smmd_status s);
 int smmd_abi_version(void);         /* bumped on any ABI change (2: Gram/poly,
                                        3: smmd_sn_layer.fold, 4: smmd_adam_flat_ex,
                                        5: smmd_conv3x3_thin*,
-                                       6: smmd_mask_pool2*) */
+                                       6: smmd_mask_pool2*, smmd_up_add,
+                                       smmd_bn_relu_fwd) */
 
 /* ---------------------------------------------------------------------------
  * Fused pairwise MMD^2 (forward + unit gradient).
