@@ -37,16 +37,24 @@ __global__ __launch_bounds__(BN_T) void bn_stats_kernel(const float *__restrict_
     int n0, n1;
     bn_rows(N, S, s, n0, n1);
     const int w4 = HW >> 2;
+    // rows shorter than the block are packed rpi per step (lane t: row t / w4,
+    // column t % w4), so every lane loads on the small maps too
+    const int rpi = w4 >= BN_T ? 1 : BN_T / w4;
+    const int r = w4 >= BN_T ? 0 : (int)threadIdx.x / w4;
+    const int col = w4 >= BN_T ? (int)threadIdx.x : (int)threadIdx.x - r * w4;
+    const int step = w4 >= BN_T ? BN_T : w4;     // column stride within a row
     float a = 0.f, q = 0.f;
-    for (int n = n0; n < n1; ++n) {
-        const float4 *row = reinterpret_cast<const float4 *>(x + ((size_t)n * C + c) * HW);
-        for (int i = threadIdx.x; i < w4; i += BN_T) {
-            const float4 v = row[i];
-            a += (v.x + v.y) + (v.z + v.w);
-            q = fmaf(v.x, v.x, q);
-            q = fmaf(v.y, v.y, q);
-            q = fmaf(v.z, v.z, q);
-            q = fmaf(v.w, v.w, q);
+    if (r < rpi) {
+        for (int n = n0 + r; n < n1; n += rpi) {
+            const float4 *row = reinterpret_cast<const float4 *>(x + ((size_t)n * C + c) * HW);
+            for (int i = col; i < w4; i += step) {
+                const float4 v = row[i];
+                a += (v.x + v.y) + (v.z + v.w);
+                q = fmaf(v.x, v.x, q);
+                q = fmaf(v.y, v.y, q);
+                q = fmaf(v.z, v.z, q);
+                q = fmaf(v.w, v.w, q);
+            }
         }
     }
     __shared__ double red[BN_T / SMMD_WAVE];
@@ -100,11 +108,16 @@ __global__ __launch_bounds__(BN_T) void bn_apply_kernel(const float *__restrict_
     int n0, n1;
     bn_rows(N, S, s, n0, n1);
     const int w4 = HW >> 2;
-    for (int n = n0; n < n1; ++n) {
+    const int rpi = w4 >= BN_T ? 1 : BN_T / w4;  // short rows packed, as in the statistics
+    const int r = w4 >= BN_T ? 0 : (int)threadIdx.x / w4;
+    const int col = w4 >= BN_T ? (int)threadIdx.x : (int)threadIdx.x - r * w4;
+    const int step = w4 >= BN_T ? BN_T : w4;
+    if (r >= rpi) return;
+    for (int n = n0 + r; n < n1; n += rpi) {
         const size_t off = ((size_t)n * C + c) * HW;
         const float4 *row = reinterpret_cast<const float4 *>(x + off);
         float4 *out = reinterpret_cast<float4 *>(y + off);
-        for (int i = threadIdx.x; i < w4; i += BN_T) {
+        for (int i = col; i < w4; i += step) {
             const float4 v = row[i];
             out[i] = make_float4(fmaxf(fmaf(v.x, sc, sf), 0.f), fmaxf(fmaf(v.y, sc, sf), 0.f),
                                  fmaxf(fmaf(v.z, sc, sf), 0.f), fmaxf(fmaf(v.w, sc, sf), 0.f));

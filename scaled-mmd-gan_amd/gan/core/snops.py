@@ -147,9 +147,8 @@ def batch_norm(c):
     return nn.BatchNorm2d(c, eps=1e-5, momentum=0.1)
 
 
-# SMMD_BN_RELU=1: the library's batch norm + ReLU for the generator outside
-# autograd (default off until measured on MI355X)
-BN_RELU = os.environ.get('SMMD_BN_RELU', '0') != '0'
+# SMMD_BN_RELU=0: torch's BatchNorm2d + relu for the generator outside autograd
+BN_RELU = os.environ.get('SMMD_BN_RELU', '1') != '0'
 
 
 def bn_relu(bn, x):
