@@ -1,7 +1,10 @@
 """Training-step benchmark: 64x64 ImageNet SMMD (SNResNet G/D), batch 64 per GPU.
 
     python bench.py --gpus N --steps K --warmup W
-    (N > 1 is launched by torch.distributed.run, one rank per GPU over RCCL)
+    (N > 1: one rank per GPU over RCCL.  Started without a launcher, the
+    process starts `torch.distributed.run --nproc-per-node N bench.py ...` as
+    a child before touching the GPU and exits with its code; started by a
+    launcher, --gpus must equal WORLD_SIZE)
 
 A step is one optimizer update of the reference schedule (5 critic updates,
 then 1 generator update; gan/core/model.py:470-478) on a synthetic batch of
@@ -137,51 +140,61 @@ def _mirror_trainer(cfg, batch, seed=2):
     return tr, imgs
 
 
-def _time_cycles(tr, imgs, cycles, budget_s):
-    """Per-step wall times over whole 5 D + 1 G cycles (at least one)."""
-    tr.train_step(imgs)                       # warm-up (allocator, threads)
+def _time_steps(tr, imgs, steps, warm=3):
+    """Per-step wall times of ``steps`` reference-loop steps (>= 20
+    after 3 warm-ups), started at a 5 D + 1 G cycle boundary."""
+    for _ in range(warm):
+        tr.train_step(imgs)                   # allocator, threads, first-touch
     tr.d_counter = tr.g_counter = 0           # cycle start
     times, kinds = [], []
-    t_start = time.perf_counter()
-    for c in range(cycles):
-        for _ in range(6):
-            t0 = time.perf_counter()
-            kinds.append(tr.train_step(imgs))
-            times.append(time.perf_counter() - t0)
-        if time.perf_counter() - t_start > budget_s:
-            break
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        kinds.append(tr.train_step(imgs))
+        times.append(time.perf_counter() - t0)
     return times, kinds
 
 
-def cpu_baseline(seconds_budget=20.0):
+def _stats(times):
+    return {'median': round(_pct(times, .5), 4), 'p10': round(_pct(times, .1), 4),
+            'p90': round(_pct(times, .9), 4), 'mean': round(sum(times) / len(times), 4)}
+
+
+def cpu_threads():
+    """Threads for the CPU baseline: the process's CPU affinity, capped at the
+    GPU box's CPU share for one GPU (the harness sets OMP_NUM_THREADS to that
+    share, 16, and asks worker pools to stay within it; the box's affinity
+    mask lists the whole host)."""
+    affinity = len(os.sched_getaffinity(0))
+    share = int(os.environ.get('OMP_NUM_THREADS', affinity) or affinity)
+    return affinity, max(1, min(affinity, share))
+
+
+def cpu_baseline(steps=24, cifar_steps=24):
     """The oracle's CPU mirror of the TF graph (oracle/tf_mirror.py), the
     reference's training loop: both gradient sets every step, 5 D + 1 G.
-    Headline: the bench's own workload (ImageNet SNResNet-64, batch 64) over
-    one full cycle; beside it BASELINE configs[0] (CIFAR-10 SNGAN 32x32,
-    batch 32, the reference's CPU case) over as many cycles as fit."""
-    affinity = len(os.sched_getaffinity(0))
-    threads = min(affinity, 16)     # the box's CPU share for one GPU (16)
+    Headline: the bench's own workload (ImageNet SNResNet-64, batch 64),
+    ``steps`` timed steps (4 whole cycles) after 3 warm-ups; beside it BASELINE
+    configs[0] (CIFAR-10 SNGAN 32x32, batch 32, the reference's CPU case)."""
+    affinity, threads = cpu_threads()
     torch.set_num_threads(threads)
-    out = {'unit': 'images/s', 'cores': threads, 'kind': 'port',
-           'host_cpus': os.cpu_count(), 'affinity_cpus': affinity, 'threads_used': threads}
+    out = {'unit': 'images/s', 'cores': threads, 'cores_meaning': 'host threads used',
+           'kind': 'port', 'host_cpus': os.cpu_count(), 'affinity_cpus': affinity,
+           'threads_used': threads, 'omp_num_threads_env': os.environ.get('OMP_NUM_THREADS')}
     tr, imgs = _mirror_trainer(imagenet_config(BATCH), BATCH)
-    times, kinds = _time_cycles(tr, imgs, 1, seconds_budget)
+    times, kinds = _time_steps(tr, imgs, steps)
     mean = sum(times) / len(times)
     out.update(value=round(BATCH / mean, 3),
-               sample='%d steps (%s) of the reference loop on the torch-CPU mirror of the TF '
-                      'graph (oracle/tf_mirror.py TFMirrorTrainer; both gradient sets per step '
-                      'as model.py:514), ImageNet SNResNet-64 SMMD, batch %d; value = batch / '
-                      'mean step time' % (len(times), ''.join(kinds), BATCH),
-               step_s={'median': round(_pct(times, .5), 4), 'p10': round(_pct(times, .1), 4),
-                       'p90': round(_pct(times, .9), 4), 'mean': round(mean, 4)})
+               sample='%d steps (%s) after 3 warm-ups of the reference loop on the torch-CPU '
+                      'mirror of the TF graph (oracle/tf_mirror.py TFMirrorTrainer; both gradient '
+                      'sets per step as model.py:514), ImageNet SNResNet-64 SMMD, batch %d; '
+                      'value = batch / mean step time' % (len(times), ''.join(kinds), BATCH),
+               steps=len(times), warmup=3, step_s=_stats(times))
     tr, imgs = _mirror_trainer(cifar_config(32), 32)
-    times, kinds = _time_cycles(tr, imgs, 4, seconds_budget / 2)
+    times, kinds = _time_steps(tr, imgs, cifar_steps)
     mean = sum(times) / len(times)
     out['configs0_cifar10_sngan_b32'] = {
-        'value': round(32 / mean, 3), 'unit': 'images/s', 'steps': len(times),
-        'schedule': ''.join(kinds),
-        'step_s': {'median': round(_pct(times, .5), 4), 'p10': round(_pct(times, .1), 4),
-                   'p90': round(_pct(times, .9), 4), 'mean': round(mean, 4)}}
+        'value': round(32 / mean, 3), 'unit': 'images/s', 'steps': len(times), 'warmup': 3,
+        'schedule': ''.join(kinds), 'step_s': _stats(times)}
     out['components'] = cpu_components()
     return out
 
@@ -461,6 +474,44 @@ def instrumented_pass(model, images, cycles, world, dev):
     return tm, tb, step_ms, 6 * cycles
 
 
+def launch_plan(gpus, env):
+    """How `bench.py --gpus N` runs (before anything touches the GPU):
+    ('run', world) when this process is a rank (WORLD_SIZE set and equal to
+    N) or N == 1; ('spawn', N) when N > 1 and no launcher started us -- the
+    parent then starts torch.distributed.run with N ranks as a child (the
+    reference's towers over num_gpus, /root/reference/gan/core/model.py:187-216,
+    num_gpus from the environment, gan/main.py:126).  A launcher that started
+    a different number of ranks than --gpus is an error."""
+    if gpus < 1:
+        raise SystemExit('bench.py: --gpus must be >= 1 (got %d)' % gpus)
+    ws = env.get('WORLD_SIZE')
+    if ws is None:
+        return ('spawn', gpus) if gpus > 1 else ('run', 1)
+    if int(ws) != gpus:
+        raise SystemExit('bench.py: --gpus %d but the launcher started WORLD_SIZE=%s ranks'
+                         % (gpus, ws))
+    return ('run', gpus)
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n, argv):
+    """Start N ranks of this script under torch.distributed.run as a child
+    process (this parent never initialises the GPU); rank 0's JSON line goes
+    to the inherited stdout.  Returns the launcher's exit code."""
+    import subprocess
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+           '--nproc-per-node', str(n), '--master-addr', '127.0.0.1',
+           '--master-port', str(_free_port()), os.path.abspath(__file__)] + list(argv)
+    print('[bench] launching %d ranks: %s' % (n, ' '.join(cmd)), file=sys.stderr, flush=True)
+    return subprocess.call(cmd)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -486,7 +537,9 @@ def main():
                     help='1: the timed steps replay HIP graphs of the captured step kinds '
                          '(model.enable_graphs; one GPU). Measured: no gain at batch 64 '
                          '(GPU-bound), 1.85x at batch 8 (host-bound)')
-    ap.add_argument('--cpu-seconds', type=float, default=20.0)
+    ap.add_argument('--cpu-steps', type=int, default=24,
+                    help='timed CPU-baseline steps of the ImageNet config (after 3 warm-ups; '
+                         'SURVEY 8d asks >= 20; 24 = 4 whole 5D+1G cycles)')
     ap.add_argument('--ref-schedule-steps', type=int, default=30,
                     help='steps timed with the reference schedule (both gradient sets '
                          'every step, model.py:514) after the main run; 0: skip')
@@ -498,6 +551,19 @@ def main():
     args = ap.parse_args()
     global BATCH
     BATCH = args.batch
+
+    mode, n = launch_plan(args.gpus, os.environ)
+    if mode == 'spawn':
+        sys.exit(spawn_ranks(n, sys.argv[1:]))
+    probe = os.environ.get('SMMD_BENCH_PROBE')
+    if probe == 'fail':        # launch check: a rank failing must fail the job
+        sys.exit(3)
+    if probe == '1':
+        # launch check without a GPU (tests/test_bench_launch.py): the rank layout
+        print(json.dumps({'probe': True, 'world': int(os.environ.get('WORLD_SIZE', '1')),
+                          'rank': int(os.environ.get('RANK', '0')), 'gpus': args.gpus}),
+              flush=True)
+        return
 
     if not args.miopen_winograd:      # read by MIOpen at its first solver query
         for k in ('MIOPEN_DEBUG_AMD_WINOGRAD_RXS_F2X3', 'MIOPEN_DEBUG_AMD_WINOGRAD_RXS_F3X2',
@@ -734,7 +800,7 @@ def main():
                                                            * 1e-3), 2)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            result['cpu_baseline'] = cpu_baseline(args.cpu_seconds)
+            result['cpu_baseline'] = cpu_baseline(args.cpu_steps)
         except Exception as e:   # report, never hide the GPU number
             result['cpu_baseline'] = {'error': repr(e)}
     if rank == 0:

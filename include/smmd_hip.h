@@ -62,6 +62,11 @@ int smmd_abi_version(void);         /* bumped on any ABI change (2: Gram/poly,
                                        5: smmd_conv3x3_thin*,
                                        6: smmd_mask_pool2*, smmd_up_add,
                                        smmd_bn_relu_fwd) */
+const char *smmd_source_hash(void); /* first 16 hex digits of the SHA-256 of the
+                                       sources this binary was built from
+                                       (csrc/*.hip, csrc/*.hpp in byte order,
+                                       then this header): gan.core._lib refuses
+                                       a binary older than its sources */
 
 /* ---------------------------------------------------------------------------
  * Fused pairwise MMD^2 (forward + unit gradient).

@@ -12,7 +12,8 @@
 //
 // Two launches over [N, C, HW] NCHW fp32, the grid (C, S) of the channel sum
 // (smmd_bias.hip): (1) block (c, s) sums and sums the squares of its rows of
-// channel c (float4 loads, per-thread float, block tree in double) into a
+// channel c, shifted by its first element (float4 loads, per-thread float,
+// block tree in double) into a
 // [S][C] double slab; (2) block (c, s) reduces channel c's S partials in a
 // fixed order (every block of the channel the same way), forms
 // scale = gamma / sqrt(var + eps), shift = beta - mean * scale, applies
@@ -43,17 +44,23 @@ __global__ __launch_bounds__(BN_T) void bn_stats_kernel(const float *__restrict_
     const int r = w4 >= BN_T ? 0 : (int)threadIdx.x / w4;
     const int col = w4 >= BN_T ? (int)threadIdx.x : (int)threadIdx.x - r * w4;
     const int step = w4 >= BN_T ? BN_T : w4;     // column stride within a row
+    // shifted sums: every thread subtracts the channel's first element k
+    // (x[0, c, 0], one cached load), so sum (x - k)^2 does not cancel
+    // against the mean when |mean| >> std (a sample lies within a few std
+    // of the mean); apply adds k back
+    const float k = x[(size_t)c * HW];
     float a = 0.f, q = 0.f;
     if (r < rpi) {
         for (int n = n0 + r; n < n1; n += rpi) {
             const float4 *row = reinterpret_cast<const float4 *>(x + ((size_t)n * C + c) * HW);
             for (int i = col; i < w4; i += step) {
                 const float4 v = row[i];
-                a += (v.x + v.y) + (v.z + v.w);
-                q = fmaf(v.x, v.x, q);
-                q = fmaf(v.y, v.y, q);
-                q = fmaf(v.z, v.z, q);
-                q = fmaf(v.w, v.w, q);
+                const float dx = v.x - k, dy = v.y - k, dz = v.z - k, dw = v.w - k;
+                a += (dx + dy) + (dz + dw);
+                q = fmaf(dx, dx, q);
+                q = fmaf(dy, dy, q);
+                q = fmaf(dz, dz, q);
+                q = fmaf(dw, dw, q);
             }
         }
     }
@@ -88,8 +95,9 @@ __global__ __launch_bounds__(BN_T) void bn_apply_kernel(const float *__restrict_
         q = wave_sum(q);
         if (threadIdx.x == 0) {
             const double cnt = (double)N * (double)HW;
-            const double mean = a / cnt;
-            double var = q / cnt - mean * mean;
+            const double ms = a / cnt;                   // mean of x - k
+            const double mean = (double)x[(size_t)c * HW] + ms;
+            double var = q / cnt - ms * ms;
             if (var < 0.0) var = 0.0;
             const double inv = 1.0 / sqrt(var + (double)eps);
             const double g = gamma ? (double)gamma[c] : 1.0;

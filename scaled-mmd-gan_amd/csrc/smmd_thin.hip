@@ -597,7 +597,9 @@ extern "C" smmd_status smmd_conv3x3_thin_wgrad(const float *gy, const float *x, 
     const float *wd = thin_in ? gy : x;       // the wide tensor, streamed once
     const float *tt = thin_in ? x : gy;       // the thin tensor, shifted
     const int E = cw * ct * 9;
-    const bool mfma = (w_img % 4) == 0 && cw <= 128 &&
+    // the MFMA kernel's B tile is one 32-column N tile: J = 9 ct taps must fit
+    // (ct <= 3); a 4-channel thin side takes the VALU kernel
+    const bool mfma = ct * 9 <= 32 && (w_img % 4) == 0 && cw <= 128 &&
                       (reinterpret_cast<uintptr_t>(wd) & 15) == 0;
     int S;
     if (mfma) {
@@ -618,8 +620,7 @@ extern "C" smmd_status smmd_conv3x3_thin_wgrad(const float *gy, const float *x, 
         switch (ct) {
             case 1: SMMD_WG_MT(1); break;
             case 2: SMMD_WG_MT(2); break;
-            case 3: SMMD_WG_MT(3); break;
-            default: SMMD_WG_MT(4); break;
+            default: SMMD_WG_MT(3); break;
         }
 #undef SMMD_WG_MT
 #undef SMMD_WG_MFMA

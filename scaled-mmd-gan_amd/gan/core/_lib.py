@@ -18,6 +18,10 @@ import torch  # noqa: F401  (must be imported before the .so: shares HIP runtime
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 LIB_PATH = os.environ.get('SMMD_HIP_LIB', os.path.join(_PKG_ROOT, 'lib', 'libsmmd_hip.so'))
+# an explicitly named library (A/B runs of another build) skips the stamp check
+_CHECK_STAMP = 'SMMD_HIP_LIB' not in os.environ
+CSRC = os.path.join(_PKG_ROOT, 'csrc')
+HEADER = os.path.join(os.path.dirname(_PKG_ROOT), 'include', 'smmd_hip.h')
 
 SMMD_MAX_TERMS = 8
 SMMD_SN_MAX_LAYERS = 32
@@ -81,6 +85,7 @@ _SZ = ctypes.c_size_t
 _SIGS = {
     'smmd_status_string': (ctypes.c_char_p, [_I]),
     'smmd_abi_version': (_I, []),
+    'smmd_source_hash': (ctypes.c_char_p, []),
     'smmd_mmd2_workspace_bytes': (_SZ, [_I, _I, _I]),
     'smmd_mmd2_fwd': (_I, [ctypes.POINTER(KernelDesc), _P, _I, _P, _I, _I, _I, _I, _I, _I, _I,
                            _P, _P, _P, _P, _P, _SZ, _P]),
@@ -139,6 +144,19 @@ _lock = threading.Lock()
 _lib = None
 
 
+def source_hash():
+    """The stamp csrc/Makefile compiles into the library: the first 16 hex
+    digits of SHA-256 over csrc/*.hip and csrc/*.hpp (names in byte order),
+    then include/smmd_hip.h."""
+    import hashlib
+    names = sorted(f for f in os.listdir(CSRC) if f.endswith(('.hip', '.hpp')))
+    h = hashlib.sha256()
+    for path in [os.path.join(CSRC, f) for f in names] + [HEADER]:
+        with open(path, 'rb') as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
 def lib():
     """Load libsmmd_hip.so once (raises SmmdLibraryError if absent)."""
     global _lib
@@ -161,6 +179,12 @@ def lib():
                 fn.argtypes = args
             if handle.smmd_abi_version() != ABI_VERSION:
                 raise SmmdLibraryError('ABI version mismatch')
+            if _CHECK_STAMP and os.path.isdir(CSRC):
+                built, now = handle.smmd_source_hash().decode(), source_hash()
+                if built != now:
+                    raise SmmdLibraryError(
+                        '%s was built from other sources (stamp %s, sources %s): rebuild '
+                        'with `make -C scaled-mmd-gan_amd/csrc`' % (LIB_PATH, built, now))
             _lib = handle
     return _lib
 

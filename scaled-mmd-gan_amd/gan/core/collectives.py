@@ -41,6 +41,18 @@ def all_reduce_(t, group):
     return t
 
 
+def broadcast_(t, src, group):
+    """In-place broadcast of ``t`` from global rank ``src``."""
+    if _host_staged(t, group):
+        h = t.detach().cpu()
+        dist.broadcast(h, src, group=group)
+        with torch.no_grad():
+            t.copy_(h)
+        return t
+    dist.broadcast(t, src, group=group)
+    return t
+
+
 def all_reduce_async(t, group):
     """SUM in place, returning the pending work (None when it completed
     synchronously: the host-staged gloo path)."""
@@ -121,6 +133,13 @@ class GradBuckets:
         self.opt, self.group = opt, group
         self.clip_norm = float(clip_norm)
         cap = _bucket_bytes() if bucket_bytes is None else int(bucket_bytes)
+        # every rank must issue the same all-reduces: rank 0's bucket size wins
+        # (an SMMD_BUCKET_MB that differs between ranks would otherwise hang)
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+            c = torch.tensor([cap], dtype=torch.int64, device=opt.flat_grad.device)
+            src = dist.get_global_rank(group, 0) if group is not None else 0
+            cap = int(broadcast_(c, src, group).item())
+        self.bucket_bytes = cap
         offs = [int(o) for o in opt.offsets]
         n = len(opt.params)
         self.buckets = []

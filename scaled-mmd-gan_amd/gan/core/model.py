@@ -651,4 +651,6 @@ class StepGraphs:
         opt.lr_t_dev.fill_(opt.lr_t(opt.step_count + 1))
         self.graphs[kind].replay()
         self._bookkeeping(critic)
-        return self.outs[kind]
+        # the capture's static outputs are overwritten by the next replay of
+        # this kind: hand out copies (train_step's values, model.last)
+        return tuple(t.clone() if torch.is_tensor(t) else t for t in self.outs[kind])

@@ -7,9 +7,10 @@ trainer.
 
 Data (gan/core/pipeline.py): cifar10 (python or binary batches under
 -data_dir), imagenet / celebA (TFRecord shards tf_records_train/train-*).
-Datasets are not shipped (no network); ``-dataset synthetic`` (or any dataset
-whose files are absent, with a warning) feeds U[0,1] images of the configured
-size, matching the reference pipeline's value range (pipeline.py:201, :403).
+Datasets are not shipped (no network); ``-dataset synthetic`` feeds U[0,1]
+images of the configured size, matching the reference pipeline's value range
+(pipeline.py:201, :403).  Any other dataset whose files are absent or
+malformed is an error, as in the reference.
 
 Checkpoints (model.py:559-566, :585-617): resumed from -checkpoint_dir/-name
 (-ckpt_name or the latest save) at start; saved every 2000 steps after a
@@ -125,6 +126,65 @@ def output_size_for(flags):
 
 
 CHECKPOINT_FREQ = 2000                   # model.py:609
+
+
+def description(flags, size):
+    """The run's directory name (model.py:62-77)."""
+    c = flags
+    lr_d = c.learning_rate_D if c.learning_rate_D >= 0 else c.learning_rate
+    lr = ('lr%.8f' % c.learning_rate if lr_d == c.learning_rate
+          else 'lr%.8fG%fD' % (c.learning_rate, lr_d))
+    d = '%s%s_%s%s_%sd%d-%d-%d_%s_%s_%s' % (
+        c.dataset, '%dx%d' % (c.gf_dim, c.df_dim), c.architecture, '_dc', c.kernel, c.dsteps,
+        c.start_dsteps, c.gsteps, c.batch_size, size, lr)
+    return d + ('_bn' if c.batch_norm else '')
+
+
+def run_dirs(flags, size, create=True):
+    """{'sample', 'log', 'checkpoint'} -> out_dir/<x>_dir/name/suffix+description
+    (model.py:105-120, _ensure_dirs).  The checkpoints themselves stay under
+    -checkpoint_dir/-name (this build's layout, see main())."""
+    desc = flags.suffix + description(flags, size)
+    out = {}
+    for folder in ('sample', 'log', 'checkpoint'):
+        sub = getattr(flags, folder + '_dir')
+        path = os.path.join(flags.out_dir, sub, flags.name, desc)
+        if sub and create:
+            os.makedirs(path, exist_ok=True)
+        out[folder] = path
+    return out
+
+
+class LogRedirect:
+    """-log (default True): stdout and stderr of the run go to
+    <sample_dir>/log.txt, line-buffered (model.py:85-94).  Restored on exit
+    (the reference never restores; a library caller keeps its streams)."""
+
+    def __init__(self, sample_dir, on=True):
+        self.path = os.path.join(sample_dir, 'log.txt')
+        self.on = on
+        self.f = None
+
+    def __enter__(self):
+        if self.on:
+            import time
+            self.old = sys.stdout, sys.stderr
+            self.f = open(self.path, 'w', buffering=1)
+            print('Execution start time: %s' % time.ctime())
+            print('Log file: %s' % self.path)
+            sys.stdout = sys.stderr = self.f
+            print('Execution start time: %s' % time.ctime())
+        return self
+
+    def __exit__(self, *exc):
+        if self.f is not None:
+            if exc[0] is not None:
+                import traceback
+                traceback.print_exception(*exc, file=self.f)
+            sys.stdout, sys.stderr = self.old
+            self.f.close()
+            self.f = None
+        return False
 SCORE_SIZE = 25000                       # gan/utils/scorer.py:27
 
 
@@ -163,26 +223,19 @@ def make_scorer(flags, pipe, dev, size):
 
 
 def make_pipeline(flags, size, c_dim, dev, rank=0, world=1):
-    """The dataset's pipeline (gan/core/pipeline.py:458-476), or synthetic
-    U[0,1] images when the dataset's files are absent."""
-    import warnings
+    """The dataset's pipeline (gan/core/pipeline.py:458-476).  U[0,1] images
+    only for ``-dataset synthetic``: an unknown dataset name, absent files or
+    malformed records raise, as the reference's pipelines do -- a run never
+    trains on noise it did not ask for."""
     from gan.core import pipeline as P
     args = (size, c_dim, flags.real_batch_size, flags.data_dir)
     kw = dict(device=dev, rank=rank, world=world)
-    try:
-        cls = P.get_pipeline(flags.dataset)
-        return cls(*args, **kw)
-    except (ValueError, FileNotFoundError) as e:
-        if flags.dataset != 'synthetic':
-            warnings.warn('dataset %r unavailable (%s): synthetic U[0,1] images'
-                          % (flags.dataset, e))
-        return P.Synthetic(*args, **kw)
+    return P.get_pipeline(flags.dataset)(*args, **kw)
 
 
 def main(argv=None):
     import torch
     import torch.distributed as dist
-    from gan.core.smmd import get_model
 
     flags = make_flags(argv=argv)
     flags.num_gpus = num_gpus_from_env()
@@ -195,10 +248,23 @@ def main(argv=None):
     if world > 1:
         dist.init_process_group('nccl', device_id=dev)
     rank = dist.get_rank() if world > 1 else 0
-    if rank == 0:
-        import pprint
-        pprint.PrettyPrinter().pprint(vars(flags))
     size, c_dim = output_size_for(flags)
+    dirs = run_dirs(flags, size, create=(rank == 0))
+    try:
+        with LogRedirect(dirs['sample'], on=bool(flags.log) and rank == 0):
+            if rank == 0:
+                import pprint
+                pprint.PrettyPrinter().pprint(vars(flags))
+            return _train(flags, dev, world, rank, size, c_dim)
+    finally:
+        if world > 1:
+            dist.destroy_process_group()
+
+
+def _train(flags, dev, world, rank, size, c_dim):
+    import torch
+    import torch.distributed as dist
+    from gan.core.smmd import get_model
     Model = get_model(flags.model)
     torch.manual_seed(rank)
     gan = Model(flags, device=dev, process_group=dist.group.WORLD if world > 1 else None,
@@ -241,8 +307,6 @@ def main(argv=None):
                         gan.set_lr_sc(float(ls[0]), float(ls[1]) if gan.sc is not None else None)
         finally:
             pipe.stop()
-    if world > 1:
-        dist.destroy_process_group()
     return gan
 
 

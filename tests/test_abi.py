@@ -102,3 +102,14 @@ def test_product_never_imports_oracle():
             if f.endswith('.py'):
                 src = open(os.path.join(dp, f)).read()
                 assert 'oracle' not in re.findall(r'^\s*(?:from|import)\s+(\w+)', src, re.M), f
+
+
+def test_library_stamp_matches_sources(L, monkeypatch):
+    """The .so carries the hash of the sources it was built from; a binary
+    older than csrc/ + include/ is refused at load (never silently run)."""
+    from gan.core import _lib
+    assert L.smmd_source_hash().decode() == _lib.source_hash()
+    monkeypatch.setattr(_lib, '_lib', None)
+    monkeypatch.setattr(_lib, 'source_hash', lambda: '0' * 16)
+    with pytest.raises(_lib.SmmdLibraryError, match='other sources'):
+        _lib.lib()

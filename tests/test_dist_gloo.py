@@ -303,3 +303,25 @@ def test_buckets_issue_in_order_when_completed_out_of_order():
         assert launched == [4, 4, 4, 4]
     finally:
         collectives.all_reduce_async = orig
+
+
+def _worker_bucket_env(rank, world, port, q):
+    import os
+    os.environ['SMMD_BUCKET_MB'] = '0.0001' if rank == 0 else '64'   # ranks disagree
+    _init(rank, world, port)
+    from gan.core.collectives import GradBuckets
+    from gan.core.optim import FlatAdam
+    net = _net()
+    opt = FlatAdam(list(net.parameters()), lr=1e-3, clip_norm=1.0)
+    bk = GradBuckets(opt, dist.group.WORLD)
+    q.put((rank, bk.bucket_bytes, list(bk.buckets)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bucket_layout_agrees_across_ranks():
+    """SMMD_BUCKET_MB read differently by the ranks: rank 0's size is
+    broadcast, so every rank forms the same buckets (no hang, no mixed sums)."""
+    res = _run(_worker_bucket_env, world=2)
+    (r0, b0, l0), (r1, b1, l1) = sorted(res)
+    assert b0 == b1 == int(0.0001 * (1 << 20)) and l0 == l1 and len(l0) > 1

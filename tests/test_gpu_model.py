@@ -6,8 +6,10 @@ oracle's CPU op-by-op mirror of the TF graph (oracle/tf_mirror.py) from the
 same weights, u vectors, images and z.  Tolerances (MIOpen fp32 convs vs CPU
 fp32 convs, same graph): d_loss rtol 1e-3; per-tensor gradients
 |d| <= max(t max|ref|, 5e-5 max over all tensors) + t |ref| with t = 2e-3, and
-t = 5e-3 at the configs' full widths and batch 64 (64x longer fp32 reductions
-over the batch in a different order: MIOpen's vs the CPU's).
+t = 5e-3 at the configs' full widths and batch >= 64 (64x longer fp32
+reductions over the batch in a different order: MIOpen's vs the CPU's); and
+per tensor a relative Frobenius error <= 1e-3 (2e-3 at batch >= 64), so a
+systematic error in a low-magnitude tensor cannot hide under the max bound.
 """
 import argparse
 
@@ -44,7 +46,8 @@ def _mirror_from(model):
     ('sngan', 32, 64, 8, False), ('snresnet', 64, 16, 8, False), ('snresnet', 64, 16, 8, True),
     ('g-resnet5', 64, 16, 8, False),
     ('g-resnet5', 64, 64, 64, False),         # celebA_smmd.yml's widths and batch at 64x64 (C3)
-    ('snresnet', 64, 64, 64, False)])         # imagenet_smmd.yml's widths and batch, once
+    ('snresnet', 64, 64, 64, False),          # imagenet_smmd.yml's widths and batch, once
+    ('snresnet', 64, 16, 256, False)])        # BASELINE configs[4]'s 256 images per GPU
 def test_critic_step_matches_tf_mirror(dev, arch, size, dim, batch, cl):
     from gan.core.smmd import SMMD
     torch.manual_seed(0)
@@ -82,10 +85,18 @@ def test_critic_step_matches_tf_mirror(dev, arch, size, dim, batch, cl):
         # exact zeros (e.g. the output bias: RBF-MMD is translation invariant) are
         # rounding noise in both (either sign): absolute floor 5e-5 of the
         # largest gradient
-        t = 5e-3 if batch == 64 else 2e-3
+        t = 5e-3 if batch >= 64 else 2e-3
         tol = max(t * np.abs(ref).max(), 5e-5 * gmax) + t * np.abs(ref)
         assert (np.abs(got - ref) <= tol + 1e-12).all(), (name, np.abs(got - ref).max(),
                                                            np.abs(ref).max())
+        # a small systematic error in one low-magnitude tensor would hide under
+        # the elementwise bound: its own relative Frobenius error stays small
+        # (tensors whose reference is rounding noise -- |ref| under the floor --
+        # are exempt)
+        nref = np.linalg.norm(ref)
+        if np.abs(ref).max() > 10 * 5e-5 * gmax:
+            rel = np.linalg.norm(got - ref) / nref
+            assert rel <= (2e-3 if batch >= 64 else 1e-3), (name, rel)
     # u advanced exactly as the reference's u.assign(u') (sn.py:39-46)
     by_weight = {id(mirror.prod[k]): k.rsplit('/', 1)[0] for k in mirror.prod}
     for e in model.sn_D.entries:
@@ -256,11 +267,17 @@ def test_main_cli_trains_on_cifar_files_and_checkpoints(dev, tmp_path):
     argv = ['-dataset', 'cifar10', '-data_dir', str(tmp_path), '-architecture', 'sngan',
             '-model', 'smmd', '-kernel', 'rbf', '-batch_size', '8', '-with_sn', 'true',
             '-with_learnable_sn_scale', 'true', '-with_scaling', 'true', '-batch_norm', 'true',
-            '-max_iteration', '1', '-checkpoint_dir', str(ck), '-name', 'run']
+            '-max_iteration', '1', '-checkpoint_dir', str(ck), '-name', 'run',
+            '-out_dir', str(tmp_path / 'out')]
     M.main(argv)
     assert (ck / 'run' / 'MMDGAN.model-0.pt').exists()
     M.main(argv)                                       # resumes at step 1 from the save
     assert open(ck / 'run' / 'checkpoint').read().strip() == 'MMDGAN.model-0'
+    # -log (default on): the run's output in <sample_dir>/log.txt (model.py:85-94)
+    logs = list((tmp_path / 'out' / 'sample' / 'run').glob('*/log.txt'))
+    assert len(logs) == 1
+    text = logs[0].read_text()
+    assert 'Execution start time' in text and 'Load SUCCESS' in text and 'G: ' in text
 
 
 def test_main_cli_scorer_drives_lr_schedule(dev, tmp_path, monkeypatch):
@@ -281,7 +298,8 @@ def test_main_cli_scorer_drives_lr_schedule(dev, tmp_path, monkeypatch):
             '-model', 'smmd', '-kernel', 'rbf', '-batch_size', '64', '-with_sn', 'true',
             '-with_learnable_sn_scale', 'true', '-with_scaling', 'true', '-batch_norm', 'true',
             '-max_iteration', '1', '-checkpoint_dir', str(tmp_path / 'ck'), '-name', 'run',
-            '-MMD_sdlr_freq', '1', '-MMD_sdlr_past_sample', '1', '-MMD_sdlr_num_test', '1']
+            '-MMD_sdlr_freq', '1', '-MMD_sdlr_past_sample', '1', '-MMD_sdlr_num_test', '1',
+            '-out_dir', str(tmp_path / 'out')]
     gan = M.main(base + ['-featurizer', 'random'])
     assert (tmp_path / 'cifar10-codes-random.npy').exists()
     codes = np.load(tmp_path / 'cifar10-codes-random.npy')

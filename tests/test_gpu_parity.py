@@ -594,6 +594,35 @@ def test_scaled_loss_vs_oracle(dev, variant, sqrt_scale):
                     'd feat')
 
 
+@pytest.mark.parametrize('variant', ['grad', 'value_and_grad'])
+def test_scaled_loss_batch256_vs_oracle(dev, variant):
+    """BASELINE configs[4]'s per-GPU size: the Jacobian of 256 real images at
+    3x64x64 (12.6 MB), J / scale / g_loss and the backward against the
+    float64 oracle (ops.py:228-233, model.py:366-403)."""
+    from gan.core import ops
+    rng = np.random.default_rng(29)
+    b = 256
+    jac = rng.standard_normal((1, b, 3, 64, 64)).astype(np.float32) * 0.05
+    feat = rng.standard_normal((b, 1)).astype(np.float32)
+    base = np.float32(0.21)
+    jt = torch.tensor(jac, device=dev, requires_grad=True)
+    ft = torch.tensor(feat, device=dev, requires_grad=True)
+    bt = torch.tensor(base, device=dev, requires_grad=True)
+    g, aux = ops.scaled_loss(bt, jt, ft, sc=10.0, variant=variant)
+    J = np.mean(O.squared_norm_per_sample(jac[0]))
+    nD = np.mean(feat.astype(np.float64) ** 2)
+    sc_ = O.scale_factor(J, 10.0, nD, variant)
+    _close(aux[3].item(), J, 0, 1e-5, 'J')
+    _close(aux[2].item(), sc_, 0, 1e-5, 'scale')
+    _close(g.item(), base * sc_, 0, 1e-5, 'g_loss')
+    g.backward()
+    coefq = base * (-10.0 * sc_ ** 2)
+    _close(bt.grad.item(), sc_, 0, 1e-5, 'd base')
+    _grad_close(jt.grad.cpu().numpy(), coefq * 2.0 / b * jac.astype(np.float64), 'd jac')
+    if variant == 'value_and_grad':
+        _grad_close(ft.grad.cpu().numpy(), coefq * 2.0 / b * feat.astype(np.float64), 'd feat')
+
+
 def test_scaled_loss_workspace_reuse(dev):
     """The squared-norm pass elects its finalizing block by a ticket at a fixed
     offset of the cached workspace; calls with fewer rows reuse the buffer

@@ -314,8 +314,11 @@ def test_snresnet_generator_up_add_equals_unfused():
         assert float((a - b).abs().max()) <= 1e-5 * scale
 
 
-@pytest.mark.parametrize('shape', [(64, 64, 64, 64), (64, 512, 8, 8), (8, 1024, 4, 4), (3, 7, 4, 4)])
-def test_bn_relu_no_grad_matches_torch(shape):
+@pytest.mark.parametrize('shape,mul,add', [((64, 64, 64, 64), 3, 1), ((64, 512, 8, 8), 3, 1),
+                                           ((8, 1024, 4, 4), 3, 1), ((3, 7, 4, 4), 3, 1),
+                                           # |mean| >> std: the variance must not cancel
+                                           ((64, 64, 64, 64), 0.01, 50), ((8, 256, 8, 8), 0.01, 50)])
+def test_bn_relu_no_grad_matches_torch(shape, mul, add):
     """smmd_bn_relu_fwd (the generator's batch norm + ReLU in a critic step,
     resnet/block.py:42-47) against nn.BatchNorm2d in training mode + relu:
     output and the updated moving averages, from the same module state."""
@@ -323,7 +326,7 @@ def test_bn_relu_no_grad_matches_torch(shape):
     from gan.core.snops import batch_norm, bn_relu
     saved, snops.BN_RELU = snops.BN_RELU, True
     g = torch.Generator(device=DEV).manual_seed(sum(shape))
-    x = torch.randn(shape, device=DEV, generator=g) * 3 + 1
+    x = torch.randn(shape, device=DEV, generator=g) * mul + add
     bns = [batch_norm(shape[1]).to(DEV) for _ in range(2)]
     with torch.no_grad():
         for bn in bns:

@@ -22,7 +22,9 @@ DEV = 'cuda:0'
 SHAPES = [(64, 3, 64, 64, 64), (64, 3, 64, 32, 32), (5, 3, 16, 13, 17), (4, 1, 8, 7, 64),
           (3, 4, 5, 9, 33), (2, 2, 3, 1, 1),
           (64, 64, 3, 64, 64), (64, 64, 3, 32, 32), (5, 16, 3, 13, 17), (3, 37, 2, 5, 64),
-          (2, 7, 4, 6, 1), (1, 300, 1, 3, 4)]
+          (2, 7, 4, 6, 1), (1, 300, 1, 3, 4),
+          # a 4-channel thin side at W % 4 == 0 (9 * 4 taps > one 32-column MFMA tile)
+          (4, 4, 64, 32, 32), (4, 64, 4, 32, 32)]
 
 
 def _data(N, ci, co, H, W, seed):

@@ -333,3 +333,31 @@ def test_prefold_cache_reuse_and_invalidation():
             p.add_(0.01)
     D(x1)
     assert D._fold_cache is not c1                   # in-place update: refolded
+
+
+def test_run_dirs_and_log_redirect(tmp_path):
+    """model.py:62-120: the run's description and out_dir/<x>_dir/name/desc
+    folders; -log sends stdout and stderr to <sample_dir>/log.txt and the
+    streams come back afterwards."""
+    import sys
+    from gan.main import LogRedirect, description, make_flags, run_dirs
+    f = make_flags(argv=['-config_file', os.path.join(CFG, 'imagenet_smmd.yml'),
+                         '-dataset', 'imagenet', '-out_dir', str(tmp_path), '-name', 'exp'])
+    d = description(f, 64)
+    assert d == 'imagenet64x64_snresnet_dc_rbfd5-10-1_64_64_lr0.00020000_bn'
+    dirs = run_dirs(f, 64)
+    assert dirs['sample'] == os.path.join(str(tmp_path), 'sample', 'exp', d)
+    assert all(os.path.isdir(p) for p in dirs.values())
+    out, err = sys.stdout, sys.stderr
+    with pytest.raises(KeyError):
+        with LogRedirect(dirs['sample']):
+            print('hello from the run')
+            print('to stderr', file=sys.stderr)
+            raise KeyError('boom')
+    assert sys.stdout is out and sys.stderr is err
+    text = open(os.path.join(dirs['sample'], 'log.txt')).read()
+    assert 'Execution start time' in text and 'hello from the run' in text
+    assert 'to stderr' in text and 'KeyError' in text
+    with LogRedirect(str(tmp_path / 'nowhere'), on=False):
+        pass                                          # -log false: nothing opened
+    assert not os.path.exists(tmp_path / 'nowhere')

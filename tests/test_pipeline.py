@@ -180,12 +180,38 @@ def test_cifar10_python_and_binary(tmp_path):
     assert n == 42
 
 
-def test_make_pipeline_falls_back(tmp_path):
+def test_make_pipeline_synthetic_only_when_asked(tmp_path):
     from gan.main import make_flags, make_pipeline
-    f = make_flags(argv=['-dataset', 'imagenet', '-data_dir', str(tmp_path), '-batch_size', '4'])
+    f = make_flags(argv=['-dataset', 'synthetic', '-data_dir', str(tmp_path), '-batch_size', '4'])
     f.real_batch_size = 4
-    with pytest.warns(UserWarning):
-        pipe = make_pipeline(f, 16, 3, torch.device('cpu'))
+    pipe = make_pipeline(f, 16, 3, torch.device('cpu'))
     assert isinstance(pipe, P.Synthetic)
     x = pipe.next()
     assert x.shape == (4, 3, 16, 16) and 0 <= float(x.min()) and float(x.max()) <= 1
+
+
+def test_make_pipeline_raises_instead_of_substituting(tmp_path):
+    """No silent noise (reference pipeline.py:458-476 raises): absent shards,
+    a typo in -dataset, malformed records."""
+    from gan.main import make_flags, make_pipeline
+    f = make_flags(argv=['-dataset', 'imagenet', '-data_dir', str(tmp_path), '-batch_size', '4'])
+    f.real_batch_size = 4
+    with pytest.raises(FileNotFoundError):
+        make_pipeline(f, 16, 3, torch.device('cpu'))
+    f.dataset = 'imagnet'
+    with pytest.raises(ValueError, match='invalid dataset'):
+        make_pipeline(f, 16, 3, torch.device('cpu'))
+    f.dataset = 'cifar10'
+    with pytest.raises((FileNotFoundError, ValueError, OSError)):
+        make_pipeline(f, 32, 3, torch.device('cpu'))
+    # a shard that is not a TFRecord file
+    shard_dir = tmp_path / 'tf_records_train'
+    shard_dir.mkdir()
+    (shard_dir / 'train-00000-of-00001').write_bytes(b'\x01\x02\x03')
+    f.dataset = 'imagenet'
+    with pytest.raises((ValueError, RuntimeError)):
+        pipe = make_pipeline(f, 16, 3, torch.device('cpu'))
+        try:
+            pipe.next()
+        finally:
+            pipe.stop()
