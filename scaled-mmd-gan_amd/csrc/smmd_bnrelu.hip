@@ -16,8 +16,8 @@
 // block tree in double) into a
 // [S][C] double slab; (2) block (c, s) reduces channel c's S partials in a
 // fixed order (every block of the channel the same way), forms
-// scale = gamma / sqrt(var + eps), shift = beta - mean * scale, applies
-// relu(x * scale + shift) to its rows, and block (c, 0) updates the moving
+// scale = gamma / sqrt(var + eps), applies relu(((x - k) - (mean - k)) * scale
+// + beta) to its rows, and block (c, 0) updates the moving
 // averages.  HBM: one read for the statistics, one read + one write to apply.
 #include "smmd_common.hpp"
 
@@ -83,7 +83,7 @@ __global__ __launch_bounds__(BN_T) void bn_apply_kernel(const float *__restrict_
                                                         float momentum, float eps,
                                                         float *__restrict__ y) {
     const int c = blockIdx.x, s = blockIdx.y;
-    __shared__ float sh[2];
+    __shared__ float sh[4];
     if (threadIdx.x < SMMD_WAVE) {
         // fixed order: lane-strided over the S partials, then the wave tree
         double a = 0.0, q = 0.0;
@@ -103,7 +103,9 @@ __global__ __launch_bounds__(BN_T) void bn_apply_kernel(const float *__restrict_
             const double g = gamma ? (double)gamma[c] : 1.0;
             const double b = beta ? (double)beta[c] : 0.0;
             sh[0] = (float)(g * inv);
-            sh[1] = (float)(b - mean * g * inv);
+            sh[1] = (float)b;
+            sh[2] = x[(size_t)c * HW];                  // the shift k
+            sh[3] = (float)ms;                           // mean - k
             if (s == 0 && run_mean && run_var) {
                 const double unb = cnt > 1.0 ? var * cnt / (cnt - 1.0) : var;
                 run_mean[c] = (float)((1.0 - momentum) * (double)run_mean[c] + momentum * mean);
@@ -112,7 +114,9 @@ __global__ __launch_bounds__(BN_T) void bn_apply_kernel(const float *__restrict_
         }
     }
     __syncthreads();
-    const float sc = sh[0], sf = sh[1];
+    // y = relu(((x - k) - (mean - k)) * scale + beta): x - k is exact (both
+    // near the mean), so no x * scale term cancels against mean * scale
+    const float sc = sh[0], bb = sh[1], k = sh[2], ms = sh[3];
     int n0, n1;
     bn_rows(N, S, s, n0, n1);
     const int w4 = HW >> 2;
@@ -127,8 +131,10 @@ __global__ __launch_bounds__(BN_T) void bn_apply_kernel(const float *__restrict_
         float4 *out = reinterpret_cast<float4 *>(y + off);
         for (int i = col; i < w4; i += step) {
             const float4 v = row[i];
-            out[i] = make_float4(fmaxf(fmaf(v.x, sc, sf), 0.f), fmaxf(fmaf(v.y, sc, sf), 0.f),
-                                 fmaxf(fmaf(v.z, sc, sf), 0.f), fmaxf(fmaf(v.w, sc, sf), 0.f));
+            out[i] = make_float4(fmaxf(fmaf((v.x - k) - ms, sc, bb), 0.f),
+                                 fmaxf(fmaf((v.y - k) - ms, sc, bb), 0.f),
+                                 fmaxf(fmaf((v.z - k) - ms, sc, bb), 0.f),
+                                 fmaxf(fmaf((v.w - k) - ms, sc, bb), 0.f));
         }
     }
 }
