@@ -57,6 +57,7 @@ PMC_FALLBACK = os.path.join(ROOT, 'profiles', 'r05', 'pmc_traffic.json')
 # the hot-path rows a1-a9 and the library entry points that
 # implement them (the roofline kernel is chosen among these)
 HOT_PATH = ('smmd_mmd2_fwd', 'smmd_scaled_loss_fwd', 'smmd_scaled_loss_bwd',
+            'smmd_smmd_loss_fwd', 'smmd_smmd_loss_bwd',
             'smmd_sn_power_iter', 'smmd_sn_weight_bwd', 'smmd_adam_flat[D]',
             'smmd_adam_flat[G]', 'smmd_adam_flat_sn[D]', 'smmd_adam_flat_sn[G]')
 
@@ -696,6 +697,12 @@ def main():
                                           for m in model.discriminator.modules()
                                           if isinstance(m, architecture._ConvMeanPool)) * 25 * 4,
             'smmd_scaled_loss_bwd': 2 * BATCH * per_img * 4,
+            # the fused loss (one process): the Jacobian read once + the
+            # features and their unit gradients; its backward as the
+            # scaled loss's (the generator step writes no Jacobian gradient:
+            # its mean bytes come from the D / G mix of the pass)
+            'smmd_smmd_loss_fwd': BATCH * per_img * 4 + 4 * BATCH * 4 + 8 * 4,
+            'smmd_smmd_loss_bwd': 2 * BATCH * per_img * 4 + 4 * BATCH * 4,
         }
         alg.update({k: int(v) for k, v in tb.items()})
         for name, (calls, ms) in tm.items():
@@ -720,7 +727,8 @@ def main():
                         'avg_ms': kernels[dom]['avg_ms'],
                         'algorithmic_bytes': kernels[dom]['bytes']}
         for k in ('smmd_sn_power_iter', 'smmd_sn_weight_bwd', 'smmd_adam_flat_sn[D]',
-                  'smmd_scaled_loss_fwd', 'smmd_scaled_loss_bwd', 'smmd_fold_pool_weights'):
+                  'smmd_scaled_loss_fwd', 'smmd_scaled_loss_bwd', 'smmd_smmd_loss_fwd',
+                  'smmd_smmd_loss_bwd', 'smmd_fold_pool_weights'):
             if k in kernels and 'bytes' in kernels[k]:
                 traffic, src = pmc_traffic(k)
                 hot[k] = {'avg_ms': kernels[k]['avg_ms'], 'algorithmic_bytes': kernels[k]['bytes'],
@@ -729,11 +737,21 @@ def main():
                           'pmc_over_algorithmic': (round(traffic / kernels[k]['bytes'], 3)
                                                    if traffic else None),
                           'pmc_source': src}
-        if 'smmd_mmd2_fwd' in kernels:
-            mk = kernels['smmd_mmd2_fwd']
+        # the loss side of a step: the fused launch and its backward (or,
+        # unfused, mmd2 + scaled loss fwd + bwd), each once per step: the sum
+        # of their mean HIP-event times per call
+        loss_keys = ('smmd_smmd_loss_fwd', 'smmd_smmd_loss_bwd', 'smmd_mmd2_fwd',
+                     'smmd_scaled_loss_fwd', 'smmd_scaled_loss_bwd')
+        hot['loss_side_us_per_step'] = {
+            'total': round(sum(kernels[k]['avg_ms'] for k in loss_keys if k in kernels) * 1e3, 2),
+            'calls': {k: round(kernels[k]['avg_ms'] * 1e3, 2) for k in loss_keys if k in kernels}}
+        mk_name = 'smmd_mmd2_fwd' if 'smmd_mmd2_fwd' in kernels else (
+            'smmd_smmd_loss_fwd' if 'smmd_smmd_loss_fwd' in kernels else None)
+        if mk_name:
+            mk = kernels[mk_name]
             P = 3 * m_all * m_all
             ops = mmd_valu_ops_per_pair('rbf', 1) * P
-            hot['smmd_mmd2_fwd'] = {
+            hot[mk_name] = {
                 'avg_ms': mk['avg_ms'], 'N_per_side': m_all, 'pairs': P,
                 'valu_frac': round(ops / (mk['avg_ms'] * 1e-3) / VALU_LANE_OPS, 5),
                 'bound': 'latency at D = 1 (one launch per critic step)'}

@@ -61,10 +61,11 @@ int smmd_abi_version(void);         /* bumped on any ABI change (2: Gram/poly,
                                        3: smmd_sn_layer.fold, 4: smmd_adam_flat_ex,
                                        5: smmd_conv3x3_thin*,
                                        6: smmd_mask_pool2*, smmd_up_add,
-                                       smmd_bn_relu_fwd) */
+                                       smmd_bn_relu_fwd, 7: smmd_smmd_loss_fwd/bwd,
+                                       smmd_source_hash) */
 const char *smmd_source_hash(void); /* first 16 hex digits of the SHA-256 of the
                                        sources this binary was built from
-                                       (csrc/*.hip, csrc/*.hpp in byte order,
+                                       (csrc .hip and .hpp files in byte order,
                                        then this header): gan.core._lib refuses
                                        a binary older than its sources */
 
@@ -171,6 +172,40 @@ smmd_status smmd_scaled_loss_bwd(const float *jac, int n_cols, int b, int b_tota
                                  int sqrt_scale, const float *g_loss_grad,
                                  float *d_base, float *gjac, float *gfeat,
                                  smmd_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * The SMMD critic loss in ONE launch: g_loss = mmd2(kernel(X, Y)) * scale
+ * (gan/core/smmd.py:10-23 set_loss + apply_scaling, model.py:366-403
+ * add_scaling) -- smmd_mmd2_fwd's tile sweep over all rows (one process, or
+ * a tower: b_total = b) and smmd_scaled_loss_fwd's squared-norm pass of
+ * the Jacobian in one grid; the last block to finish forms the estimator's
+ * scaled loss with base = out_mmd2.  Outputs as those two calls
+ * (out_sums, out_mmd2, grad_x / grad_y = d mmd2 / dX, dY; out[8] of
+ * smmd_scaled_loss_fwd).  ws: smmd_mmd2_workspace_bytes(m, n, d); loss_ws:
+ * smmd_scaled_loss_workspace_bytes(n_cols * b, per_sample).  Returns
+ * SMMD_EUNSUPPORTED where smmd_mmd2_fwd would not take its 2-D tiled path
+ * (d > 8, or the MFMA Gram path): the caller then makes the two calls.
+ *
+ * smmd_smmd_loss_bwd: the backward of both outputs in one launch:
+ *   dX, dY = (g_mmd2 + g_loss f) * grad_x, grad_y  (f = scale, or sqrt(scale)
+ *   with sqrt_scale), gjac and gfeat as smmd_scaled_loss_bwd with dL/dg_loss
+ *   = g_loss_grad (device scalar, required); g_mmd2_grad may be NULL (0);
+ *   gjac / gfeat may be NULL (not written: the Jacobian is a constant).
+ * ------------------------------------------------------------------------- */
+smmd_status smmd_smmd_loss_fwd(const smmd_kernel_desc *desc, const float *X, int m,
+                               const float *Y, int n, int d, int biased, const float *jac,
+                               int n_cols, int b, int64_t per_sample, const float *feat, int dof,
+                               float sc, int variant, int sqrt_scale, float *out_sums,
+                               float *out_mmd2, float *grad_x, float *grad_y, float *out,
+                               float *per_sample_out, void *ws, size_t ws_bytes, void *loss_ws,
+                               size_t loss_ws_bytes, smmd_stream_t stream);
+
+smmd_status smmd_smmd_loss_bwd(const float *jac, int n_cols, int b, int64_t per_sample,
+                               const float *feat, int dof, const float *fwd_out, float sc,
+                               int variant, int sqrt_scale, const float *g_loss_grad,
+                               const float *g_mmd2_grad, const float *gx_unit, int m,
+                               const float *gy_unit, int n, int d, float *gjac, float *gfeat,
+                               float *dX, float *dY, smmd_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * Spectral normalisation, all layers of a network in one set of launches.

@@ -147,6 +147,10 @@ constexpr size_t MMD_WS_HEADER = 16384;
 constexpr int TILE_MAX_RT = (int)(MMD_WS_HEADER / sizeof(unsigned)) - 64;
 bool tile_supported(int d);
 size_t tile_ws_bytes(int rows, int cols, int d);      // body bytes (after the header)
-smmd_status tile_mmd2_launch(TileArgs a, int kind, void *ws, hipStream_t s);
+struct ScaledLossArgs;
+// q != nullptr: the fused SMMD loss launch (smmd_smmd_loss_fwd), q->nblocks
+// squared-norm blocks after the tile grid
+smmd_status tile_mmd2_launch(TileArgs a, int kind, void *ws, hipStream_t s,
+                             const ScaledLossArgs *q = nullptr);
 
 }  // namespace smmd

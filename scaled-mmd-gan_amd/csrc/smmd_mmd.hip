@@ -15,6 +15,7 @@
 // release/acquire, CDNA4 guide G16) and writes the estimator.
 #include "smmd_common.hpp"
 #include "smmd_kern.hpp"
+#include "smmd_scale_dev.hpp"
 
 #include <stdlib.h>
 
@@ -753,7 +754,7 @@ const char *smmd_status_string(smmd_status s) {
     return "SMMD_?: unknown status";
 }
 
-int smmd_abi_version(void) { return 6; }
+int smmd_abi_version(void) { return 7; }
 
 // Path choice.  d > 32: the MFMA Gram path (the row sweep holds a row in
 // registers up to 32 features).  d <= 32: the row sweep, except where the
@@ -893,6 +894,70 @@ smmd_status smmd_mmd2_fwd(const smmd_kernel_desc *desc, const float *X, int m, c
     }
     if (!ok) return SMMD_EINVAL;
     return last_launch_status();
+}
+
+smmd_status smmd_smmd_loss_fwd(const smmd_kernel_desc *desc, const float *X, int m,
+                               const float *Y, int n, int d, int biased, const float *jac,
+                               int n_cols, int b, int64_t per_sample, const float *feat, int dof,
+                               float sc, int variant, int sqrt_scale, float *out_sums,
+                               float *out_mmd2, float *grad_x, float *grad_y, float *out,
+                               float *per_sample_out, void *ws, size_t ws_bytes, void *loss_ws,
+                               size_t loss_ws_bytes, smmd_stream_t stream) {
+    if (!desc || !X || !Y || m < 1 || n < 1 || d < 1) return SMMD_EINVAL;
+    if (!out_mmd2 || !grad_x || !grad_y || !jac || !out) return SMMD_EINVAL;
+    if (n_cols < 1 || b < 1 || per_sample < 1) return SMMD_EINVAL;
+    if (variant != 0 && variant != 1) return SMMD_EINVAL;
+    if (variant == 1 && (!feat || dof < 1)) return SMMD_EINVAL;
+    KParams kp;
+    if (!make_kparams(desc, kp)) return SMMD_EINVAL;
+    if (!use_tile(m, n, d)) return SMMD_EUNSUPPORTED;      // the caller runs two launches
+    if (!ws || ws_bytes < smmd_mmd2_workspace_bytes(m, n, d)) return SMMD_EWORKSPACE;
+    const int rows_j = n_cols * b;
+    if (!loss_ws || loss_ws_bytes < smmd_scaled_loss_workspace_bytes(rows_j, per_sample))
+        return SMMD_EWORKSPACE;
+    const double md = m, nd = n;
+    const int is_biased = biased ? 1 : 0;
+    const double wxx = is_biased ? 1.0 / (md * md) : 1.0 / (md * (md - 1.0));
+    const double wyy = is_biased ? 1.0 / (nd * nd) : 1.0 / (nd * (nd - 1.0));
+    TileArgs t;
+    memset(&t, 0, sizeof(t));
+    t.X = X; t.Y = Y; t.m = m; t.n = n; t.d = d;
+    t.nrows = m + n; t.nxr = m; t.x_begin = 0; t.y_begin = 0;
+    t.tanh_in = desc->tanh_inputs ? 1 : 0;
+    t.biased = is_biased;
+    t.has_const = desc->has_const_diag ? 1 : 0;
+    t.const_diag = desc->const_diag;
+    t.trace_mode = (!is_biased && !t.has_const) ? 1 : 0;
+    t.need_grad = 1;
+    t.gw_same_x = (float)(2.0 * wxx);
+    t.gw_same_y = (float)(2.0 * wyy);
+    t.gw_cross = (float)(-2.0 / (md * nd));
+    t.grad_x = grad_x; t.grad_y = grad_y;
+    t.out_sums = out_sums; t.out_mmd2 = out_mmd2;
+    t.kp = kp;
+    ScaledLossArgs q;
+    memset(&q, 0, sizeof(q));
+    const int nchunk = (int)((per_sample + SQ_CHUNK - 1) / SQ_CHUNK);
+    if ((int64_t)rows_j * nchunk > 0x7fffffff) return SMMD_EINVAL;
+    q.jac = jac;
+    q.per_sample = per_sample;
+    q.nchunk = nchunk;
+    q.vec = (per_sample % 4 == 0) && ((uintptr_t)jac % 16 == 0);
+    q.counter = (unsigned *)loss_ws;          // ticket at a fixed offset, as the fwd
+    q.part = (double *)((char *)loss_ws + SQ_WS_HEADER);
+    q.n_cols = n_cols;
+    q.b = b;
+    q.b_total = b;
+    q.dof = dof;
+    q.variant = variant;
+    q.sqrt_scale = sqrt_scale;
+    q.feat = feat;
+    q.base_loss = out_mmd2;                    // the estimator, stored by the MMD grid
+    q.sc = sc;
+    q.out = out;
+    q.per_sample_out = per_sample_out;
+    q.nblocks = rows_j * nchunk;
+    return tile_mmd2_launch(t, desc->kind, ws, (hipStream_t)stream, &q);
 }
 
 smmd_status smmd_mmd2_combine(const smmd_kernel_desc *desc, const float *sums, int m, int n,

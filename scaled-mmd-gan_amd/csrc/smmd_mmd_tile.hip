@@ -27,6 +27,7 @@
 // them to the oracle at the fp32 tolerances).
 #include "smmd_common.hpp"
 #include "smmd_kern.hpp"
+#include "smmd_scale_dev.hpp"
 
 #include <stdlib.h>
 
@@ -170,9 +171,13 @@ __device__ __forceinline__ void publish6(double *rec, const double (&S)[6], int 
 // (no private arrays may be indexed by a lane-dependent value here: the
 // compiler then moves them to LDS, addressed through the dispatch packet --
 // a scalar load from the host-side queue measured at ~10 us per launch)
-template <int DT, int KIND, int NT, bool TANH, bool GRAD>
-__global__ __launch_bounds__(TILE_ROWS * TILE_WAVES) void mmd2_tile_kernel(
-    TileArgs a, const float *__restrict__ X, const float *__restrict__ Y) {
+// The body of workgroup `bid` of the grid.  FUSED (the SMMD loss launch
+// below): every workgroup publishes its sums record (lane 0 of wave 0,
+// write-through) and no grid ticket is taken here -- the launch's loss ticket
+// collects the records; the row tiles' gradient tickets work as usual.
+template <int DT, int KIND, int NT, bool TANH, bool GRAD, bool FUSED = false>
+__device__ __forceinline__ void mmd2_tile_body(const TileArgs &a, const float *__restrict__ X,
+                                               const float *__restrict__ Y, int bid) {
     constexpr int NV = DT + 1;                 // acc[DT], aacc
     __shared__ float lds_v[TILE_WAVES][NV][TILE_ROWS];
     __shared__ double lds_s[TILE_WAVES][6];
@@ -180,8 +185,8 @@ __global__ __launch_bounds__(TILE_ROWS * TILE_WAVES) void mmd2_tile_kernel(
     __shared__ int lds_flag[2];
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int ch = blockIdx.x % a.n_ch;        // column chunk
-    const int rt = blockIdx.x / a.n_ch;        // row tile
+    const int ch = bid % a.n_ch;               // column chunk
+    const int rt = bid / a.n_ch;               // row tile
     const int r = rt * TILE_ROWS + lane;
     const bool active = r < a.nrows;
     const bool isx = r < a.nxr;
@@ -266,8 +271,30 @@ __global__ __launch_bounds__(TILE_ROWS * TILE_WAVES) void mmd2_tile_kernel(
     // the row tile's ticket exists only when there are gradients to gather
     // over several chunks; every counter taken is reset by its last taker
     const bool rt_ticket = GRAD && a.n_ch > 1;
-    bool rt_last = GRAD, g_last = true;
-    if (nb > 1) {
+    bool rt_last = GRAD, g_last = !FUSED;
+    if (FUSED) {
+        // the sums record for the loss ticket's last taker; the row tile's
+        // gradient ticket as below
+        if (w == 0) {
+            if (rt_ticket) {
+#pragma unroll
+                for (int k = 0; k < NV; ++k)
+                    store_wt(a.part + ((size_t)ch * NV + k) * a.rows_pad + r, v[k]);
+            }
+            publish6(a.blk_sums + (size_t)bid * 8, S, lane);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            unsigned prev = 0;
+            if (lane == 0 && rt_ticket)
+                prev = __hip_atomic_fetch_add(a.rt_counter + rt, 1u, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+            prev = __shfl(prev, 0, SMMD_WAVE);
+            if (lane == 0) lds_flag[0] = GRAD && (!rt_ticket || prev == (unsigned)a.n_ch - 1);
+        }
+        __syncthreads();
+        rt_last = lds_flag[0] != 0;
+        if (!rt_last) return;
+        if (rt_ticket) acquire_block();
+    } else if (nb > 1) {
         // publish (wave 0): this chunk's per-row partials and the block's sums,
         // write-through; drain; then BOTH tickets at once -- the row tile's
         // (lane 0) and the whole grid's (lane 1) -- so the gradient and the
@@ -278,7 +305,7 @@ __global__ __launch_bounds__(TILE_ROWS * TILE_WAVES) void mmd2_tile_kernel(
                 for (int k = 0; k < NV; ++k)
                     store_wt(a.part + ((size_t)ch * NV + k) * a.rows_pad + r, v[k]);
             }
-            publish6(a.blk_sums + (size_t)blockIdx.x * 8, S, lane);
+            publish6(a.blk_sums + (size_t)bid * 8, S, lane);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             unsigned prev = 0;
             if (lane == 0 && rt_ticket)
@@ -300,7 +327,7 @@ __global__ __launch_bounds__(TILE_ROWS * TILE_WAVES) void mmd2_tile_kernel(
         acquire_block();                       // every wave reads other blocks' data
     }
 
-    if (g_last && nb > 1) {                    // 256 threads over the block records
+    if (!FUSED && g_last && nb > 1) {          // 256 threads over the block records
         double tt[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
         for (int b = threadIdx.x; b < nb; b += TILE_ROWS * TILE_WAVES) {
 #pragma unroll
@@ -313,11 +340,10 @@ __global__ __launch_bounds__(TILE_ROWS * TILE_WAVES) void mmd2_tile_kernel(
             for (int k = 0; k < 6; ++k) lds_s2[w][k] = tt[k];
         }
     }
-    if (nb > 1) __syncthreads();
-    if (w != 0) return;
+    if (!FUSED && nb > 1) __syncthreads();
 
     // the row tile's last chunk: its rows' gradients, chunks summed in order
-    if (rt_last) {
+    if (w == 0 && rt_last) {
         if (rt_ticket) {
 #pragma unroll
             for (int k = 0; k < NV; ++k) v[k] = 0.f;
@@ -356,7 +382,7 @@ __global__ __launch_bounds__(TILE_ROWS * TILE_WAVES) void mmd2_tile_kernel(
     }
 
     // the grid's last block: the estimator from every block's sums
-    if (g_last && lane == 0) {
+    if (!FUSED && w == 0 && g_last && lane == 0) {
         if (nb > 1) {
 #pragma unroll
             for (int k = 0; k < 6; ++k)
@@ -365,14 +391,102 @@ __global__ __launch_bounds__(TILE_ROWS * TILE_WAVES) void mmd2_tile_kernel(
         }
         if (a.out_sums) {
 #pragma unroll
+            for (int k = 0; k < 6; ++k) store_wt(a.out_sums + k, (float)S[k]);
+            store_wt(a.out_sums + 6, 0.f);
+            store_wt(a.out_sums + 7, 0.f);
+        }
+        if (a.out_mmd2)
+            store_wt(a.out_mmd2, (float)estimator(S, (double)a.m, (double)a.n, a.biased,
+                                                  a.has_const, a.const_diag));
+    }
+}
+
+template <int DT, int KIND, int NT, bool TANH, bool GRAD>
+__global__ __launch_bounds__(TILE_ROWS * TILE_WAVES) void mmd2_tile_kernel(
+    TileArgs a, const float *__restrict__ X, const float *__restrict__ Y) {
+    mmd2_tile_body<DT, KIND, NT, TANH, GRAD>(a, X, Y, blockIdx.x);
+}
+
+// The scaled SMMD loss in ONE launch (smmd_smmd_loss_fwd): workgroups
+// [0, nb) run the MMD^2 tile sweep above, the rest the Jacobian's
+// squared-norm partials (smmd_scale_dev.hpp); every workgroup publishes its
+// record and takes the ONE loss ticket, and its last taker forms the
+// estimator from the nb sums records (the order of the unfused grid's last
+// block), then the scaled-loss finalize with base = that estimator.  Two
+// dependent launches with two ticket levels each become one launch with one.
+template <int DT, int KIND, int NT, bool TANH, bool GRAD>
+__global__ __launch_bounds__(TILE_ROWS * TILE_WAVES) void smmd_loss_kernel(
+    TileArgs a, const float *__restrict__ X, const float *__restrict__ Y, ScaledLossArgs q) {
+    static_assert(TILE_ROWS * TILE_WAVES == 256, "the norm blocks are 256 threads");
+    const int nb = a.n_rt * a.n_ch;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    __shared__ int last;
+    if ((int)blockIdx.x < nb) {
+        mmd2_tile_body<DT, KIND, NT, TANH, GRAD, true>(a, X, Y, blockIdx.x);
+    } else {
+        const int blk = blockIdx.x - nb;
+        const double s = sqnorm_block(q, blk);
+        if (threadIdx.x == 0) store_wt(q.part + blk, s);
+    }
+    // two-level ticket (MI355X_MICROARCH fanin: ~12 ns per arrival on one
+    // device-scope counter): shard blockIdx % 8 first, its last arriver then
+    // the top counter; every counter is reset by its last taker
+    if (w == 0) {                              // the wave whose lane 0 published
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int G = (int)gridDim.x;
+        const int shard = (int)(blockIdx.x % SQ_SHARDS);
+        const int in_shard = (G - shard + SQ_SHARDS - 1) / SQ_SHARDS;
+        const int shards = G < SQ_SHARDS ? G : SQ_SHARDS;
+        int l = 0;
+        if (lane == 0) {
+            unsigned *sc = q.counter + SQ_SHARD_STRIDE * (1 + shard);
+            const unsigned p = __hip_atomic_fetch_add(sc, 1u, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+            if (p == (unsigned)in_shard - 1) {
+                __hip_atomic_store(sc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned t = __hip_atomic_fetch_add(q.counter, 1u, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT);
+                l = t == (unsigned)shards - 1;
+            }
+            last = l;
+        }
+    }
+    __syncthreads();
+    if (!last) return;
+    acquire_block();
+    // the estimator: the records summed as the unfused grid's last block does
+    __shared__ double s2[TILE_WAVES][6];
+    __shared__ float base;
+    double tt[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    for (int b = threadIdx.x; b < nb; b += TILE_ROWS * TILE_WAVES) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) tt[k] += a.blk_sums[(size_t)b * 8 + k];
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) tt[k] = wave_sum(tt[k]);
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) s2[w][k] = tt[k];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double S[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) S[k] = ((s2[0][k] + s2[1][k]) + s2[2][k]) + s2[3][k];
+        if (a.out_sums) {
+#pragma unroll
             for (int k = 0; k < 6; ++k) a.out_sums[k] = (float)S[k];
             a.out_sums[6] = 0.f;
             a.out_sums[7] = 0.f;
         }
-        if (a.out_mmd2)
-            a.out_mmd2[0] = (float)estimator(S, (double)a.m, (double)a.n, a.biased, a.has_const,
-                                             a.const_diag);
+        const float e = (float)estimator(S, (double)a.m, (double)a.n, a.biased, a.has_const,
+                                         a.const_diag);
+        a.out_mmd2[0] = e;
+        base = e;
     }
+    __syncthreads();
+    scaled_loss_final(q, base);
+    ticket_reset(q.counter);
 }
 
 // ---------------------------------------------------------------------------
@@ -386,16 +500,21 @@ __global__ __launch_bounds__(TILE_ROWS * TILE_WAVES) void mmd2_tile_kernel(
 // SMMD_TILE_BLOCKS / SMMD_TILE_MINCPW override both (tuning runs).
 constexpr int TILE_TARGET_BLOCKS = 512;
 constexpr int TILE_MIN_CPW = 32;
+// The fused loss launch at small N (<= 256 rows): the sweep is on its
+// critical path while the row tiles' gradient combines are not (nothing in
+// the launch waits for them), so columns go 8 per wave: 4x the waves
+constexpr int TILE_FUSED_MIN_CPW = 8;
+constexpr int TILE_FUSED_SMALL_ROWS = 256;
 
 static int env_int(const char *k, int dflt) {
     const char *e = getenv(k);
     return (e && e[0]) ? atoi(e) : dflt;
 }
 
-static void tile_shape(int rows, int cols, int &n_rt, int &n_ch, int &cpw) {
+static void tile_shape(int rows, int cols, int &n_rt, int &n_ch, int &cpw, int min_cpw) {
     n_rt = (rows + TILE_ROWS - 1) / TILE_ROWS;
-    int mincpw = env_int("SMMD_TILE_MINCPW", TILE_MIN_CPW);
-    if (mincpw < TILE_MIN_CPW) mincpw = TILE_MIN_CPW;
+    int mincpw = env_int("SMMD_TILE_MINCPW", min_cpw);
+    if (mincpw < min_cpw) mincpw = min_cpw;
     const int max_ch = (cols + TILE_WAVES * mincpw - 1) / (TILE_WAVES * mincpw);
     const int target = env_int("SMMD_TILE_BLOCKS", TILE_TARGET_BLOCKS);
     int ch = (target + n_rt - 1) / n_rt;
@@ -422,7 +541,9 @@ size_t tile_ws_bytes(int rows, int cols, int d) {
     // a bound over every local row count <= rows (the row-sharded calls):
     // tile_shape never gives more tiles or chunks than these
     const int n_rt = (rows + TILE_ROWS - 1) / TILE_ROWS;
-    const int n_ch = (cols + TILE_WAVES * TILE_MIN_CPW - 1) / (TILE_WAVES * TILE_MIN_CPW);
+    int n_ch = (cols + TILE_WAVES * TILE_MIN_CPW - 1) / (TILE_WAVES * TILE_MIN_CPW);
+    if (rows <= TILE_FUSED_SMALL_ROWS)          // the fused loss launch's finer split
+        n_ch = (cols + TILE_WAVES * TILE_FUSED_MIN_CPW - 1) / (TILE_WAVES * TILE_FUSED_MIN_CPW);
     const size_t rows_pad = (size_t)n_rt * TILE_ROWS;
     size_t b = align_up((size_t)n_rt * n_ch * 8 * sizeof(double), 256);
     b += align_up((size_t)n_ch * (dt + 1) * rows_pad * sizeof(float), 256);
@@ -430,8 +551,17 @@ size_t tile_ws_bytes(int rows, int cols, int d) {
 }
 
 template <int DT, int KIND, int NT>
-static void launch_tile_k(const TileArgs &a, hipStream_t s) {
-    const dim3 grid(a.n_rt * a.n_ch), block(TILE_ROWS * TILE_WAVES);
+static void launch_tile_k(const TileArgs &a, hipStream_t s, const ScaledLossArgs *q) {
+    const dim3 block(TILE_ROWS * TILE_WAVES);
+    if (q) {                                   // the fused SMMD loss (with gradient)
+        const dim3 grid(a.n_rt * a.n_ch + q->nblocks);
+        if (a.tanh_in)
+            hipLaunchKernelGGL((smmd_loss_kernel<DT, KIND, NT, true, true>), grid, block, 0, s, a, a.X, a.Y, *q);
+        else
+            hipLaunchKernelGGL((smmd_loss_kernel<DT, KIND, NT, false, true>), grid, block, 0, s, a, a.X, a.Y, *q);
+        return;
+    }
+    const dim3 grid(a.n_rt * a.n_ch);
     if (a.tanh_in) {
         if (a.need_grad)
             hipLaunchKernelGGL((mmd2_tile_kernel<DT, KIND, NT, true, true>), grid, block, 0, s, a, a.X, a.Y);
@@ -447,32 +577,34 @@ static void launch_tile_k(const TileArgs &a, hipStream_t s) {
 
 // term counts with a compiled fast form: rbf (1), mix_rq* (3), mix_rbf (6)
 template <int DT, int KIND>
-static void launch_tile_terms(const TileArgs &a, hipStream_t s) {
+static void launch_tile_terms(const TileArgs &a, hipStream_t s, const ScaledLossArgs *q) {
     switch (a.kp.n_terms) {
-        case 1: launch_tile_k<DT, KIND, 1>(a, s); break;
-        case 3: launch_tile_k<DT, KIND, 3>(a, s); break;
-        case 6: launch_tile_k<DT, KIND, 6>(a, s); break;
-        default: launch_tile_k<DT, KIND, 0>(a, s); break;
+        case 1: launch_tile_k<DT, KIND, 1>(a, s, q); break;
+        case 3: launch_tile_k<DT, KIND, 3>(a, s, q); break;
+        case 6: launch_tile_k<DT, KIND, 6>(a, s, q); break;
+        default: launch_tile_k<DT, KIND, 0>(a, s, q); break;
     }
 }
 
 template <int DT>
-static bool launch_tile_dt(const TileArgs &a, int kind, hipStream_t s) {
+static bool launch_tile_dt(const TileArgs &a, int kind, hipStream_t s, const ScaledLossArgs *q) {
     switch (kind) {
-        case SMMD_KIND_RBF: launch_tile_terms<DT, SMMD_KIND_RBF>(a, s); return true;
-        case SMMD_KIND_RQ: launch_tile_terms<DT, SMMD_KIND_RQ>(a, s); return true;
-        case SMMD_KIND_DISTANCE: launch_tile_k<DT, SMMD_KIND_DISTANCE, 0>(a, s); return true;
-        case SMMD_KIND_DOT: launch_tile_k<DT, SMMD_KIND_DOT, 0>(a, s); return true;
+        case SMMD_KIND_RBF: launch_tile_terms<DT, SMMD_KIND_RBF>(a, s, q); return true;
+        case SMMD_KIND_RQ: launch_tile_terms<DT, SMMD_KIND_RQ>(a, s, q); return true;
+        case SMMD_KIND_DISTANCE: launch_tile_k<DT, SMMD_KIND_DISTANCE, 0>(a, s, q); return true;
+        case SMMD_KIND_DOT: launch_tile_k<DT, SMMD_KIND_DOT, 0>(a, s, q); return true;
     }
     return false;
 }
 
 // ws: the whole workspace; counters in its header (g_counter = word 0,
 // rt_counter from byte 256), data from MMD_WS_HEADER
-smmd_status tile_mmd2_launch(TileArgs a, int kind, void *ws, hipStream_t s) {
+smmd_status tile_mmd2_launch(TileArgs a, int kind, void *ws, hipStream_t s,
+                             const ScaledLossArgs *q) {
     const int dt = tile_dt(a.d);
     if (!dt) return SMMD_EUNSUPPORTED;
-    tile_shape(a.nrows, a.m + a.n, a.n_rt, a.n_ch, a.cpw);
+    tile_shape(a.nrows, a.m + a.n, a.n_rt, a.n_ch, a.cpw,
+               (q && a.nrows <= TILE_FUSED_SMALL_ROWS) ? TILE_FUSED_MIN_CPW : TILE_MIN_CPW);
     if (a.n_rt > TILE_MAX_RT) return SMMD_EUNSUPPORTED;
     a.rows_pad = a.n_rt * TILE_ROWS;
     a.g_counter = (unsigned *)ws;
@@ -482,11 +614,13 @@ smmd_status tile_mmd2_launch(TileArgs a, int kind, void *ws, hipStream_t s) {
     p += align_up((size_t)a.n_rt * a.n_ch * 8 * sizeof(double), 256);
     a.part = (float *)p;
     bool ok = false;
+    if (q && (!a.need_grad || (int64_t)a.n_rt * a.n_ch + q->nblocks > 0x7fffffff))
+        return SMMD_EINVAL;
     switch (dt) {
-        case 1: ok = launch_tile_dt<1>(a, kind, s); break;
-        case 2: ok = launch_tile_dt<2>(a, kind, s); break;
-        case 4: ok = launch_tile_dt<4>(a, kind, s); break;
-        case 8: ok = launch_tile_dt<8>(a, kind, s); break;
+        case 1: ok = launch_tile_dt<1>(a, kind, s, q); break;
+        case 2: ok = launch_tile_dt<2>(a, kind, s, q); break;
+        case 4: ok = launch_tile_dt<4>(a, kind, s, q); break;
+        case 8: ok = launch_tile_dt<8>(a, kind, s, q); break;
     }
     if (!ok) return SMMD_EINVAL;
     return last_launch_status();

@@ -4,55 +4,18 @@
 // Reference: gan/core/ops.py:228-233 (squared_norm_jacobian),
 // gan/core/model.py:366-403 (add_scaling), gan/core/smmd.py:21-23, :40-42
 // (apply_scaling), gan/core/model.py:444-468 (clip_by_norm + Adam).
+#include "smmd_scale_dev.hpp"
 #include "smmd_sn_tile.hpp"
 
 #include <stdlib.h>
 
 namespace smmd {
 
-constexpr int SQ_CHUNK = 4096;   // floats per block of the squared-norm pass
-
-struct ScaledLossArgs {
-    const float *jac;
-    int64_t per_sample;
-    int nchunk, vec;
-    double *part;        // ws + 256: [rows * nchunk] partials
-    unsigned *counter;   // ws + 0: arrival ticket (zero at rest)
-    int n_cols, b, b_total, dof, variant, sqrt_scale;
-    const float *feat;
-    const float *base_loss;
-    float sc;
-    float *out;
-    float *per_sample_out;
-};
-
-__device__ void scaled_loss_final(const ScaledLossArgs &a);
-
-// ---- per-(row, chunk) partial sum of squares; the last block to arrive runs
-// the finalize (per-sample norms, J, nD, scale, losses) ---------------------
+// ---- the squared-norm pass; the last block to arrive runs the finalize
+// (per-sample norms, J, nD, scale, losses) ------------------------------------
 __global__ __launch_bounds__(256) void sqnorm_partial_kernel(ScaledLossArgs a) {
-    const float *__restrict__ jac = a.jac;
-    const int64_t per_sample = a.per_sample;
-    const int nchunk = a.nchunk, vec = a.vec;
-    const int row = blockIdx.x / nchunk, ch = blockIdx.x % nchunk;
-    const float *p = jac + (size_t)row * per_sample;
-    const int64_t b0 = (int64_t)ch * SQ_CHUNK;
-    const int64_t e0 = (b0 + SQ_CHUNK < per_sample) ? b0 + SQ_CHUNK : per_sample;
-    float acc = 0.f;
-    if (vec) {
-        for (int64_t i = b0 + threadIdx.x * 4; i < e0; i += 1024) {
-            const float4 x = *reinterpret_cast<const float4 *>(p + i);
-            acc = fmaf(x.x, x.x, acc);
-            acc = fmaf(x.y, x.y, acc);
-            acc = fmaf(x.z, x.z, acc);
-            acc = fmaf(x.w, x.w, acc);
-        }
-    } else {
-        for (int64_t i = b0 + threadIdx.x; i < e0; i += 256) acc = fmaf(p[i], p[i], acc);
-    }
-    __shared__ double red[4];
+    const double s = sqnorm_block(a, blockIdx.x);
     __shared__ int last;
-    const double s = block_sum<4>((double)acc, red);
     if (threadIdx.x < 64) {      // wave 0: publish the partial write-through, then the ticket
         if (threadIdx.x == 0) store_wt(a.part + blockIdx.x, s);
         const int l = wave_ticket(a.counter, gridDim.x);
@@ -61,58 +24,8 @@ __global__ __launch_bounds__(256) void sqnorm_partial_kernel(ScaledLossArgs a) {
     __syncthreads();
     if (!last) return;
     acquire_block();
-    scaled_loss_final(a);
+    scaled_loss_final(a, a.base_loss ? a.base_loss[0] : 0.f);
     ticket_reset(a.counter);
-}
-
-// ---- finalize: per-sample norms, J, nD, scale, losses (one 256-thread block;
-// partials summed in fixed order) --------------------------------------------
-__device__ void scaled_loss_final(const ScaledLossArgs &a) {
-    const double *__restrict__ part = a.part;
-    const int n_cols = a.n_cols, b = a.b, b_total = a.b_total, nchunk = a.nchunk;
-    const float *feat = a.feat;
-    const int dof = a.dof, variant = a.variant, sqrt_scale = a.sqrt_scale;
-    const float *base_loss = a.base_loss;
-    const float sc = a.sc;
-    float *out = a.out, *per_sample_out = a.per_sample_out;
-    __shared__ double red[4];
-    double jsum = 0.0;
-    for (int s = threadIdx.x; s < b; s += 256) {
-        double ps = 0.0;
-        for (int c = 0; c < n_cols; ++c) {          // ops.py:232 sum over columns
-            const double *q = part + ((size_t)c * b + s) * nchunk;
-            double t = 0.0;
-            for (int k = 0; k < nchunk; ++k) t += q[k];
-            ps += t;
-        }
-        if (per_sample_out) per_sample_out[s] = (float)ps;
-        jsum += ps;
-    }
-    jsum = block_sum<4>(jsum, red);
-    double nd = 0.0;
-    if (variant == 1 && feat) {
-        double fs = 0.0;
-        for (int i = threadIdx.x; i < b * dof; i += 256) fs += (double)feat[i] * (double)feat[i];
-        fs = block_sum<4>(fs, red);
-        nd = fs / ((double)b_total * dof);              // model.py:385
-    }
-    if (threadIdx.x == 0) {
-        const float J = (float)(jsum / (double)b_total); // model.py:384
-        const float nD = (float)nd;
-        const float q = (variant == 1) ? (J + nD) : J;  // model.py:387-390
-        const float scale = 1.f / (sc * q + 1.f);
-        const float base = base_loss ? base_loss[0] : 0.f;
-        const float f = sqrt_scale ? sqrtf(scale) : scale;   // smmd.py:22 / :41
-        const float g = base * f;
-        out[0] = g;
-        out[1] = -g;
-        out[2] = scale;
-        out[3] = J;
-        out[4] = nD;
-        out[5] = base;
-        out[6] = 0.f;
-        out[7] = 0.f;
-    }
 }
 
 // ---- backward: d base, d jac, d feat ---------------------------------------
@@ -127,11 +40,20 @@ __global__ void scaled_loss_finalize_kernel(float *out, float sc, int variant, i
     }
 }
 
+// Optional MMD part (the fused SMMD loss, smmd_smmd_loss_bwd): base = mmd2,
+// so dX, dY = (g_mmd2 + go f) * the forward's unit gradients gxu, gyu.
+struct MmdBwdPart {
+    const float *g_mmd2;           // upstream gradient of the mmd2 output (may be null)
+    const float *gxu, *gyu;        // d mmd2 / dX, dY of the forward
+    int64_t nx, ny;
+    float *dX, *dY;
+};
+
 __global__ __launch_bounds__(256) void scaled_loss_bwd_kernel(
     const float *__restrict__ jac, int64_t n_jac, int b, const float *__restrict__ feat,
     int64_t n_feat, int dof, const float *fwd_out, float sc, int variant, int sqrt_scale,
     const float *g_loss_grad, float *d_base, float *__restrict__ gjac, float *__restrict__ gfeat,
-    int vec) {
+    int vec, MmdBwdPart mp) {
     const float go = g_loss_grad ? g_loss_grad[0] : 1.f;
     const float scale = fwd_out[2];
     const float base = fwd_out[5];
@@ -142,7 +64,14 @@ __global__ __launch_bounds__(256) void scaled_loss_bwd_kernel(
     const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const size_t nth = (size_t)gridDim.x * blockDim.x;
     if (tid == 0 && d_base) d_base[0] = go * f;
-    if (vec) {
+    if (mp.dX) {
+        const float dm = (mp.g_mmd2 ? mp.g_mmd2[0] : 0.f) + go * f;
+        for (size_t i = tid; i < (size_t)mp.nx; i += nth) mp.dX[i] = mp.gxu[i] * dm;
+        for (size_t i = tid; i < (size_t)mp.ny; i += nth) mp.dY[i] = mp.gyu[i] * dm;
+    }
+    if (!gjac) {
+        // no Jacobian gradient wanted (a generator step: jac is a constant)
+    } else if (vec) {
         const int64_t n4 = n_jac / 4;
         for (size_t i = tid; i < (size_t)n4; i += nth) {
             const float4 x = reinterpret_cast<const float4 *>(jac)[i];
@@ -442,7 +371,7 @@ extern "C" {
 size_t smmd_scaled_loss_workspace_bytes(int rows, int64_t per_sample) {
     if (rows < 1 || per_sample < 1) return 0;
     const int64_t nchunk = (per_sample + SQ_CHUNK - 1) / SQ_CHUNK;
-    return 256 + align_up((size_t)rows * nchunk * sizeof(double), 256);   // ticket + partials
+    return SQ_WS_HEADER + align_up((size_t)rows * nchunk * sizeof(double), 256);   // tickets + partials
 }
 
 smmd_status smmd_scaled_loss_fwd(const float *jac, int n_cols, int b, int b_total,
@@ -466,7 +395,7 @@ smmd_status smmd_scaled_loss_fwd(const float *jac, int n_cols, int b, int b_tota
     // ticket first, at a fixed offset: a cached workspace reused for fewer rows
     // must not find its counter inside an earlier call's partials
     a.counter = (unsigned *)ws;
-    a.part = (double *)((char *)ws + 256);
+    a.part = (double *)((char *)ws + SQ_WS_HEADER);
     a.n_cols = n_cols;
     a.b = b;
     a.b_total = b_total;
@@ -478,6 +407,7 @@ smmd_status smmd_scaled_loss_fwd(const float *jac, int n_cols, int b, int b_tota
     a.sc = sc;
     a.out = out;
     a.per_sample_out = per_sample_out;
+    a.nblocks = rows * nchunk;
     hipLaunchKernelGGL(sqnorm_partial_kernel, dim3(rows * nchunk), dim3(256), 0,
                        (hipStream_t)stream, a);
     return last_launch_status();
@@ -504,9 +434,44 @@ smmd_status smmd_scaled_loss_bwd(const float *jac, int n_cols, int b, int b_tota
     int64_t blocks = (n_jac / 4 + 255) / 256;
     if (blocks > 4096) blocks = 4096;
     if (blocks < 1) blocks = 1;
+    MmdBwdPart mp;
+    memset(&mp, 0, sizeof(mp));
     hipLaunchKernelGGL(scaled_loss_bwd_kernel, dim3((unsigned)blocks), dim3(256), 0,
                        (hipStream_t)stream, jac, n_jac, b_total, feat, (int64_t)b * (dof > 0 ? dof : 0),
-                       dof, fwd_out, sc, variant, sqrt_scale, g_loss_grad, d_base, gjac, gfeat, vec);
+                       dof, fwd_out, sc, variant, sqrt_scale, g_loss_grad, d_base, gjac, gfeat, vec,
+                       mp);
+    return last_launch_status();
+}
+
+smmd_status smmd_smmd_loss_bwd(const float *jac, int n_cols, int b, int64_t per_sample,
+                               const float *feat, int dof, const float *fwd_out, float sc,
+                               int variant, int sqrt_scale, const float *g_loss_grad,
+                               const float *g_mmd2_grad, const float *gx_unit, int m,
+                               const float *gy_unit, int n, int d, float *gjac, float *gfeat,
+                               float *dX, float *dY, smmd_stream_t stream) {
+    if (!jac || !fwd_out || !g_loss_grad || n_cols < 1 || b < 1 || per_sample < 1)
+        return SMMD_EINVAL;
+    if (!gx_unit || !gy_unit || !dX || !dY || m < 1 || n < 1 || d < 1) return SMMD_EINVAL;
+    if (variant != 0 && variant != 1) return SMMD_EINVAL;
+    if (variant == 1 && gfeat && (!feat || dof < 1)) return SMMD_EINVAL;
+    const int64_t n_jac = (int64_t)n_cols * b * per_sample;
+    const int vec = ((uintptr_t)jac % 16 == 0) && ((uintptr_t)gjac % 16 == 0);
+    // without gjac (a generator step) only the small dX / dY loops run
+    int64_t blocks = gjac ? (n_jac / 4 + 255) / 256 : ((int64_t)(m + n) * d + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    if (blocks < 1) blocks = 1;
+    MmdBwdPart mp;
+    mp.g_mmd2 = g_mmd2_grad;
+    mp.gxu = gx_unit;
+    mp.gyu = gy_unit;
+    mp.nx = (int64_t)m * d;
+    mp.ny = (int64_t)n * d;
+    mp.dX = dX;
+    mp.dY = dY;
+    hipLaunchKernelGGL(scaled_loss_bwd_kernel, dim3((unsigned)blocks), dim3(256), 0,
+                       (hipStream_t)stream, jac, n_jac, b, feat, (int64_t)b * (dof > 0 ? dof : 0),
+                       dof, fwd_out, sc, variant, sqrt_scale, g_loss_grad, nullptr, gjac, gfeat,
+                       vec, mp);
     return last_launch_status();
 }
 

@@ -28,7 +28,7 @@ SMMD_SN_MAX_LAYERS = 32
 SN_P1_READY = 1            # smmd_sn_power_iter_ex flag
 OPT_MAX_FUSED = 96         # tensors smmd_adam_flat_sn takes in one call
 SN_MAX_FUSED = 16          # SN layers smmd_adam_flat_sn takes in one call
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 KIND_RBF, KIND_RQ, KIND_DISTANCE, KIND_DOT = 0, 1, 2, 3
 
@@ -100,6 +100,11 @@ _SIGS = {
     'smmd_scaled_loss_fwd': (_I, [_P, _I, _I, _I, _I64, _P, _I, _P, _F, _I, _I, _P, _P, _P, _SZ,
                                   _P]),
     'smmd_scaled_loss_finalize': (_I, [_P, _F, _I, _I, _P]),
+    'smmd_smmd_loss_fwd': (_I, [ctypes.POINTER(KernelDesc), _P, _I, _P, _I, _I, _I, _P, _I, _I,
+                                _I64, _P, _I, _F, _I, _I, _P, _P, _P, _P, _P, _P, _P, _SZ, _P,
+                                _SZ, _P]),
+    'smmd_smmd_loss_bwd': (_I, [_P, _I, _I, _I64, _P, _I, _P, _F, _I, _I, _P, _P, _P, _I, _P, _I,
+                                _I, _P, _P, _P, _P, _P]),
     'smmd_scaled_loss_bwd': (_I, [_P, _I, _I, _I, _I64, _P, _I, _P, _F, _I, _I, _P, _P, _P, _P,
                                   _P]),
     'smmd_sn_workspace_bytes': (_SZ, [ctypes.POINTER(SnLayer), _I]),

@@ -210,6 +210,133 @@ def mmd2_fused(X, Y, kernel='rbf', biased=False, process_group=None, return_sums
 
 
 # ---------------------------------------------------------------------------
+# the SMMD loss in one launch: mmd2 and the scaled loss of one process (or a
+# tower), when the Jacobian of the scaling regulariser is already known as
+# mmd2 runs (model.set_tower_loss computes it ahead, ``pending_scale``)
+# ---------------------------------------------------------------------------
+TILE_MAX_ROWS = (16384 // 4 - 64) * 64      # csrc/smmd_kern.hpp TILE_MAX_RT * 64
+
+
+def fused_loss_path(m, n, d):
+    """smmd_smmd_loss_fwd applies: smmd_mmd2_fwd's 2-D tiled path
+    (csrc/smmd_mmd.hip use_tile) and SMMD_FUSED_LOSS not 0."""
+    if os.environ.get('SMMD_FUSED_LOSS', '1') == '0':
+        return False
+    if d > 8 or os.environ.get('SMMD_MMD_GRAM') == '1' or os.environ.get('SMMD_MMD_TILE') == '0':
+        return False
+    return m + n <= TILE_MAX_ROWS
+
+
+class _SMMDLoss(torch.autograd.Function):
+    """(mmd2, g_loss = mmd2 * scale) of one launch (smmd_smmd_loss_fwd) and
+    their joint backward (smmd_smmd_loss_bwd)."""
+
+    @staticmethod
+    def forward(ctx, X, Y, jac, feat, spec, biased, sc, variant):
+        X = _features(X)
+        Y = _features(Y)
+        _lib.require_cuda(jac, feat)
+        jac = jac.contiguous()
+        feat_c = feat.contiguous() if feat is not None else None
+        dev = X.device
+        L = _lib.lib()
+        m, n, d = X.shape[0], Y.shape[0], X.shape[1]
+        n_cols, b = jac.shape[0], jac.shape[1]
+        per = jac[0, 0].numel()
+        dof = feat_c.shape[1] if feat_c is not None else 0
+        sums = torch.empty(8, device=dev, dtype=torch.float32)
+        mm = torch.empty(1, device=dev, dtype=torch.float32)
+        gx = torch.empty((m, d), device=dev, dtype=torch.float32)
+        gy = torch.empty((n, d), device=dev, dtype=torch.float32)
+        out = torch.empty(8, device=dev, dtype=torch.float32)
+        per_sample = torch.empty(b, device=dev, dtype=torch.float32)
+        ws = _lib.workspace('mmd2', L.smmd_mmd2_workspace_bytes(m, n, d), dev)
+        lws = _lib.workspace('scaled_loss', L.smmd_scaled_loss_workspace_bytes(n_cols * b, per),
+                             dev)
+        with _lib.timed('smmd_smmd_loss_fwd'):
+            st = L.smmd_smmd_loss_fwd(
+                spec.desc(), _lib.ptr(X), m, _lib.ptr(Y), n, d, 1 if biased else 0,
+                _lib.ptr(jac), n_cols, b, per, _lib.ptr(feat_c), dof, float(sc), variant, 0,
+                _lib.ptr(sums), _lib.ptr(mm), _lib.ptr(gx), _lib.ptr(gy), _lib.ptr(out),
+                _lib.ptr(per_sample), _lib.ptr(ws), ws.numel(), _lib.ptr(lws), lws.numel(),
+                _lib.stream_handle(dev))
+        _lib.check(st, 'smmd_smmd_loss_fwd')
+        ctx.save_for_backward(gx, gy, jac, feat_c, out)
+        ctx.cfg = (n_cols, b, per, dof, float(sc), variant, m, n, d)
+        ctx.mark_non_differentiable(sums, out)
+        return mm.view(()), out[0].view(()), sums, out
+
+    @staticmethod
+    def backward(ctx, g_mmd, g_loss, g_sums, g_out):
+        gx, gy, jac, feat, out = ctx.saved_tensors
+        n_cols, b, per, dof, sc, variant, m, n, d = ctx.cfg
+        dev = gx.device
+        go = (g_loss.reshape(1).contiguous().to(torch.float32) if g_loss is not None
+              else torch.zeros(1, device=dev, dtype=torch.float32))
+        gm = g_mmd.reshape(1).contiguous().to(torch.float32) if g_mmd is not None else None
+        dX, dY = torch.empty_like(gx), torch.empty_like(gy)
+        gjac = torch.empty_like(jac) if ctx.needs_input_grad[2] else None
+        gfeat = (torch.empty_like(feat) if (feat is not None and variant == 1
+                                            and ctx.needs_input_grad[3]) else None)
+        with _lib.timed('smmd_smmd_loss_bwd'):
+            st = _lib.lib().smmd_smmd_loss_bwd(
+                _lib.ptr(jac), n_cols, b, per, _lib.ptr(feat), dof, _lib.ptr(out), sc, variant, 0,
+                _lib.ptr(go), _lib.ptr(gm), _lib.ptr(gx), m, _lib.ptr(gy), n, d, _lib.ptr(gjac),
+                _lib.ptr(gfeat), _lib.ptr(dX), _lib.ptr(dY), _lib.stream_handle(dev))
+        _lib.check(st, 'smmd_smmd_loss_bwd')
+        if feat is not None and gfeat is None and ctx.needs_input_grad[3]:
+            gfeat = torch.zeros_like(feat)
+        return dX, dY, gjac, gfeat, None, None, None, None
+
+
+class ScalePending:
+    """The scaling regulariser's inputs known before ``set_loss`` runs (the
+    Jacobian columns of the real batch, the critic output for nD): the first
+    mmd2 of a KernelMatrices inside ``pending_scale(p)`` then runs fused with
+    the scaled loss, leaving (mmd2, g_loss, aux) in ``p.result`` for
+    ``add_scaling`` to pick up."""
+
+    def __init__(self, jac, feat, sc, variant, fuse=True):
+        self.jac, self.feat, self.sc = jac, feat, sc
+        self.variant = {'grad': 0, 'value_and_grad': 1}[variant]
+        self.fuse = fuse          # False: only the Jacobian is provided ahead
+        self.result = None
+
+
+class pending_scale:
+    def __init__(self, pending):
+        self.pending = pending
+
+    def __enter__(self):
+        self.prev = getattr(_scope, 'pending', None)
+        _scope.pending = self.pending
+        return self
+
+    def __exit__(self, *a):
+        _scope.pending = self.prev
+        return False
+
+
+def current_pending():
+    return getattr(_scope, 'pending', None)
+
+
+def _mmd2_scaled(K, biased, p):
+    """mmd2 of K fused with the pending scaled loss, or None when it does not apply."""
+    X, Y = K.X, K.Y
+    if X.dim() == 1 or Y.dim() == 1 or X.shape[1] != Y.shape[1]:
+        return None
+    if not fused_loss_path(X.shape[0], Y.shape[0], X.shape[1]):
+        return None
+    feat = p.feat if p.variant == 1 else None
+    if p.variant == 1 and feat is None:
+        return None
+    val, g, _, out = _SMMDLoss.apply(X, Y, p.jac, feat, K.spec, bool(biased), p.sc, p.variant)
+    p.result = (val, g, out)
+    return val
+
+
+# ---------------------------------------------------------------------------
 # materialised kernel matrices (tuple API)
 # ---------------------------------------------------------------------------
 class _KernelMatrix(torch.autograd.Function):
@@ -390,6 +517,11 @@ def mmd2(K, biased=False):
     """gan/core/mmd.py:194-196.  A KernelMatrices argument takes the fused
     path; an explicit 4-tuple of matrices is reduced as given."""
     if isinstance(K, KernelMatrices):
+        p = current_pending()
+        if p is not None and p.fuse and p.result is None and current_loss_group() is None:
+            val = _mmd2_scaled(K, biased, p)
+            if val is not None:
+                return val
         return mmd2_fused(K.X, K.Y, K.spec, biased, process_group=current_loss_group(),
                           exchange=current_exchange())
     K_XX, K_XY, K_YY, const_diagonal = K

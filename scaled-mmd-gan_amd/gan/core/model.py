@@ -199,12 +199,36 @@ class MMD_GAN:
         # mode, and one all-gather carries the features and the scale's partials
         grp = self._loss_group()
         self._ex = self._prepare_exchange(grp) if grp is not None else None
+        pend = self._prepare_scale() if grp is None else None
         try:
-            with mmd.loss_group(grp, self._ex):
+            with mmd.loss_group(grp, self._ex), mmd.pending_scale(pend):
                 self.set_loss(self.d_G, self.d_images)
         finally:
             self._ex = None
+        # the loss ran as ONE launch (smmd_smmd_loss_fwd)
+        self.fused_loss = pend is not None and pend.result is not None
         return self.g_loss, self.d_loss, self.aux
+
+    def _scaling_ahead(self):
+        c = self.config
+        return (getattr(c, 'with_scaling', False) and not getattr(c, 'use_gaussian_noise', False)
+                and c.scaling_variant in ('grad', 'value_and_grad'))
+
+    def _prepare_scale(self):
+        """One process (or a tower): the Jacobian of the scaling regulariser
+        computed BEFORE set_loss, so the loss's mmd2 runs in one launch with
+        the scaled loss (mmd.ScalePending, csrc smmd_smmd_loss_fwd) when
+        apply_scaling is SMMD's own; add_scaling uses the same Jacobian
+        otherwise."""
+        if not self._scaling_ahead():
+            return None
+        need = self._need_critic_grad
+        jac = ops.jacobian_columns(self.d_images, self.images, create_graph=need)
+        feat = self.d_images
+        if not need:
+            jac, feat = jac.detach(), feat.detach()
+        return mmd.ScalePending(jac, feat, self.sc, self.config.scaling_variant,
+                                fuse=self._fused_scaling() == 'mul')
 
     def _prepare_exchange(self, grp):
         """The all-gather mode's StepExchange: with the scaling regulariser on
@@ -292,9 +316,19 @@ class MMD_GAN:
             raise ValueError('scaling_variant must be grad or value_and_grad (model.py:387-390)')
         need = self._need_critic_grad
         ex, pre = getattr(self, '_ex', None), None
+        pend = mmd.current_pending()
+        fused = self._fused_scaling()
+        if (pend is not None and pend.result is not None and fused == 'mul'
+                and self.g_loss is pend.result[0]):
+            # set_loss's mmd2 ran fused with this very scaling (one launch)
+            _, self.g_loss, self.aux = pend.result
+            self.d_loss = -self.g_loss
+            return
         if ex is not None and ex.jac is not None:
             jac, feat = ex.jac, ex.feat            # computed ahead (_prepare_exchange)
             pre = ex.stats_total                    # None if no mmd2 gathered them
+        elif pend is not None:
+            jac, feat = pend.jac, pend.feat        # computed ahead (_prepare_scale)
         else:
             if getattr(c, "use_gaussian_noise", False):
                 x_hat_data = (torch.randn(self.images.shape, device=self.device) * 10.0) \
@@ -306,7 +340,6 @@ class MMD_GAN:
             if not need:
                 jac = jac.detach()
             feat = x_hat if need else x_hat.detach()
-        fused = self._fused_scaling()
         if fused is not None:
             self.g_loss, self.aux = ops.scaled_loss(
                 self.g_loss, jac, feat, sc=self.sc, variant=c.scaling_variant,

@@ -111,6 +111,27 @@ class FakeLib:
             _arr(gfeat, b * dof)[:] = cq * 2.0 / (b_total * dof) * _arr(feat, b * dof)
         return 0
 
+    def smmd_smmd_loss_fwd(self, desc, X, m, Y, n, d, biased, jac, n_cols, b, per, feat, dof, sc,
+                           variant, sqrt_scale, sums, mm, gx, gy, out, per_sample, ws, wsb, lws,
+                           lwsb, stream):
+        self.smmd_mmd2_fwd(desc, X, m, Y, n, d, biased, 0, m, 0, n, sums, mm, gx, gy, ws, wsb,
+                           stream)
+        return self.smmd_scaled_loss_fwd(jac, n_cols, b, b, per, feat, dof, mm, sc, variant,
+                                         sqrt_scale, out, per_sample, lws, lwsb, stream)
+
+    def smmd_smmd_loss_bwd(self, jac, n_cols, b, per, feat, dof, fwd, sc, variant, sqrt_scale, go,
+                           gm, gx, m, gy, n, d, gjac, gfeat, dX, dY, stream):
+        o = _arr(fwd, 8).astype(np.float64)
+        f = np.sqrt(o[2]) if sqrt_scale else o[2]
+        g = float(_arr(go, 1)[0])
+        dm = (float(_arr(gm, 1)[0]) if _arr(gm, 1) is not None else 0.0) + g * f
+        _arr(dX, m * d)[:] = _arr(gx, m * d) * dm
+        _arr(dY, n * d)[:] = _arr(gy, n * d) * dm
+        if _arr(gjac, 1) is not None:
+            self.smmd_scaled_loss_bwd(jac, n_cols, b, b, per, feat, dof, fwd, sc, variant,
+                                      sqrt_scale, go, None, gjac, gfeat, stream)
+        return 0
+
     def smmd_opt_workspace_bytes(self, offs, n):
         return 256
 

@@ -623,6 +623,72 @@ def test_scaled_loss_batch256_vs_oracle(dev, variant):
         _grad_close(ft.grad.cpu().numpy(), coefq * 2.0 / b * feat.astype(np.float64), 'd feat')
 
 
+@pytest.mark.parametrize('kernel,variant,b,both', [
+    ('rbf', 'grad', 64, False), ('rbf', 'value_and_grad', 64, False), ('rbf', 'grad', 64, True),
+    ('mix_rq_dot', 'grad', 32, False), ('mix_rbf', 'value_and_grad', 24, True),
+    ('tanh_mix_rq', 'value_and_grad', 16, False), ('distance', 'grad', 20, False),
+    ('rbf', 'grad', 256, False)])
+def test_smmd_loss_fused_vs_oracle(dev, kernel, variant, b, both):
+    """The SMMD loss in one launch (smmd_smmd_loss_fwd / _bwd, through
+    mmd.pending_scale + mmd.mmd2 as set_tower_loss runs it): mmd2, J, scale,
+    g_loss = mmd2 * scale and the gradients w.r.t. the features (X = d_G, Y =
+    d_images, which is also nD's feature) and the Jacobian, against the float64
+    oracle (smmd.py:10-23, model.py:366-403).  ``both``: mmd2 and g_loss both
+    feed the backward."""
+    from gan.core import mmd
+    rng = np.random.default_rng(31 + b)
+    X = rng.standard_normal((b, 1)).astype(np.float32)
+    Y = (rng.standard_normal((b, 1)) * 0.7 + 0.3).astype(np.float32)
+    jac = rng.standard_normal((1, b, 3, 16, 16)).astype(np.float32) * 0.05
+    Xt = torch.tensor(X, device=dev, requires_grad=True)
+    Yt = torch.tensor(Y, device=dev, requires_grad=True)
+    jt = torch.tensor(jac, device=dev, requires_grad=True)
+    p = mmd.ScalePending(jt, Yt, 10.0, variant)
+    with mmd.pending_scale(p):
+        val = mmd.mmd2(mmd.get_kernel(kernel)(Xt, Yt))
+    assert p.result is not None and p.result[0] is val
+    _, g, out = p.result
+    spec = O.kernel_spec(kernel)
+    mm = O.mmd2(spec, X, Y)
+    J = np.mean(O.squared_norm_per_sample(jac[0]))
+    nD = np.mean(Y.astype(np.float64) ** 2)
+    sc_ = O.scale_factor(J, 10.0, nD, variant)
+    _close(val.item(), mm, 1e-5, 1e-4, 'mmd2')
+    _close(out[3].item(), J, 0, 1e-5, 'J')
+    _close(out[2].item(), sc_, 0, 1e-5, 'scale')
+    _close(g.item(), mm * sc_, 1e-6, 1e-4, 'g_loss')
+    (g + val if both else g).backward()
+    dX, dY = O.mmd2_grad(spec, X, Y)
+    w = sc_ + (1.0 if both else 0.0)
+    coefq = mm * (-10.0 * sc_ ** 2)
+    gy_ref = w * dY
+    if variant == 'value_and_grad':
+        gy_ref = gy_ref + coefq * 2.0 / b * Y.astype(np.float64)
+    _grad_close(Xt.grad.cpu().numpy(), w * dX, 'dX')
+    _grad_close(Yt.grad.cpu().numpy(), gy_ref, 'dY')
+    _grad_close(jt.grad.cpu().numpy(), coefq * 2.0 / b * jac.astype(np.float64), 'd jac')
+
+
+def test_smmd_loss_fused_without_jacobian_grad(dev):
+    """A generator step: the Jacobian is a constant, so the backward writes
+    only the feature gradients (gjac NULL) and they are the same."""
+    from gan.core import mmd
+    rng = np.random.default_rng(5)
+    X = rng.standard_normal((64, 1)).astype(np.float32)
+    Y = rng.standard_normal((64, 1)).astype(np.float32)
+    jac = rng.standard_normal((1, 64, 3, 8, 8)).astype(np.float32) * 0.1
+    grads = []
+    for need in (True, False):
+        Xt = torch.tensor(X, device=dev, requires_grad=True)
+        jt = torch.tensor(jac, device=dev, requires_grad=need)
+        p = mmd.ScalePending(jt, None, 10.0, 'grad')
+        with mmd.pending_scale(p):
+            mmd.mmd2(mmd._rbf_kernel(Xt, torch.tensor(Y, device=dev)))
+        p.result[1].backward()
+        grads.append(Xt.grad.clone())
+    assert torch.equal(grads[0], grads[1])
+
+
 def test_scaled_loss_workspace_reuse(dev):
     """The squared-norm pass elects its finalizing block by a ticket at a fixed
     offset of the cached workspace; calls with fewer rows reuse the buffer

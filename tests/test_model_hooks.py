@@ -94,6 +94,9 @@ def test_apply_scaling_override_matches_fused(fake):
     assert a._fused_scaling() == 'mul' and b._fused_scaling() is None
     ga, da, *_ = one_critic_loss(a)
     gb, db, *_ = one_critic_loss(b)
+    # SMMD's own apply_scaling: mmd2 and the scaled loss in one launch
+    # (smmd_smmd_loss_fwd); the override: mmd2, then scale, then its product
+    assert a.fused_loss and not b.fused_loss
     assert float(gb) == pytest.approx(float(ga), rel=1e-6, abs=1e-9)
     assert float(b.seen_scale) == pytest.approx(float(a.aux[2]), rel=1e-6)
     for x, y in zip(critic_grads(a, da), critic_grads(b, db)):
