@@ -57,7 +57,7 @@ PMC_FALLBACK = os.path.join(ROOT, 'profiles', 'r05', 'pmc_traffic.json')
 # the hot-path rows a1-a9 and the library entry points that
 # implement them (the roofline kernel is chosen among these)
 HOT_PATH = ('smmd_mmd2_fwd', 'smmd_scaled_loss_fwd', 'smmd_scaled_loss_bwd',
-            'smmd_smmd_loss_fwd', 'smmd_smmd_loss_bwd',
+            'smmd_smmd_loss_fwd', 'smmd_smmd_loss_bwd', 'smmd_sn_grad_stats',
             'smmd_sn_power_iter', 'smmd_sn_weight_bwd', 'smmd_adam_flat[D]',
             'smmd_adam_flat[G]', 'smmd_adam_flat_sn[D]', 'smmd_adam_flat_sn[G]')
 
@@ -675,14 +675,23 @@ def main():
         # pool-folded 4 x 4 filter the bank writes directly (16 floats per 9)
         sn_out = sum(e.N * e.K * 16 // 9 if e.fold else e.N * e.K for e in model.sn_D.entries)
         per_img = 3 * size * size
+        gdirect = model._gdirect()
+        adam_sn_d = model.d_optim.numel * 4 * 8
+        if gdirect:
+            # G-direct: the SN weights' gradient is never formed: no norm-pass
+            # read of it; the update reads G (W_eff's or W''s size) + p, m, v
+            # and writes p, m, v; every other tensor as the plain update
+            adam_sn_d = (model.d_optim.numel - sn_kn) * 4 * 8 + sn_kn * 4 * 6 + sn_out * 4
         alg = {
             # sqsum pass reads g; update pass reads g, p, m, v and writes p, m, v
             'smmd_adam_flat[D]': model.d_optim.numel * 4 * 8,
             'smmd_adam_flat[G]': model.g_optim.numel * 4 * 8,
             # the same update with the SN weights' first power-iteration pass
             # folded in (its column-partial writes are < 0.1 % of these bytes)
-            'smmd_adam_flat_sn[D]': model.d_optim.numel * 4 * 8,
+            'smmd_adam_flat_sn[D]': adam_sn_d,
             'smmd_adam_flat_sn[G]': model.g_optim.numel * 4 * 8,
+            # the G-direct backward: one read of G and of W
+            'smmd_sn_grad_stats': (sn_out + sn_kn) * 4,
             # one read of W + one write of W_eff (2 K N 4 B per
             # iteration; the folded filters' 16 / 9 larger output for ConvMeanPool)
             'smmd_sn_power_iter': (sn_kn + sn_out) * 4,
@@ -726,7 +735,8 @@ def main():
                         'traffic': traffic, 'traffic_source': src,
                         'avg_ms': kernels[dom]['avg_ms'],
                         'algorithmic_bytes': kernels[dom]['bytes']}
-        for k in ('smmd_sn_power_iter', 'smmd_sn_weight_bwd', 'smmd_adam_flat_sn[D]',
+        for k in ('smmd_sn_power_iter', 'smmd_sn_weight_bwd', 'smmd_sn_grad_stats',
+                  'smmd_adam_flat_sn[D]',
                   'smmd_scaled_loss_fwd', 'smmd_scaled_loss_bwd', 'smmd_smmd_loss_fwd',
                   'smmd_smmd_loss_bwd', 'smmd_fold_pool_weights'):
             if k in kernels and 'bytes' in kernels[k]:

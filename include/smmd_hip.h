@@ -62,7 +62,8 @@ int smmd_abi_version(void);         /* bumped on any ABI change (2: Gram/poly,
                                        5: smmd_conv3x3_thin*,
                                        6: smmd_mask_pool2*, smmd_up_add,
                                        smmd_bn_relu_fwd, 7: smmd_smmd_loss_fwd/bwd,
-                                       smmd_source_hash) */
+                                       smmd_source_hash, smmd_sn_grad_stats,
+                                       smmd_adam_flat_sn2) */
 const char *smmd_source_hash(void); /* first 16 hex digits of the SHA-256 of the
                                        sources this binary was built from
                                        (csrc .hip and .hpp files in byte order,
@@ -273,6 +274,17 @@ smmd_status smmd_sn_power_iter_ex(const smmd_sn_layer *layers, int n_layers,
 smmd_status smmd_sn_weight_bwd(const smmd_sn_layer *layers, int n_layers,
                                void *ws, size_t ws_bytes, smmd_stream_t stream);
 
+/* The backward WITHOUT forming dL/dW (the G-direct update, one process):
+ * from G (layers[].G, dL/dW_eff or dL/dW' of a fold layer) and W it reduces
+ * d = <G, W> (the sums and order of smmd_sn_weight_bwd), ||G||^2 and
+ * u'^T G v, writes gs = d / sigma (layers[].gs, may be NULL) and keeps per
+ * layer in ws the record {coef = s d / sigma^2, ||dL/dW||^2 (analytic:
+ * (s/sigma)^2 ||G||^2 - 2 (s/sigma) coef u'^T G v + coef^2 ||u'||^2 ||v||^2),
+ * sigma, s} that smmd_adam_flat_sn2 with SMMD_ADAM_SN_GDIRECT reads.  G must
+ * stay alive (unchanged) until that update has run. */
+smmd_status smmd_sn_grad_stats(const smmd_sn_layer *layers, int n_layers,
+                               void *ws, size_t ws_bytes, smmd_stream_t stream);
+
 /* ---------------------------------------------------------------------------
  * Materialised kernel matrix K(A, B) [na, nb] (row-major) and its backward
  * (gA = dL/dA, gB = dL/dB from G = dL/dK; either output may be NULL).
@@ -337,6 +349,23 @@ smmd_status smmd_adam_flat_ex(float *param, const float *grad, float *m, float *
                               const smmd_sn_layer *layers, const int32_t *sn_tensor,
                               int n_layers, void *sn_ws, size_t sn_ws_bytes,
                               smmd_stream_t stream);
+
+/* smmd_adam_flat_sn and smmd_adam_flat_ex in one entry, with flags:
+ * lr_t != NULL reads the step size from that device scalar (graph replay;
+ * lr and step unused), else lr_t = lr sqrt(1 - b2^step) / (1 - b1^step).
+ * flags = SMMD_ADAM_SN_GDIRECT: the SN weights' gradients are NOT in grad:
+ * each is formed in the update from layers[].G / .fold / .v and the record
+ * smmd_sn_grad_stats left in sn_ws, dL/dW = (s G)/sigma - coef u' v^T, and
+ * clipped by the record's norm; the norm pass skips those tensors.  One read
+ * of G replaces dL/dW's write, its accumulation into grad and its two reads. */
+#define SMMD_ADAM_SN_GDIRECT 1
+smmd_status smmd_adam_flat_sn2(float *param, const float *grad, float *m, float *v,
+                               const int64_t *offsets, int n_tensors, float grad_scale,
+                               float clip_norm, float lr, float beta1, float beta2, float eps,
+                               int64_t step, const float *lr_t, void *ws, size_t ws_bytes,
+                               const smmd_sn_layer *layers, const int32_t *sn_tensor,
+                               int n_layers, void *sn_ws, size_t sn_ws_bytes, int flags,
+                               smmd_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * Polynomial-kernel MMD statistics of the KID scorer and the 3-sample LR

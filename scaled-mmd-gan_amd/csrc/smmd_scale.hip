@@ -135,6 +135,7 @@ __global__ __launch_bounds__(256) void opt_sqsum_kernel(OptTable t, const float 
                                                         float gscale, int vec,
                                                         double *__restrict__ part) {
     const int ti = opt_find(t, blockIdx.x);
+    if (t.skip[ti]) return;     // a tensor whose norm comes from elsewhere (G-direct SN)
     int64_t lo, hi;
     opt_range(t, ti, blockIdx.x, lo, hi);
     float acc0 = 0.f, acc1 = 0.f;
@@ -167,7 +168,7 @@ __global__ __launch_bounds__(256) void opt_sqsum_kernel(OptTable t, const float 
     }
     __shared__ double red[4];
     const double s = block_sum<4>((double)acc0 + (double)acc1, red);
-    if (threadIdx.x == 0) part[blockIdx.x] = s;
+    if (threadIdx.x == 0) part[t.sblk[ti] + (blockIdx.x - t.blk[ti])] = s;
 }
 
 __device__ __forceinline__ float clip_factor(const OptTable &t, int ti, const double *part,
@@ -283,11 +284,11 @@ __global__ __launch_bounds__(256) void opt_adam_kernel(OptTable t, AdamArgs a) {
 // one launch for a critic update with SN layers: the SN weight tiles first
 // (tile-shaped, with the next power iteration's P1), then the blocks of every
 // other tensor
-template <int H>
+template <int H, bool GD = false>
 __global__ __launch_bounds__(256) void opt_adam_sn_kernel(OptTable t, SnAdamTable st,
                                                           AdamArgs a) {
     if ((int)blockIdx.x < st.total_tiles)
-        sn_adam_tile<H>(st, blockIdx.x, adam_k(a), a.part, a.clip);
+        sn_adam_tile<H, GD>(st, blockIdx.x, adam_k(a), a.part, a.clip);
     else
         opt_adam_block(t, blockIdx.x - st.total_tiles, a);
 }
@@ -555,7 +556,7 @@ static smmd_status adam_flat_sn_impl(float *param, const float *grad, float *m, 
                                      float beta1, float beta2, float eps, void *ws,
                                      size_t ws_bytes, const smmd_sn_layer *layers,
                                      const int32_t *sn_tensor, int n_layers, void *sn_ws,
-                                     size_t sn_ws_bytes, hipStream_t s) {
+                                     size_t sn_ws_bytes, hipStream_t s, int gdirect = 0) {
     if (!param || !grad || !m || !v || !offsets || n_tensors < 1) return SMMD_EINVAL;
     if (!layers || !sn_tensor || n_layers < 1 || n_layers > SMMD_SN_MAX_LAYERS) return SMMD_EINVAL;
     if (n_tensors > OPT_MAX) return SMMD_EUNSUPPORTED;     // one partial slab for every tensor
@@ -568,7 +569,9 @@ static smmd_status adam_flat_sn_impl(float *param, const float *grad, float *m, 
         skip[ti] = 1;
     }
     OptTable ts, tu;
-    if (!build_opt(offsets, 0, n_tensors, OPT_SQ_CHUNK, ts) ||
+    // G-direct: the SN tensors' norms come from their grad-stats records, so
+    // the norm pass skips them too (their flat gradient is never formed)
+    if (!build_opt(offsets, 0, n_tensors, OPT_SQ_CHUNK, ts, gdirect ? skip : nullptr) ||
         !build_opt(offsets, 0, n_tensors, OPT_UP_CHUNK, tu, skip))
         return SMMD_EINVAL;
     const int vec = opt_vec(offsets, n_tensors, param, grad, m, v);
@@ -579,6 +582,7 @@ static smmd_status adam_flat_sn_impl(float *param, const float *grad, float *m, 
     h.grad = grad;
     h.offsets = offsets;
     h.sblk = ts.sblk;
+    h.gdirect = gdirect;
     SnAdamTable snt;
     const smmd_status r = sn_adam_table(layers, sn_tensor, n_layers, h, sn_ws, sn_ws_bytes, snt);
     if (r != SMMD_OK) return r;
@@ -590,6 +594,10 @@ static smmd_status adam_flat_sn_impl(float *param, const float *grad, float *m, 
     aa.lr_t_dev = lr_t_dev;
     const dim3 grid(snt.total_tiles + tu.total_blocks);
     const int hg = sn_adam_groups();
+    if (gdirect) {     // H = 2: the fold staging of H = 1 would not fit beside it
+        hipLaunchKernelGGL((opt_adam_sn_kernel<2, true>), grid, dim3(256), 0, s, tu, snt, aa);
+        return last_launch_status();
+    }
     if (hg == 1)
         hipLaunchKernelGGL(opt_adam_sn_kernel<1>, grid, dim3(256), 0, s, tu, snt, aa);
     else if (hg == 4)
@@ -627,6 +635,21 @@ smmd_status smmd_adam_flat_ex(float *param, const float *grad, float *m, float *
     return adam_flat_sn_impl(param, grad, m, v, offsets, n_tensors, grad_scale, clip_norm, 0.0,
                              lr_t, beta1, beta2, eps, ws, ws_bytes, layers, sn_tensor, n_layers,
                              sn_ws, sn_ws_bytes, (hipStream_t)stream);
+}
+
+smmd_status smmd_adam_flat_sn2(float *param, const float *grad, float *m, float *v,
+                               const int64_t *offsets, int n_tensors, float grad_scale,
+                               float clip_norm, float lr, float beta1, float beta2, float eps,
+                               int64_t step, const float *lr_t, void *ws, size_t ws_bytes,
+                               const smmd_sn_layer *layers, const int32_t *sn_tensor,
+                               int n_layers, void *sn_ws, size_t sn_ws_bytes, int flags,
+                               smmd_stream_t stream) {
+    if (flags & ~SMMD_ADAM_SN_GDIRECT) return SMMD_EINVAL;
+    if (!lr_t && step < 1) return SMMD_EINVAL;
+    return adam_flat_sn_impl(param, grad, m, v, offsets, n_tensors, grad_scale, clip_norm,
+                             lr_t ? 0.0 : adam_lr_t(lr, beta1, beta2, step), lr_t, beta1, beta2,
+                             eps, ws, ws_bytes, layers, sn_tensor, n_layers, sn_ws, sn_ws_bytes,
+                             (hipStream_t)stream, (flags & SMMD_ADAM_SN_GDIRECT) ? 1 : 0);
 }
 
 }  // extern "C"

@@ -73,7 +73,10 @@ __device__ __forceinline__ double sqnorm_block(const ScaledLossArgs &a, int blk)
 // partials summed in fixed order).  base: the loss being scaled. ------------
 constexpr int SQ_FIN_LDS = 2048;    // partials staged through LDS (16 KiB)
 
-__device__ __forceinline__ void scaled_loss_final(const ScaledLossArgs &a, float base) {
+// pre: the partials already staged in LDS by the caller (the fused loss
+// launch), or nullptr to load them here.
+__device__ __forceinline__ void scaled_loss_final(const ScaledLossArgs &a, float base,
+                                                  const double *pre = nullptr) {
     const double *__restrict__ part = a.part;
     const int n_cols = a.n_cols, b = a.b, b_total = a.b_total, nchunk = a.nchunk;
     const float *feat = a.feat;
@@ -83,7 +86,7 @@ __device__ __forceinline__ void scaled_loss_final(const ScaledLossArgs &a, float
     __shared__ double red[4];
     __shared__ double pl[SQ_FIN_LDS];
     const int tot = n_cols * b * nchunk;
-    const bool staged = tot <= SQ_FIN_LDS;
+    const bool staged = pre == nullptr && tot <= SQ_FIN_LDS;
     if (staged) {
         // every partial loaded with 8 loads in flight per thread (one memory
         // round trip for the configs' 64 x 3 partials), then summed from LDS
@@ -100,7 +103,7 @@ __device__ __forceinline__ void scaled_loss_final(const ScaledLossArgs &a, float
         }
         __syncthreads();
     }
-    const double *src = staged ? pl : part;
+    const double *src = pre ? pre : (staged ? pl : part);
     double jsum = 0.0;
     for (int s = threadIdx.x; s < b; s += 256) {
         double ps = 0.0;

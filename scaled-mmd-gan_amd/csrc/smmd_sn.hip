@@ -45,6 +45,9 @@ struct SnLayerDev {
     float *q2;       // ws [N][nctp] row partials, one contiguous 16-B aligned row per n
     float *ucur;     // ws [N]  u' of the last iteration
     float *dotp;     // ws [units] backward partial <G, W>
+    float *ggp;      // ws [units] partial ||G||^2 (adjoint G for fold layers)
+    float *ugvp;     // ws [units] partial u'^T G v
+    float *stats;    // ws [16] smmd_sn_grad_stats record (SnGradStats)
     int N, K, nrt, nct;
     int nctp;        // nct rounded up to a multiple of 4
     int tile_begin;
@@ -420,7 +423,12 @@ __device__ void sn_layer_epilogue(const SnTable &t, const SnLayerDev &L, int las
         L.ucur[n] = un;
         if (upd) L.u[n] = un;
     }
-    if (tid == 0) L.sigma[0] = (float)(uu / (double)nu);     // (v W) . u', sn.py:42
+    if (tid == 0) {
+        L.sigma[0] = (float)(uu / (double)nu);     // (v W) . u', sn.py:42
+        // ||v||^2 and ||u'||^2 for the G-direct clip norm (sn_gstat_r_kernel)
+        L.stats[4] = (float)(sa / ((double)nv * (double)nv));
+        L.stats[5] = (float)(uu / ((double)nu * (double)nu));
+    }
 }
 
 // R2: one 1024-thread block per layer runs the epilogue
@@ -566,6 +574,115 @@ __global__ __launch_bounds__(256) void sn_bwd_b_kernel(SnTable t) {
     }
 }
 
+// ---- gradient statistics for the G-direct update (smmd_sn_grad_stats) ------
+// Instead of writing dL/dW, the backward reduces what the optimizer needs to
+// form it on the fly from G (smmd_adam_flat_sn2, SMMD_ADAM_SN_GDIRECT):
+// d = <G, W> (the same partials and order as sn_bwd_a, so the same bits),
+// ||G||^2 and u'^T G v (G = the adjoint of G' on fold layers).  Then per
+// layer: gs = d / sigma, coef = s d / sigma^2 and the clip norm
+// ||dL/dW||^2 = a^2 ||G||^2 - 2 a coef u'^T G v + coef^2 ||u'||^2 ||v||^2
+// with a = s / sigma (dL/dW = a G - coef u' v^T).
+__global__ __launch_bounds__(256) void sn_gstat_a_kernel(SnTable t) {
+    const int unit = blockIdx.x;
+    const SnLayerDev L = t.L[find_unit_layer(t, unit)];
+    const int lt = unit - L.unit_begin;
+    __shared__ float red[4];
+    float ad = 0.f, ag = 0.f, au = 0.f;
+    if (L.fold) {
+        __shared__ float s9[SNF_T * 9];
+        __shared__ float s16[16 * SNF_S16];
+        const int64_t nf = (int64_t)L.N * L.nfc;
+        const int64_t q0 = (int64_t)lt * SNF_T;
+        const int nb = (int)min<int64_t>(SNF_T, nf - q0);
+        snf_load16(L.G + q0 * 16, s16, nb);
+        snf_load9(L.W + q0 * 9, s9, nb * 9);
+        const int f = threadIdx.x;
+        float un = 0.f, vk[9];
+        {
+            const int64_t q = q0 + (f < nb ? f : 0);
+            const int n = (int)(q / L.nfc), c = (int)(q - (int64_t)n * L.nfc);
+            un = L.ucur[n];
+#pragma unroll
+            for (int j = 0; j < 9; ++j) vk[j] = L.v[c * 9 + j];
+        }
+        __syncthreads();
+        if (f < nb) {
+            float g[9];
+            snf_adjoint(s16, f, g);
+            float gv = 0.f;
+#pragma unroll
+            for (int j = 0; j < 9; ++j) {
+                ad = fmaf(g[j], s9[f * 9 + j], ad);
+                ag = fmaf(g[j], g[j], ag);
+                gv = fmaf(g[j], vk[j], gv);
+            }
+            au = un * gv;
+        }
+    } else {
+        const int rt = lt / L.nct, ct = lt % L.nct;
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+        const int r0 = rt * SN_TR + w * SN_RPW;
+        const int c0 = ct * SN_TC + lane * 4;
+        float4 wt[SN_RPW], gt[SN_RPW];
+        load_tile(L.W, L.N, L.K, L.vec, r0, c0, wt);
+        load_tile(L.G, L.N, L.K, L.vec, r0, c0, gt);
+        float vv[4], uc[SN_RPW];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) vv[k] = (c0 + k < L.K) ? L.v[c0 + k] : 0.f;
+#pragma unroll
+        for (int i = 0; i < SN_RPW; ++i) uc[i] = (r0 + i < L.N) ? L.ucur[r0 + i] : 0.f;
+#pragma unroll
+        for (int i = 0; i < SN_RPW; ++i) {
+            ad = fmaf(gt[i].x, wt[i].x, ad);
+            ad = fmaf(gt[i].y, wt[i].y, ad);
+            ad = fmaf(gt[i].z, wt[i].z, ad);
+            ad = fmaf(gt[i].w, wt[i].w, ad);
+            ag = fmaf(gt[i].x, gt[i].x, ag);
+            ag = fmaf(gt[i].y, gt[i].y, ag);
+            ag = fmaf(gt[i].z, gt[i].z, ag);
+            ag = fmaf(gt[i].w, gt[i].w, ag);
+            const float gv = fmaf(gt[i].w, vv[3], fmaf(gt[i].z, vv[2],
+                                  fmaf(gt[i].y, vv[1], gt[i].x * vv[0])));
+            au = fmaf(uc[i], gv, au);
+        }
+    }
+    ad = block_sum<4>(ad, red);
+    ag = block_sum<4>(ag, red);
+    au = block_sum<4>(au, red);
+    if (threadIdx.x == 0) {
+        L.dotp[lt] = ad;
+        L.ggp[lt] = ag;
+        L.ugvp[lt] = au;
+    }
+}
+
+// one 64-thread block per layer: the layer sums in sn_bwd_b's order for d,
+// then the record {coef, ||dL/dW||^2, sigma, s} and gs
+__global__ __launch_bounds__(64) void sn_gstat_r_kernel(SnTable t) {
+    const SnLayerDev L = t.L[blockIdx.x];
+    const int lane = threadIdx.x;
+    const int units = layer_units(L);
+    double dd = wave_sum(strided_sum(L.dotp, lane, units, 64));
+    double gg = wave_sum(strided_sum(L.ggp, lane, units, 64));
+    double ug = wave_sum(strided_sum(L.ugvp, lane, units, 64));
+    if (lane == 0) {
+        const double vv = L.stats[4], uu = L.stats[5];   // ||v||^2, ||u'||^2 (refresh R2)
+        const float d = (float)dd;                       // layer_dot's value
+        const float sigma = L.sigma[0];
+        const float s = L.s ? L.s[0] : 1.f;
+        if (L.gs) L.gs[0] = d / sigma;                   // dL/ds, as sn_bwd_b
+        const float coef = (s * d) / (sigma * sigma);    // as sn_bwd_b
+        const double a = (double)s / (double)sigma;
+        double nsq = a * a * gg - 2.0 * a * (double)coef * ug +
+                     (double)coef * (double)coef * uu * vv;
+        if (!(nsq > 0.0)) nsq = 0.0;
+        L.stats[0] = coef;
+        L.stats[1] = (float)nsq;
+        L.stats[2] = sigma;
+        L.stats[3] = s;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // host side: workspace carve and launch sets
 // ---------------------------------------------------------------------------
@@ -586,6 +703,8 @@ static size_t layer_ws_bytes(int N, int K) {
     b += align_up((size_t)((nct + 3) & ~3) * N * 4, 256);   // q2
     b += align_up((size_t)N * 4, 256);         // ucur
     b += align_up((size_t)dotp_slots(N, K) * 4, 256);       // dotp
+    b += 2 * align_up((size_t)dotp_slots(N, K) * 4, 256);   // ggp, ugvp
+    b += 256;                                                // stats
     return b;
 }
 
@@ -638,6 +757,9 @@ static bool build_table(const smmd_sn_layer *layers, int first, int count, char 
         L.q2 = (float *)p;   p += align_up((size_t)L.nctp * L.N * 4, 256);
         L.ucur = (float *)p; p += align_up((size_t)L.N * 4, 256);
         L.dotp = (float *)p; p += align_up((size_t)dotp_slots(L.N, L.K) * 4, 256);
+        L.ggp = (float *)p;  p += align_up((size_t)dotp_slots(L.N, L.K) * 4, 256);
+        L.ugvp = (float *)p; p += align_up((size_t)dotp_slots(L.N, L.K) * 4, 256);
+        L.stats = (float *)p; p += 256;
         off += layer_ws_bytes(L.N, L.K);
     }
     t.total_tiles = tiles;
@@ -676,6 +798,19 @@ smmd_status sn_adam_table(const smmd_sn_layer *layers, const int32_t *sn_tensor,
         L.vec = (src.K % 4 == 0) && (al % 16 == 0);
         L.sb0 = a.sblk[ti];
         L.sb1 = a.sblk[ti + 1];
+        L.G = nullptr;
+        if (a.gdirect) {
+            // dL/dW formed from G and the smmd_sn_grad_stats record
+            if (!src.G || !src.v || (src.fold && (src.K % 9 != 0 || ((uintptr_t)src.G & 15))))
+                return SMMD_EINVAL;
+            L.G = src.G;
+            L.ucur = st.L[i].ucur;
+            L.vsn = src.v;
+            L.stats = st.L[i].stats;
+            L.fold = src.fold;
+            L.nfc = src.fold ? src.K / 9 : 0;
+            L.gvec = !src.fold && (src.K % 4 == 0) && ((uintptr_t)src.G % 16 == 0);
+        }
     }
     return SMMD_OK;
 }
@@ -727,6 +862,25 @@ smmd_status smmd_sn_power_iter_ex(const smmd_sn_layer *layers, int n_layers, int
         bool any_eff = false;
         for (int i = 0; i < count; ++i) any_eff |= (t.L[i].W_eff != nullptr);
         if (any_eff) hipLaunchKernelGGL(sn_p3_kernel, dim3(t.total_units), dim3(256), 0, s, t);
+        smmd_status st = last_launch_status();
+        if (st != SMMD_OK) return st;
+    }
+    return SMMD_OK;
+}
+
+smmd_status smmd_sn_grad_stats(const smmd_sn_layer *layers, int n_layers, void *ws,
+                               size_t ws_bytes, smmd_stream_t stream) {
+    if (!layers || n_layers < 1 || n_layers > SMMD_SN_MAX_LAYERS) return SMMD_EINVAL;
+    for (int i = 0; i < n_layers; ++i)
+        if (!layers[i].G || !layers[i].v || !layers[i].sigma) return SMMD_EINVAL;
+    if (!ws || ws_bytes < smmd_sn_workspace_bytes(layers, n_layers)) return SMMD_EWORKSPACE;
+    hipStream_t s = (hipStream_t)stream;
+    for (int first = 0; first < n_layers; first += SN_CHUNK) {
+        const int count = (n_layers - first < SN_CHUNK) ? n_layers - first : SN_CHUNK;
+        SnTable t;
+        if (!build_table(layers, first, count, (char *)ws + 256, t)) return SMMD_EINVAL;
+        hipLaunchKernelGGL(sn_gstat_a_kernel, dim3(t.total_units), dim3(256), 0, s, t);
+        hipLaunchKernelGGL(sn_gstat_r_kernel, dim3(t.n_layers), dim3(64), 0, s, t);
         smmd_status st = last_launch_status();
         if (st != SMMD_OK) return st;
     }

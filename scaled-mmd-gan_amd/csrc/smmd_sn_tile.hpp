@@ -137,6 +137,13 @@ struct SnAdamLayerDev {
     const float *u;
     float *p1;
     int N, K, nct, tile_begin, vec, sb0, sb1;
+    // G-direct (smmd_adam_flat_sn2 with SMMD_ADAM_SN_GDIRECT): dL/dW formed
+    // here from G = dL/dW_eff (or dL/dW' of a fold layer) and the layer's
+    // smmd_sn_grad_stats record {coef, ||dL/dW||^2, sigma, s}; G == nullptr:
+    // dL/dW read from the flat gradient
+    const float *G;
+    const float *ucur, *vsn, *stats;
+    int fold, nfc, gvec;
 };
 
 struct SnAdamTable {
@@ -149,7 +156,63 @@ struct SnAdamTable {
 // 8 rows of a wave go in H groups: H = 1 keeps all 32 float4 of p, g, m, v in
 // flight at once (155 VGPRs, 3 waves / SIMD), H = 2 halves the registers for
 // twice the occupancy.  Same arithmetic in the same order either way.
-template <int H>
+// G-direct: the adjoint of the fold, G[n][c][u][v] = 1/4 sum_{a,b}
+// G'[n][c][u+a][v+b] (smmd_sn.hip snf_adjoint's order), for this thread's 4
+// columns of its NR rows.  Each wave stages its rows' span of 4 x 4 filters
+// (<= 30 per 256 columns) through LDS: 16-byte loads, the whole span of the
+// NR rows in flight at once.
+constexpr int SNG_FMAX = 30;                     // filters touched by 256 columns
+
+template <int NR>
+__device__ __forceinline__ void sn_fold_adjoint(const SnAdamLayerDev &L, int ct, int r0, int c0,
+                                                float (*lds)[SNG_FMAX * 16], float4 (&gg)[NR]) {
+    const int lane = threadIdx.x & 63;
+    const int fa = (ct * SN_TC) / 9;
+    int fb = (ct * SN_TC + SN_TC - 1) / 9;
+    if (fb > L.nfc - 1) fb = L.nfc - 1;
+    const int n4 = (fb - fa + 1) * 4;            // float4 of one row's span
+    float4 x[NR][2];
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+        const int r = r0 + i;
+        const float4 *src = reinterpret_cast<const float4 *>(L.G + ((size_t)r * L.nfc + fa) * 16);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int q = lane + 64 * h;
+            x[i][h] = (r < L.N && q < n4) ? src[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
+    __syncthreads();                             // the previous group's reads are done
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int q = lane + 64 * h;
+            if (q < n4) *reinterpret_cast<float4 *>(&lds[i][4 * q]) = x[i][h];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+        float o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int kk = c0 + j;
+            float a = 0.f;
+            if (kk < L.K) {
+                const int f = kk / 9 - fa, tap = kk - (kk / 9) * 9;
+                const int u = tap / 3, vq = tap - u * 3;
+                const float *b = &lds[i][f * 16];
+                a = (((b[u * 4 + vq] + b[u * 4 + vq + 1]) + b[(u + 1) * 4 + vq]) +
+                     b[(u + 1) * 4 + vq + 1]) * 0.25f;
+            }
+            o[j] = a;
+        }
+        gg[i] = make_float4(o[0], o[1], o[2], o[3]);
+    }
+}
+
+template <int H, bool GD>
 __device__ __forceinline__ void sn_adam_tile(const SnAdamTable &t, int tile, AdamK k,
                                              const double *part, float clip) {
     constexpr int NR = SN_RPW / H;
@@ -165,15 +228,58 @@ __device__ __forceinline__ void sn_adam_tile(const SnAdamTable &t, int tile, Ada
     const int c0 = ct * SN_TC + lane * 4;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     __shared__ float sh[1];
+    constexpr bool gd = GD;     // the G-direct instantiation (every SN layer of the call)
+    float coef = 0.f, sigma = 1.f, s = 1.f;
+    if constexpr (GD) {
+        coef = L.stats[0];
+        sigma = L.stats[2];
+        s = L.stats[3];
+    }
 #pragma unroll
     for (int h = 0; h < H; ++h) {
         const int r0 = rt * SN_TR + w * SN_RPW + h * NR;
         float4 pp[NR], gg[NR], mm[NR], vv[NR];
-        load_tile(L.g, L.N, L.K, L.vec, r0, c0, gg);
-        load_tile(L.p, L.N, L.K, L.vec, r0, c0, pp);
-        load_tile<NR, true>(L.m, L.N, L.K, L.vec, r0, c0, mm);
-        load_tile<NR, true>(L.v, L.N, L.K, L.vec, r0, c0, vv);
-        if (h == 0) k.f = (clip > 0.f) ? clip_factor_slab(part, L.sb0, L.sb1, clip, sh) : 1.f;
+        float uc[NR], vk[4];
+        if constexpr (GD) {
+            // p, m, v in flight first: the fold staging below waits on its own loads
+            load_tile(L.p, L.N, L.K, L.vec, r0, c0, pp);
+            load_tile<NR, true>(L.m, L.N, L.K, L.vec, r0, c0, mm);
+            load_tile<NR, true>(L.v, L.N, L.K, L.vec, r0, c0, vv);
+#pragma unroll
+            for (int i = 0; i < NR; ++i) uc[i] = (r0 + i < L.N) ? L.ucur[r0 + i] : 0.f;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) vk[j] = (c0 + j < L.K) ? L.vsn[c0 + j] : 0.f;
+            __shared__ float lds_g[4][NR][SNG_FMAX * 16];   // fold staging
+            if (L.fold) sn_fold_adjoint<NR>(L, ct, r0, c0, lds_g[w], gg);
+            else load_tile(L.G, L.N, L.K, L.gvec, r0, c0, gg);
+        } else {
+            load_tile(L.g, L.N, L.K, L.vec, r0, c0, gg);
+            load_tile(L.p, L.N, L.K, L.vec, r0, c0, pp);
+            load_tile<NR, true>(L.m, L.N, L.K, L.vec, r0, c0, mm);
+            load_tile<NR, true>(L.v, L.N, L.K, L.vec, r0, c0, vv);
+        }
+        if (h == 0) {
+            if (!(clip > 0.f)) {
+                k.f = 1.f;
+            } else if (gd) {                         // the analytic norm of the record
+                const float ss = L.stats[1];
+                const float inv = (ss > 0.f) ? rsqrtf(ss) : INFINITY;
+                k.f = clip * fminf(inv, 1.f / clip);
+            } else {
+                k.f = clip_factor_slab(part, L.sb0, L.sb1, clip, sh);
+            }
+        }
+        if constexpr (GD) {
+            // dL/dW = (s G) / sigma - (coef u'_n) v_k   (sn_bwd_b's form)
+#pragma unroll
+            for (int i = 0; i < NR; ++i) {
+                const float cu = coef * uc[i];
+                gg[i].x = (s * gg[i].x) / sigma - cu * vk[0];
+                gg[i].y = (s * gg[i].y) / sigma - cu * vk[1];
+                gg[i].z = (s * gg[i].z) / sigma - cu * vk[2];
+                gg[i].w = (s * gg[i].w) / sigma - cu * vk[3];
+            }
+        }
 #pragma unroll
         for (int i = 0; i < NR; ++i) {
             k.upd(pp[i].x, gg[i].x, mm[i].x, vv[i].x);
@@ -195,6 +301,7 @@ struct SnAdamHost {
     const float *param, *m, *v, *grad;
     const int64_t *offsets;       // n_tensors + 1
     const int *sblk;              // first norm-pass partial of each tensor
+    int gdirect;                  // layers[].G / .fold: the G-direct update
 };
 smmd_status sn_adam_table(const smmd_sn_layer *layers, const int32_t *sn_tensor, int n_layers,
                           const SnAdamHost &a, void *sn_ws, size_t sn_ws_bytes, SnAdamTable &t);

@@ -26,6 +26,7 @@ HEADER = os.path.join(os.path.dirname(_PKG_ROOT), 'include', 'smmd_hip.h')
 SMMD_MAX_TERMS = 8
 SMMD_SN_MAX_LAYERS = 32
 SN_P1_READY = 1            # smmd_sn_power_iter_ex flag
+ADAM_SN_GDIRECT = 1        # smmd_adam_flat_sn2 flag
 OPT_MAX_FUSED = 96         # tensors smmd_adam_flat_sn takes in one call
 SN_MAX_FUSED = 16          # SN layers smmd_adam_flat_sn takes in one call
 ABI_VERSION = 7
@@ -111,6 +112,10 @@ _SIGS = {
     'smmd_sn_power_iter': (_I, [ctypes.POINTER(SnLayer), _I, _I, _F, _I, _P, _SZ, _P]),
     'smmd_sn_power_iter_ex': (_I, [ctypes.POINTER(SnLayer), _I, _I, _F, _I, _I, _P, _SZ, _P]),
     'smmd_sn_weight_bwd': (_I, [ctypes.POINTER(SnLayer), _I, _P, _SZ, _P]),
+    'smmd_sn_grad_stats': (_I, [ctypes.POINTER(SnLayer), _I, _P, _SZ, _P]),
+    'smmd_adam_flat_sn2': (_I, [_P, _P, _P, _P, ctypes.POINTER(ctypes.c_int64), _I, _F, _F, _F,
+                                _F, _F, _F, _I64, _P, _P, _SZ, ctypes.POINTER(SnLayer),
+                                ctypes.POINTER(ctypes.c_int32), _I, _P, _SZ, _I, _P]),
     'smmd_opt_workspace_bytes': (_SZ, [ctypes.POINTER(ctypes.c_int64), _I]),
     'smmd_clip_by_norm_flat': (_I, [_P, ctypes.POINTER(ctypes.c_int64), _I, _F, _P, _SZ, _P]),
     'smmd_adam_flat': (_I, [_P, _P, _P, _P, ctypes.POINTER(ctypes.c_int64), _I, _F, _F, _F, _F,

@@ -407,14 +407,30 @@ class MMD_GAN:
         self._arm(self.d_optim)
         if ref:       # the generator's gradient set, computed and discarded
             torch.autograd.grad(g_loss, self.g_vars, retain_graph=True)
-            d_loss.backward(inputs=self.d_vars)
-        else:
-            # the real images are a leaf only for the Jacobian: the critic's
-            # first conv skips the input gradient nobody reads
-            with convops.no_input_grad(self._last_images):
-                d_loss.backward()
+        gd = self._gdirect()
+        self.sn_D.arm_gdirect(gd)
+        try:
+            if ref:
+                d_loss.backward(inputs=self.d_vars)
+            else:
+                # the real images are a leaf only for the Jacobian: the critic's
+                # first conv skips the input gradient nobody reads
+                with convops.no_input_grad(self._last_images):
+                    d_loss.backward()
+        finally:
+            self.sn_D.arm_gdirect(False)
         self._exchange(self.d_optim)
         return self._detach_step_state()
+
+    def _gdirect(self):
+        """The critic's SN weight gradients go straight from G into the
+        fused update (sn._SNBatch._backward_gdirect, smmd_adam_flat_sn2):
+        one process, an SN-fused optimizer, SMMD_SN_GDIRECT not 0.  With
+        several ranks the flat gradient is what the buckets all-reduce, so
+        dL/dW is formed as before."""
+        import os
+        return (self.world == 1 and self.d_optim._sn is not None and bool(self.sn_D.entries)
+                and os.environ.get('SMMD_SN_GDIRECT', '1') != '0')
 
     def _detach_step_state(self):
         """After a step's backward: keep the reference attributes (self.g_loss,

@@ -82,6 +82,8 @@ class FlatAdam:
 
     def zero_grad(self, set_to_none=False):
         self.flat_grad.zero_()
+        if self._sn is not None:
+            self._sn[0]._gd_pending = None
         # re-attach views in case autograd replaced a .grad tensor
         for i, p in enumerate(self.params):
             o, n = self.offsets[i], p.numel()
@@ -133,6 +135,7 @@ class FlatAdam:
         bank, idx = self._sn
         base = self.flat_param.data_ptr()
         arr = (_lib.SnLayer * len(bank.entries))()
+        pend = bank._gd_pending
         for k, e in enumerate(bank.entries):
             W = e.weight
             if W.data_ptr() != base + 4 * self.offsets[idx[k]]:
@@ -140,7 +143,41 @@ class FlatAdam:
             arr[k].W = W.data_ptr()
             arr[k].u = e.u.data_ptr()
             arr[k].N, arr[k].K = e.N, e.K
+            if pend is not None:    # the G-direct update: G of the backward
+                arr[k].G = pend[0][k].data_ptr()
+                arr[k].fold = 1 if pend[1][k] else 0
+                arr[k].v = e.v.data_ptr()
         return arr
+
+    def dense_grad(self):
+        """The flat gradient with every SN weight's dL/dW formed (a copy): under
+        the G-direct update those ranges of ``flat_grad`` are never written
+        (smmd_sn_weight_bwd from the kept G, for inspection and tests)."""
+        g = self.flat_grad.clone()
+        if self._sn is None or self._sn[0]._gd_pending is None:
+            return g
+        bank, idx = self._sn
+        G, folds = bank._gd_pending
+        n = len(bank.entries)
+        arr = (_lib.SnLayer * n)()
+        gs = torch.empty(n, device=g.device, dtype=torch.float32)
+        for k, e in enumerate(bank.entries):
+            L = arr[k]
+            L.W = e.weight.data_ptr()
+            L.u = e.u.data_ptr()
+            L.v = e.v.data_ptr()
+            L.sigma = e.sigma.data_ptr()
+            s = e.scale
+            L.s = s.data_ptr() if s is not None and s.numel() > 0 else None
+            L.G = G[k].data_ptr()
+            L.gW = g.data_ptr() + 4 * self.offsets[idx[k]]
+            L.gs = gs[k:k + 1].data_ptr()
+            L.N, L.K = e.N, e.K
+            L.fold = 1 if folds[k] else 0
+        _lib.check(_lib.lib().smmd_sn_weight_bwd(arr, n, _lib.ptr(bank.ws), bank.ws.numel(),
+                                                  _lib.stream_handle(g.device)),
+                   'smmd_sn_weight_bwd')
+        return g
 
     def lr_t(self, step=None, lr=None):
         """tf.train.AdamOptimizer's lr_t = lr sqrt(1 - b2^t) / (1 - b1^t) in
@@ -171,10 +208,13 @@ class FlatAdam:
         layers = self._sn_layers() if self._sn is not None else None
         if layers is not None:
             bank, idx = self._sn
+            gd = bank._gd_pending is not None
             with _lib.timed('smmd_adam_flat_sn[%s]' % self.name):
-                st = _lib.lib().smmd_adam_flat_sn(*args, layers, idx, len(bank.entries),
-                                                  _lib.ptr(bank.ws), bank.ws.numel(), stream)
-            _lib.check(st, 'smmd_adam_flat_sn')
+                st = _lib.lib().smmd_adam_flat_sn2(
+                    *args[:13], None, *args[13:], layers, idx, len(bank.entries),
+                    _lib.ptr(bank.ws), bank.ws.numel(), _lib.ADAM_SN_GDIRECT if gd else 0, stream)
+            _lib.check(st, 'smmd_adam_flat_sn2')
+            bank._gd_pending = None
             bank.mark_p1_ready()
             return
         with _lib.timed('smmd_adam_flat[%s]' % self.name):
@@ -192,17 +232,24 @@ class FlatAdam:
         layers = self._sn_layers() if self._sn is not None else None
         if layers is not None:
             bank, idx = self._sn
-            n, sn_ws, sn_b = len(bank.entries), _lib.ptr(bank.ws), bank.ws.numel()
-        else:
-            idx, n, sn_ws, sn_b = None, 0, None, 0
+            gd = bank._gd_pending is not None
+            st = _lib.lib().smmd_adam_flat_sn2(
+                _lib.ptr(self.flat_param), _lib.ptr(self.flat_grad), _lib.ptr(self.m),
+                _lib.ptr(self.v), self.offsets, len(self.params), float(grad_scale), c, 0.0,
+                float(self.beta1), float(self.beta2), float(self.eps), 0,
+                _lib.ptr(self.lr_t_dev), _lib.ptr(self.ws), self.ws.numel(), layers, idx,
+                len(bank.entries), _lib.ptr(bank.ws), bank.ws.numel(),
+                _lib.ADAM_SN_GDIRECT if gd else 0, stream)
+            _lib.check(st, 'smmd_adam_flat_sn2')
+            bank._gd_pending = None
+            bank.mark_p1_ready()
+            return
         st = _lib.lib().smmd_adam_flat_ex(
             _lib.ptr(self.flat_param), _lib.ptr(self.flat_grad), _lib.ptr(self.m),
             _lib.ptr(self.v), self.offsets, len(self.params), float(grad_scale), c,
             _lib.ptr(self.lr_t_dev), float(self.beta1), float(self.beta2), float(self.eps),
-            _lib.ptr(self.ws), self.ws.numel(), layers, idx, n, sn_ws, sn_b, stream)
+            _lib.ptr(self.ws), self.ws.numel(), None, None, 0, None, 0, stream)
         _lib.check(st, 'smmd_adam_flat_ex')
-        if layers is not None:
-            bank.mark_p1_ready()
 
     def state_dict(self):
         return {'m': self.m.clone(), 'v': self.v.clone(), 'step': self.step_count,

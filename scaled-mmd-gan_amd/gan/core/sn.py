@@ -83,6 +83,8 @@ class _SNBatch(torch.autograd.Function):
         n = len(bank.entries)
         saved = ctx.saved_tensors
         Ws, ss = saved[:n], saved[n:]
+        if bank._gd_armed:
+            return _SNBatch._backward_gdirect(ctx, bank, Ws, ss, grads)
         arr = (_lib.SnLayer * n)()
         gWs, gss, keep = [], [], []
         for i, (e, W, s, G) in enumerate(zip(bank.entries, Ws, ss, grads)):
@@ -118,6 +120,45 @@ class _SNBatch(torch.autograd.Function):
             else:
                 gs_out.append(gs.view_as(s))
         return (None, None, None, *gWs, *gs_out)
+
+
+    @staticmethod
+    def _backward_gdirect(ctx, bank, Ws, ss, grads):
+        """The G-direct backward (one process, the critic's update next):
+        dL/dW is not formed.  smmd_sn_grad_stats reduces what the fused
+        update needs from G and writes dL/ds straight into the scale's
+        gradient (a view of the optimizer's flat buffer); G is kept on the
+        bank for FlatAdam.step (smmd_adam_flat_sn2, SMMD_ADAM_SN_GDIRECT).
+        No gradient is returned for W or s, so autograd runs no accumulation
+        for them."""
+        n = len(bank.entries)
+        arr = (_lib.SnLayer * n)()
+        keep = []
+        for i, (e, W, s, G) in enumerate(zip(bank.entries, Ws, ss, grads)):
+            fold = ctx.folds[i]
+            if G is None:
+                G = (torch.zeros(W.shape[0], W.shape[1], 4, 4, device=W.device,
+                                 dtype=torch.float32) if fold else torch.zeros_like(W))
+            G = G.contiguous() if fold else G.contiguous(memory_format=_memfmt(W))
+            keep.append(G)
+            L = arr[i]
+            L.W = W.data_ptr()
+            L.u = e.u.data_ptr()
+            L.v = e.v.data_ptr()
+            L.sigma = e.sigma.data_ptr()
+            has_s = s is not None and s.numel() > 0
+            L.s = s.data_ptr() if has_s else None
+            sg = e.scale.grad if has_s else None
+            L.gs = sg.data_ptr() if sg is not None else None
+            L.G = G.data_ptr()
+            L.N, L.K = e.N, e.K
+            L.fold = 1 if fold else 0
+        args = (arr, n, _lib.ptr(bank.ws), bank.ws.numel(), _lib.stream_handle(Ws[0].device))
+        with _lib.timed('smmd_sn_grad_stats'):
+            st = _lib.lib().smmd_sn_grad_stats(*args)
+        _lib.check(st, 'smmd_sn_grad_stats')
+        bank._gd_pending = (keep, [bool(f) for f in ctx.folds])
+        return (None, None, None) + (None,) * (2 * n)
 
 
 def _memfmt(W):
@@ -173,6 +214,10 @@ class SpectralNormBank:
         self.num_iters = num_iters
         self.ws = None
         self._p1_token = None
+        # G-direct (one process): while armed, the SN backward leaves
+        # (G tensors, folds) in _gd_pending for the optimizer's fused update
+        self._gd_armed = False
+        self._gd_pending = None
         self._alloc_ws()
 
     def _state_token(self):
@@ -222,6 +267,12 @@ class SpectralNormBank:
             else:
                 e.module.w_eff, e.module.w_fold = w, None
         return list(outs)
+
+    def arm_gdirect(self, on=True):
+        """Arm (or disarm) the G-direct backward for the next backward pass."""
+        self._gd_armed = bool(on)
+        if on:
+            self._gd_pending = None
 
     def sigmas(self):
         return torch.cat([e.sigma for e in self.entries])

@@ -59,7 +59,7 @@ def _critic_update(model, images, z):
     step = model.d_optim.step
 
     def hooked(*a, **k):
-        cap['g'] = model.d_optim.flat_grad.detach().clone()
+        cap['g'] = model.d_optim.dense_grad()
         return step(*a, **k)
     model.d_optim.step = hooked
     _, d_loss, aux = model.d_step(images)

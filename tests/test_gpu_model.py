@@ -65,7 +65,7 @@ def test_critic_step_matches_tf_mirror(dev, arch, size, dim, batch, cl):
     orig = model.d_optim.step
 
     def cap(*a, **k):
-        captured['g'] = model.d_optim.flat_grad.detach().cpu().clone()
+        captured['g'] = model.d_optim.dense_grad().cpu()
         return orig(*a, **k)
     model.d_optim.step = cap
     model.step = 25
@@ -164,7 +164,7 @@ def test_tower_and_global_agree_on_one_gpu(dev):
         orig = model.d_optim.step
 
         def step(*a, _o=orig, _c=cap, _m=model, **k):
-            _c['g'] = _m.d_optim.flat_grad.clone()
+            _c['g'] = _m.d_optim.dense_grad()
             return _o(*a, **k)
         model.d_optim.step = step
         torch.manual_seed(5)
@@ -200,7 +200,7 @@ def test_reference_schedule_applies_the_lean_update(dev):
         cap = {}
         for opt in (mdl.d_optim, mdl.g_optim):      # the gradient each update applies
             def step(*a, _o=opt.step, _c=cap, _opt=opt, **k):
-                _c[_opt.name] = _opt.flat_grad.clone()
+                _c[_opt.name] = _opt.dense_grad()
                 return _o(*a, **k)
             opt.step = step
         caps.append(cap)
