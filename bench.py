@@ -51,8 +51,8 @@ VALU_LANE_OPS = FP32_PEAK_TFS / 2 * 1e12
 TRANS_SLOTS = 4                # v_exp_f32 / v_log_f32: quarter rate (MI355X_MICROARCH.md)
 BATCH = 64
 
-PMC_TRAFFIC = os.path.join(ROOT, 'profiles', 'r06', 'pmc_traffic.json')
-PMC_FALLBACK = os.path.join(ROOT, 'profiles', 'r05', 'pmc_traffic.json')
+PMC_TRAFFIC = os.path.join(ROOT, 'profiles', 'r07', 'pmc_traffic.json')
+PMC_FALLBACK = os.path.join(ROOT, 'profiles', 'r06', 'pmc_traffic.json')
 
 # the hot-path rows a1-a9 and the library entry points that
 # implement them (the roofline kernel is chosen among these)

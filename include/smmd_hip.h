@@ -63,7 +63,7 @@ int smmd_abi_version(void);         /* bumped on any ABI change (2: Gram/poly,
                                        6: smmd_mask_pool2*, smmd_up_add,
                                        smmd_bn_relu_fwd, 7: smmd_smmd_loss_fwd/bwd,
                                        smmd_source_hash, smmd_sn_grad_stats,
-                                       smmd_adam_flat_sn2) */
+                                       smmd_adam_flat_sn2, smmd_bn_relu_fwd_save / _bwd) */
 const char *smmd_source_hash(void); /* first 16 hex digits of the SHA-256 of the
                                        sources this binary was built from
                                        (csrc .hip and .hpp files in byte order,
@@ -500,6 +500,25 @@ smmd_status smmd_bn_relu_fwd(const float *x, int N, int C, int HW, const float *
                              const float *beta, float *running_mean, float *running_var,
                              float momentum, float eps, float *y, void *ws, size_t ws_bytes,
                              smmd_stream_t stream);
+
+/* The same forward, also writing save[4 C] = per channel {k, mean - k,
+ * 1 / sqrt(var + eps), gamma / sqrt(var + eps)} (k: the channel's first
+ * element, the statistics' shift) for the backward; save may be NULL. */
+smmd_status smmd_bn_relu_fwd_save(const float *x, int N, int C, int HW, const float *gamma,
+                                  const float *beta, float *running_mean, float *running_var,
+                                  float momentum, float eps, float *y, float *save, void *ws,
+                                  size_t ws_bytes, smmd_stream_t stream);
+
+/* Backward of y = relu(batch_norm(x)) in training mode (the generator step,
+ * resnet/block.py:42-47, snops.py:31-40 / resnet/ops/batchnorm.py:8-18 with
+ * TF's autodiff): with z recomputed from x and save exactly as the forward
+ * formed it (the ReLU mask bit for bit), gz = gy [z > 0], M = N HW:
+ * gbeta = sum gz, ggamma = sum gz xhat (per channel; either may be NULL),
+ * gx = gamma inv (gz - gbeta / M - xhat ggamma / M).  Workspace as the
+ * forward's.  x, gy, gx NCHW fp32, 16-byte aligned, HW % 4 == 0. */
+smmd_status smmd_bn_relu_bwd(const float *x, const float *gy, int N, int C, int HW,
+                             const float *beta, const float *save, float *gx, float *ggamma,
+                             float *gbeta, void *ws, size_t ws_bytes, smmd_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * Thin 3x3 convolutions: stride 1, zero padding 1 (TF SAME at stride 1), NCHW

@@ -81,7 +81,8 @@ __global__ __launch_bounds__(BN_T) void bn_apply_kernel(const float *__restrict_
                                                         float *__restrict__ run_mean,
                                                         float *__restrict__ run_var,
                                                         float momentum, float eps,
-                                                        float *__restrict__ y) {
+                                                        float *__restrict__ y,
+                                                        float *__restrict__ save) {
     const int c = blockIdx.x, s = blockIdx.y;
     __shared__ float sh[4];
     if (threadIdx.x < SMMD_WAVE) {
@@ -106,6 +107,12 @@ __global__ __launch_bounds__(BN_T) void bn_apply_kernel(const float *__restrict_
             sh[1] = (float)b;
             sh[2] = x[(size_t)c * HW];                  // the shift k
             sh[3] = (float)ms;                           // mean - k
+            if (s == 0 && save) {                        // for smmd_bn_relu_bwd
+                save[4 * c + 0] = sh[2];
+                save[4 * c + 1] = sh[3];
+                save[4 * c + 2] = (float)inv;
+                save[4 * c + 3] = sh[0];
+            }
             if (s == 0 && run_mean && run_var) {
                 const double unb = cnt > 1.0 ? var * cnt / (cnt - 1.0) : var;
                 run_mean[c] = (float)((1.0 - momentum) * (double)run_mean[c] + momentum * mean);
@@ -139,6 +146,118 @@ __global__ __launch_bounds__(BN_T) void bn_apply_kernel(const float *__restrict_
     }
 }
 
+// ---- backward of relu(batch_norm(x)) (training mode) ------------------------
+// With z = xhat gamma + beta (the forward's value: the same float ops from the
+// saved {k, mean - k, 1/sqrt(var + eps), gamma / sqrt(var + eps)}), so the ReLU
+// mask is the forward's bit for bit), gz = gy [z > 0], M = N HW:
+//   dbeta = sum gz,  dgamma = sum gz xhat,
+//   dx = gamma inv (gz - dbeta / M - xhat dgamma / M)
+// Pass 1 (grid (C, S)): per-block (sum gz, sum gz xhat) in double to a slab;
+// pass 2: every block reduces its channel's partials in a fixed order, block
+// (c, 0) writes dgamma, dbeta, all write dx.  HBM: x, gy read twice, dx once.
+__device__ __forceinline__ void bn_bwd_elem(float x, float g, float k, float ms, float inv,
+                                            float sc, float bb, float &gz, float &xh) {
+    const float xm = (x - k) - ms;
+    gz = (fmaf(xm, sc, bb) > 0.f) ? g : 0.f;
+    xh = xm * inv;
+}
+
+__global__ __launch_bounds__(BN_T) void bn_bwd_stats_kernel(const float *__restrict__ x,
+                                                            const float *__restrict__ gy, int N,
+                                                            int C, int HW, int S,
+                                                            const float *__restrict__ save,
+                                                            const float *__restrict__ beta,
+                                                            double *__restrict__ part) {
+    const int c = blockIdx.x, s = blockIdx.y;
+    int n0, n1;
+    bn_rows(N, S, s, n0, n1);
+    const int w4 = HW >> 2;
+    const int rpi = w4 >= BN_T ? 1 : BN_T / w4;
+    const int r = w4 >= BN_T ? 0 : (int)threadIdx.x / w4;
+    const int col = w4 >= BN_T ? (int)threadIdx.x : (int)threadIdx.x - r * w4;
+    const int step = w4 >= BN_T ? BN_T : w4;
+    const float k = save[4 * c + 0], ms = save[4 * c + 1], inv = save[4 * c + 2];
+    const float sc = save[4 * c + 3], bb = beta ? beta[c] : 0.f;
+    float a = 0.f, q = 0.f;
+    if (r < rpi) {
+        for (int n = n0 + r; n < n1; n += rpi) {
+            const size_t off = ((size_t)n * C + c) * HW;
+            const float4 *xr = reinterpret_cast<const float4 *>(x + off);
+            const float4 *gr = reinterpret_cast<const float4 *>(gy + off);
+            for (int i = col; i < w4; i += step) {
+                const float4 v = xr[i], g = gr[i];
+                float gz, xh;
+                bn_bwd_elem(v.x, g.x, k, ms, inv, sc, bb, gz, xh); a += gz; q = fmaf(gz, xh, q);
+                bn_bwd_elem(v.y, g.y, k, ms, inv, sc, bb, gz, xh); a += gz; q = fmaf(gz, xh, q);
+                bn_bwd_elem(v.z, g.z, k, ms, inv, sc, bb, gz, xh); a += gz; q = fmaf(gz, xh, q);
+                bn_bwd_elem(v.w, g.w, k, ms, inv, sc, bb, gz, xh); a += gz; q = fmaf(gz, xh, q);
+            }
+        }
+    }
+    __shared__ double red[BN_T / SMMD_WAVE];
+    const double sa = block_sum<BN_T / SMMD_WAVE>((double)a, red);
+    const double sq = block_sum<BN_T / SMMD_WAVE>((double)q, red);
+    if (threadIdx.x == 0) {
+        part[((size_t)s * C + c) * 2 + 0] = sa;
+        part[((size_t)s * C + c) * 2 + 1] = sq;
+    }
+}
+
+__global__ __launch_bounds__(BN_T) void bn_bwd_apply_kernel(
+    const float *__restrict__ x, const float *__restrict__ gy, int N, int C, int HW, int S,
+    const double *__restrict__ part, const float *__restrict__ save,
+    const float *__restrict__ beta, float *__restrict__ gx, float *__restrict__ ggamma,
+    float *__restrict__ gbeta) {
+    const int c = blockIdx.x, s = blockIdx.y;
+    __shared__ float sh[2];
+    if (threadIdx.x < SMMD_WAVE) {
+        double a = 0.0, q = 0.0;
+        for (int j = threadIdx.x; j < S; j += SMMD_WAVE) {
+            a += part[((size_t)j * C + c) * 2 + 0];
+            q += part[((size_t)j * C + c) * 2 + 1];
+        }
+        a = wave_sum(a);
+        q = wave_sum(q);
+        if (threadIdx.x == 0) {
+            const double cnt = (double)N * (double)HW;
+            sh[0] = (float)(a / cnt);
+            sh[1] = (float)(q / cnt);
+            if (s == 0) {
+                if (gbeta) gbeta[c] = (float)a;
+                if (ggamma) ggamma[c] = (float)q;
+            }
+        }
+    }
+    __syncthreads();
+    const float mb = sh[0], mq = sh[1];
+    const float k = save[4 * c + 0], ms = save[4 * c + 1], inv = save[4 * c + 2];
+    const float sc = save[4 * c + 3], bb = beta ? beta[c] : 0.f;
+    int n0, n1;
+    bn_rows(N, S, s, n0, n1);
+    const int w4 = HW >> 2;
+    const int rpi = w4 >= BN_T ? 1 : BN_T / w4;
+    const int r = w4 >= BN_T ? 0 : (int)threadIdx.x / w4;
+    const int col = w4 >= BN_T ? (int)threadIdx.x : (int)threadIdx.x - r * w4;
+    const int step = w4 >= BN_T ? BN_T : w4;
+    if (r >= rpi) return;
+    for (int n = n0 + r; n < n1; n += rpi) {
+        const size_t off = ((size_t)n * C + c) * HW;
+        const float4 *xr = reinterpret_cast<const float4 *>(x + off);
+        const float4 *gr = reinterpret_cast<const float4 *>(gy + off);
+        float4 *out = reinterpret_cast<float4 *>(gx + off);
+        for (int i = col; i < w4; i += step) {
+            const float4 v = xr[i], g = gr[i];
+            float gz, xh;
+            float4 o;
+            bn_bwd_elem(v.x, g.x, k, ms, inv, sc, bb, gz, xh); o.x = sc * ((gz - mb) - xh * mq);
+            bn_bwd_elem(v.y, g.y, k, ms, inv, sc, bb, gz, xh); o.y = sc * ((gz - mb) - xh * mq);
+            bn_bwd_elem(v.z, g.z, k, ms, inv, sc, bb, gz, xh); o.z = sc * ((gz - mb) - xh * mq);
+            bn_bwd_elem(v.w, g.w, k, ms, inv, sc, bb, gz, xh); o.w = sc * ((gz - mb) - xh * mq);
+            out[i] = o;
+        }
+    }
+}
+
 inline int bn_split(int N, int C) {
     if (C >= 512) return 1;
     int S = (2048 + C - 1) / C;
@@ -155,10 +274,11 @@ extern "C" size_t smmd_bn_relu_workspace_bytes(int N, int C) {
     return (size_t)bn_split(N, C) * C * 2 * sizeof(double);
 }
 
-extern "C" smmd_status smmd_bn_relu_fwd(const float *x, int N, int C, int HW, const float *gamma,
-                                        const float *beta, float *running_mean,
-                                        float *running_var, float momentum, float eps, float *y,
-                                        void *ws, size_t ws_bytes, smmd_stream_t stream) {
+extern "C" smmd_status smmd_bn_relu_fwd_save(const float *x, int N, int C, int HW,
+                                             const float *gamma, const float *beta,
+                                             float *running_mean, float *running_var,
+                                             float momentum, float eps, float *y, float *save,
+                                             void *ws, size_t ws_bytes, smmd_stream_t stream) {
     if (!x || !y || N < 1 || C < 1 || HW < 4 || (HW & 3)) return SMMD_EINVAL;
     if (((uintptr_t)x & 15) || ((uintptr_t)y & 15)) return SMMD_EINVAL;
     const int S = bn_split(N, C);
@@ -171,6 +291,34 @@ extern "C" smmd_status smmd_bn_relu_fwd(const float *x, int N, int C, int HW, co
     if (e != SMMD_OK) return e;
     hipLaunchKernelGGL(bn_apply_kernel, dim3(C, S), dim3(BN_T), 0, st, x, N, C, HW, S,
                        (const double *)part, gamma, beta, running_mean, running_var, momentum,
-                       eps, y);
+                       eps, y, save);
+    return last_launch_status();
+}
+
+extern "C" smmd_status smmd_bn_relu_fwd(const float *x, int N, int C, int HW, const float *gamma,
+                                        const float *beta, float *running_mean,
+                                        float *running_var, float momentum, float eps, float *y,
+                                        void *ws, size_t ws_bytes, smmd_stream_t stream) {
+    return smmd_bn_relu_fwd_save(x, N, C, HW, gamma, beta, running_mean, running_var, momentum,
+                                 eps, y, nullptr, ws, ws_bytes, stream);
+}
+
+extern "C" smmd_status smmd_bn_relu_bwd(const float *x, const float *gy, int N, int C, int HW,
+                                        const float *beta, const float *save, float *gx,
+                                        float *ggamma, float *gbeta, void *ws, size_t ws_bytes,
+                                        smmd_stream_t stream) {
+    if (!x || !gy || !gx || !save || N < 1 || C < 1 || HW < 4 || (HW & 3)) return SMMD_EINVAL;
+    if (((uintptr_t)x & 15) || ((uintptr_t)gy & 15) || ((uintptr_t)gx & 15)) return SMMD_EINVAL;
+    const int S = bn_split(N, C);
+    if (S > 65535) return SMMD_EINVAL;
+    if (!ws || ws_bytes < smmd_bn_relu_workspace_bytes(N, C)) return SMMD_EWORKSPACE;
+    hipStream_t st = (hipStream_t)stream;
+    double *part = static_cast<double *>(ws);
+    hipLaunchKernelGGL(bn_bwd_stats_kernel, dim3(C, S), dim3(BN_T), 0, st, x, gy, N, C, HW, S,
+                       save, beta, part);
+    smmd_status e = last_launch_status();
+    if (e != SMMD_OK) return e;
+    hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(C, S), dim3(BN_T), 0, st, x, gy, N, C, HW, S,
+                       (const double *)part, save, beta, gx, ggamma, gbeta);
     return last_launch_status();
 }

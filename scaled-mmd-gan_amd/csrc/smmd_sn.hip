@@ -577,7 +577,7 @@ __global__ __launch_bounds__(256) void sn_bwd_b_kernel(SnTable t) {
 // ---- gradient statistics for the G-direct update (smmd_sn_grad_stats) ------
 // Instead of writing dL/dW, the backward reduces what the optimizer needs to
 // form it on the fly from G (smmd_adam_flat_sn2, SMMD_ADAM_SN_GDIRECT):
-// d = <G, W> (the same partials and order as sn_bwd_a, so the same bits),
+// d = <G, W> (sn_bwd_a's partials; the layer sum in a fixed order of its own),
 // ||G||^2 and u'^T G v (G = the adjoint of G' on fold layers).  Then per
 // layer: gs = d / sigma, coef = s d / sigma^2 and the clip norm
 // ||dL/dW||^2 = a^2 ||G||^2 - 2 a coef u'^T G v + coef^2 ||u'||^2 ||v||^2
@@ -656,18 +656,46 @@ __global__ __launch_bounds__(256) void sn_gstat_a_kernel(SnTable t) {
     }
 }
 
-// one 64-thread block per layer: the layer sums in sn_bwd_b's order for d,
-// then the record {coef, ||dL/dW||^2, sigma, s} and gs
-__global__ __launch_bounds__(64) void sn_gstat_r_kernel(SnTable t) {
+// one 256-thread block per layer: the layer sums (4 waves, each lane
+// strided by 256, 8 loads per slab in flight; waves added in order), then the
+// record {coef, ||dL/dW||^2, sigma, s} and gs
+__global__ __launch_bounds__(256) void sn_gstat_r_kernel(SnTable t) {
     const SnLayerDev L = t.L[blockIdx.x];
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int units = layer_units(L);
-    double dd = wave_sum(strided_sum(L.dotp, lane, units, 64));
-    double gg = wave_sum(strided_sum(L.ggp, lane, units, 64));
-    double ug = wave_sum(strided_sum(L.ugvp, lane, units, 64));
+    double dd = 0.0, gg = 0.0, ug = 0.0;
+    for (int base = threadIdx.x; base < units; base += 8 * 256) {
+        float a[8], b[8], c[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int i = base + j * 256;
+            a[j] = (i < units) ? L.dotp[i] : 0.f;
+            b[j] = (i < units) ? L.ggp[i] : 0.f;
+            c[j] = (i < units) ? L.ugvp[i] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            dd += (double)a[j];
+            gg += (double)b[j];
+            ug += (double)c[j];
+        }
+    }
+    __shared__ double red[3][4];
+    dd = wave_sum(dd);
+    gg = wave_sum(gg);
+    ug = wave_sum(ug);
     if (lane == 0) {
+        red[0][w] = dd;
+        red[1][w] = gg;
+        red[2][w] = ug;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        dd = ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
+        gg = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
+        ug = ((red[2][0] + red[2][1]) + red[2][2]) + red[2][3];
         const double vv = L.stats[4], uu = L.stats[5];   // ||v||^2, ||u'||^2 (refresh R2)
-        const float d = (float)dd;                       // layer_dot's value
+        const float d = (float)dd;
         const float sigma = L.sigma[0];
         const float s = L.s ? L.s[0] : 1.f;
         if (L.gs) L.gs[0] = d / sigma;                   // dL/ds, as sn_bwd_b
@@ -880,7 +908,7 @@ smmd_status smmd_sn_grad_stats(const smmd_sn_layer *layers, int n_layers, void *
         SnTable t;
         if (!build_table(layers, first, count, (char *)ws + 256, t)) return SMMD_EINVAL;
         hipLaunchKernelGGL(sn_gstat_a_kernel, dim3(t.total_units), dim3(256), 0, s, t);
-        hipLaunchKernelGGL(sn_gstat_r_kernel, dim3(t.n_layers), dim3(64), 0, s, t);
+        hipLaunchKernelGGL(sn_gstat_r_kernel, dim3(t.n_layers), dim3(256), 0, s, t);
         smmd_status st = last_launch_status();
         if (st != SMMD_OK) return st;
     }

@@ -141,6 +141,8 @@ _SIGS = {
     'smmd_up_add': (_I, [_P, _P, _P, _P, _I, _I64, _I, _I, _P, _P]),
     'smmd_bn_relu_workspace_bytes': (_SZ, [_I, _I]),
     'smmd_bn_relu_fwd': (_I, [_P, _I, _I, _I, _P, _P, _P, _P, _F, _F, _P, _P, _SZ, _P]),
+    'smmd_bn_relu_fwd_save': (_I, [_P, _I, _I, _I, _P, _P, _P, _P, _F, _F, _P, _P, _P, _SZ, _P]),
+    'smmd_bn_relu_bwd': (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _SZ, _P]),
     'smmd_conv3x3_thin_wgrad_workspace_bytes': (_SZ, [_I, _I, _I, _I, _I]),
     'smmd_conv3x3_thin_wgrad': (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P, _SZ, _P]),
     'smmd_poly_diff_ratio': (_I, [ctypes.POINTER(PolySums), ctypes.POINTER(PolySums),

@@ -253,6 +253,7 @@ class _SMMDLoss(torch.autograd.Function):
         ws = _lib.workspace('mmd2', L.smmd_mmd2_workspace_bytes(m, n, d), dev)
         lws = _lib.workspace('scaled_loss', L.smmd_scaled_loss_workspace_bytes(n_cols * b, per),
                              dev)
+        _lib.add_bytes('smmd_smmd_loss_fwd', jac.numel() * 4 + 4 * (m + n) * d * 4)
         with _lib.timed('smmd_smmd_loss_fwd'):
             st = L.smmd_smmd_loss_fwd(
                 spec.desc(), _lib.ptr(X), m, _lib.ptr(Y), n, d, 1 if biased else 0,
@@ -278,6 +279,10 @@ class _SMMDLoss(torch.autograd.Function):
         gjac = torch.empty_like(jac) if ctx.needs_input_grad[2] else None
         gfeat = (torch.empty_like(feat) if (feat is not None and variant == 1
                                             and ctx.needs_input_grad[3]) else None)
+        # the Jacobian read and its gradient written (critic steps), the
+        # features' unit gradients read and dX, dY written
+        _lib.add_bytes('smmd_smmd_loss_bwd', (2 * jac.numel() * 4 if gjac is not None else 0)
+                       + 2 * (m + n) * d * 4)
         with _lib.timed('smmd_smmd_loss_bwd'):
             st = _lib.lib().smmd_smmd_loss_bwd(
                 _lib.ptr(jac), n_cols, b, per, _lib.ptr(feat), dof, _lib.ptr(out), sc, variant, 0,

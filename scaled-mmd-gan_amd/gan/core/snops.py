@@ -151,31 +151,100 @@ def batch_norm(c):
 BN_RELU = os.environ.get('SMMD_BN_RELU', '1') != '0'
 
 
-def bn_relu(bn, x):
-    """relu(bn(x)) (resnet/block.py:42-47 Normalize then tf.nn.relu): when no
-    gradient is taken -- the generator's forward in every critic step -- a
-    training-mode nn.BatchNorm2d on an NCHW device tensor runs as the
-    library's two-pass smmd_bn_relu_fwd (batch statistics, moving averages,
-    normalise + ReLU in one write); otherwise the torch modules."""
-    if (BN_RELU and isinstance(bn, nn.BatchNorm2d) and bn.training and bn.track_running_stats
-            and bn.momentum is not None and not torch.is_grad_enabled() and x.is_cuda
-            and x.dtype == torch.float32 and x.dim() == 4 and x.is_contiguous()
-            and (x.shape[2] * x.shape[3]) % 4 == 0 and x.data_ptr() % 16 == 0):
-        from . import _lib
+# SMMD_BN_RELU_GRAD=0: with a gradient (the generator step) torch's / MIOpen's
+# batch norm + relu instead of the library's forward and backward
+BN_RELU_GRAD = os.environ.get('SMMD_BN_RELU_GRAD', '1') != '0'
+
+
+def _bn_relu_fwd(bn, x, save):
+    from . import _lib
+    N, C, H, W = x.shape
+    L = _lib.lib()
+    ws = _lib.workspace('bn_relu', L.smmd_bn_relu_workspace_bytes(N, C), x.device)
+    y = torch.empty_like(x)
+    _lib.add_bytes('smmd_bn_relu_fwd', 3 * x.numel() * 4)
+    with _lib.timed('smmd_bn_relu_fwd'):
+        st = L.smmd_bn_relu_fwd_save(_lib.ptr(x), N, C, H * W, _lib.ptr(bn.weight),
+                                     _lib.ptr(bn.bias), _lib.ptr(bn.running_mean),
+                                     _lib.ptr(bn.running_var), float(bn.momentum), float(bn.eps),
+                                     _lib.ptr(y), _lib.ptr(save), _lib.ptr(ws), ws.numel(),
+                                     _lib.stream_handle(x.device))
+    _lib.check(st, 'smmd_bn_relu_fwd')
+    with torch.no_grad():
+        bn.num_batches_tracked.add_(1)
+    return y
+
+
+class _BNReLU(torch.autograd.Function):
+    """relu(batch_norm(x)) in training mode with the library's two-pass
+    forward (statistics; normalise + ReLU + moving averages) and backward
+    (smmd_bn_relu_bwd: the channel sums of gz and gz xhat; then dx, dgamma,
+    dbeta).  A second-order backward (a critic with batch norm inside the
+    scaling regulariser's double backward) is formed from torch ops on the
+    saved statistics, so it stays differentiable."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, bn):
+        C = x.shape[1]
+        save = torch.empty(4 * C, device=x.device, dtype=torch.float32)
+        y = _bn_relu_fwd(bn, x, save)
+        ctx.save_for_backward(x, gamma, beta, save)
+        ctx.eps = float(bn.eps)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, gamma, beta, save = ctx.saved_tensors
         N, C, H, W = x.shape
+        if torch.is_grad_enabled():             # create_graph: differentiable torch ops
+            # the batch statistics recomputed from x, so the second order keeps
+            # their dependence on x
+            mean = x.mean((0, 2, 3), keepdim=True)
+            inv = torch.rsqrt(x.var((0, 2, 3), unbiased=False, keepdim=True) + ctx.eps)
+            xh = (x - mean) * inv
+            z = xh * gamma.view(1, C, 1, 1) + beta.view(1, C, 1, 1)
+            gz = gy * (z > 0).to(gy.dtype)
+            gb = gz.sum((0, 2, 3))
+            gg = (gz * xh).sum((0, 2, 3))
+            M = float(N * H * W)
+            gx = (gamma.view(1, C, 1, 1) * inv) * (gz - gb.view(1, C, 1, 1) / M
+                                                   - xh * gg.view(1, C, 1, 1) / M)
+            return gx, gg, gb, None
+        from . import _lib
+        gy = gy.contiguous()
         L = _lib.lib()
         ws = _lib.workspace('bn_relu', L.smmd_bn_relu_workspace_bytes(N, C), x.device)
-        y = torch.empty_like(x)
-        _lib.add_bytes('smmd_bn_relu_fwd', 3 * x.numel() * 4)
-        with _lib.timed('smmd_bn_relu_fwd'):
-            st = L.smmd_bn_relu_fwd(_lib.ptr(x), N, C, H * W, _lib.ptr(bn.weight),
-                                    _lib.ptr(bn.bias), _lib.ptr(bn.running_mean),
-                                    _lib.ptr(bn.running_var), float(bn.momentum), float(bn.eps),
-                                    _lib.ptr(y), _lib.ptr(ws), ws.numel(),
-                                    _lib.stream_handle(x.device))
-        _lib.check(st, 'smmd_bn_relu_fwd')
-        bn.num_batches_tracked.add_(1)
-        return y
+        gx = torch.empty_like(x)
+        gg = torch.empty(C, device=x.device, dtype=torch.float32)
+        gb = torch.empty(C, device=x.device, dtype=torch.float32)
+        _lib.add_bytes('smmd_bn_relu_bwd', 5 * x.numel() * 4)
+        with _lib.timed('smmd_bn_relu_bwd'):
+            st = L.smmd_bn_relu_bwd(_lib.ptr(x), _lib.ptr(gy), N, C, H * W, _lib.ptr(beta),
+                                    _lib.ptr(save), _lib.ptr(gx), _lib.ptr(gg), _lib.ptr(gb),
+                                    _lib.ptr(ws), ws.numel(), _lib.stream_handle(x.device))
+        _lib.check(st, 'smmd_bn_relu_bwd')
+        return gx, gg, gb, None
+
+
+def _bn_relu_ok(bn, x):
+    return (isinstance(bn, nn.BatchNorm2d) and bn.training and bn.track_running_stats
+            and bn.affine and bn.momentum is not None and x.is_cuda
+            and x.dtype == torch.float32 and x.dim() == 4 and x.is_contiguous()
+            and (x.shape[2] * x.shape[3]) % 4 == 0 and x.data_ptr() % 16 == 0)
+
+
+def bn_relu(bn, x):
+    """relu(bn(x)) (resnet/block.py:42-47 Normalize then tf.nn.relu) for a
+    training-mode nn.BatchNorm2d on an NCHW device tensor, on the library:
+    without a gradient (the generator's forward in every critic step) the
+    two-pass smmd_bn_relu_fwd (batch statistics, moving averages, normalise +
+    ReLU in one write); with one (the generator step) the same forward and
+    smmd_bn_relu_bwd (_BNReLU).  Otherwise the torch modules."""
+    if BN_RELU and _bn_relu_ok(bn, x):
+        if not torch.is_grad_enabled():
+            return _bn_relu_fwd(bn, x, None)
+        if BN_RELU_GRAD:
+            return _BNReLU.apply(x, bn.weight, bn.bias, bn)
     return F.relu(bn(x))
 
 

@@ -349,3 +349,73 @@ def test_bn_relu_no_grad_matches_torch(shape, mul, add):
     assert int(a.num_batches_tracked) == 1
     for got, want in ((a.running_mean, rm), (a.running_var, rv)):
         assert float((got.double() - want).abs().max()) <= 1e-5 * float(want.abs().max()) + 1e-7
+
+
+@pytest.mark.parametrize('shape,mul,add', [((64, 64, 64, 64), 3, 1), ((64, 512, 8, 8), 3, 1),
+                                           ((8, 1024, 4, 4), 1, 0), ((3, 7, 4, 4), 3, 1),
+                                           ((16, 32, 16, 16), 0.01, 50)])
+def test_bn_relu_backward_matches_float64(shape, mul, add):
+    """The generator step's batch norm + ReLU with a gradient (snops._BNReLU:
+    smmd_bn_relu_fwd_save + smmd_bn_relu_bwd; resnet/block.py:42-47) against
+    torch's training-mode batch norm + relu in float64 on the same state:
+    output, the moving averages, dx, dgamma, dbeta."""
+    from gan.core import snops
+    from gan.core.snops import batch_norm, bn_relu
+    g = torch.Generator(device=DEV).manual_seed(sum(shape) + 1)
+    x = torch.randn(shape, device=DEV, generator=g) * mul + add
+    gy = torch.randn(shape, device=DEV, generator=g)
+    bn = batch_norm(shape[1]).to(DEV)
+    with torch.no_grad():
+        bn.weight.copy_(torch.rand(shape[1], device=DEV, generator=g) + 0.5)
+        bn.bias.copy_(torch.randn(shape[1], device=DEV, generator=g))
+    w64 = bn.weight.detach().double().requires_grad_(True)
+    b64 = bn.bias.detach().double().requires_grad_(True)
+    rm, rv = bn.running_mean.double().clone(), bn.running_var.double().clone()
+    x64 = x.double().requires_grad_(True)
+    ref = torch.relu(torch.nn.functional.batch_norm(x64, rm, rv, w64, b64, training=True,
+                                                    momentum=bn.momentum, eps=bn.eps))
+    ref.backward(gy.double())
+    saved = snops.BN_RELU, snops.BN_RELU_GRAD
+    snops.BN_RELU = snops.BN_RELU_GRAD = True
+    try:
+        xx = x.clone().requires_grad_(True)
+        y = bn_relu(bn, xx)
+        assert y.grad_fn is not None and 'BNReLU' in type(y.grad_fn).__name__
+        y.backward(gy)
+    finally:
+        snops.BN_RELU, snops.BN_RELU_GRAD = saved
+    assert float((y.double() - ref).abs().max()) <= 2e-5 * float(ref.abs().max()) + 1e-6
+    for got, want in ((bn.running_mean, rm), (bn.running_var, rv)):
+        assert float((got.double() - want).abs().max()) <= 1e-5 * float(want.abs().max()) + 1e-7
+    for got, want, what in ((xx.grad, x64.grad, 'dx'), (bn.weight.grad, w64.grad, 'dgamma'),
+                            (bn.bias.grad, b64.grad, 'dbeta')):
+        err = float((got.double() - want).abs().max())
+        assert err <= 1e-4 * float(want.abs().max()) + 1e-6, (what, err)
+
+
+def test_bn_relu_double_backward_is_differentiable():
+    """create_graph through _BNReLU (a critic with batch norm inside the
+    scaling regulariser's double backward): the second-order gradient equals
+    torch's composition."""
+    from gan.core import snops
+    from gan.core.snops import batch_norm, bn_relu
+    g = torch.Generator(device=DEV).manual_seed(3)
+    x = torch.randn(6, 5, 4, 4, device=DEV, generator=g)
+    outs = []
+    for lib in (True, False):
+        bn = batch_norm(5).to(DEV)
+        with torch.no_grad():
+            bn.weight.fill_(1.3)
+            bn.bias.fill_(0.2)
+        saved = snops.BN_RELU, snops.BN_RELU_GRAD
+        snops.BN_RELU = snops.BN_RELU_GRAD = lib
+        try:
+            xx = x.clone().requires_grad_(True)
+            y = bn_relu(bn, xx)
+            gx, = torch.autograd.grad((y * y.detach().cos()).sum(), xx, create_graph=True)
+            gw, = torch.autograd.grad((gx * gx).sum(), bn.weight)
+        finally:
+            snops.BN_RELU, snops.BN_RELU_GRAD = saved
+        outs.append((gx.detach(), gw.detach()))
+    for a, b in zip(*outs):
+        assert torch.allclose(a, b, rtol=1e-4, atol=1e-5 * float(b.abs().max()))

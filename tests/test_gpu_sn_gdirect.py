@@ -9,7 +9,7 @@ pool fold on ConvMeanPool layers), clipped by the analytic norm of the
 stats record.  Reference: sn.py:42-51 / snops.py:82-84 (the SN weight's TF
 autodiff), model.py:444-468 (clip_by_norm + Adam).
 
-Tolerances: dL/ds bit-identical from the same state (same partials, same
+Tolerances: dL/ds to 1e-5 (the same partials summed in another fixed
 order); the Adam
 moments m, v (= (1-b) clipped g) within 1e-5 of their max + 1e-4 relative
 (g differs from the formed dL/dW by rounding, the clip factor by the analytic
@@ -85,13 +85,9 @@ def test_gdirect_update_matches_formed_gradient(dev, scale):
         sg = float(gb.abs().max())
         assert torch.allclose(ga, gb, rtol=1e-4, atol=1e-6 * sg), step
         for m_a, m_b in zip(ma, mb):
-            # dL/ds: same partials, same order -- the same bits from the same
-            # state (step 0); later the states differ by the updates' rounding
-            if step == 0:
-                assert torch.equal(m_a.sn_scale.grad, m_b.sn_scale.grad)
-            else:
-                assert torch.allclose(m_a.sn_scale.grad, m_b.sn_scale.grad, rtol=1e-4,
-                                      atol=1e-7), step
+            # dL/ds: the same partials, summed in another fixed order
+            assert torch.allclose(m_a.sn_scale.grad, m_b.sn_scale.grad, rtol=1e-5,
+                                  atol=1e-7), step
         p0 = opt_a.flat_param.clone()
         opt_a.step()
         opt_b.step()

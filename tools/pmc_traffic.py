@@ -16,11 +16,18 @@ from collections import defaultdict
 GROUPS = {
     'smmd_sn_power_iter': ('sn_p1_kernel', 'sn_p2_kernel', 'sn_r2_kernel', 'sn_p3_kernel'),
     'smmd_sn_weight_bwd': ('sn_bwd_a_kernel', 'sn_bwd_b_kernel'),
+    'smmd_sn_grad_stats': ('sn_gstat_a_kernel', 'sn_gstat_r_kernel'),
+    'smmd_smmd_loss_fwd': ('smmd_loss_kernel',),
+    # the fused loss's backward runs scaled_loss_bwd_kernel too: in a run of
+    # the fused path this entry is that backward
+    'smmd_smmd_loss_bwd': ('scaled_loss_bwd_kernel',),
+    'smmd_bn_relu_fwd': ('bn_stats_kernel', 'bn_apply_kernel'),
+    'smmd_bn_relu_bwd': ('bn_bwd_stats_kernel', 'bn_bwd_apply_kernel'),
     'smmd_adam_flat': ('opt_sqsum@opt_adam_kernel', 'opt_adam_kernel'),
     'smmd_adam_flat_sn': ('opt_sqsum@opt_adam_sn_kernel', 'opt_adam_sn_kernel'),
     'smmd_clip_by_norm_flat': ('opt_sqsum@opt_clip_kernel', 'opt_clip_kernel'),
     'smmd_mmd2_fwd': ('mmd2_fused_kernel', 'mmd2_tile_kernel'),
-    'smmd_scaled_loss_fwd': ('sqnorm_partial_kernel', 'scaled_loss_final_kernel'),
+    'smmd_scaled_loss_fwd': ('sqnorm_partial_kernel',),
     'smmd_scaled_loss_bwd': ('scaled_loss_bwd_kernel',),
     'smmd_fold_pool_weights': ('fold_fwd_kernel', 'fold_adj_kernel'),
     'smmd_channel_sum': ('chan_sum_partial_kernel', 'chan_sum_final_kernel'),
