@@ -270,7 +270,10 @@ smmd_status smmd_sn_power_iter_ex(const smmd_sn_layer *layers, int n_layers,
 
 /* dL/dW = (s/sigma) (G - (<G,W>/sigma) u' v^T),  dL/ds = <G,W>/sigma,
  * u', v, sigma from the last smmd_sn_power_iter (stop_gradient, sn.py:32-34);
- * ws must be the workspace that call used (it holds u'). */
+ * ws must be the workspace that call used (it holds u'), and layers[] the
+ * same array of layers (the workspace is carved by it): a layer whose G is
+ * NULL is skipped, so a subset (one gradient bucket's layers) is the same
+ * array with the other layers' G NULL. */
 smmd_status smmd_sn_weight_bwd(const smmd_sn_layer *layers, int n_layers,
                                void *ws, size_t ws_bytes, smmd_stream_t stream);
 

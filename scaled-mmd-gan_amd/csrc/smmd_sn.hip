@@ -481,6 +481,7 @@ __global__ __launch_bounds__(256) void sn_p3_kernel(SnTable t) {
 __global__ __launch_bounds__(256) void sn_bwd_a_kernel(SnTable t) {
     const int unit = blockIdx.x;
     const SnLayerDev L = t.L[find_unit_layer(t, unit)];
+    if (!L.G) return;                            // a layer of another group this call
     const int lt = unit - L.unit_begin;
     if (L.fold) {
         snf_bwd_a(L, lt, lt);
@@ -529,6 +530,7 @@ __device__ __forceinline__ float layer_dot(const SnLayerDev &L, float *sh) {
 __global__ __launch_bounds__(256) void sn_bwd_b_kernel(SnTable t) {
     const int unit = blockIdx.x;
     const SnLayerDev L = t.L[find_unit_layer(t, unit)];
+    if (!L.G) return;
     const int lt = unit - L.unit_begin;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     __shared__ float sh_d[1];
@@ -918,12 +920,20 @@ smmd_status smmd_sn_grad_stats(const smmd_sn_layer *layers, int n_layers, void *
 smmd_status smmd_sn_weight_bwd(const smmd_sn_layer *layers, int n_layers, void *ws,
                                size_t ws_bytes, smmd_stream_t stream) {
     if (!layers || n_layers < 1 || n_layers > SMMD_SN_MAX_LAYERS) return SMMD_EINVAL;
-    for (int i = 0; i < n_layers; ++i)
-        if (!layers[i].G || !layers[i].gW || !layers[i].v || !layers[i].sigma) return SMMD_EINVAL;
+    int any = 0;
+    for (int i = 0; i < n_layers; ++i) {
+        if (!layers[i].G) continue;              // skipped (its gradient comes another call)
+        if (!layers[i].gW || !layers[i].v || !layers[i].sigma) return SMMD_EINVAL;
+        any = 1;
+    }
+    if (!any) return SMMD_EINVAL;
     if (!ws || ws_bytes < smmd_sn_workspace_bytes(layers, n_layers)) return SMMD_EWORKSPACE;
     hipStream_t s = (hipStream_t)stream;
     for (int first = 0; first < n_layers; first += SN_CHUNK) {
         const int count = (n_layers - first < SN_CHUNK) ? n_layers - first : SN_CHUNK;
+        int here = 0;
+        for (int i = first; i < first + count; ++i) here |= layers[i].G != nullptr;
+        if (!here) continue;
         SnTable t;
         if (!build_table(layers, first, count, (char *)ws + 256, t)) return SMMD_EINVAL;
         hipLaunchKernelGGL(sn_bwd_a_kernel, dim3(t.total_units), dim3(256), 0, s, t);

@@ -178,6 +178,11 @@ class GradBuckets:
                 self._launch(self.next)
         return fn
 
+    def notify(self, i):
+        """Tensor i's gradient is in place without autograd's accumulation
+        (the SN group backward writes it directly): count it as a hook would."""
+        self._hook(i)(self.opt.params[i])
+
     def _launch(self, b):
         lo, hi = self.buckets[b]
         self.next = b + 1

@@ -133,6 +133,7 @@ class MMD_GAN:
             self._broadcast_params()
             for opt in (self.d_optim, self.g_optim):
                 self._bucket_for(opt)
+            self._group_sn(self.sn_D, self.d_optim)
 
     # ------------------------------------------------------------------
     def _dist_group(self):
@@ -377,6 +378,31 @@ class MMD_GAN:
             bk[id(opt)] = GradBuckets(opt, self.group, clip_norm=clip)
         return bk[id(opt)]
 
+    def _group_sn(self, bank, opt):
+        """Data parallel: one SN autograd node per gradient bucket of ``opt``
+        (sn._SNGroup), whose backward writes dL/dW and dL/ds straight into the
+        flat gradient and counts them for their buckets, so a bucket's
+        all-reduce is issued as soon as its layers' gradients exist instead of
+        after the single SN backward at the end (and autograd adds nothing).
+        SMMD_SN_DIRECT=0 keeps the single node."""
+        import os
+        if not bank.entries or os.environ.get('SMMD_SN_DIRECT', '1') == '0':
+            return
+        bk = self._bucket_for(opt)
+        index = {id(p): i for i, p in enumerate(opt.params)}
+        if any(id(e.weight) not in index for e in bank.entries):
+            return
+        groups = [[j for j, e in enumerate(bank.entries) if lo <= index[id(e.weight)] < hi]
+                  for lo, hi in bk.buckets]
+
+        def direct(members, _bk=bk, _bank=bank, _index=index):
+            for j in members:
+                e = _bank.entries[j]
+                for p in (e.weight, e.scale):
+                    if p is not None and p.requires_grad and id(p) in _index:
+                        _bk.notify(_index[id(p)])
+        bank.set_groups(groups, direct)
+
     def _arm(self, opt):
         if self.world > 1:
             self._bucket_for(opt).arm()
@@ -409,6 +435,7 @@ class MMD_GAN:
             torch.autograd.grad(g_loss, self.g_vars, retain_graph=True)
         gd = self._gdirect()
         self.sn_D.arm_gdirect(gd)
+        self.sn_D.arm_direct(self.world > 1)        # the grouped SN nodes' direct writes
         try:
             if ref:
                 d_loss.backward(inputs=self.d_vars)
@@ -419,6 +446,7 @@ class MMD_GAN:
                     d_loss.backward()
         finally:
             self.sn_D.arm_gdirect(False)
+            self.sn_D.arm_direct(False)
         self._exchange(self.d_optim)
         return self._detach_step_state()
 

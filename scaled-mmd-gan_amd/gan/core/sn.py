@@ -39,41 +39,49 @@ def truncated_normal_(t, std=1.0):
     return t
 
 
+def _launch_refresh(bank, update_u, flags, Ws, ss):
+    """The refresh launch set (smmd_sn_power_iter_ex): every layer's W_eff or
+    pool-folded W'.  Returns (outs, folds)."""
+    n = len(bank.entries)
+    outs = []
+    arr = (_lib.SnLayer * n)()
+    for i, (e, W, s) in enumerate(zip(bank.entries, Ws, ss)):
+        # each output channel's K values must be contiguous: true for the
+        # default and the channels_last layouts (SN is invariant to the
+        # order of K, see the module docstring)
+        if _memfmt(W) is None:
+            raise ValueError('SN weight %d is neither contiguous nor channels_last' % i)
+        fold = _folds(e, W)
+        W_eff = (torch.empty(W.shape[0], W.shape[1], 4, 4, device=W.device,
+                             dtype=torch.float32) if fold else torch.empty_like(W))
+        outs.append(W_eff)
+        L = arr[i]
+        L.fold = 1 if fold else 0
+        L.W = W.data_ptr()
+        L.W_eff = W_eff.data_ptr()
+        L.u = e.u.data_ptr()
+        L.v = e.v.data_ptr()
+        L.sigma = e.sigma.data_ptr()
+        L.s = s.data_ptr() if s is not None and s.numel() > 0 else None
+        L.N, L.K = e.N, e.K
+    dev = Ws[0].device
+    lib = _lib.lib()
+    args = (arr, n, bank.num_iters, SN_EPS, 1 if update_u else 0, flags, _lib.ptr(bank.ws),
+            bank.ws.numel(), _lib.stream_handle(dev))
+    with _lib.timed('smmd_sn_power_iter'):
+        st = lib.smmd_sn_power_iter_ex(*args)
+    _lib.check(st, 'smmd_sn_power_iter_ex')
+    return outs, [bool(a.fold) for a in arr]
+
+
 class _SNBatch(torch.autograd.Function):
     @staticmethod
     def forward(ctx, bank, update_u, flags, *tensors):
         n = len(bank.entries)
         Ws, ss = tensors[:n], tensors[n:]
-        outs = []
-        arr = (_lib.SnLayer * n)()
-        for i, (e, W, s) in enumerate(zip(bank.entries, Ws, ss)):
-            # each output channel's K values must be contiguous: true for the
-            # default and the channels_last layouts (SN is invariant to the
-            # order of K, see the module docstring)
-            if _memfmt(W) is None:
-                raise ValueError('SN weight %d is neither contiguous nor channels_last' % i)
-            fold = _folds(e, W)
-            W_eff = (torch.empty(W.shape[0], W.shape[1], 4, 4, device=W.device,
-                                 dtype=torch.float32) if fold else torch.empty_like(W))
-            outs.append(W_eff)
-            L = arr[i]
-            L.fold = 1 if fold else 0
-            L.W = W.data_ptr()
-            L.W_eff = W_eff.data_ptr()
-            L.u = e.u.data_ptr()
-            L.v = e.v.data_ptr()
-            L.sigma = e.sigma.data_ptr()
-            L.s = s.data_ptr() if s is not None and s.numel() > 0 else None
-            L.N, L.K = e.N, e.K
-        dev = Ws[0].device
-        lib = _lib.lib()
-        args = (arr, n, bank.num_iters, SN_EPS, 1 if update_u else 0, flags, _lib.ptr(bank.ws),
-                bank.ws.numel(), _lib.stream_handle(dev))
-        with _lib.timed('smmd_sn_power_iter'):
-            st = lib.smmd_sn_power_iter_ex(*args)
-        _lib.check(st, 'smmd_sn_power_iter_ex')
+        outs, folds = _launch_refresh(bank, update_u, flags, Ws, ss)
         ctx.bank = bank
-        ctx.folds = [bool(a.fold) for a in arr]
+        ctx.folds = folds
         ctx.save_for_backward(*Ws, *ss)
         return tuple(outs)
 
@@ -161,6 +169,29 @@ class _SNBatch(torch.autograd.Function):
         return (None, None, None) + (None,) * (2 * n)
 
 
+class _SNGroup(torch.autograd.Function):
+    """One gradient bucket's SN layers as their own autograd node (data
+    parallel runs, ``SpectralNormBank.set_groups``): the refresh ran once for
+    all layers (the outputs are the bank's), but each group's backward fires
+    as soon as ITS layers' W_eff gradients are complete, so its bucket's
+    all-reduce is issued while the rest of the backward runs."""
+
+    @staticmethod
+    def forward(ctx, bank, members, *tensors):
+        k = len(members)
+        ctx.bank, ctx.members = bank, members
+        ctx.save_for_backward(*tensors)
+        return tuple(bank._fresh[i] for i in members) if k > 1 else bank._fresh[members[0]]
+
+    @staticmethod
+    def backward(ctx, *grads):
+        bank, members = ctx.bank, ctx.members
+        k = len(members)
+        saved = ctx.saved_tensors
+        res = bank._group_backward(members, saved[:k], saved[k:], grads)
+        return (None, None) + res
+
+
 def _memfmt(W):
     if W.is_contiguous():
         return torch.contiguous_format
@@ -218,6 +249,14 @@ class SpectralNormBank:
         # (G tensors, folds) in _gd_pending for the optimizer's fused update
         self._gd_armed = False
         self._gd_pending = None
+        # data parallel: the layers split into autograd groups (one per
+        # gradient bucket, set_groups) and, while armed, their dL/dW and dL/ds
+        # written straight into the optimizer's flat gradient (_direct)
+        self.groups = None
+        self._direct = None
+        self._direct_armed = False
+        self._fresh = None
+        self._folds = None
         self._alloc_ws()
 
     def _state_token(self):
@@ -260,13 +299,92 @@ class SpectralNormBank:
         _lib.require_cuda(*Ws)
         ready = self._p1_token is not None and self._p1_token == self._state_token()
         self._p1_token = None
-        outs = _SNBatch.apply(self, bool(update_u), _lib.SN_P1_READY if ready else 0, *Ws, *ss)
+        flags = _lib.SN_P1_READY if ready else 0
+        if (self.groups is not None and torch.is_grad_enabled()
+                and any(t.requires_grad for t in list(Ws) + list(ss))):
+            with torch.no_grad():
+                fresh, self._folds = _launch_refresh(self, bool(update_u), flags, Ws, ss)
+            self._fresh = fresh
+            outs = [None] * len(Ws)
+            for members in self.groups:
+                m = tuple(members)
+                r = _SNGroup.apply(self, m, *[Ws[i] for i in m], *[ss[i] for i in m])
+                r = r if isinstance(r, tuple) else (r,)
+                for i, t in zip(m, r):
+                    outs[i] = t
+            self._fresh = None
+        else:
+            outs = _SNBatch.apply(self, bool(update_u), flags, *Ws, *ss)
         for e, w in zip(self.entries, outs):
             if w.shape != e.weight.shape:        # the pool-folded 4 x 4 filter
                 e.module.w_eff, e.module.w_fold = None, w
             else:
                 e.module.w_eff, e.module.w_fold = w, None
         return list(outs)
+
+    def set_groups(self, groups, direct=None):
+        """Split the bank's autograd node into ``groups`` (lists of layer
+        indices, in the order their gradients should be ready: the gradient
+        buckets' order).  ``direct(members)``: called after a group's backward
+        wrote its gradients into the parameters' .grad views (the armed
+        direct mode), e.g. to issue the bucket's all-reduce."""
+        groups = [list(g) for g in groups if len(g)] if groups else None
+        if groups:
+            covered = {i for g in groups for i in g}
+            rest = [i for i in range(len(self.entries)) if i not in covered]
+            if rest:
+                groups.append(rest)
+        self.groups = groups
+        self._direct = direct
+
+    def arm_direct(self, on=True):
+        """Arm the direct-write group backward for the next backward pass."""
+        self._direct_armed = bool(on) and self._direct is not None
+
+    def _group_backward(self, members, Ws, ss, grads):
+        """smmd_sn_weight_bwd for the group's layers (the full layer array with
+        the others' G NULL: the workspace is carved by the whole array)."""
+        n = len(self.entries)
+        arr = (_lib.SnLayer * n)()
+        direct = self._direct_armed
+        outs_W, outs_s, keep = [], [], []
+        for i, e in enumerate(self.entries):
+            L = arr[i]
+            L.N, L.K = e.N, e.K
+            L.W = e.weight.data_ptr()
+            L.u = e.u.data_ptr()
+            L.v = e.v.data_ptr()
+            L.sigma = e.sigma.data_ptr()
+            L.fold = 1 if self._folds[i] else 0
+        for j, i in enumerate(members):
+            e, W, s, G = self.entries[i], Ws[j], ss[j], grads[j]
+            fold = self._folds[i]
+            if G is None:
+                G = (torch.zeros(W.shape[0], W.shape[1], 4, 4, device=W.device,
+                                 dtype=torch.float32) if fold else torch.zeros_like(W))
+            G = G.contiguous() if fold else G.contiguous(memory_format=_memfmt(W))
+            keep.append(G)
+            has_s = s is not None and s.numel() > 0
+            if direct:
+                gW, gs = e.weight.grad, (e.scale.grad if has_s else None)
+            else:
+                gW = torch.empty_like(W)
+                gs = torch.empty(1, device=W.device, dtype=torch.float32) if has_s else None
+            outs_W.append(None if direct else gW)
+            outs_s.append(None if (direct or gs is None) else gs.view_as(s))
+            L = arr[i]
+            L.W = W.data_ptr()
+            L.s = s.data_ptr() if has_s else None
+            L.G = G.data_ptr()
+            L.gW = gW.data_ptr()
+            L.gs = gs.data_ptr() if gs is not None else None
+        args = (arr, n, _lib.ptr(self.ws), self.ws.numel(), _lib.stream_handle(Ws[0].device))
+        with _lib.timed('smmd_sn_weight_bwd'):
+            st = _lib.lib().smmd_sn_weight_bwd(*args)
+        _lib.check(st, 'smmd_sn_weight_bwd')
+        if direct:
+            self._direct(members)
+        return tuple(outs_W) + tuple(outs_s)
 
     def arm_gdirect(self, on=True):
         """Arm (or disarm) the G-direct backward for the next backward pass."""

@@ -132,6 +132,52 @@ class FakeLib:
                                       sqrt_scale, go, None, gjac, gfeat, stream)
         return 0
 
+    # spectral norm (fold = 0 layers): u' of each layer kept per workspace, as
+    # the library keeps it in ws between the refresh and the backward
+    _ucur = {}
+
+    def smmd_sn_workspace_bytes(self, arr, n):
+        return 256
+
+    def _layer(self, L):
+        N, K = L.N, L.K
+        W = _arr(L.W, N * K).reshape(N, K).astype(np.float64)
+        s = float(_arr(L.s, 1)[0]) if L.s else 1.0
+        return N, K, W, s
+
+    def smmd_sn_power_iter_ex(self, arr, n, iters, eps, update_u, flags, ws, wsb, stream):
+        key = ws.value if isinstance(ws, ctypes.c_void_p) else int(ws or 0)
+        for i in range(n):
+            L = arr[i]
+            assert not L.fold, 'fake_lib: fold layers are GPU-only'
+            N, K, W, s = self._layer(L)
+            sigma, u1, v1 = O.spectral_norm_rows(W, _arr(L.u, N).astype(np.float64), iters)
+            _arr(L.v, K)[:] = v1
+            _arr(L.sigma, 1)[0] = sigma
+            if update_u:
+                _arr(L.u, N)[:] = u1
+            self._ucur[(key, i)] = u1
+            if L.W_eff:
+                _arr(L.W_eff, N * K)[:] = ((W.astype(np.float32) / np.float32(sigma))
+                                           * np.float32(s)).ravel()
+        return 0
+
+    def smmd_sn_weight_bwd(self, arr, n, ws, wsb, stream):
+        key = ws.value if isinstance(ws, ctypes.c_void_p) else int(ws or 0)
+        for i in range(n):
+            L = arr[i]
+            if not L.G:
+                continue
+            N, K, W, s = self._layer(L)
+            G = _arr(L.G, N * K).reshape(N, K)
+            sigma = float(_arr(L.sigma, 1)[0])
+            gW, gs = O.sn_weight_backward(W, s, sigma, self._ucur[(key, i)],
+                                          _arr(L.v, K).astype(np.float64), G)
+            _arr(L.gW, N * K)[:] = gW.ravel()
+            if L.gs:
+                _arr(L.gs, 1)[0] = gs
+        return 0
+
     def smmd_opt_workspace_bytes(self, offs, n):
         return 256
 

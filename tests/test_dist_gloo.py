@@ -325,3 +325,109 @@ def test_bucket_layout_agrees_across_ranks():
     res = _run(_worker_bucket_env, world=2)
     (r0, b0, l0), (r1, b1, l1) = sorted(res)
     assert b0 == b1 == int(0.0001 * (1 << 20)) and l0 == l1 and len(l0) > 1
+
+
+def _sn_net():
+    from gan.core.snops import Linear
+    torch.manual_seed(9)
+    return torch.nn.ModuleList([Linear(6, 5, with_sn=True, with_learnable_sn_scale=True),
+                                Linear(5, 4, with_sn=True, with_learnable_sn_scale=True),
+                                Linear(4, 1, with_sn=True, with_learnable_sn_scale=True)])
+
+
+def _sn_forward(net, x):
+    h = torch.tanh(net[0](x))
+    h = torch.tanh(net[1](h))
+    return net[2](h)
+
+
+def _sn_setup():
+    from gan.core.optim import FlatAdam
+    from gan.core.sn import SpectralNormBank
+    from gan.core.snops import sn_modules
+    net = _sn_net()
+    bank = SpectralNormBank(sn_modules(net))
+    g = torch.Generator().manual_seed(4)
+    for e in bank.entries:
+        e.u.copy_(torch.randn(e.N, generator=g))
+    opt = FlatAdam([p for p in net.parameters() if p.requires_grad], lr=1e-3, clip_norm=1.0)
+    return net, bank, opt
+
+
+def _sn_loss(net, bank, rank):
+    x = torch.tensor(np.random.default_rng(300 + rank).standard_normal((3, 6)),
+                     dtype=torch.float32)
+    bank.refresh(update_u=False)
+    return (_sn_forward(net, x) ** 2).sum().mul(3.0)
+
+
+def _worker_sn_buckets(rank, world, port, mode, q):
+    _init(rank, world, port)
+    from gan.core.collectives import GradBuckets
+    from gan.core.model import MMD_GAN
+    net, bank, opt = _sn_setup()
+    m = MMD_GAN.__new__(MMD_GAN)
+    m.world, m.group, m.dp_mode = world, dist.group.WORLD, mode
+    m._buckets = {id(opt): GradBuckets(opt, m.group, bucket_bytes=64,
+                                       clip_norm=opt.clip_norm if mode == 'tower' else 0.0)}
+    m._group_sn(bank, opt)
+    assert bank.groups is not None and len(bank.groups) >= 2
+    opt.zero_grad()
+    m._arm(opt)
+    loss = _sn_loss(net, bank, rank)
+    fired = []
+    orig = bank._direct
+    bank._direct = lambda members: (fired.append(tuple(members)), orig(members))
+    bank.arm_direct(True)
+    cnt = _Count()
+    loss.backward()
+    bank.arm_direct(False)
+    bk = m._buckets[id(opt)]
+    issued = len(bk.launch_log)
+    order = list(bk.launch_log)
+    m._exchange(opt)
+    q.put((rank, np.concatenate([p.detach().numpy().ravel() for p in net.parameters()]),
+           issued, len(bk.buckets), cnt.n['all_reduce'], order, fired))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world', [2, 4])
+@pytest.mark.parametrize('mode', ['tower', 'global'])
+def test_sn_buckets_issued_inside_backward(mode, world, monkeypatch):
+    """Data parallel with SN layers: one SN autograd node per gradient bucket
+    (sn._SNGroup) writes dL/dW, dL/ds straight into the flat gradient and
+    counts them for their buckets, so every bucket -- the SN weights' ones
+    included -- is issued from inside the backward, in bucket order, one
+    all-reduce each; the update equals the reference's exchange semantics
+    (tower: per-rank clip, mean; global: sum, clip; model.py:444-456) on the
+    per-rank gradients of the single-node SN backward."""
+    import fake_lib
+    from gan.core import _lib
+    f = fake_lib.FakeLib()
+    monkeypatch.setattr(_lib, '_lib', f)
+    monkeypatch.setattr(_lib, 'lib', lambda: f)
+    monkeypatch.setattr(_lib, 'require_cuda', lambda *t: None)
+    monkeypatch.setattr(_lib, 'stream_handle', lambda device=None: None)
+    monkeypatch.setattr(_lib, 'workspace', lambda tag, nbytes, device: torch.zeros(
+        max(int(nbytes), 256), dtype=torch.uint8))
+    grads, params = [], None
+    for r in range(world):                       # one process, the single SN node
+        net, bank, opt = _sn_setup()
+        opt.zero_grad()
+        _sn_loss(net, bank, r).backward()
+        grads.append([p.grad.detach().numpy().astype(np.float64).ravel().copy()
+                      for p in net.parameters()])
+        params = [p.detach().numpy().astype(np.float64).ravel().copy()
+                  for p in net.parameters()]
+    expect = []
+    for i in range(len(params)):
+        gs = [g[i] for g in grads]
+        g = (np.mean([O.clip_by_norm(x, 1.0) for x in gs], axis=0) if mode == 'tower'
+             else O.clip_by_norm(sum(gs), 1.0))
+        expect.append(O.adam_step(params[i], 0, 0, g, 1, 1e-3)[0])
+    res = _run(_worker_sn_buckets, mode, world=world)
+    for rank, flat, issued, nb, n_ar, order, fired in res:
+        assert nb >= 3 and issued == nb and order == list(range(nb)) and n_ar == nb
+        assert len(fired) >= 2                   # several SN groups, each from the backward
+        np.testing.assert_allclose(flat, np.concatenate(expect), rtol=2e-5, atol=1e-7)
