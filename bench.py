@@ -52,6 +52,37 @@ TRANS_SLOTS = 4                # v_exp_f32 / v_log_f32: quarter rate (MI355X_MIC
 BATCH = 64
 
 PMC_TRAFFIC = os.path.join(ROOT, 'profiles', 'r07', 'pmc_traffic.json')
+# executed FLOPs per kernel class over whole 5D+1G cycles of this workload
+# (tools/gpu_step_pmc.sh -> tools/step_flops_pmc.py: rocprofv3 SQ_INSTS_VALU_*
+# and SQ_INSTS_VALU_MFMA_MOPS_F32 counters + a kernel trace)
+STEP_PMC = os.path.join(ROOT, 'profiles', 'r07', 'step_flops_pmc.json')
+
+
+def step_counters(ms_step):
+    """The counter-based step roofline: executed TFLOP per step
+    from the committed PMC file, its rate over the GPU-busy time it was
+    measured with and over this run's step time, and per kernel class
+    (Winograd, implicit-GEMM fwd / bwd-data / wrw, transposes, elementwise,
+    the library) the time share, executed TFLOP/s and fraction of the fp32
+    peak."""
+    try:
+        with open(STEP_PMC) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    tf_step = d['executed_tflop_per_step']
+    out = {'source': os.path.relpath(STEP_PMC, ROOT),
+           'executed_tflop_per_step': tf_step,
+           'executed_tflops_over_gpu_busy': d['executed_tflops_over_busy'],
+           'frac_of_fp32_peak_over_gpu_busy': d['frac_of_fp32_peak_over_busy'],
+           'gpu_busy_ms_per_step_measured': d['gpu_busy_ms_per_step'],
+           'executed_tflops_this_run': round(tf_step / (ms_step * 1e-3), 2),
+           'frac_of_fp32_peak_this_run': round(tf_step / (ms_step * 1e-3) / FP32_PEAK_TFS, 4),
+           'classes': {k: {q: v.get(q) for q in ('ms_per_step', 'time_frac',
+                                                   'executed_gflop_per_step', 'tflops',
+                                                   'frac_of_fp32_peak')}
+                       for k, v in d['classes'].items()}}
+    return out
 PMC_FALLBACK = os.path.join(ROOT, 'profiles', 'r06', 'pmc_traffic.json')
 
 # SURVEY 8(a): the hot-path rows a1-a9 and the library entry points that
@@ -778,7 +809,9 @@ def main():
                        note='algorithmic = the reference\'s literal conv layers (no fold, '
                             'direct-conv MAC count); the product runs Winograd and folded '
                             'stride-2 convs, which execute fewer MACs, so this is a '
-                            'work-rate against the fp32 peak, not a utilisation counter')
+                            'work-rate against the fp32 peak, not a utilisation counter; '
+                            '`counters` holds the executed-FLOP figures',
+                       counters=step_counters(ms_step))
 
     sweep = None
     if args.mmd_sweep:

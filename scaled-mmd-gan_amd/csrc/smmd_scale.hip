@@ -203,6 +203,7 @@ struct AdamArgs {
     const float *lr_t_dev;  // non-NULL: lr_t read at execution time (graph replay)
     float clip;             // > 0: per-tensor clip_by_norm
     int vec;
+    int norm_inblock;       // every tensor one update block: its norm summed in the block
     AdamK k;                // k.f set per tensor
 };
 
@@ -223,9 +224,24 @@ __device__ __forceinline__ void opt_adam_block(const OptTable &t, int b, const A
     const int vec = a.vec;
     __shared__ float sh[1];
     AdamK k = adam_k(a);
-    k.f = (a.clip > 0.f) ? clip_factor(t, ti, a.part, a.clip, sh) : 1.f;
     int64_t lo, hi;
     opt_range(t, ti, b, lo, hi);
+    if (!(a.clip > 0.f)) {
+        k.f = 1.f;
+    } else if (a.norm_inblock) {
+        // the whole tensor is this block's range: its norm here, no norm pass
+        __shared__ double red[4];
+        float acc = 0.f;
+        for (int64_t i = lo + threadIdx.x; i < hi; i += 256) {
+            const float x = g[i] * k.gscale;
+            acc = fmaf(x, x, acc);
+        }
+        const float ss = (float)block_sum<4>((double)acc, red);
+        const float inv = (ss > 0.f) ? rsqrtf(ss) : INFINITY;
+        k.f = a.clip * fminf(inv, 1.f / a.clip);
+    } else {
+        k.f = clip_factor(t, ti, a.part, a.clip, sh);
+    }
     if (vec && hi - lo == OPT_UP_CHUNK) {     // full block: 4 x OPT_UP_IT float4 loads in flight
         const int64_t b4 = lo / 4 + threadIdx.x;
         float4 *p4 = reinterpret_cast<float4 *>(p) + b4;
@@ -313,6 +329,7 @@ static AdamArgs adam_args(float *p, const float *g, float *m, float *v, const vo
     a.lr_t_dev = nullptr;
     a.clip = clip;
     a.vec = vec;
+    a.norm_inblock = 0;
     a.k.gscale = gscale;
     a.k.f = 1.f;
     a.k.lr_t = (float)lr_t;
@@ -586,12 +603,19 @@ static smmd_status adam_flat_sn_impl(float *param, const float *grad, float *m, 
     SnAdamTable snt;
     const smmd_status r = sn_adam_table(layers, sn_tensor, n_layers, h, sn_ws, sn_ws_bytes, snt);
     if (r != SMMD_OK) return r;
-    if (clip_norm > 0.f)
+    // G-direct with every other tensor within one update block (the critics'
+    // biases and scales): each block sums its tensor's norm itself and the
+    // norm-pass launch goes away
+    int inblock = gdirect;
+    for (int i = 0; i < n_tensors && inblock; ++i)
+        if (!skip[i] && offsets[i + 1] - offsets[i] > OPT_UP_CHUNK) inblock = 0;
+    if (clip_norm > 0.f && !inblock)
         hipLaunchKernelGGL(opt_sqsum_kernel, dim3(ts.total_blocks), dim3(256), 0, s, ts, grad,
                            grad_scale, vec, (double *)ws);
     AdamArgs aa = adam_args(param, grad, m, v, ws, grad_scale, clip_norm, lr_t, beta1, beta2, eps,
                             vec);
     aa.lr_t_dev = lr_t_dev;
+    aa.norm_inblock = inblock;
     const dim3 grid(snt.total_tiles + tu.total_blocks);
     const int hg = sn_adam_groups();
     if (gdirect) {     // H = 2: the fold staging of H = 1 would not fit beside it
