@@ -1,6 +1,6 @@
-// smmd_bnrelu.hip -- training-mode batch norm + ReLU of the generator's
-// forward when no gradient is taken (every critic step runs G(z) that way),
-// gfx950 / MI355X.
+// smmd_bnrelu.hip -- training-mode batch norm + ReLU of the generator
+// (gfx950 / MI355X): the forward, with or without the record its backward
+// needs, and that backward (the generator step).
 //
 // Reference: tf.layers.batch_normalization(training=True, momentum=0.9,
 // epsilon=1e-5) then tf.nn.relu (gan/core/snops.py:31-40 batch_norm,

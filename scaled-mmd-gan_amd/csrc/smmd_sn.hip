@@ -24,6 +24,13 @@
 // (arrival tickets, write-through partials).  It removes the R2 launch but puts
 // each reducer's serial chain of dependent L2 loads at the tail of its kernel:
 // P1 11 -> 19 us, P2 + R2 20 -> 34 us on the SNResNet-64 critic.
+// Also measured and not kept: P2 + R2 + P3 as ONE launch that reads W once
+// (each tile keeps W in registers, row-tile and layer tickets, sigma
+// broadcast behind a generation flag that every tile polls, a timeout rescue
+// for non-resident grids): 57 us against 35 us for P2 + R2 + P3.  With no
+// wait it took 33 us: the re-read P3 saves is served by the Infinity Cache
+// (W is 40 MB), while the hand-off chain (about 8 dependent hops of ~2-3 us
+// under load) costs 25 us (profiles/r08/sn_p23_experiment.txt).
 #include "smmd_sn_tile.hpp"
 
 #include <stdlib.h>
@@ -48,12 +55,6 @@ struct SnLayerDev {
     float *ggp;      // ws [units] partial ||G||^2 (adjoint G for fold layers)
     float *ugvp;     // ws [units] partial u'^T G v
     float *stats;    // ws [16] smmd_sn_grad_stats record (SnGradStats)
-    unsigned *sync;  // ws [nrt + 3] fused refresh: row-tile tickets, layer ticket,
-                     // departures, sigma generation (sn_p23_kernel)
-    double *apart;   // ws [nct] ||v_raw||^2 over each column tile
-    double *bpart;   // ws [nrt] ||W v_raw||^2 over each row tile
-    float *rec;      // ws [4] {sigma, ||v_raw|| + eps, ||u_raw|| + eps} published to the layer
-    unsigned *gaveup;   // ws [tiles] tiles whose wait timed out (their duties left)
     int N, K, nrt, nct;
     int nctp;        // nct rounded up to a multiple of 4
     int tile_begin;
@@ -70,12 +71,9 @@ struct SnTable {
     int iter;        // current power iteration (0 -> read layer.u)
     int last_iter;
     int update_u;
-    int giveup;      // sn_p23_kernel test hook: waiting tiles give up at once
-    int dbg;         // TEMP timing knobs
     float eps;
     SnLayerDev L[SN_CHUNK];
 };
-static_assert(sizeof(SnTable) <= 4096, "the layer table is passed as a kernel argument");
 
 // Layer of a tile: static-index scan of the (monotone) tile_begin fields, then
 // readfirstlane so the index is provably wave-uniform and the descriptor is
@@ -169,28 +167,6 @@ __device__ __forceinline__ void snf_adjoint(const float *s16, int f, float (&g)[
     }
 }
 
-// the 4 x 4 pool-folded filter of one 3 x 3 filter k (block.py:63-66):
-// o[s][t] = 1/4 sum_{a,b} k[s-a][t-b], the sums in (a, b) order
-__device__ __forceinline__ void fold16(const float (&k)[9], float (&o)[16]) {
-#pragma clang fp contract(off)
-#pragma unroll
-    for (int si = 0; si < 4; ++si) {
-#pragma unroll
-        for (int ti = 0; ti < 4; ++ti) {
-            float acc = 0.f;
-#pragma unroll
-            for (int a = 0; a < 2; ++a) {
-#pragma unroll
-                for (int b = 0; b < 2; ++b) {
-                    const int u = si - a, v = ti - b;
-                    if (u >= 0 && u < 3 && v >= 0 && v < 3) acc += k[u * 3 + v];
-                }
-            }
-            o[si * 4 + ti] = acc * 0.25f;   // block.py:65 mean
-        }
-    }
-}
-
 // P3 of a fold layer: W' = fold((W / sigma) * s) for the block's filters.
 // No contraction: each W_bar element is rounded before the sums (an fma of
 // the product into the sum would differ in the last bit), so W' is
@@ -208,12 +184,25 @@ __device__ __forceinline__ void snf_p3(const SnLayerDev &L, int unit) {
     const float s = L.s ? L.s[0] : 1.f;
     const int f = threadIdx.x;
     if (f < nb) {
-        float k[9], o[16];
+        float k[9];
 #pragma unroll
         for (int j = 0; j < 9; ++j) k[j] = (s9[f * 9 + j] / sigma) * s;   // sn.py:43, snops.py:84
-        fold16(k, o);
 #pragma unroll
-        for (int j = 0; j < 16; ++j) s16[j * SNF_S16 + f] = o[j];
+        for (int si = 0; si < 4; ++si) {
+#pragma unroll
+            for (int ti = 0; ti < 4; ++ti) {
+                float acc = 0.f;
+#pragma unroll
+                for (int a = 0; a < 2; ++a) {
+#pragma unroll
+                    for (int b = 0; b < 2; ++b) {
+                        const int u = si - a, v = ti - b;
+                        if (u >= 0 && u < 3 && v >= 0 && v < 3) acc += k[u * 3 + v];
+                    }
+                }
+                s16[(si * 4 + ti) * SNF_S16 + f] = acc * 0.25f;   // block.py:65 mean
+            }
+        }
     }
     __syncthreads();
     snf_store16(L.W_eff + q0 * 16, s16, nb);
@@ -495,362 +484,6 @@ __global__ __launch_bounds__(256) void sn_p3_kernel(SnTable t) {
     }
 }
 
-// ---- fused refresh: P2 + R2 + P3 in one launch (sn_p23_kernel) -------------
-// The launch set above reads W twice: P2, then P3 once sigma is known.  Here
-// a tile keeps its W in registers across the layer-wide reduction.  After
-// its P2 work it takes up to two tickets: its row tile's (the last of the
-// row tile's nct tiles sums the 32 rows of q2 into u_raw, in q2_row_sum's
-// order, and the ||u_raw||^2 partial) and the layer's (arrivals: the row
-// tile 0 tiles with the ||v_raw||^2 partials of their columns, and the row
-// tiles' last takers).  The layer's last taker forms nv, nu and sigma as
-// sn_layer_epilogue does and publishes them; every tile of the layer,
-// having polled for them, writes W_eff (or the folded W') from its
-// registers, and v and u' where it owns them.
-//
-// Every hand-off is MI355X_MICROARCH's row 1: write-through (sc1) stores,
-// each storing wave drained, a workgroup barrier, one lane's agent-scope add;
-// the reader is the workgroup whose add came last, or whose poll matched,
-// and it loads every handed-off word with sc1 loads.  Tickets are reset by
-// their last taker; the sigma flag is a generation (never reset), read by
-// each tile before it arrives anywhere.
-//
-// Residency: the host launches this only when the grid fits the chip at
-// the occupancy query's blocks per CU.  A tile still waiting after
-// SN23_WAIT (another process on the GPU, say) gives up: it records itself
-// in gaveup and departs, and the layer's last departing tile does the duties
-// of every tile that gave up -- so every wave ends and every output is
-// written whatever the residency.
-constexpr uint64_t SN23_WAIT = 20000;   // s_memrealtime ticks (100 MHz): 200 us
-
-__device__ __forceinline__ unsigned ld_sc1(const unsigned *p) {
-    return __hip_atomic_load(const_cast<unsigned *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float ld_sc1(const float *p) {
-    return __hip_atomic_load(const_cast<float *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double ld_sc1(const double *p) {
-    return __hip_atomic_load(const_cast<double *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void store_wt(unsigned *p, unsigned x) {
-    __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned ticket_add(unsigned *p, unsigned x) {
-    return __hip_atomic_fetch_add(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// W_eff = (W / sigma) * s of the thread's rows and columns (sn_p3_kernel's)
-__device__ __forceinline__ void p23_store_tile(const SnLayerDev &L, int r0, int c0,
-                                               const float4 (&wt)[SN_RPW], float sigma,
-                                               float s) {
-    const bool full_cols = (c0 + 3 < L.K);
-#pragma unroll
-    for (int i = 0; i < SN_RPW; ++i) {
-        const int r = r0 + i;
-        if (r >= L.N) break;
-        float4 o;
-        o.x = (wt[i].x / sigma) * s;
-        o.y = (wt[i].y / sigma) * s;
-        o.z = (wt[i].z / sigma) * s;
-        o.w = (wt[i].w / sigma) * s;
-        float *p = L.W_eff + (size_t)r * L.K + c0;
-        if (L.vec && full_cols) {
-            *reinterpret_cast<float4 *>(p) = o;
-        } else {
-            if (c0 + 0 < L.K) p[0] = o.x;
-            if (c0 + 1 < L.K) p[1] = o.y;
-            if (c0 + 2 < L.K) p[2] = o.z;
-            if (c0 + 3 < L.K) p[3] = o.w;
-        }
-    }
-}
-
-// The folded W' of the filters that START in this tile's columns: each wave
-// stages one of its rows at a time in LDS (its float4s plus the <= 8 columns
-// of the next tile a filter may run into: `halo`, lane l holding row l / 8's
-// column 256 + l % 8, loaded with the tile), then lane j folds filter fa + j
-// (<= 29 filters per row).  The arithmetic is snf_p3's, so W' has its bits.
-constexpr int P23_ROW = SN_TC + 12;
-
-__device__ __forceinline__ float p23_load_halo(const SnLayerDev &L, int ct, int r0) {
-    const int lane = threadIdx.x & 63;
-    const int r = r0 + (lane >> 3), c = (ct + 1) * SN_TC + (lane & 7);
-    return (L.fold && r < L.N && c < L.K) ? L.W[(size_t)r * L.K + c] : 0.f;
-}
-
-__device__ __forceinline__ void p23_store_fold(const SnLayerDev &L, int ct, int r0,
-                                               const float4 (&wt)[SN_RPW], float halo,
-                                               float sigma, float s) {
-#pragma clang fp contract(off)
-    __shared__ float rowbuf[4][P23_ROW];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    float *rb = rowbuf[w];
-    const int cb = ct * SN_TC;
-    const int ce = min(cb + SN_TC, L.K);
-    const int fa = (cb + 8) / 9;
-    const int nfl = (ce + 8) / 9 - fa;
-    const int f = fa + lane;
-    const int o = 9 * f - cb;                    // the filter's first column in the tile
-#pragma unroll
-    for (int i = 0; i < SN_RPW; ++i) {
-        const int r = r0 + i;
-        if (r >= L.N) break;                     // wave-uniform
-        *reinterpret_cast<float4 *>(rb + lane * 4) = wt[i];
-        if ((lane >> 3) == i) rb[SN_TC + (lane & 7)] = halo;
-        __builtin_amdgcn_wave_barrier();
-        if (lane < nfl) {
-            float k[9], out[16];
-#pragma unroll
-            for (int j = 0; j < 9; ++j) k[j] = (rb[o + j] / sigma) * s;   // sn.py:43, snops.py:84
-            fold16(k, out);
-            float4 *dst = reinterpret_cast<float4 *>(L.W_eff + ((size_t)r * L.nfc + f) * 16);
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                dst[q] = make_float4(out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]);
-        }
-        __builtin_amdgcn_wave_barrier();
-    }
-}
-
-__device__ __forceinline__ void p23_store(const SnLayerDev &L, int ct, int r0, int c0,
-                                          const float4 (&wt)[SN_RPW], float halo, float sigma) {
-    if (!L.W_eff) return;
-    const float s = L.s ? L.s[0] : 1.f;
-    if (L.fold) p23_store_fold(L, ct, r0, wt, halo, sigma, s);
-    else p23_store_tile(L, r0, c0, wt, sigma, s);
-}
-
-// The layer's last departing tile: the duties of the tiles that gave up
-// (rare: only when the grid was not all resident).  Their handed-off words
-// (v_raw, u_raw, the record) were stored write-through before their
-// departures, so sc1 loads read them.
-__device__ __forceinline__ void sn_p23_rescue(const SnTable &t, const SnLayerDev &L) {
-    __shared__ unsigned gv[256];
-    __shared__ float rc[3];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int ntile = L.nrt * L.nct;
-    if (threadIdx.x == 0) {
-        rc[0] = ld_sc1(L.rec + 0);
-        rc[1] = ld_sc1(L.rec + 1);
-        rc[2] = ld_sc1(L.rec + 2);
-    }
-    for (int j0 = 0; j0 < ntile; j0 += 256) {
-        __syncthreads();
-        gv[threadIdx.x] = (j0 + (int)threadIdx.x < ntile) ? ld_sc1(L.gaveup + j0 + threadIdx.x) : 0u;
-        __syncthreads();
-        const float sigma = rc[0], nv = rc[1], nu = rc[2];
-        for (int jj = 0; jj < 256 && j0 + jj < ntile; ++jj) {
-            const unsigned g = gv[jj];
-            if (!g) continue;
-            const int lt = j0 + jj;
-            const int rt = lt / L.nct, ct = lt % L.nct;
-            const int r0 = rt * SN_TR + w * SN_RPW;
-            const int c0 = ct * SN_TC + lane * 4;
-            float4 wt[SN_RPW];
-            load_tile(L.W, L.N, L.K, L.vec, r0, c0, wt);
-            const float halo = p23_load_halo(L, ct, r0);
-            p23_store(L, ct, r0, c0, wt, halo, sigma);
-            const int c = ct * SN_TC + threadIdx.x;
-            if (rt == 0 && c < L.K) L.v[c] = ld_sc1(L.vraw + c) / nv;
-            const int n = rt * SN_TR + threadIdx.x;
-            if ((g & 2u) && threadIdx.x < SN_TR && n < L.N) {
-                const float un = (ld_sc1(L.ucur + n) / nv) / nu;
-                L.ucur[n] = un;
-                if (t.update_u && t.last_iter) L.u[n] = un;
-            }
-            if (threadIdx.x == 0) L.gaveup[lt] = 0u;
-        }
-    }
-}
-
-__global__ __launch_bounds__(256) void sn_p23_kernel(SnTable t) {
-    const int tile = blockIdx.x;
-    const SnLayerDev L = t.L[find_layer(t, tile)];
-    const int lt = tile - L.tile_begin;
-    const int rt = lt / L.nct, ct = lt % L.nct;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int r0 = rt * SN_TR + w * SN_RPW;
-    const int c0 = ct * SN_TC + lane * 4;
-    const unsigned ntile = (unsigned)(L.nrt * L.nct);
-    unsigned *const tk_layer = L.sync + L.nrt;
-    unsigned *const tk_dep = L.sync + L.nrt + 1;
-    unsigned *const flag = L.sync + L.nrt + 2;
-    __shared__ float vr[SN_TC];
-    __shared__ double red[4];
-    __shared__ unsigned shu[4];
-    __shared__ float shf[3];
-
-    float4 wt[SN_RPW];
-    load_tile(L.W, L.N, L.K, L.vec, r0, c0, wt);
-    const float halo = p23_load_halo(L, ct, r0);
-    // the sigma generation, read before this tile arrives anywhere (the last
-    // taker publishes generation + 1 only after every tile has arrived)
-    unsigned gen0 = 0;
-    if (threadIdx.x == 0) gen0 = ld_sc1(flag);
-
-    // P2: v_raw for the tile's columns (sn_p2_kernel's sum), the row partials
-    const int c = ct * SN_TC + threadIdx.x;
-    float vs = 0.f;
-    if (c < L.K) {
-        const float *col = L.p1 + c;
-        for (int b0 = 0; b0 < L.nrt; b0 += 16) {
-            float tq[16];
-#pragma unroll
-            for (int j = 0; j < 16; ++j)
-                tq[j] = (b0 + j < L.nrt) ? col[(size_t)(b0 + j) * L.K] : 0.f;
-#pragma unroll
-            for (int j = 0; j < 16; ++j)
-                if (b0 + j < L.nrt) vs += tq[j];
-        }
-    }
-    vr[threadIdx.x] = vs;
-    if (rt == 0 && c < L.K) store_wt(L.vraw + c, vs);
-    __syncthreads();
-    {
-        const float v0 = vr[lane * 4 + 0], v1 = vr[lane * 4 + 1];
-        const float v2 = vr[lane * 4 + 2], v3 = vr[lane * 4 + 3];
-        float part[SN_RPW];
-#pragma unroll
-        for (int i = 0; i < SN_RPW; ++i)
-            part[i] = fmaf(v3, wt[i].w, fmaf(v2, wt[i].z, fmaf(v1, wt[i].y, v0 * wt[i].x)));
-#pragma unroll
-        for (int i = 0; i < SN_RPW; ++i) part[i] = wave_sum(part[i]);
-        if (lane == 0) {
-#pragma unroll
-            for (int i = 0; i < SN_RPW; ++i)
-                if (r0 + i < L.N) store_wt(L.q2 + (size_t)(r0 + i) * L.nctp + ct, part[i]);
-        }
-    }
-    if (rt == 0) {                               // ||v_raw||^2 over the tile's columns
-        const double a = block_sum<4>((double)vs * (double)vs, red);
-        if (threadIdx.x == 0) store_wt(L.apart + ct, a);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) shu[0] = (ticket_add(L.sync + rt, 1u) == (unsigned)L.nct - 1u);
-    __syncthreads();
-    const bool elected = shu[0] != 0;
-
-    // the row tile's last taker: u_raw of its 32 rows, ||u_raw||^2's partial
-    float uraw = 0.f;
-    if (elected) {
-        if (threadIdx.x == 0) store_wt(L.sync + rt, 0u);
-        const int n = rt * SN_TR + threadIdx.x;
-        double b = 0.0;
-        if (threadIdx.x < SN_TR && n < L.N) {
-            const float *q = L.q2 + (size_t)n * L.nctp;
-            float s = 0.f;
-            for (int b0 = 0; b0 < L.nct; b0 += 16) {
-                float tq[16];
-#pragma unroll
-                for (int j = 0; j < 16; ++j) tq[j] = (b0 + j < L.nct) ? ld_sc1(q + b0 + j) : 0.f;
-#pragma unroll
-                for (int j = 0; j < 16; ++j)
-                    if (b0 + j < L.nct) s += tq[j];
-            }
-            uraw = s;
-            store_wt(L.ucur + n, s);             // for a departer doing this tile's duties
-            b = (double)s * (double)s;
-        }
-        b = block_sum<4>(b, red);
-        if (threadIdx.x == 0) store_wt(L.bpart + rt, b);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-    }
-    const unsigned arr = (rt == 0 ? 1u : 0u) + (elected ? 1u : 0u);
-    if (threadIdx.x == 0) {
-        unsigned fin = 0;
-        if (arr) fin = (ticket_add(tk_layer, arr) + arr == (unsigned)(L.nrt + L.nct));
-        shu[1] = fin;
-    }
-    __syncthreads();
-
-    bool have = true;
-    if (t.dbg & 1) {
-        if (threadIdx.x == 0) { shf[0] = 1.f; shf[1] = 1.f; shf[2] = 1.f; if (shu[1]) store_wt(tk_layer, 0u); }
-        __syncthreads();
-    } else if (shu[1]) {
-        // the layer's last taker: sn_layer_epilogue's norms and sigma
-        if (threadIdx.x < 64) {
-            double a = 0.0, b = 0.0;
-            for (int i = lane; i < L.nct; i += 64) a += ld_sc1(L.apart + i);
-            for (int i = lane; i < L.nrt; i += 64) b += ld_sc1(L.bpart + i);
-            a = wave_sum(a);
-            b = wave_sum(b);
-            if (threadIdx.x == 0) {
-                store_wt(tk_layer, 0u);
-                const float nv = (float)sqrt(a) + t.eps;               // sn.py:13
-                const double uu = b / ((double)nv * (double)nv);       // ||u_raw||^2
-                const float nu = (float)sqrt(uu) + t.eps;
-                const float sg = (float)(uu / (double)nu);             // sn.py:42
-                L.sigma[0] = sg;
-                L.stats[4] = (float)(a / ((double)nv * (double)nv));
-                L.stats[5] = (float)(uu / ((double)nu * (double)nu));
-                store_wt(L.rec + 0, sg);
-                store_wt(L.rec + 1, nv);
-                store_wt(L.rec + 2, nu);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                store_wt(flag, gen0 + 1u);
-                shf[0] = sg;
-                shf[1] = nv;
-                shf[2] = nu;
-            }
-        }
-        __syncthreads();
-    } else {
-        if (threadIdx.x == 0) {
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            unsigned ok = 0;
-            for (;;) {
-                if (t.giveup) break;
-                if (ld_sc1(flag) != gen0) {
-                    ok = 1;
-                    break;
-                }
-                if (__builtin_amdgcn_s_memrealtime() - t0 > SN23_WAIT) break;
-                if (t.dbg & 4) __builtin_amdgcn_s_sleep(60);
-                else __builtin_amdgcn_s_sleep(8);
-            }
-            if (ok) {
-                shf[0] = ld_sc1(L.rec + 0);
-                shf[1] = ld_sc1(L.rec + 1);
-                shf[2] = ld_sc1(L.rec + 2);
-            }
-            shu[2] = ok;
-        }
-        __syncthreads();
-        have = shu[2] != 0;
-    }
-
-    if (have) {
-        const float sigma = shf[0], nv = shf[1], nu = shf[2];
-        if (!(t.dbg & 2)) p23_store(L, ct, r0, c0, wt, halo, sigma);
-        if (rt == 0 && c < L.K) L.v[c] = vr[threadIdx.x] / nv;
-        const int n = rt * SN_TR + threadIdx.x;
-        if (elected && threadIdx.x < SN_TR && n < L.N) {
-            const float un = (uraw / nv) / nu;                          // u' = l2n(v W)
-            L.ucur[n] = un;
-            if (t.update_u && t.last_iter) L.u[n] = un;
-        }
-    } else if (threadIdx.x == 0) {
-        store_wt(L.gaveup + lt, 1u | (elected ? 2u : 0u));
-    }
-
-    // departure: low 16 bits count tiles, high bits the ones that gave up
-    if (t.dbg & 8) return;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const unsigned add = have ? 1u : 0x10001u;
-        const unsigned tot = ticket_add(tk_dep, add) + add;
-        shu[3] = ((tot & 0xffffu) == ntile) ? 1u + (tot >> 16) : 0u;
-    }
-    __syncthreads();
-    const unsigned dep = shu[3];
-    if (!dep) return;
-    if (threadIdx.x == 0) store_wt(tk_dep, 0u);
-    if (dep > 1) sn_p23_rescue(t, L);
-}
-
 // backward A: partial <G, W> per unit (tile, or fold block)
 __global__ __launch_bounds__(256) void sn_bwd_a_kernel(SnTable t) {
     const int unit = blockIdx.x;
@@ -1109,11 +742,6 @@ static size_t layer_ws_bytes(int N, int K) {
     b += align_up((size_t)dotp_slots(N, K) * 4, 256);       // dotp
     b += 2 * align_up((size_t)dotp_slots(N, K) * 4, 256);   // ggp, ugvp
     b += 256;                                                // stats
-    b += align_up((size_t)(nrt + 3) * 4, 256);               // sync
-    b += align_up((size_t)nct * 8, 256);                     // apart
-    b += align_up((size_t)nrt * 8, 256);                     // bpart
-    b += 256;                                                // rec
-    b += align_up((size_t)nrt * nct * 4, 256);               // gaveup
     return b;
 }
 
@@ -1169,44 +797,10 @@ static bool build_table(const smmd_sn_layer *layers, int first, int count, char 
         L.ggp = (float *)p;  p += align_up((size_t)dotp_slots(L.N, L.K) * 4, 256);
         L.ugvp = (float *)p; p += align_up((size_t)dotp_slots(L.N, L.K) * 4, 256);
         L.stats = (float *)p; p += 256;
-        L.sync = (unsigned *)p; p += align_up((size_t)(L.nrt + 3) * 4, 256);
-        L.apart = (double *)p;  p += align_up((size_t)L.nct * 8, 256);
-        L.bpart = (double *)p;  p += align_up((size_t)L.nrt * 8, 256);
-        L.rec = (float *)p;     p += 256;
-        L.gaveup = (unsigned *)p; p += align_up((size_t)L.nrt * L.nct * 4, 256);
         off += layer_ws_bytes(L.N, L.K);
     }
     t.total_tiles = tiles;
     t.total_units = (int)units;
-    return true;
-}
-
-// The fused refresh (sn_p23_kernel) when its grid fits the chip: blocks per
-// CU from the occupancy query (at most 8, the 256-thread admission limit)
-// times the CUs.  A layer's departure count must fit its 16 bits.
-// SMMD_SN_P23 (read each call): 0 keeps the launch set; "rescue" runs the
-// fused kernel with every waiting tile giving up at once (the test of the
-// path a non-resident grid takes).
-static bool p23_fits(SnTable &t) {
-    const char *e = getenv("SMMD_SN_P23");
-    if (e && e[0] == '0') return false;
-    t.giveup = (e && strcmp(e, "rescue") == 0) ? 1 : 0;
-    const char *d = getenv("SMMD_SN_P23_DBG");
-    t.dbg = d ? atoi(d) : 0;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
-    static int cap[64];                          // 0: not yet queried
-    if (cap[dev] == 0) {
-        int cus = 0, nb = 0;
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sn_p23_kernel, 256, 0) != hipSuccess)
-            cap[dev] = -1;
-        else
-            cap[dev] = cus * (nb < 8 ? nb : 8);   // 6 at this build's 77 VGPRs / 106 SGPRs
-    }
-    if (t.total_tiles > cap[dev]) return false;
-    for (int i = 0; i < t.n_layers; ++i)
-        if (t.L[i].nrt * t.L[i].nct >= 0xffff) return false;
     return true;
 }
 
@@ -1294,23 +888,17 @@ smmd_status smmd_sn_power_iter_ex(const smmd_sn_layer *layers, int n_layers, int
         if (!build_table(layers, first, count, (char *)ws + 256, t)) return SMMD_EINVAL;
         t.eps = eps;
         t.update_u = update_u ? 1 : 0;
-        const bool fused = p23_fits(t);
         for (int it = 0; it < num_iters; ++it) {
             t.iter = it;
             t.last_iter = (it == num_iters - 1);
             if (it > 0 || !(flags & SMMD_SN_P1_READY))   // else written by smmd_adam_flat_sn
                 hipLaunchKernelGGL(sn_p1_kernel, dim3(t.total_tiles), dim3(256), 0, s, t);
-            if (fused && t.last_iter) {
-                hipLaunchKernelGGL(sn_p23_kernel, dim3(t.total_tiles), dim3(256), 0, s, t);
-            } else {
-                hipLaunchKernelGGL(sn_p2_kernel, dim3(t.total_tiles), dim3(256), 0, s, t);
-                hipLaunchKernelGGL(sn_r2_kernel, dim3(t.n_layers), dim3(1024), 0, s, t);
-            }
+            hipLaunchKernelGGL(sn_p2_kernel, dim3(t.total_tiles), dim3(256), 0, s, t);
+            hipLaunchKernelGGL(sn_r2_kernel, dim3(t.n_layers), dim3(1024), 0, s, t);
         }
         bool any_eff = false;
         for (int i = 0; i < count; ++i) any_eff |= (t.L[i].W_eff != nullptr);
-        if (any_eff && !fused)
-            hipLaunchKernelGGL(sn_p3_kernel, dim3(t.total_units), dim3(256), 0, s, t);
+        if (any_eff) hipLaunchKernelGGL(sn_p3_kernel, dim3(t.total_units), dim3(256), 0, s, t);
         smmd_status st = last_launch_status();
         if (st != SMMD_OK) return st;
     }

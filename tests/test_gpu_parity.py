@@ -550,60 +550,6 @@ def test_sn_repeated_calls_track_weights(dev):
         _check_sn(mods, bank, u0, outs, None)
 
 
-def _sn_refresh_state(dev, shapes, fold, seed, calls):
-    torch.manual_seed(seed)                      # the banks' initial u
-    mods, bank, rng = _sn_bank(dev, shapes, seed, fold=fold)
-    got = []
-    for _ in range(calls):
-        with torch.no_grad():
-            for m in mods:
-                m.weight.add_(torch.randn(m.weight.shape, generator=torch.Generator().manual_seed(
-                    len(got)), dtype=torch.float32).to(dev) * 0.01)
-        outs = bank.refresh(update_u=True)
-        got.append([(o.detach().cpu().numpy(), e.sigma.item(), e.u.cpu().numpy(),
-                     e.v.cpu().numpy()) for o, e in zip(outs, bank.entries)])
-    return got
-
-
-@pytest.mark.parametrize('mode', ['1', 'rescue'])
-def test_sn_fused_refresh_matches_launch_set(dev, monkeypatch, mode):
-    """sn_p23_kernel (P2 + R2 + P3 in one launch, W read once) against the
-    launch set (SMMD_SN_P23=0) over three calls on the same workspace (its
-    tickets and the sigma generation carried between calls), plain and fold
-    layers mixed.  'rescue': every waiting tile gives up and the layer's last
-    departing tile does their duties (the path of a grid that is not all
-    resident).  u_raw is summed in the launch set's order; the two double
-    norms in another fixed order, so sigma, u', v and W_eff agree to a few
-    float ulps (rtol 1e-6), and W' of the fold layers is their fold."""
-    shapes = SN_FOLD_SHAPES + [(64, 27), (1, 1024), (7, 13)]
-    fold = (1, 1, 0, 1, 0, 1, 0, 0, 0)
-    monkeypatch.setenv('SMMD_SN_P23', '0')
-    ref = _sn_refresh_state(dev, shapes, fold, 31, 3)
-    monkeypatch.setenv('SMMD_SN_P23', mode)
-    got = _sn_refresh_state(dev, shapes, fold, 31, 3)
-    for call, (a, b) in enumerate(zip(got, ref)):
-        for i, (x, y) in enumerate(zip(a, b)):
-            np.testing.assert_allclose(x[1], y[1], rtol=1e-6, err_msg='sigma %d %d' % (call, i))
-            for j, what in ((0, 'W_eff'), (2, 'u'), (3, 'v')):
-                np.testing.assert_allclose(x[j], y[j], rtol=1e-6,
-                                           atol=1e-6 * float(np.abs(y[j]).max()),
-                                           err_msg='%s %d %d' % (what, call, i))
-
-
-def test_sn_fused_refresh_vs_oracle(dev, monkeypatch):
-    """The fused refresh on the SNResNet-64 critic's 14 layers (10.1 M weights,
-    1256 tiles: within the chip's resident capacity) against the oracle,
-    forward and backward."""
-    monkeypatch.setenv('SMMD_SN_P23', '1')
-    from gan.core.architecture import SNResNetDiscriminator
-    from gan.core.snops import sn_modules
-    D = SNResNetDiscriminator(64, 1, False, with_sn=True, with_learnable_sn_scale=True)
-    layers = sn_modules(D)
-    shapes = [tuple(m.weight.shape) for m in layers]
-    folds = [bool(getattr(m, 'sn_fold', False)) for m in layers]
-    _sn_roundtrip(dev, shapes, 12, fold=folds)
-
-
 def test_sn_reference_layout(dev):
     """spectral_normed_weight on a TF-layout conv weight [kh, kw, Cin, Cout]."""
     from gan.core import sn
