@@ -63,7 +63,8 @@ int smmd_abi_version(void);         /* bumped on any ABI change (2: Gram/poly,
                                        6: smmd_mask_pool2*, smmd_up_add,
                                        smmd_bn_relu_fwd, 7: smmd_smmd_loss_fwd/bwd,
                                        smmd_source_hash, smmd_sn_grad_stats,
-                                       smmd_adam_flat_sn2, smmd_bn_relu_fwd_save / _bwd) */
+                                       smmd_adam_flat_sn2, smmd_bn_relu_fwd_save / _bwd,
+                                       8: smmd_wino3x3_*) */
 const char *smmd_source_hash(void); /* first 16 hex digits of the SHA-256 of the
                                        sources this binary was built from
                                        (csrc .hip and .hpp files in byte order,
@@ -555,6 +556,43 @@ size_t smmd_conv3x3_thin_wgrad_workspace_bytes(int n, int ci, int co, int h, int
 smmd_status smmd_conv3x3_thin_wgrad(const float *gy, const float *x, float *gw, int n, int ci,
                                     int co, int h, int w_img, void *ws, size_t ws_bytes,
                                     smmd_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * 3x3 stride-1 SAME convolutions as fused Winograd F(2x2, 3x3) on the f32
+ * MFMA: the critics' and generators' wide 3x3 layers (snops.conv2d /
+ * resnet Conv2D with padding SAME, gan/core/snops.py:69-90,
+ * gan/core/resnet/ops/conv2d.py:16-39, in the residual blocks of
+ * gan/core/resnet/block.py:38-50 and architecture.py:395-434), forward and
+ * input gradient (TF's Conv2DBackpropInput), to every order of the critic's
+ * double backward.  NCHW fp32, tap t = 3 kh + kw reads (h + kh - 1, w + kw - 1),
+ * zero outside.
+ *
+ * smmd_wino3x3_filter: u = the 16 transform-point images of the filters,
+ *   U = G g G^T per (ko, ci), in the conv kernel's staging order;
+ *   mode 0: g = w[ko][ci], w [ko, ci, 3, 3] (the convolution);
+ *   mode 1: g[a][b] = w[ci][ko][2 - a][2 - b], w [ci, ko, 3, 3] (the input
+ *           gradient of a convolution with weight w).
+ *   u holds smmd_wino3x3_filter_bytes(ko, ci) bytes; needs ko % 64 == 0 and
+ *   ci % 8 == 0.
+ * smmd_wino3x3_conv: y[n][ko][p] = bias[ko] + sum_{ci, t} g[ko][ci][t] x[n][ci][p + d(t)]
+ *   x [n, ci, h, w_img], y [n, ko, h, w_img] (16-byte aligned), bias [ko] or
+ *   NULL, u from smmd_wino3x3_filter; h and w_img even (smmd_wino3x3_supported).
+ *   Small grids split the input channels over several workgroups and add the
+ *   partial outputs in slice order from the workspace
+ *   (smmd_wino3x3_workspace_bytes; 0 = none needed).  Deterministic.
+ * ------------------------------------------------------------------------- */
+int smmd_wino3x3_supported(int n, int ci, int ko, int h, int w_img);
+
+size_t smmd_wino3x3_filter_bytes(int ko, int ci);
+
+smmd_status smmd_wino3x3_filter(const float *w, int ko, int ci, int mode, float *u,
+                                size_t u_bytes, smmd_stream_t stream);
+
+size_t smmd_wino3x3_workspace_bytes(int n, int ci, int ko, int h, int w_img);
+
+smmd_status smmd_wino3x3_conv(const float *x, const float *u, const float *bias, float *y, int n,
+                              int ci, int ko, int h, int w_img, void *ws, size_t ws_bytes,
+                              smmd_stream_t stream);
 
 #ifdef __cplusplus
 }

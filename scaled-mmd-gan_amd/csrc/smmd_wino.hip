@@ -1,0 +1,411 @@
+// smmd_wino.hip -- 3x3 stride-1 SAME convolutions as Winograd F(2x2, 3x3) on
+// the f32 MFMA (gfx950), fused: input transform, the 16 transform-point GEMMs
+// and the output transform in ONE launch, nothing but x, the transformed
+// filter and y touching HBM.
+//
+// The critic's and generator's 3x3 convs (gan/core/resnet/block.py:38-50,
+// snops.py:60-80 conv2d with padding SAME; C, K in {64 .. 512}, H = W in
+// {8 .. 64}) are the largest single class of step time.  MIOpen runs them as
+// F(2,3) Winograd on the VALU (55 TF/s executed, 0.35 of the f32 peak); the
+// multiply stage here is `v_mfma_f32_32x32x2_f32` (exact f32 fma chains).
+//
+//   y[n][k][2ty+a][2tx+b] = bias[k] + (A^T M A)[a][b],
+//   M_p[k][t] = sum_c U_p[k][c] V_p[c][t]          (16 points p = 4 i + j)
+//   V = B^T d B  (d: the 4x4 input patch at (2ty-1, 2tx-1), zero outside)
+//   U = G g G^T  (g: the 3x3 filter [k][c]; the backward-data conv uses the
+//                 flipped, transposed filter, mode 1 of the filter transform)
+//
+// Block: 64 tiles (lanes of the transform waves) x 64 output channels, 4
+// waves; wave w computes the 32 x 32 (k, tile) quadrant (kh = w >> 1, th =
+// w & 1) for all 16 points: 16 f32x16 accumulators (256 AGPRs), so for one
+// (k, tile) every point lives in the same lane and register and the output
+// transform runs in registers.  Input channels go 8 per chunk through a
+// double-buffered LDS stage (V 32 KB + U 32 KB per buffer): chunk c+1's
+// global loads are issued before chunk c's 64 MFMAs per wave, transformed and
+// stored after them, one barrier per chunk.
+#include "smmd_common.hpp"
+
+namespace smmd {
+
+namespace {
+
+constexpr int WN_T = 256;                 // threads per block
+constexpr int WN_TB = 64;                 // tiles per block
+constexpr int WN_KB = 64;                 // output channels per block
+constexpr int WN_CC = 8;                  // input channels per chunk
+constexpr int WN_STAGE = 16 * WN_CC * 64; // floats per V (and per U) stage
+constexpr size_t WN_LDS = 2 * 2 * WN_STAGE * sizeof(float);   // 128 KB
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float wn_from_left(float v) {   // lane l gets lane l-1's v (lane 0: 0)
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
+                                                                 0x138, 0xf, 0xf, false));
+}
+
+__device__ __forceinline__ float wn_from_right(float v) {  // lane l gets lane l+1's v (lane 63: 0)
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
+                                                                 0x130, 0xf, 0xf, false));
+}
+
+// U = G g G^T for one (ko, ci) filter, stored in the conv kernel's LDS order:
+// u[kb][chunk][p][h][k64][c4], c = 4 h + c4 within the chunk of 8
+__global__ void wino_filter_kernel(const float *__restrict__ w, int KO, int CI, int mode,
+                                   float *__restrict__ u) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (int64_t)KO * CI) return;
+    const int ci = (int)(idx % CI), ko = (int)(idx / CI);
+    float g[3][3];
+    if (mode == 0) {
+        const float *s = w + ((int64_t)ko * CI + ci) * 9;
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) g[i][j] = s[i * 3 + j];
+    } else {            // w is [CI][KO][3][3] of the forward conv; flip both taps
+        const float *s = w + ((int64_t)ci * KO + ko) * 9;
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) g[i][j] = s[(2 - i) * 3 + (2 - j)];
+    }
+    float t[4][3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        t[0][j] = g[0][j];
+        t[1][j] = 0.5f * (g[0][j] + g[1][j] + g[2][j]);
+        t[2][j] = 0.5f * (g[0][j] - g[1][j] + g[2][j]);
+        t[3][j] = g[2][j];
+    }
+    const int kb = ko >> 6, kl = ko & 63, cc = ci >> 3, cl = ci & 7;
+    const int64_t base = ((int64_t)kb * (CI >> 3) + cc) * 16;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const float r[4] = {t[i][0], 0.5f * (t[i][0] + t[i][1] + t[i][2]),
+                            0.5f * (t[i][0] - t[i][1] + t[i][2]), t[i][2]};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            u[(((base + i * 4 + j) * 2 + (cl >> 2)) * 64 + kl) * 4 + (cl & 3)] = r[j];
+    }
+}
+
+struct WnGeom {
+    int N, C, K, H, W, TW, Timg;
+    int64_t T, slab;        // slab: floats between split-C partial outputs
+};
+
+// raw 4 x 2 centre columns of one channel's patch rows (2ty-1 .. 2ty+2, cols
+// 2tx, 2tx+1): a row outside the image loads the clamped row, which the
+// transform replaces by zero (so nothing waits on the loads before it)
+__device__ __forceinline__ void wn_load_rows(const float *__restrict__ xc, int ty, int tx, bool ok,
+                                             const WnGeom &g, float2 (&r)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int yy = 2 * ty - 1 + i;
+        const int yc = min(max(yy, 0), g.H - 1);
+        r[i] = *reinterpret_cast<const float2 *>(xc + (int64_t)yc * g.W + 2 * tx);
+    }
+}
+
+// V = B^T d B of one channel's patch; d's outer columns come from the
+// neighbouring tiles' lanes (the tile to the left holds column 2tx-1 as its
+// .y, the one to the right column 2tx+2 as its .x), or from memory at a wave
+// edge inside a tile row
+template <bool EDGE>
+__device__ __forceinline__ void wn_transform(const float2 (&r)[4], const float *__restrict__ xc,
+                                             int ty, int tx, bool ok, const WnGeom &g, int lane,
+                                             float (&v)[16]) {
+    float d[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int yy = 2 * ty - 1 + i;
+        const bool row = ok && yy >= 0 && yy < g.H;
+        const float cx = row ? r[i].x : 0.f, cy = row ? r[i].y : 0.f;
+        float L = wn_from_left(cy), R = wn_from_right(cx);
+        if (EDGE) {        // a tile row wider than a wave: its wave edges load
+            if (tx > 0 && lane == 0) L = row ? xc[(int64_t)yy * g.W + 2 * tx - 1] : 0.f;
+            if (tx < g.TW - 1 && lane == 63) R = row ? xc[(int64_t)yy * g.W + 2 * tx + 2] : 0.f;
+        }
+        L = tx == 0 ? 0.f : L;
+        R = tx == g.TW - 1 ? 0.f : R;
+        d[i][0] = L;
+        d[i][1] = cx;
+        d[i][2] = cy;
+        d[i][3] = R;
+    }
+    float t[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        t[0][j] = d[0][j] - d[2][j];
+        t[1][j] = d[1][j] + d[2][j];
+        t[2][j] = d[2][j] - d[1][j];
+        t[3][j] = d[1][j] - d[3][j];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        v[i * 4 + 0] = t[i][0] - t[i][2];
+        v[i * 4 + 1] = t[i][1] + t[i][2];
+        v[i * 4 + 2] = t[i][2] - t[i][1];
+        v[i * 4 + 3] = t[i][1] - t[i][3];
+    }
+}
+
+template <bool EDGE>
+__global__ __launch_bounds__(WN_T, 1) void wino_conv_kernel(
+    const float *__restrict__ x, const float *__restrict__ u, const float *__restrict__ bias,
+    float *__restrict__ y, WnGeom g) {
+    extern __shared__ float4 wn_lds[];
+    float4 *const Vs = wn_lds;                         // [2][p][h][t64]  (float4 = c4)
+    float4 *const Us = wn_lds + 2 * (WN_STAGE / 4);    // [2][p][h][k64]
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int kb = blockIdx.y;
+    const int64_t tile0 = (int64_t)blockIdx.x * WN_TB;
+    const int nch = g.C / WN_CC;
+    // input-channel slice blockIdx.z of gridDim.z: chunks [c0, c0 + nchunk)
+    const int c0 = (int)((int64_t)nch * blockIdx.z / gridDim.z);
+    const int nchunk = (int)((int64_t)nch * (blockIdx.z + 1) / gridDim.z) - c0;
+    y += (int64_t)blockIdx.z * g.slab;
+
+    // transform role: lane = tile, wave w = channels 2w, 2w+1 of each chunk
+    const int64_t gt = tile0 + lane;
+    const bool tok = gt < g.T;
+    int tn = 0, tty = 0, ttx = 0;
+    if (tok) {
+        tn = (int)(gt / g.Timg);
+        const int r = (int)(gt - (int64_t)tn * g.Timg);
+        tty = r / g.TW;
+        ttx = r - tty * g.TW;
+    }
+    const int64_t HW = (int64_t)g.H * g.W;
+    const float *xn = x + (int64_t)tn * g.C * HW;
+    const float4 *ub =
+        reinterpret_cast<const float4 *>(u) + ((int64_t)kb * nch + c0) * (WN_STAGE / 4);
+    xn += (int64_t)c0 * WN_CC * HW;
+
+    float2 raw[2][4];
+    // the filter stage goes through registers, loaded by inline asm so the
+    // compiler can neither sink the loads to their use after the MFMAs nor
+    // drain them ahead of the LDS reads (an LDS-DMA would be waited for
+    // before every ds_read); `wn_wait_u` retires them before the LDS write
+    f4v ur[8];
+#define WN_LOAD_CHUNK(CC_)                                                                   \
+    do {                                                                                     \
+        _Pragma("unroll") for (int e = 0; e < 2; ++e)                                        \
+            wn_load_rows(xn + (int64_t)((CC_) * WN_CC + 2 * w + e) * HW, tty, ttx, tok, g,    \
+                         raw[e]);                                                            \
+        const float4 *src_ = ub + (int64_t)(CC_) * (WN_STAGE / 4) + w * 512 + lane;          \
+        _Pragma("unroll") for (int i = 0; i < 8; ++i)                                        \
+            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(ur[i]) : "v"(src_ + i * 64)); \
+    } while (0)
+#define WN_STORE_CHUNK(CC_, BUF_)                                                            \
+    do {                                                                                     \
+        asm volatile("s_waitcnt vmcnt(0)"                                                    \
+                     : "+v"(ur[0]), "+v"(ur[1]), "+v"(ur[2]), "+v"(ur[3]), "+v"(ur[4]),      \
+                       "+v"(ur[5]), "+v"(ur[6]), "+v"(ur[7])::"memory");                     \
+        f4v *U_ = reinterpret_cast<f4v *>(Us + (BUF_) * (WN_STAGE / 4) + w * 512 + lane);    \
+        _Pragma("unroll") for (int i = 0; i < 8; ++i) U_[i * 64] = ur[i];                    \
+        float v_[2][16];                                                                     \
+        _Pragma("unroll") for (int e = 0; e < 2; ++e)                                        \
+            wn_transform<EDGE>(raw[e], xn + (int64_t)((CC_) * WN_CC + 2 * w + e) * HW, tty,  \
+                               ttx, tok, g, lane, v_[e]);                                    \
+        float2 *V2_ = reinterpret_cast<float2 *>(Vs + (BUF_) * (WN_STAGE / 4));              \
+        _Pragma("unroll") for (int p = 0; p < 16; ++p)                                       \
+            V2_[((p * 2 + (w >> 1)) * 64 + lane) * 2 + (w & 1)] =                            \
+                make_float2(v_[0][p], v_[1][p]);                                             \
+    } while (0)
+
+    f32x16 acc[16];
+#pragma unroll
+    for (int p = 0; p < 16; ++p) acc[p] = f32x16{};
+
+    const int th = w & 1, kh = w >> 1, hl = lane >> 5, l32 = lane & 31;
+// 64 MFMAs per wave per chunk, the points taken in pairs so consecutive
+// MFMAs never share an accumulator; the next pair's fragments are read while
+// this pair's MFMAs run
+#define WN_MFMA_CHUNK(BUF_)                                                                  \
+    do {                                                                                     \
+        const float4 *V_ = Vs + (BUF_) * (WN_STAGE / 4);                                     \
+        const float4 *U_ = Us + (BUF_) * (WN_STAGE / 4);                                     \
+        float4 a0 = U_[hl * 64 + kh * 32 + l32], b0 = V_[hl * 64 + th * 32 + l32];          \
+        float4 a1 = U_[(2 + hl) * 64 + kh * 32 + l32], b1 = V_[(2 + hl) * 64 + th * 32 + l32]; \
+        _Pragma("unroll") for (int pp = 0; pp < 8; ++pp) {                                   \
+            const int p = 2 * pp;                                                            \
+            const float4 ca0 = a0, cb0 = b0, ca1 = a1, cb1 = b1;                             \
+            if (pp < 7) {                                                                    \
+                a0 = U_[((p + 2) * 2 + hl) * 64 + kh * 32 + l32];                            \
+                b0 = V_[((p + 2) * 2 + hl) * 64 + th * 32 + l32];                            \
+                a1 = U_[((p + 3) * 2 + hl) * 64 + kh * 32 + l32];                            \
+                b1 = V_[((p + 3) * 2 + hl) * 64 + th * 32 + l32];                            \
+            }                                                                                \
+            acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca0.x, cb0.x, acc[p], 0, 0, 0);    \
+            acc[p + 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca1.x, cb1.x, acc[p + 1], 0, 0, 0); \
+            acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca0.y, cb0.y, acc[p], 0, 0, 0);    \
+            acc[p + 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca1.y, cb1.y, acc[p + 1], 0, 0, 0); \
+            acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca0.z, cb0.z, acc[p], 0, 0, 0);    \
+            acc[p + 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca1.z, cb1.z, acc[p + 1], 0, 0, 0); \
+            acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca0.w, cb0.w, acc[p], 0, 0, 0);    \
+            acc[p + 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca1.w, cb1.w, acc[p + 1], 0, 0, 0); \
+        }                                                                                    \
+        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);                                   \
+        _Pragma("unroll") for (int pp = 0; pp < 7; ++pp) {                                   \
+            __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);                               \
+            __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);                               \
+        }                                                                                    \
+        __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);                                   \
+    } while (0)
+
+    WN_LOAD_CHUNK(0);
+    WN_STORE_CHUNK(0, 0);
+    __syncthreads();
+    for (int cc = 0; cc + 1 < nchunk; ++cc) {
+        WN_LOAD_CHUNK(cc + 1);          // in flight during this chunk's MFMAs
+        __builtin_amdgcn_sched_barrier(0);
+        WN_MFMA_CHUNK(cc & 1);
+        __builtin_amdgcn_sched_barrier(0);
+        WN_STORE_CHUNK(cc + 1, (cc + 1) & 1);
+        __syncthreads();
+    }
+    WN_MFMA_CHUNK((nchunk - 1) & 1);
+
+    // epilogue: C_p[k][tile], k = (r & 3) + 8 (r >> 2) + 4 hl, tile = l32
+    const int64_t et = tile0 + th * 32 + l32;
+    if (et >= g.T) return;
+    const int en = (int)(et / g.Timg);
+    const int er = (int)(et - (int64_t)en * g.Timg);
+    const int ety = er / g.TW, etx = er - ety * g.TW;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int k = kb * WN_KB + kh * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+        float m[16];
+#pragma unroll
+        for (int p = 0; p < 16; ++p) m[p] = acc[p][r];
+        float s0[4], s1[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            s0[j] = m[j] + m[4 + j] + m[8 + j];
+            s1[j] = m[4 + j] - m[8 + j] - m[12 + j];
+        }
+        const float b = bias ? bias[k] : 0.f;
+        float *o = y + (((int64_t)en * g.K + k) * g.H + 2 * ety) * g.W + 2 * etx;
+        *reinterpret_cast<float2 *>(o) =
+            make_float2(s0[0] + s0[1] + s0[2] + b, s0[1] - s0[2] - s0[3] + b);
+        *reinterpret_cast<float2 *>(o + g.W) =
+            make_float2(s1[0] + s1[1] + s1[2] + b, s1[1] - s1[2] - s1[3] + b);
+    }
+}
+
+// y = bias + sum over the S partial slabs in slice order (float4 when the
+// plane size allows)
+__global__ void wino_reduce_kernel(const float *__restrict__ part, const float *__restrict__ bias,
+                                   float *__restrict__ y, int64_t n4, int S, int K, int HW) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n4) return;
+    const float4 *p4 = reinterpret_cast<const float4 *>(part);
+    float4 s = p4[i];
+    for (int z = 1; z < S; ++z) {
+        const float4 t = p4[i + z * n4];
+        s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
+    }
+    if (bias) {
+        const float b = bias[(int)((i * 4 / HW) % K)];
+        s.x += b; s.y += b; s.z += b; s.w += b;
+    }
+    reinterpret_cast<float4 *>(y)[i] = s;
+}
+
+}  // namespace
+
+// input-channel slices for a grid of `blocks` workgroups: enough for one
+// workgroup per CU, at least 4 chunks (32 channels) per slice (measured on the
+// 512-channel 8 x 8 layer: 128 workgroups 183 us, 4 slices 115 us; on the
+// 256-channel 16 x 16 one, 256 workgroups, 2 slices 115 us vs none 100 us)
+static int wino_slices(int64_t blocks, int nch, int HW) {
+    int S = 1;
+    while (blocks * S < 256 && nch / (2 * S) >= 4 && HW % 4 == 0) S *= 2;
+    return S;
+}
+
+}  // namespace smmd
+
+using namespace smmd;
+
+extern "C" size_t smmd_wino3x3_filter_bytes(int ko, int ci) {
+    if (ko <= 0 || ci <= 0) return 0;
+    return (size_t)16 * ko * ci * sizeof(float);
+}
+
+extern "C" int smmd_wino3x3_supported(int n, int ci, int ko, int h, int w_img) {
+    return n > 0 && ci > 0 && ko > 0 && ci % WN_CC == 0 && ko % WN_KB == 0 && h > 0 &&
+           w_img > 0 && h % 2 == 0 && w_img % 2 == 0 && (int64_t)n * ci * h * w_img < (1ll << 40);
+}
+
+extern "C" smmd_status smmd_wino3x3_filter(const float *w, int ko, int ci, int mode, float *u,
+                                           size_t u_bytes, smmd_stream_t stream) {
+    if (ko <= 0 || ci <= 0 || (mode != 0 && mode != 1) || !w || !u) return SMMD_EINVAL;
+    if (ko % WN_KB || ci % WN_CC) return SMMD_EUNSUPPORTED;
+    if (u_bytes < smmd_wino3x3_filter_bytes(ko, ci)) return SMMD_EWORKSPACE;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const int64_t n = (int64_t)ko * ci;
+    wino_filter_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st>>>(w, ko, ci, mode, u);
+    return last_launch_status();
+}
+
+extern "C" size_t smmd_wino3x3_workspace_bytes(int n, int ci, int ko, int h, int w_img) {
+    if (!smmd_wino3x3_supported(n, ci, ko, h, w_img)) return 0;
+    const int64_t T = (int64_t)n * (h / 2) * (w_img / 2);
+    const int S = wino_slices(((T + WN_TB - 1) / WN_TB) * (ko / WN_KB), ci / WN_CC, h * w_img);
+    return S > 1 ? (size_t)S * n * ko * h * w_img * sizeof(float) : 0;
+}
+
+extern "C" smmd_status smmd_wino3x3_conv(const float *x, const float *u, const float *bias,
+                                         float *y, int n, int ci, int ko, int h, int w_img,
+                                         void *ws, size_t ws_bytes, smmd_stream_t stream) {
+    if (n < 0 || ci <= 0 || ko <= 0 || h < 0 || w_img < 0) return SMMD_EINVAL;
+    if (n == 0 || h == 0 || w_img == 0) return SMMD_OK;
+    if (!x || !u || !y) return SMMD_EINVAL;
+    if (!smmd_wino3x3_supported(n, ci, ko, h, w_img)) return SMMD_EUNSUPPORTED;
+    if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15) return SMMD_EINVAL;
+    WnGeom g;
+    g.N = n; g.C = ci; g.K = ko; g.H = h; g.W = w_img;
+    g.TW = w_img / 2;
+    g.Timg = (h / 2) * g.TW;
+    g.T = (int64_t)n * g.Timg;
+    const int64_t tb = (g.T + WN_TB - 1) / WN_TB;
+    if (tb > 0x7fffffff) return SMMD_EINVAL;
+    const int S = wino_slices(tb * (ko / WN_KB), ci / WN_CC, h * w_img);
+    const int64_t total = (int64_t)n * ko * h * w_img;
+    float *out = y;
+    if (S > 1) {
+        if (!ws || ws_bytes < (size_t)S * total * sizeof(float)) return SMMD_EWORKSPACE;
+        if (reinterpret_cast<uintptr_t>(ws) & 15) return SMMD_EINVAL;
+        out = static_cast<float *>(ws);
+    }
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(wino_conv_kernel<false>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)WN_LDS) != hipSuccess ||
+            hipFuncSetAttribute(reinterpret_cast<const void *>(wino_conv_kernel<true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)WN_LDS) != hipSuccess)
+            return SMMD_EHIP;
+        attr = true;
+    }
+    g.slab = S > 1 ? total : 0;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const dim3 grid((unsigned)tb, (unsigned)(ko / WN_KB), (unsigned)S);
+    const float *b1 = S > 1 ? nullptr : bias;
+    // tile rows that are whole lane groups of a wave need no edge loads
+    if (64 % g.TW == 0)
+        wino_conv_kernel<false><<<grid, dim3(WN_T), WN_LDS, st>>>(x, u, b1, out, g);
+    else
+        wino_conv_kernel<true><<<grid, dim3(WN_T), WN_LDS, st>>>(x, u, b1, out, g);
+    smmd_status e = last_launch_status();
+    if (e != SMMD_OK || S == 1) return e;
+    const int64_t n4 = total / 4;
+    wino_reduce_kernel<<<dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st>>>(
+        out, bias, y, n4, S, ko, h * w_img);
+    return last_launch_status();
+}

@@ -18,7 +18,10 @@ with the three standard primitives on the layer's own shapes:
 so it uses MIOpen's forward, backward-data and backward-weights kernels --
 except for the thin 3x3 layers (a critic's 3-channel input conv, a
 generator's 3-channel output layer), whose three primitives run on the
-library's `smmd_conv3x3_thin*` kernels (csrc/smmd_thin.hip).
+library's `smmd_conv3x3_thin*` kernels (csrc/smmd_thin.hip), and the wide 3x3
+stride-1 layers, whose forward and backward-data primitives run on the
+library's fused Winograd F(2x2, 3x3) MFMA kernel (`smmd_wino3x3_*`,
+csrc/smmd_wino.hip); their weight gradient stays on MIOpen.
 """
 from __future__ import annotations
 
@@ -125,6 +128,64 @@ def _thin_wgrad(gy, x):
     return gw
 
 
+# ---------------------------------------------------------------------------
+# wide 3x3 stride-1 convolutions on the library's Winograd kernel
+# (SMMD_WINO=0: MIOpen for them)
+# ---------------------------------------------------------------------------
+WINO = os.environ.get('SMMD_WINO', '1') != '0'
+
+
+def wino_applicable(x, cin, cout, k, stride, padding):
+    """True when conv(x, [cout, cin, 3, 3], stride 1, padding 1) runs on
+    `smmd_wino3x3_conv`: an NCHW fp32 contiguous device tensor with even height
+    and width, cin % 8 == 0 and cout % 64 == 0."""
+    s = tuple(stride) if isinstance(stride, (list, tuple)) else (stride, stride)
+    p = tuple(padding) if isinstance(padding, (list, tuple)) else (padding, padding)
+    return (WINO and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
+            and x.is_contiguous() and k == 3 and s == (1, 1) and p == (1, 1)
+            and x.shape[1] == cin and cin % 8 == 0 and cout % 64 == 0
+            and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0 and x.shape[2] > 0
+            and x.shape[3] > 0 and x.shape[0] > 0)
+
+
+def _wino_conv(x, w, b, mode):
+    """smmd_wino3x3_filter + smmd_wino3x3_conv: mode 0 conv(x, w) + b
+    (w [co, ci, 3, 3]); mode 1 the input gradient of a conv with weight
+    w [ci', co', 3, 3] at upstream x."""
+    from . import _lib
+    x = x.contiguous()
+    w = w.contiguous()
+    if b is not None:
+        b = b.contiguous()
+    _lib.require_cuda(x, w, b)
+    N, ci, H, W = x.shape
+    co = w.shape[0] if mode == 0 else w.shape[1]
+    L = _lib.lib()
+    u = torch.empty(16 * co * ci, dtype=x.dtype, device=x.device)
+    with _lib.timed('smmd_wino3x3_filter'):
+        st = L.smmd_wino3x3_filter(_lib.ptr(w), co, ci, int(mode), _lib.ptr(u), u.numel() * 4,
+                                   _lib.stream_handle(x.device))
+    _lib.check(st, 'smmd_wino3x3_filter')
+    y = torch.empty((N, co, H, W), dtype=x.dtype, device=x.device)
+    nb = L.smmd_wino3x3_workspace_bytes(N, ci, co, H, W)
+    ws = _lib.workspace('wino', nb, x.device) if nb else None
+    _lib.add_bytes('smmd_wino3x3_conv', (x.numel() + y.numel()) * 4)
+    with _lib.timed('smmd_wino3x3_conv'):
+        st = L.smmd_wino3x3_conv(_lib.ptr(x), _lib.ptr(u), _lib.ptr(b), _lib.ptr(y), N, ci, co, H,
+                                 W, _lib.ptr(ws), nb, _lib.stream_handle(x.device))
+    _lib.check(st, 'smmd_wino3x3_conv')
+    return y
+
+
+def _is_wino(x, w, stride, padding, mode):
+    """mode 0: conv(x, w); mode 1: its input gradient at upstream x (x has
+    w.shape[0] channels, the result w.shape[1])."""
+    if w.dim() != 4 or w.shape[2] != 3 or w.shape[3] != 3:
+        return False
+    ci, co = (w.shape[1], w.shape[0]) if mode == 0 else (w.shape[0], w.shape[1])
+    return wino_applicable(x, ci, co, 3, stride, padding)
+
+
 def _is_thin(x, w, stride, padding):
     return thin_applicable(x, w.shape[1], w.shape[0], w.shape[2], stride, padding) \
         and w.shape[2] == w.shape[3]
@@ -134,6 +195,8 @@ def _fwd(x, w, b, stride, padding):
     """conv(x, w) + b: the library's thin kernel or MIOpen."""
     if _is_thin(x, w, stride, padding):
         return _thin_conv(x, w, b, 0)
+    if _is_wino(x, w, stride, padding, 0):
+        return _wino_conv(x, w, b, 0)
     return F.conv2d(x, w, b, stride, padding)
 
 
@@ -142,6 +205,13 @@ def _bwd(gy, x, w, stride, padding, mask):
     if _is_thin(x, w, stride, padding):
         gx = _thin_conv(gy, w, None, 1) if mask[0] else None
         gw = _thin_wgrad(gy, x) if mask[1] else None
+        return gx, gw
+    if mask[0] and _is_wino(gy, w, stride, padding, 1):
+        gx = _wino_conv(gy, w, None, 1)
+        gw = None
+        if mask[1]:
+            _, gw, _ = _aten.convolution_backward(gy, x, w, None, stride, padding, [1, 1], False,
+                                                  [0, 0], 1, [False, True, False])
         return gx, gw
     gx, gw, _ = _aten.convolution_backward(gy, x, w, None, stride, padding, [1, 1], False,
                                            [0, 0], 1, [mask[0], mask[1], False])

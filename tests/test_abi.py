@@ -39,7 +39,7 @@ def test_status_strings(L):
     from gan.core import _lib
     assert L.smmd_status_string(0) == b'SMMD_OK'
     assert b'EINVAL' in L.smmd_status_string(1)
-    assert L.smmd_abi_version() == _lib.ABI_VERSION == 7
+    assert L.smmd_abi_version() == _lib.ABI_VERSION == 8
 
 
 def test_workspace_sizing(L):
@@ -93,6 +93,20 @@ def test_argument_validation_without_gpu(L):
     assert L.smmd_adam_flat_sn(x, x, x, x, big, 97, 1.0, 1.0, 1e-4, 0.5, 0.9, 1e-8, 1, x,
                                1 << 20, arr, (ctypes.c_int32 * 1)(0), 1, x, 1 << 20, None) == 4
     assert L.smmd_witness_bwd(d, x, 4, x, 4, x, 4, 1, None, x, x, x, None) == 1
+    # Winograd 3x3: shapes it does not tile, missing operands, a short workspace
+    assert L.smmd_wino3x3_supported(64, 64, 64, 64, 64) == 1
+    assert L.smmd_wino3x3_supported(64, 60, 64, 64, 64) == 0       # ci % 8
+    assert L.smmd_wino3x3_supported(64, 64, 96, 64, 64) == 0       # ko % 64
+    assert L.smmd_wino3x3_supported(64, 64, 64, 63, 64) == 0       # odd height
+    assert L.smmd_wino3x3_filter(x, 96, 64, 0, x, 1 << 30, None) == 4
+    assert L.smmd_wino3x3_filter(x, 64, 64, 2, x, 1 << 30, None) == 1
+    assert L.smmd_wino3x3_filter(x, 64, 64, 0, x, 16 * 64 * 64 * 4 - 1, None) == 3
+    assert L.smmd_wino3x3_conv(None, x, None, x, 2, 8, 64, 4, 4, None, 0, None) == 1
+    assert L.smmd_wino3x3_conv(x, x, None, x, 2, 8, 64, 5, 4, None, 0, None) == 4
+    need = L.smmd_wino3x3_workspace_bytes(64, 512, 512, 8, 8)       # split input channels
+    assert need >= 2 * 64 * 512 * 64 * 4
+    assert L.smmd_wino3x3_conv(x, x, None, x, 64, 512, 512, 8, 8, x, need - 1, None) == 3
+    assert L.smmd_wino3x3_workspace_bytes(64, 64, 64, 64, 64) == 0
 
 
 def test_product_never_imports_oracle():

@@ -1,0 +1,14 @@
+# Winograd conv: its GPU tests, the critic-step mirror tests, then the bench
+# with SMMD_WINO=0/1 (interleaved pairs).  bash tools/gpu_wino_ab.sh TAG
+set -o pipefail
+TAG=${1:-wino}
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests/test_gpu_wino.py tests/test_gpu_model.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/${TAG}_tests.txt 2>&1 || { echo "tests rc=$?"; tail -40 gpurun_out/${TAG}_tests.txt; exit 1; }
+tail -2 gpurun_out/${TAG}_tests.txt
+for i in 1 2; do
+  for v in 0 1; do
+    SMMD_WINO=$v timeout -k 10 300 python bench.py --steps 30 --warmup 6 --no-cpu-baseline --mmd-sweep 2 --ref-schedule-steps 0 > gpurun_out/${TAG}_bench_w${v}_${i}.json 2> gpurun_out/${TAG}_bench_w${v}_${i}.err || { echo "bench rc=$?"; tail -20 gpurun_out/${TAG}_bench_w${v}_${i}.err; exit 1; }
+    python -c "import json; r=json.load(open('gpurun_out/${TAG}_bench_w${v}_${i}.json')); print('SMMD_WINO=$v', r['value'], r['ms_per_step'], r.get('step_ms_by_kind'))"
+  done
+done
