@@ -502,6 +502,7 @@ def instrumented_pass(model, images, cycles, world, dev):
     _lib.enable_timing(False)
     tm = _lib.timing_ms()
     tb = _lib.timing_bytes()
+    tb.update({k + '#flops': v for k, v in _lib.timing_flops().items()})
     step_ms = {k: sum(a.elapsed_time(b) for a, b in v) / len(v) for k, v in ev.items() if v}
     return tm, tb, step_ms, 6 * cycles
 
@@ -744,7 +745,8 @@ def main():
             'smmd_smmd_loss_fwd': BATCH * per_img * 4 + 4 * BATCH * 4 + 8 * 4,
             'smmd_smmd_loss_bwd': 2 * BATCH * per_img * 4 + 4 * BATCH * 4,
         }
-        alg.update({k: int(v) for k, v in tb.items()})
+        alg.update({k: int(v) for k, v in tb.items() if not k.endswith('#flops')})
+        mfma_flops = {k[:-6]: v for k, v in tb.items() if k.endswith('#flops')}
         for name, (calls, ms) in tm.items():
             b = alg.get(name)
             row = {'calls': calls, 'avg_ms': round(ms, 5),
@@ -758,6 +760,11 @@ def main():
         # bound at D = 1 and is reported in roofline_hot_path)
         cands = [k for k in kernels if k in HOT_PATH and 'GB_s' in kernels[k]
                  and k != 'smmd_mmd2_fwd']
+        for name, fl in mfma_flops.items():
+            if name in kernels:
+                tf = fl / (kernels[name]['avg_ms'] * 1e-3) / 1e12
+                kernels[name].update(mfma_flops=int(fl), tflops=round(tf, 2),
+                                     mfma_frac=round(tf / MFMA_F32_PEAK_TFS, 4))
         if cands:
             dom = max(cands, key=lambda k: kernels[k]['ms_per_step'])
             traffic, src = pmc_traffic(dom)
@@ -766,6 +773,24 @@ def main():
                         'traffic': traffic, 'traffic_source': src,
                         'avg_ms': kernels[dom]['avg_ms'],
                         'algorithmic_bytes': kernels[dom]['bytes']}
+        # the library's dominant kernel by time per step: the Winograd
+        # convolution (matrix-core bound) once it serves the 3x3 layers
+        wk = 'smmd_wino3x3_conv'
+        if wk in kernels and 'tflops' in kernels[wk] and (
+                roofline is None or kernels[wk]['ms_per_step'] > kernels[roofline['kernel']]['ms_per_step']):
+            hot['hbm_roofline_kernel'] = roofline
+            traffic, src = pmc_traffic(wk)
+            roofline = {'bound': 'mfma', 'kernel': wk, 'achieved': kernels[wk]['tflops'],
+                        'peak': MFMA_F32_PEAK_TFS, 'unit': 'TFLOP/s',
+                        'frac': kernels[wk]['mfma_frac'], 'traffic': traffic,
+                        'traffic_source': src, 'avg_ms': kernels[wk]['avg_ms'],
+                        'calls_per_step': round(kernels[wk]['calls'] / n_inst, 2),
+                        'ms_per_step': kernels[wk]['ms_per_step'],
+                        'executed_flops_per_call': kernels[wk]['mfma_flops'],
+                        'algorithmic_bytes': kernels[wk].get('bytes'),
+                        'note': 'executed flops = the F(2x2,3x3) point products (16 per '
+                                '2x2 tile and channel pair, f32 MFMA); the direct-conv '
+                                'equivalent is 2.25x these'}
         for k in ('smmd_sn_power_iter', 'smmd_sn_weight_bwd', 'smmd_sn_grad_stats',
                   'smmd_adam_flat_sn[D]',
                   'smmd_scaled_loss_fwd', 'smmd_scaled_loss_bwd', 'smmd_smmd_loss_fwd',

@@ -21,8 +21,12 @@
 // (k, tile) every point lives in the same lane and register and the output
 // transform runs in registers.  Input channels go 8 per chunk through a
 // double-buffered LDS stage (V 32 KB + U 32 KB per buffer): chunk c+1's
-// global loads are issued before chunk c's 64 MFMAs per wave, transformed and
-// stored after them, one barrier per chunk.
+// global loads are issued before chunk c's 64 MFMAs per wave; its transform
+// and LDS stores are cut into 32 slices issued one after each of the second
+// half's MFMAs (in the matrix core's shadow), one barrier per chunk.
+// Measured and not kept: a 16x16x4 form with 32 output channels per block,
+// 128 accumulator registers and two workgroups per CU (129 / 110 / 101 / 118
+// us vs 132 / 112 / 97 / 102 us on the four SNResNet-64 layers).
 #include "smmd_common.hpp"
 
 namespace smmd {
@@ -49,45 +53,56 @@ __device__ __forceinline__ float wn_from_right(float v) {  // lane l gets lane l
                                                                  0x130, 0xf, 0xf, false));
 }
 
-// U = G g G^T for one (ko, ci) filter, stored in the conv kernel's LDS order:
-// u[kb][chunk][p][h][k64][c4], c = 4 h + c4 within the chunk of 8
+// U = G g G^T for the filters (ko, 4 q .. 4 q + 3), stored in the conv
+// kernel's LDS order u[kb][chunk][p][h][k64][c4] (c = 4 h + c4 within the
+// chunk of 8): a thread owns one ko and four consecutive ci, so each point's
+// four values are one float4 store and consecutive lanes (consecutive ko)
+// store consecutive 16 bytes
 __global__ void wino_filter_kernel(const float *__restrict__ w, int KO, int CI, int mode,
                                    float *__restrict__ u) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= (int64_t)KO * CI) return;
-    const int ci = (int)(idx % CI), ko = (int)(idx / CI);
-    float g[3][3];
-    if (mode == 0) {
-        const float *s = w + ((int64_t)ko * CI + ci) * 9;
+    if (idx >= (int64_t)KO * (CI >> 2)) return;
+    const int ko = (int)(idx % KO), q = (int)(idx / KO);
+    float r[16][4];
 #pragma unroll
-        for (int i = 0; i < 3; ++i)
+    for (int e = 0; e < 4; ++e) {
+        const int ci = 4 * q + e;
+        float g[3][3];
+        if (mode == 0) {
+            const float *s = w + ((int64_t)ko * CI + ci) * 9;
 #pragma unroll
-            for (int j = 0; j < 3; ++j) g[i][j] = s[i * 3 + j];
-    } else {            // w is [CI][KO][3][3] of the forward conv; flip both taps
-        const float *s = w + ((int64_t)ci * KO + ko) * 9;
+            for (int i = 0; i < 3; ++i)
 #pragma unroll
-        for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j) g[i][j] = s[i * 3 + j];
+        } else {        // w is [CI][KO][3][3] of the forward conv; flip both taps
+            const float *s = w + ((int64_t)ci * KO + ko) * 9;
 #pragma unroll
-            for (int j = 0; j < 3; ++j) g[i][j] = s[(2 - i) * 3 + (2 - j)];
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) g[i][j] = s[(2 - i) * 3 + (2 - j)];
+        }
+        float t[4][3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            t[0][j] = g[0][j];
+            t[1][j] = 0.5f * (g[0][j] + g[1][j] + g[2][j]);
+            t[2][j] = 0.5f * (g[0][j] - g[1][j] + g[2][j]);
+            t[3][j] = g[2][j];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            r[i * 4 + 0][e] = t[i][0];
+            r[i * 4 + 1][e] = 0.5f * (t[i][0] + t[i][1] + t[i][2]);
+            r[i * 4 + 2][e] = 0.5f * (t[i][0] - t[i][1] + t[i][2]);
+            r[i * 4 + 3][e] = t[i][2];
+        }
     }
-    float t[4][3];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        t[0][j] = g[0][j];
-        t[1][j] = 0.5f * (g[0][j] + g[1][j] + g[2][j]);
-        t[2][j] = 0.5f * (g[0][j] - g[1][j] + g[2][j]);
-        t[3][j] = g[2][j];
-    }
-    const int kb = ko >> 6, kl = ko & 63, cc = ci >> 3, cl = ci & 7;
+    const int kb = ko >> 6, kl = ko & 63, cc = q >> 1, h = q & 1;
+    float4 *u4 = reinterpret_cast<float4 *>(u);
     const int64_t base = ((int64_t)kb * (CI >> 3) + cc) * 16;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const float r[4] = {t[i][0], 0.5f * (t[i][0] + t[i][1] + t[i][2]),
-                            0.5f * (t[i][0] - t[i][1] + t[i][2]), t[i][2]};
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            u[(((base + i * 4 + j) * 2 + (cl >> 2)) * 64 + kl) * 4 + (cl & 3)] = r[j];
-    }
+    for (int p = 0; p < 16; ++p)
+        u4[((base + p) * 2 + h) * 64 + kl] = make_float4(r[p][0], r[p][1], r[p][2], r[p][3]);
 }
 
 struct WnGeom {
@@ -151,6 +166,41 @@ __device__ __forceinline__ void wn_transform(const float2 (&r)[4], const float *
     }
 }
 
+// one patch row of V's input: d[i][0..3] = (left neighbour, 2tx, 2tx+1,
+// right neighbour), zero outside the image
+template <bool EDGE>
+__device__ __forceinline__ void wn_row(float2 r, const float *__restrict__ xc, int ty, int tx,
+                                       bool ok, const WnGeom &g, int lane, int i, float (&d)[4]) {
+    const int yy = 2 * ty - 1 + i;
+    const bool row = ok && yy >= 0 && yy < g.H;
+    const float cx = row ? r.x : 0.f, cy = row ? r.y : 0.f;
+    float L = wn_from_left(cy), R = wn_from_right(cx);
+    if (EDGE) {
+        if (tx > 0 && lane == 0) L = row ? xc[(int64_t)yy * g.W + 2 * tx - 1] : 0.f;
+        if (tx < g.TW - 1 && lane == 63) R = row ? xc[(int64_t)yy * g.W + 2 * tx + 2] : 0.f;
+    }
+    d[0] = tx == 0 ? 0.f : L;
+    d[1] = cx;
+    d[2] = cy;
+    d[3] = tx == g.TW - 1 ? 0.f : R;
+}
+
+// column j of t = B^T d
+__device__ __forceinline__ void wn_bt_col(const float (&d)[4][4], int j, float (&t)[4][4]) {
+    t[0][j] = d[0][j] - d[2][j];
+    t[1][j] = d[1][j] + d[2][j];
+    t[2][j] = d[2][j] - d[1][j];
+    t[3][j] = d[1][j] - d[3][j];
+}
+
+// row i of v = t B
+__device__ __forceinline__ void wn_b_row(const float (&t)[4][4], int i, float (&v)[4][4]) {
+    v[i][0] = t[i][0] - t[i][2];
+    v[i][1] = t[i][1] + t[i][2];
+    v[i][2] = t[i][2] - t[i][1];
+    v[i][3] = t[i][1] - t[i][3];
+}
+
 template <bool EDGE>
 __global__ __launch_bounds__(WN_T, 1) void wino_conv_kernel(
     const float *__restrict__ x, const float *__restrict__ u, const float *__restrict__ bias,
@@ -185,10 +235,8 @@ __global__ __launch_bounds__(WN_T, 1) void wino_conv_kernel(
     xn += (int64_t)c0 * WN_CC * HW;
 
     float2 raw[2][4];
-    // the filter stage goes through registers, loaded by inline asm so the
-    // compiler can neither sink the loads to their use after the MFMAs nor
-    // drain them ahead of the LDS reads (an LDS-DMA would be waited for
-    // before every ds_read); `wn_wait_u` retires them before the LDS write
+    // the filter stage goes through registers (an LDS-DMA load would make
+    // the compiler wait for it before every ds_read of the MFMA phase)
     f4v ur[8];
 #define WN_LOAD_CHUNK(CC_)                                                                   \
     do {                                                                                     \
@@ -197,13 +245,10 @@ __global__ __launch_bounds__(WN_T, 1) void wino_conv_kernel(
                          raw[e]);                                                            \
         const float4 *src_ = ub + (int64_t)(CC_) * (WN_STAGE / 4) + w * 512 + lane;          \
         _Pragma("unroll") for (int i = 0; i < 8; ++i)                                        \
-            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(ur[i]) : "v"(src_ + i * 64)); \
+            ur[i] = *reinterpret_cast<const f4v *>(src_ + i * 64);                            \
     } while (0)
 #define WN_STORE_CHUNK(CC_, BUF_)                                                            \
     do {                                                                                     \
-        asm volatile("s_waitcnt vmcnt(0)"                                                    \
-                     : "+v"(ur[0]), "+v"(ur[1]), "+v"(ur[2]), "+v"(ur[3]), "+v"(ur[4]),      \
-                       "+v"(ur[5]), "+v"(ur[6]), "+v"(ur[7])::"memory");                     \
         f4v *U_ = reinterpret_cast<f4v *>(Us + (BUF_) * (WN_STAGE / 4) + w * 512 + lane);    \
         _Pragma("unroll") for (int i = 0; i < 8; ++i) U_[i * 64] = ur[i];                    \
         float v_[2][16];                                                                     \
@@ -248,33 +293,100 @@ __global__ __launch_bounds__(WN_T, 1) void wino_conv_kernel(
             acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca0.w, cb0.w, acc[p], 0, 0, 0);    \
             acc[p + 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca1.w, cb1.w, acc[p + 1], 0, 0, 0); \
         }                                                                                    \
-        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);                                   \
-        _Pragma("unroll") for (int pp = 0; pp < 7; ++pp) {                                   \
-            __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);                               \
-            __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);                               \
-        }                                                                                    \
-        __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);                                   \
     } while (0)
 
     WN_LOAD_CHUNK(0);
     WN_STORE_CHUNK(0, 0);
     __syncthreads();
     for (int cc = 0; cc + 1 < nchunk; ++cc) {
+        const int buf = cc & 1, nbuf = buf ^ 1;
         WN_LOAD_CHUNK(cc + 1);          // in flight during this chunk's MFMAs
         __builtin_amdgcn_sched_barrier(0);
-        WN_MFMA_CHUNK(cc & 1);
+        const float4 *V_ = Vs + buf * (WN_STAGE / 4);
+        const float4 *U_ = Us + buf * (WN_STAGE / 4);
+        float4 a0 = U_[hl * 64 + kh * 32 + l32], b0 = V_[hl * 64 + th * 32 + l32];
+        float4 a1 = U_[(2 + hl) * 64 + kh * 32 + l32], b1 = V_[(2 + hl) * 64 + th * 32 + l32];
+        // first half: 32 MFMAs, the loads' cover
+#pragma unroll
+        for (int pp = 0; pp < 4; ++pp) {
+            const int p = 2 * pp;
+            const float4 ca0 = a0, cb0 = b0, ca1 = a1, cb1 = b1;
+            a0 = U_[((p + 2) * 2 + hl) * 64 + kh * 32 + l32];
+            b0 = V_[((p + 2) * 2 + hl) * 64 + th * 32 + l32];
+            a1 = U_[((p + 3) * 2 + hl) * 64 + kh * 32 + l32];
+            b1 = V_[((p + 3) * 2 + hl) * 64 + th * 32 + l32];
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) {
+                acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca0[s4], cb0[s4], acc[p], 0, 0, 0);
+                acc[p + 1] =
+                    __builtin_amdgcn_mfma_f32_32x32x2f32(ca1[s4], cb1[s4], acc[p + 1], 0, 0, 0);
+            }
+        }
         __builtin_amdgcn_sched_barrier(0);
-        WN_STORE_CHUNK(cc + 1, (cc + 1) & 1);
+        // second half: after each MFMA one slice of the next chunk's
+        // transform and LDS stores (the other buffer), issued in the MFMA's
+        // shadow; sched_barrier pins the order
+        float d0[4][4], d1[4][4], t0[4][4], t1[4][4], v0[4][4], v1[4][4];
+        const float *xc0 = xn + (int64_t)((cc + 1) * WN_CC + 2 * w) * HW;
+        f4v *Un = reinterpret_cast<f4v *>(Us + nbuf * (WN_STAGE / 4) + w * 512 + lane);
+        float2 *Vn = reinterpret_cast<float2 *>(Vs + nbuf * (WN_STAGE / 4));
+#pragma unroll
+        for (int pp = 4; pp < 8; ++pp) {
+            const int p = 2 * pp;
+            const float4 ca0 = a0, cb0 = b0, ca1 = a1, cb1 = b1;
+            if (pp < 7) {
+                a0 = U_[((p + 2) * 2 + hl) * 64 + kh * 32 + l32];
+                b0 = V_[((p + 2) * 2 + hl) * 64 + th * 32 + l32];
+                a1 = U_[((p + 3) * 2 + hl) * 64 + kh * 32 + l32];
+                b1 = V_[((p + 3) * 2 + hl) * 64 + th * 32 + l32];
+            }
+#pragma unroll
+            for (int m = 0; m < 8; ++m) {
+                const int s4 = m >> 1, q = m & 1;
+                if (q == 0)
+                    acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca0[s4], cb0[s4], acc[p], 0, 0, 0);
+                else
+                    acc[p + 1] =
+                        __builtin_amdgcn_mfma_f32_32x32x2f32(ca1[s4], cb1[s4], acc[p + 1], 0, 0, 0);
+                const int K = (pp - 4) * 8 + m;
+                if (K < 8) {                         // patch rows of channel K / 4
+                    const int e = K >> 2, i = K & 3;
+                    wn_row<EDGE>(raw[e][i], xc0 + e * HW, tty, ttx, tok, g, lane, i,
+                                 e ? d1[i] : d0[i]);
+                } else if (K < 16) {                 // the filter stage
+                    Un[(K - 8) * 64] = ur[K - 8];
+                } else if (K < 20) {                 // B^T d, column j, channel 0
+                    wn_bt_col(d0, K - 16, t0);
+                } else if (K < 24) {                 // (B^T d) B, row i, channel 0
+                    wn_b_row(t0, K - 20, v0);
+                } else if (K < 28) {
+                    wn_bt_col(d1, K - 24, t1);
+                } else {                             // channel 1's row i, both stored
+                    const int i = K - 28;
+                    wn_b_row(t1, i, v1);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        Vn[(((i * 4 + j) * 2 + (w >> 1)) * 64 + lane) * 2 + (w & 1)] =
+                            make_float2(v0[i][j], v1[i][j]);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
         __syncthreads();
     }
     WN_MFMA_CHUNK((nchunk - 1) & 1);
 
-    // epilogue: C_p[k][tile], k = (r & 3) + 8 (r >> 2) + 4 hl, tile = l32
+    // epilogue: C_p[k][tile], k = (r & 3) + 8 (r >> 2) + 4 hl, tile = l32.
+    // With an even tile-row width the lane pair (2i, 2i+1) holds two
+    // neighbouring tiles: the even lane stores row 0 of both, the odd lane
+    // row 1 (one DPP swap of two floats), so every store is a float4
     const int64_t et = tile0 + th * 32 + l32;
-    if (et >= g.T) return;
-    const int en = (int)(et / g.Timg);
+    const bool eok = et < g.T;
+    const int en = eok ? (int)(et / g.Timg) : 0;
     const int er = (int)(et - (int64_t)en * g.Timg);
     const int ety = er / g.TW, etx = er - ety * g.TW;
+    const bool pairs = (g.TW & 1) == 0;
+    const bool odd = lane & 1;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const int k = kb * WN_KB + kh * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
@@ -288,11 +400,26 @@ __global__ __launch_bounds__(WN_T, 1) void wino_conv_kernel(
             s1[j] = m[4 + j] - m[8 + j] - m[12 + j];
         }
         const float b = bias ? bias[k] : 0.f;
+        const float y00 = s0[0] + s0[1] + s0[2] + b, y01 = s0[1] - s0[2] - s0[3] + b;
+        const float y10 = s1[0] + s1[1] + s1[2] + b, y11 = s1[1] - s1[2] - s1[3] + b;
         float *o = y + (((int64_t)en * g.K + k) * g.H + 2 * ety) * g.W + 2 * etx;
-        *reinterpret_cast<float2 *>(o) =
-            make_float2(s0[0] + s0[1] + s0[2] + b, s0[1] - s0[2] - s0[3] + b);
-        *reinterpret_cast<float2 *>(o + g.W) =
-            make_float2(s1[0] + s1[1] + s1[2] + b, s1[1] - s1[2] - s1[3] + b);
+        if (pairs) {
+            // even lanes send row 1, odd lanes row 0, to the partner lane
+            const float sx = odd ? y00 : y10, sy = odd ? y01 : y11;
+            const float rx = __builtin_bit_cast(
+                float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, sx), 0xb1, 0xf, 0xf, false));
+            const float ry = __builtin_bit_cast(
+                float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, sy), 0xb1, 0xf, 0xf, false));
+            if (eok) {
+                if (!odd)
+                    *reinterpret_cast<float4 *>(o) = make_float4(y00, y01, rx, ry);
+                else
+                    *reinterpret_cast<float4 *>(o + g.W - 2) = make_float4(rx, ry, y10, y11);
+            }
+        } else if (eok) {
+            *reinterpret_cast<float2 *>(o) = make_float2(y00, y01);
+            *reinterpret_cast<float2 *>(o + g.W) = make_float2(y10, y11);
+        }
     }
 }
 
@@ -345,9 +472,10 @@ extern "C" smmd_status smmd_wino3x3_filter(const float *w, int ko, int ci, int m
                                            size_t u_bytes, smmd_stream_t stream) {
     if (ko <= 0 || ci <= 0 || (mode != 0 && mode != 1) || !w || !u) return SMMD_EINVAL;
     if (ko % WN_KB || ci % WN_CC) return SMMD_EUNSUPPORTED;
+    if (reinterpret_cast<uintptr_t>(u) & 15) return SMMD_EINVAL;
     if (u_bytes < smmd_wino3x3_filter_bytes(ko, ci)) return SMMD_EWORKSPACE;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    const int64_t n = (int64_t)ko * ci;
+    const int64_t n = (int64_t)ko * (ci / 4);
     wino_filter_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st>>>(w, ko, ci, mode, u);
     return last_launch_status();
 }
@@ -366,7 +494,9 @@ extern "C" smmd_status smmd_wino3x3_conv(const float *x, const float *u, const f
     if (n == 0 || h == 0 || w_img == 0) return SMMD_OK;
     if (!x || !u || !y) return SMMD_EINVAL;
     if (!smmd_wino3x3_supported(n, ci, ko, h, w_img)) return SMMD_EUNSUPPORTED;
-    if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15) return SMMD_EINVAL;
+    if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y) |
+         reinterpret_cast<uintptr_t>(u)) & 15)
+        return SMMD_EINVAL;
     WnGeom g;
     g.N = n; g.C = ci; g.K = ko; g.H = h; g.W = w_img;
     g.TW = w_img / 2;

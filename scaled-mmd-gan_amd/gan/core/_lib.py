@@ -239,6 +239,7 @@ class _Timing:
     enabled = False
     records = {}
     nbytes = {}       # entry point -> algorithmic bytes summed over its timed calls
+    nflops = {}       # entry point -> executed MFMA flops summed over its timed calls
 
 
 class _NullCtx:
@@ -280,6 +281,19 @@ def add_bytes(name, n):
         _Timing.nbytes[name] = _Timing.nbytes.get(name, 0) + int(n)
 
 
+def add_flops(name, n):
+    """Executed matrix-core flops of one call (the Winograd convolution's
+    point products; bench.py reports the mean per call)."""
+    if _Timing.enabled:
+        _Timing.nflops[name] = _Timing.nflops.get(name, 0) + int(n)
+
+
+def timing_flops():
+    """{entry point: mean executed flops per timed call} (add_flops users)."""
+    return {k: f / len(_Timing.records[k]) for k, f in _Timing.nflops.items()
+            if _Timing.records.get(k)}
+
+
 def timing_bytes():
     """{entry point: mean algorithmic bytes per timed call} (add_bytes users)."""
     return {k: b / len(_Timing.records[k]) for k, b in _Timing.nbytes.items()
@@ -300,6 +314,7 @@ def timing_ms():
 def reset_timing():
     _Timing.records = {}
     _Timing.nbytes = {}
+    _Timing.nflops = {}
 
 
 # ---------------------------------------------------------------------------

@@ -34,6 +34,8 @@ GROUPS = {
     'smmd_conv3x3_thin': ('thin_in_kernel', 'thin_out_kernel'),
     'smmd_conv3x3_thin_wgrad': ('thin_wgrad_mfma_kernel', 'thin_wgrad_kernel',
                                 'thin_wgrad_final_kernel'),
+    'smmd_wino3x3_conv': ('wino_conv_kernel', 'wino_reduce_kernel'),
+    'smmd_wino3x3_filter': ('wino_filter_kernel',),
 }
 # entry points whose calls each run ONE of their kernels (fold or adjoint;
 # thin_in or thin_out):
