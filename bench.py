@@ -773,11 +773,15 @@ def main():
                         'traffic': traffic, 'traffic_source': src,
                         'avg_ms': kernels[dom]['avg_ms'],
                         'algorithmic_bytes': kernels[dom]['bytes']}
-        # the library's dominant kernel by time per step: the Winograd
-        # convolution (matrix-core bound) once it serves the 3x3 layers
-        wk = 'smmd_wino3x3_conv'
-        if wk in kernels and 'tflops' in kernels[wk] and (
-                roofline is None or kernels[wk]['ms_per_step'] > kernels[roofline['kernel']]['ms_per_step']):
+        # the library's dominant kernel by time per step: a Winograd
+        # convolution (matrix-core bound) once they serve the conv layers
+        mf = [k for k in kernels if 'tflops' in kernels[k]]
+        for k in mf:
+            hot[k] = {q: kernels[k][q] for q in ('avg_ms', 'ms_per_step', 'calls', 'mfma_flops',
+                                                 'tflops', 'mfma_frac')}
+        wk = max(mf, key=lambda k: kernels[k]['ms_per_step']) if mf else None
+        if wk and (roofline is None
+                   or kernels[wk]['ms_per_step'] > kernels[roofline['kernel']]['ms_per_step']):
             hot['hbm_roofline_kernel'] = roofline
             traffic, src = pmc_traffic(wk)
             roofline = {'bound': 'mfma', 'kernel': wk, 'achieved': kernels[wk]['tflops'],
@@ -788,9 +792,10 @@ def main():
                         'ms_per_step': kernels[wk]['ms_per_step'],
                         'executed_flops_per_call': kernels[wk]['mfma_flops'],
                         'algorithmic_bytes': kernels[wk].get('bytes'),
-                        'note': 'executed flops = the F(2x2,3x3) point products (16 per '
-                                '2x2 tile and channel pair, f32 MFMA); the direct-conv '
-                                'equivalent is 2.25x these'}
+                        'note': 'executed flops = the Winograd point products on the f32 '
+                                'MFMA (F(2x2,3x3): 16 per 2x2 tile and channel pair, 2.25x '
+                                'fewer than the direct conv; F(2x2,2x2) polyphase: 9 per tile '
+                                'and phase channel, 1.78x fewer)'}
         for k in ('smmd_sn_power_iter', 'smmd_sn_weight_bwd', 'smmd_sn_grad_stats',
                   'smmd_adam_flat_sn[D]',
                   'smmd_scaled_loss_fwd', 'smmd_scaled_loss_bwd', 'smmd_smmd_loss_fwd',

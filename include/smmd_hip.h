@@ -64,7 +64,7 @@ int smmd_abi_version(void);         /* bumped on any ABI change (2: Gram/poly,
                                        smmd_bn_relu_fwd, 7: smmd_smmd_loss_fwd/bwd,
                                        smmd_source_hash, smmd_sn_grad_stats,
                                        smmd_adam_flat_sn2, smmd_bn_relu_fwd_save / _bwd,
-                                       8: smmd_wino3x3_*) */
+                                       8: smmd_wino3x3_*, smmd_wino4x4s2*) */
 const char *smmd_source_hash(void); /* first 16 hex digits of the SHA-256 of the
                                        sources this binary was built from
                                        (csrc .hip and .hpp files in byte order,
@@ -593,6 +593,51 @@ size_t smmd_wino3x3_workspace_bytes(int n, int ci, int ko, int h, int w_img);
 smmd_status smmd_wino3x3_conv(const float *x, const float *u, const float *bias, float *y, int n,
                               int ci, int ko, int h, int w_img, void *ws, size_t ws_bytes,
                               smmd_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * 4x4 stride-2 padding-1 convolutions as polyphase Winograd F(2x2, 2x2) on the
+ * f32 MFMA: the critics' ConvMeanPool layers (gan/core/resnet/block.py:63-66;
+ * mean_pool2(conv3x3(x, W)) is conv4x4_s2(x, W'), W' the pool-folded filter,
+ * smmd_fold_pool_weights) and their input gradient, which is also the
+ * generators' UpsampleConv folded into one transposed conv
+ * (block.py:53-60).  NCHW fp32; x split into its four 2 x 2 phases makes each
+ * an F(2x2, 2x2) problem: 9 point products per 2 x 2 output tile against 16
+ * multiplies of the direct conv.
+ *
+ * smmd_wino4x4s2_filter / smmd_wino4x4s2t_filter: the transformed filters of
+ *   W' [ko, ci, 4, 4] for the conv, or of W' [k, c, 4, 4] for the transposed
+ *   conv; u holds smmd_wino4x4s2_filter_bytes(ko, ci) bytes (16-byte aligned).
+ * smmd_wino4x4s2_conv: y [n, ko, h/2, w/2] = conv2d(x [n, ci, h, w], W',
+ *   stride 2, padding 1) + bias; needs h, w % 4 == 0, ci % 2 == 0, ko % 64 == 0.
+ * smmd_wino4x4s2t_conv: dx [n, c, 2 hg, 2 wg] = conv_transpose2d(gy [n, k, hg,
+ *   wg], W', stride 2, padding 1) + bias; needs hg, wg even, k % 8 == 0,
+ *   c % 64 == 0.
+ * Small grids split the reduction over several workgroups and add the partial
+ * outputs in slice order from the workspace (*_workspace_bytes; 0 = none).
+ * ------------------------------------------------------------------------- */
+int smmd_wino4x4s2_supported(int n, int ci, int ko, int h, int w_img);
+
+int smmd_wino4x4s2t_supported(int n, int k, int c, int hg, int wg);
+
+size_t smmd_wino4x4s2_filter_bytes(int ko, int ci);
+
+smmd_status smmd_wino4x4s2_filter(const float *w, int ko, int ci, float *u, size_t u_bytes,
+                                  smmd_stream_t stream);
+
+smmd_status smmd_wino4x4s2t_filter(const float *w, int k, int c, float *u, size_t u_bytes,
+                                   smmd_stream_t stream);
+
+size_t smmd_wino4x4s2_workspace_bytes(int n, int ci, int ko, int h, int w_img);
+
+size_t smmd_wino4x4s2t_workspace_bytes(int n, int k, int c, int hg, int wg);
+
+smmd_status smmd_wino4x4s2_conv(const float *x, const float *u, const float *bias, float *y,
+                                int n, int ci, int ko, int h, int w_img, void *ws,
+                                size_t ws_bytes, smmd_stream_t stream);
+
+smmd_status smmd_wino4x4s2t_conv(const float *gy, const float *u, const float *bias, float *dx,
+                                 int n, int k, int c, int hg, int wg, void *ws, size_t ws_bytes,
+                                 smmd_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,635 @@
+// smmd_wino_s2.hip -- 4x4 stride-2 pad-1 convolutions (the folded ConvMeanPool
+// layers of the critic, gan/core/resnet/block.py:63-66 as one strided conv,
+// convops.fold_pool_weight) as polyphase Winograd F(2x2, 2x2) on the f32 MFMA.
+//
+// Split x into its four 2 x 2 phases and W' into four 2 x 2 taps: the conv is
+// the sum over (c, phase) of 2 x 2 stride-1 correlations, i.e. one F(2x2, 2x2)
+// problem with 4 C reduction channels: 9 point products per 2 x 2 output tile
+// and (phase channel, k) pair, against 16 multiplies of the direct conv
+// (1.78x fewer).  For output tile (ty, tx) and phase (pi, pj) the 3 x 3 input
+// tile is x rows 4ty-1+pi+2a, cols 4tx-1+pj+2b (a, b in 0..2), the filter
+// g[a][b] = W'[k][c][2a+pi][2b+pj] (a, b in 0..1).
+//
+//   V = B^T d B,  B^T = [[1,-1,0],[0,1,0],[0,-1,1]]
+//   U = G g G^T,  G   = [[1,0],[1,1],[0,1]]
+//   y = A^T M A,  A^T = [[1,1,0],[0,1,1]]
+//
+// Block: 64 tiles x 64 output channels, 4 waves, wave (kh, th) the 32 x 32
+// quadrant for all 9 points (9 f32x16 accumulators); chunks of 8 phase
+// channels (2 input channels x 4 phases) through a double-buffered 36 KB LDS
+// stage, so two workgroups fit a CU.
+#include "smmd_common.hpp"
+
+namespace smmd {
+
+namespace {
+
+constexpr int S2_T = 256;
+constexpr int S2_TB = 64;
+constexpr int S2_KB = 64;
+constexpr int S2_CC = 2;                     // input channels per chunk (8 phase channels)
+constexpr int S2_STAGE = 9 * 8 * 64;         // floats per V (and per U) stage
+constexpr size_t S2_LDS = 2 * 2 * S2_STAGE * sizeof(float);   // 72 KB
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float s2_from_left(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
+                                                                 0x138, 0xf, 0xf, false));
+}
+
+__device__ __forceinline__ float s2_from_right(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
+                                                                 0x130, 0xf, 0xf, false));
+}
+
+// U for (ko, ci): 4 phases x 9 points, stored u[kb][chunk][p9][h2][k64][c4]
+// with phase channel pc = 4 (ci & 1) + 2 pi + pj = 4 h + c4
+__global__ void s2_filter_kernel(const float *__restrict__ w, int KO, int CI,
+                                 float *__restrict__ u) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (int64_t)KO * CI) return;
+    const int ko = (int)(idx % KO), ci = (int)(idx / KO);
+    const float *s = w + ((int64_t)ko * CI + ci) * 16;
+    float f[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) f[i] = s[i];
+    const int kb = ko >> 6, kl = ko & 63, cc = ci >> 1, h = ci & 1;
+    const int64_t base = ((int64_t)kb * (CI >> 1) + cc) * 9;
+#pragma unroll
+    for (int pi = 0; pi < 2; ++pi)
+#pragma unroll
+        for (int pj = 0; pj < 2; ++pj) {
+            const float g00 = f[(pi) * 4 + pj], g01 = f[(pi) * 4 + 2 + pj];
+            const float g10 = f[(2 + pi) * 4 + pj], g11 = f[(2 + pi) * 4 + 2 + pj];
+            // Gg: rows (g0, g0 + g1, g1) over a, columns b
+            const float t[3][2] = {{g00, g01}, {g00 + g10, g01 + g11}, {g10, g11}};
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                const float r[3] = {t[i][0], t[i][0] + t[i][1], t[i][1]};
+#pragma unroll
+                for (int j = 0; j < 3; ++j)
+                    u[(((base + i * 3 + j) * 2 + h) * 64 + kl) * 4 + 2 * pi + pj] = r[j];
+            }
+        }
+}
+
+struct S2Geom {
+    int N, C, K, H, W, TW, Timg;   // H, W: the input's; output H/2 x W/2
+    int64_t T, slab;
+};
+
+template <bool EDGE>
+__global__ __launch_bounds__(S2_T, 2) void s2_conv_kernel(
+    const float *__restrict__ x, const float *__restrict__ u, const float *__restrict__ bias,
+    float *__restrict__ y, S2Geom g) {
+    extern __shared__ float4 s2_lds[];
+    float4 *const Vs = s2_lds;                         // [2][p9][h2][t64]  (float4 = c4)
+    float4 *const Us = s2_lds + 2 * (S2_STAGE / 4);    // [2][p9][h2][k64]
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int kb = blockIdx.y;
+    const int64_t tile0 = (int64_t)blockIdx.x * S2_TB;
+    const int nch = g.C / S2_CC;
+    const int c0 = (int)((int64_t)nch * blockIdx.z / gridDim.z);
+    const int nchunk = (int)((int64_t)nch * (blockIdx.z + 1) / gridDim.z) - c0;
+    y += (int64_t)blockIdx.z * g.slab;
+
+    // transform role: lane = tile; wave w = input channel e = w >> 1 of the
+    // chunk and row phase pi = w & 1, both column phases
+    const int e = w >> 1, pi = w & 1;
+    const int64_t gt = tile0 + lane;
+    const bool tok = gt < g.T;
+    int tn = 0, tty = 0, ttx = 0;
+    if (tok) {
+        tn = (int)(gt / g.Timg);
+        const int r = (int)(gt - (int64_t)tn * g.Timg);
+        tty = r / g.TW;
+        ttx = r - tty * g.TW;
+    }
+    const int64_t HW = (int64_t)g.H * g.W;
+    const float *xn = x + ((int64_t)tn * g.C + (int64_t)c0 * S2_CC + e) * HW;
+    const float4 *ub =
+        reinterpret_cast<const float4 *>(u) + ((int64_t)kb * nch + c0) * (S2_STAGE / 4);
+
+    float4 raw[3];
+    f4v ur[5];
+    auto load = [&](int cc) {
+        const float *xc = xn + (int64_t)cc * S2_CC * HW;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const int yy = 4 * tty - 1 + pi + 2 * a;
+            const int yc = min(max(yy, 0), g.H - 1);
+            raw[a] = *reinterpret_cast<const float4 *>(xc + (int64_t)yc * g.W + 4 * ttx);
+        }
+        const float4 *src = ub + (int64_t)cc * (S2_STAGE / 4) + tid;
+#pragma unroll
+        for (int i = 0; i < 5; ++i)
+            if (i * S2_T + tid < S2_STAGE / 4)
+                ur[i] = *reinterpret_cast<const f4v *>(src + i * S2_T);
+    };
+    auto store = [&](int cc, int buf) {
+        f4v *U = reinterpret_cast<f4v *>(Us + buf * (S2_STAGE / 4)) + tid;
+#pragma unroll
+        for (int i = 0; i < 5; ++i)
+            if (i * S2_T + tid < S2_STAGE / 4) U[i * S2_T] = ur[i];
+        const float *xc = xn + (int64_t)cc * S2_CC * HW;
+        // rows: columns 4tx-1 .. 4tx+4; pj = 0 takes (-1, 1, 3), pj = 1 (0, 2, 4)
+        float d0[3][3], d1[3][3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const int yy = 4 * tty - 1 + pi + 2 * a;
+            const bool row = tok && yy >= 0 && yy < g.H;
+            const float c0v = row ? raw[a].x : 0.f, c1v = row ? raw[a].y : 0.f;
+            const float c2v = row ? raw[a].z : 0.f, c3v = row ? raw[a].w : 0.f;
+            float L = s2_from_left(c3v), R = s2_from_right(c0v);
+            if (EDGE) {
+                if (ttx > 0 && lane == 0) L = row ? xc[(int64_t)yy * g.W + 4 * ttx - 1] : 0.f;
+                if (ttx < g.TW - 1 && lane == 63) R = row ? xc[(int64_t)yy * g.W + 4 * ttx + 4] : 0.f;
+            }
+            L = ttx == 0 ? 0.f : L;
+            R = ttx == g.TW - 1 ? 0.f : R;
+            d0[a][0] = L;   d0[a][1] = c1v; d0[a][2] = c3v;
+            d1[a][0] = c0v; d1[a][1] = c2v; d1[a][2] = R;
+        }
+        float v0[9], v1[9];
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {      // B^T d per column
+            const float t00 = d0[0][b] - d0[1][b], t01 = d0[1][b], t02 = d0[2][b] - d0[1][b];
+            const float t10 = d1[0][b] - d1[1][b], t11 = d1[1][b], t12 = d1[2][b] - d1[1][b];
+            d0[0][b] = t00; d0[1][b] = t01; d0[2][b] = t02;
+            d1[0][b] = t10; d1[1][b] = t11; d1[2][b] = t12;
+        }
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {      // (B^T d) B per row
+            v0[i * 3 + 0] = d0[i][0] - d0[i][1];
+            v0[i * 3 + 1] = d0[i][1];
+            v0[i * 3 + 2] = d0[i][2] - d0[i][1];
+            v1[i * 3 + 0] = d1[i][0] - d1[i][1];
+            v1[i * 3 + 1] = d1[i][1];
+            v1[i * 3 + 2] = d1[i][2] - d1[i][1];
+        }
+        float2 *V2 = reinterpret_cast<float2 *>(Vs + buf * (S2_STAGE / 4));
+#pragma unroll
+        for (int p = 0; p < 9; ++p)
+            V2[((p * 2 + e) * 64 + lane) * 2 + pi] = make_float2(v0[p], v1[p]);
+    };
+
+    f32x16 acc[9];
+#pragma unroll
+    for (int p = 0; p < 9; ++p) acc[p] = f32x16{};
+
+    const int th = w & 1, kh = w >> 1, hl = lane >> 5, l32 = lane & 31;
+    auto mfma_chunk = [&](int buf) {
+        const float4 *V = Vs + buf * (S2_STAGE / 4);
+        const float4 *U = Us + buf * (S2_STAGE / 4);
+#pragma unroll
+        for (int p = 0; p < 9; ++p) {
+            const float4 a = U[(p * 2 + hl) * 64 + kh * 32 + l32];
+            const float4 b = V[(p * 2 + hl) * 64 + th * 32 + l32];
+            acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, acc[p], 0, 0, 0);
+            acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, acc[p], 0, 0, 0);
+            acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, acc[p], 0, 0, 0);
+            acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, acc[p], 0, 0, 0);
+        }
+    };
+
+    load(0);
+    store(0, 0);
+    __syncthreads();
+    for (int cc = 0; cc + 1 < nchunk; ++cc) {
+        load(cc + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_chunk(cc & 1);
+        __builtin_amdgcn_sched_barrier(0);
+        store(cc + 1, (cc + 1) & 1);
+        __syncthreads();
+    }
+    mfma_chunk((nchunk - 1) & 1);
+
+    // epilogue: C_p[k][tile]; output tile (2ty, 2tx) of y [N, K, H/2, W/2]
+    const int64_t et = tile0 + th * 32 + l32;
+    if (et >= g.T) return;
+    const int en = (int)(et / g.Timg);
+    const int er = (int)(et - (int64_t)en * g.Timg);
+    const int ety = er / g.TW, etx = er - ety * g.TW;
+    const int Ho = g.H / 2, Wo = g.W / 2;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int k = kb * S2_KB + kh * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+        float m[9];
+#pragma unroll
+        for (int p = 0; p < 9; ++p) m[p] = acc[p][r];
+        // rows: s_a[j] = m[a][j] + m[a+1][j]
+        float s0[3], s1[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            s0[j] = m[j] + m[3 + j];
+            s1[j] = m[3 + j] + m[6 + j];
+        }
+        const float b = bias ? bias[k] : 0.f;
+        float *o = y + (((int64_t)en * g.K + k) * Ho + 2 * ety) * Wo + 2 * etx;
+        *reinterpret_cast<float2 *>(o) = make_float2(s0[0] + s0[1] + b, s0[1] + s0[2] + b);
+        *reinterpret_cast<float2 *>(o + Wo) = make_float2(s1[0] + s1[1] + b, s1[1] + s1[2] + b);
+    }
+}
+
+// ---- the transposed conv: dx = conv_transpose2d(gy, W', stride 2, pad 1) ----
+// (the input gradient of the 4x4 stride-2 conv; also the generator's folded
+// UpsampleConv, a transposed conv with K [cin, cout, 4, 4]).  Output phase
+// (qi, qj) of dx is a 2 x 2 stride-1 correlation of gy: dx[2r+qi][2s+qj] =
+// sum_k sum_{a,b in 0..1} gy[k][r-1+qi+a][s-1+qj+b] W'[k][c][3-qi-2a][3-qj-2b],
+// one F(2x2, 2x2) problem per phase with K reduction channels.  Block: one
+// phase (blockIdx.z & 3), 64 phase tiles x 64 output channels; as the
+// forward kernel otherwise (chunks of 8 k, 9 accumulators per wave).
+
+// U for the transposed conv: ut[q4][cb][kchunk][p9][h2][c64][k4], from W' [K][C][4][4]
+__global__ void s2t_filter_kernel(const float *__restrict__ w, int K, int C,
+                                  float *__restrict__ u) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (int64_t)K * C) return;
+    const int c = (int)(idx % C), k = (int)(idx / C);
+    const float *s = w + ((int64_t)k * C + c) * 16;
+    float f[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) f[i] = s[i];
+    const int cb = c >> 6, cl = c & 63, kc = k >> 3, h = (k >> 2) & 1, k4 = k & 3;
+    const int64_t per_phase = (int64_t)C * K * 9;
+#pragma unroll
+    for (int qi = 0; qi < 2; ++qi)
+#pragma unroll
+        for (int qj = 0; qj < 2; ++qj) {
+            // g[a][b] = W'[3 - qi - 2a][3 - qj - 2b]
+            const float g00 = f[(3 - qi) * 4 + 3 - qj], g01 = f[(3 - qi) * 4 + 1 - qj];
+            const float g10 = f[(1 - qi) * 4 + 3 - qj], g11 = f[(1 - qi) * 4 + 1 - qj];
+            const float t[3][2] = {{g00, g01}, {g00 + g10, g01 + g11}, {g10, g11}};
+            const int64_t base = (qi * 2 + qj) * per_phase + ((int64_t)cb * (K >> 3) + kc) * 9 * 512;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                const float r[3] = {t[i][0], t[i][0] + t[i][1], t[i][1]};
+#pragma unroll
+                for (int j = 0; j < 3; ++j)
+                    u[base + (((i * 3 + j) * 2 + h) * 64 + cl) * 4 + k4] = r[j];
+            }
+        }
+}
+
+struct S2TGeom {
+    int N, K, C, Hg, Wg, TW, Timg;  // gy [N, K, Hg, Wg]; dx [N, C, 2Hg, 2Wg]; tiles of a phase
+    int64_t T, slab;
+};
+
+template <bool EDGE>
+__global__ __launch_bounds__(S2_T, 2) void s2t_conv_kernel(
+    const float *__restrict__ gy, const float *__restrict__ u, const float *__restrict__ bias,
+    float *__restrict__ dx, S2TGeom g) {
+    extern __shared__ float4 s2_lds[];
+    float4 *const Vs = s2_lds;
+    float4 *const Us = s2_lds + 2 * (S2_STAGE / 4);
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int cb = blockIdx.y;
+    const int q = blockIdx.z & 3, qi = q >> 1, qj = q & 1;
+    const int sl = blockIdx.z >> 2, S = gridDim.z >> 2;
+    const int64_t tile0 = (int64_t)blockIdx.x * S2_TB;
+    const int nch = g.K / 8;
+    const int c0 = (int)((int64_t)nch * sl / S);
+    const int nchunk = (int)((int64_t)nch * (sl + 1) / S) - c0;
+    dx += (int64_t)sl * g.slab;
+
+    // transform role: lane = tile, wave w = k channels 2w, 2w+1 of the chunk
+    const int64_t gt = tile0 + lane;
+    const bool tok = gt < g.T;
+    int tn = 0, tty = 0, ttx = 0;
+    if (tok) {
+        tn = (int)(gt / g.Timg);
+        const int r = (int)(gt - (int64_t)tn * g.Timg);
+        tty = r / g.TW;
+        ttx = r - tty * g.TW;
+    }
+    const int64_t HW = (int64_t)g.Hg * g.Wg;
+    const float *gn = gy + ((int64_t)tn * g.K + (int64_t)c0 * 8 + 2 * w) * HW;
+    const float4 *ub = reinterpret_cast<const float4 *>(u) + (int64_t)q * g.C * g.K * 9 / 4 +
+                       ((int64_t)cb * nch + c0) * (S2_STAGE / 4);
+
+    float2 raw[2][3];
+    f4v ur[5];
+    auto load = [&](int cc) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const float *gc = gn + ((int64_t)cc * 8 + e) * HW;
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                const int yy = 2 * tty - 1 + qi + a;
+                const int yc = min(max(yy, 0), g.Hg - 1);
+                raw[e][a] = *reinterpret_cast<const float2 *>(gc + (int64_t)yc * g.Wg + 2 * ttx);
+            }
+        }
+        const float4 *src = ub + (int64_t)cc * (S2_STAGE / 4) + tid;
+#pragma unroll
+        for (int i = 0; i < 5; ++i)
+            if (i * S2_T + tid < S2_STAGE / 4)
+                ur[i] = *reinterpret_cast<const f4v *>(src + i * S2_T);
+    };
+    auto store = [&](int cc, int buf) {
+        f4v *U = reinterpret_cast<f4v *>(Us + buf * (S2_STAGE / 4)) + tid;
+#pragma unroll
+        for (int i = 0; i < 5; ++i)
+            if (i * S2_T + tid < S2_STAGE / 4) U[i * S2_T] = ur[i];
+        float v[2][9];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const float *gc = gn + ((int64_t)cc * 8 + e) * HW;
+            float d[3][3];
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                const int yy = 2 * tty - 1 + qi + a;
+                const bool row = tok && yy >= 0 && yy < g.Hg;
+                const float cx = row ? raw[e][a].x : 0.f, cy = row ? raw[e][a].y : 0.f;
+                float L = s2_from_left(cy), R = s2_from_right(cx);
+                if (EDGE) {
+                    if (ttx > 0 && lane == 0) L = row ? gc[(int64_t)yy * g.Wg + 2 * ttx - 1] : 0.f;
+                    if (ttx < g.TW - 1 && lane == 63)
+                        R = row ? gc[(int64_t)yy * g.Wg + 2 * ttx + 2] : 0.f;
+                }
+                L = ttx == 0 ? 0.f : L;
+                R = ttx == g.TW - 1 ? 0.f : R;
+                // columns 2tx - 1 + qj + b
+                d[a][0] = qj ? cx : L;
+                d[a][1] = qj ? cy : cx;
+                d[a][2] = qj ? R : cy;
+            }
+#pragma unroll
+            for (int b = 0; b < 3; ++b) {
+                const float t0 = d[0][b] - d[1][b], t2 = d[2][b] - d[1][b];
+                d[0][b] = t0;
+                d[2][b] = t2;
+            }
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                v[e][i * 3 + 0] = d[i][0] - d[i][1];
+                v[e][i * 3 + 1] = d[i][1];
+                v[e][i * 3 + 2] = d[i][2] - d[i][1];
+            }
+        }
+        float2 *V2 = reinterpret_cast<float2 *>(Vs + buf * (S2_STAGE / 4));
+#pragma unroll
+        for (int p = 0; p < 9; ++p)
+            V2[((p * 2 + (w >> 1)) * 64 + lane) * 2 + (w & 1)] = make_float2(v[0][p], v[1][p]);
+    };
+
+    f32x16 acc[9];
+#pragma unroll
+    for (int p = 0; p < 9; ++p) acc[p] = f32x16{};
+
+    const int th = w & 1, kh = w >> 1, hl = lane >> 5, l32 = lane & 31;
+    auto mfma_chunk = [&](int buf) {
+        const float4 *V = Vs + buf * (S2_STAGE / 4);
+        const float4 *U = Us + buf * (S2_STAGE / 4);
+#pragma unroll
+        for (int p = 0; p < 9; ++p) {
+            const float4 a = U[(p * 2 + hl) * 64 + kh * 32 + l32];
+            const float4 b = V[(p * 2 + hl) * 64 + th * 32 + l32];
+            acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, acc[p], 0, 0, 0);
+            acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, acc[p], 0, 0, 0);
+            acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, acc[p], 0, 0, 0);
+            acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, acc[p], 0, 0, 0);
+        }
+    };
+
+    load(0);
+    store(0, 0);
+    __syncthreads();
+    for (int cc = 0; cc + 1 < nchunk; ++cc) {
+        load(cc + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_chunk(cc & 1);
+        __builtin_amdgcn_sched_barrier(0);
+        store(cc + 1, (cc + 1) & 1);
+        __syncthreads();
+    }
+    mfma_chunk((nchunk - 1) & 1);
+
+    // epilogue: phase tile (ty, tx) -> dx rows 2 (2ty + a) + qi, cols 2 (2tx + b) + qj
+    const int64_t et = tile0 + th * 32 + l32;
+    if (et >= g.T) return;
+    const int en = (int)(et / g.Timg);
+    const int er = (int)(et - (int64_t)en * g.Timg);
+    const int ety = er / g.TW, etx = er - ety * g.TW;
+    const int Hx = 2 * g.Hg, Wx = 2 * g.Wg;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int c = cb * 64 + kh * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+        float m[9];
+#pragma unroll
+        for (int p = 0; p < 9; ++p) m[p] = acc[p][r];
+        float s0[3], s1[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            s0[j] = m[j] + m[3 + j];
+            s1[j] = m[3 + j] + m[6 + j];
+        }
+        const float b = bias ? bias[c] : 0.f;
+        float *o = dx + (((int64_t)en * g.C + c) * Hx + 4 * ety + qi) * Wx + 4 * etx + qj;
+        o[0] = s0[0] + s0[1] + b;
+        o[2] = s0[1] + s0[2] + b;
+        o[2 * Wx] = s1[0] + s1[1] + b;
+        o[2 * Wx + 2] = s1[1] + s1[2] + b;
+    }
+}
+
+__global__ void s2_reduce_kernel(const float *__restrict__ part, const float *__restrict__ bias,
+                                 float *__restrict__ y, int64_t n4, int S, int K, int HW) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n4) return;
+    const float4 *p4 = reinterpret_cast<const float4 *>(part);
+    float4 s = p4[i];
+    for (int z = 1; z < S; ++z) {
+        const float4 t = p4[i + z * n4];
+        s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
+    }
+    if (bias) {
+        const float b = bias[(int)((i * 4 / HW) % K)];
+        s.x += b; s.y += b; s.z += b; s.w += b;
+    }
+    reinterpret_cast<float4 *>(y)[i] = s;
+}
+
+}  // namespace
+
+static int s2t_slices(int64_t blocks, int nch) {
+    int S = 1;
+    while (blocks * S < 512 && nch / (2 * S) >= 4) S *= 2;
+    return S;
+}
+
+static int s2_slices(int64_t blocks, int nch, int HWo) {
+    int S = 1;
+    while (blocks * S < 512 && nch / (2 * S) >= 8 && HWo % 4 == 0) S *= 2;
+    return S;
+}
+
+}  // namespace smmd
+
+using namespace smmd;
+
+extern "C" int smmd_wino4x4s2_supported(int n, int ci, int ko, int h, int w_img) {
+    return n > 0 && ci > 0 && ko > 0 && ci % S2_CC == 0 && ko % S2_KB == 0 && h > 0 &&
+           w_img > 0 && h % 4 == 0 && w_img % 4 == 0 && (int64_t)n * ci * h * w_img < (1ll << 40);
+}
+
+extern "C" size_t smmd_wino4x4s2_filter_bytes(int ko, int ci) {
+    if (ko <= 0 || ci <= 0) return 0;
+    return (size_t)36 * ko * ci * sizeof(float);
+}
+
+extern "C" smmd_status smmd_wino4x4s2_filter(const float *w, int ko, int ci, float *u,
+                                             size_t u_bytes, smmd_stream_t stream) {
+    if (ko <= 0 || ci <= 0 || !w || !u) return SMMD_EINVAL;
+    if (ko % S2_KB || ci % S2_CC) return SMMD_EUNSUPPORTED;
+    if (reinterpret_cast<uintptr_t>(u) & 15) return SMMD_EINVAL;
+    if (u_bytes < smmd_wino4x4s2_filter_bytes(ko, ci)) return SMMD_EWORKSPACE;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const int64_t n = (int64_t)ko * ci;
+    s2_filter_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st>>>(w, ko, ci, u);
+    return last_launch_status();
+}
+
+extern "C" size_t smmd_wino4x4s2_workspace_bytes(int n, int ci, int ko, int h, int w_img) {
+    if (!smmd_wino4x4s2_supported(n, ci, ko, h, w_img)) return 0;
+    const int64_t T = (int64_t)n * (h / 4) * (w_img / 4);
+    const int S = s2_slices(((T + S2_TB - 1) / S2_TB) * (ko / S2_KB), ci / S2_CC,
+                            (h / 2) * (w_img / 2));
+    return S > 1 ? (size_t)S * n * ko * (h / 2) * (w_img / 2) * sizeof(float) : 0;
+}
+
+extern "C" smmd_status smmd_wino4x4s2_conv(const float *x, const float *u, const float *bias,
+                                           float *y, int n, int ci, int ko, int h, int w_img,
+                                           void *ws, size_t ws_bytes, smmd_stream_t stream) {
+    if (n < 0 || ci <= 0 || ko <= 0 || h < 0 || w_img < 0) return SMMD_EINVAL;
+    if (n == 0 || h == 0 || w_img == 0) return SMMD_OK;
+    if (!x || !u || !y) return SMMD_EINVAL;
+    if (!smmd_wino4x4s2_supported(n, ci, ko, h, w_img)) return SMMD_EUNSUPPORTED;
+    if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y) |
+         reinterpret_cast<uintptr_t>(u)) & 15)
+        return SMMD_EINVAL;
+    S2Geom g;
+    g.N = n; g.C = ci; g.K = ko; g.H = h; g.W = w_img;
+    g.TW = w_img / 4;
+    g.Timg = (h / 4) * g.TW;
+    g.T = (int64_t)n * g.Timg;
+    const int64_t tb = (g.T + S2_TB - 1) / S2_TB;
+    if (tb > 0x7fffffff) return SMMD_EINVAL;
+    const int HWo = (h / 2) * (w_img / 2);
+    const int S = s2_slices(tb * (ko / S2_KB), ci / S2_CC, HWo);
+    const int64_t total = (int64_t)n * ko * HWo;
+    float *out = y;
+    if (S > 1) {
+        if (!ws || ws_bytes < (size_t)S * total * sizeof(float)) return SMMD_EWORKSPACE;
+        if (reinterpret_cast<uintptr_t>(ws) & 15) return SMMD_EINVAL;
+        out = static_cast<float *>(ws);
+    }
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(s2_conv_kernel<false>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)S2_LDS) != hipSuccess ||
+            hipFuncSetAttribute(reinterpret_cast<const void *>(s2_conv_kernel<true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)S2_LDS) != hipSuccess)
+            return SMMD_EHIP;
+        attr = true;
+    }
+    g.slab = S > 1 ? total : 0;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const dim3 grid((unsigned)tb, (unsigned)(ko / S2_KB), (unsigned)S);
+    const float *b1 = S > 1 ? nullptr : bias;
+    if (64 % g.TW == 0)
+        s2_conv_kernel<false><<<grid, dim3(S2_T), S2_LDS, st>>>(x, u, b1, out, g);
+    else
+        s2_conv_kernel<true><<<grid, dim3(S2_T), S2_LDS, st>>>(x, u, b1, out, g);
+    smmd_status e = last_launch_status();
+    if (e != SMMD_OK || S == 1) return e;
+    const int64_t n4 = total / 4;
+    s2_reduce_kernel<<<dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st>>>(out, bias, y, n4,
+                                                                              S, ko, HWo);
+    return last_launch_status();
+}
+
+extern "C" int smmd_wino4x4s2t_supported(int n, int k, int c, int hg, int wg) {
+    return n > 0 && k > 0 && c > 0 && k % 8 == 0 && c % 64 == 0 && hg > 0 && wg > 0 &&
+           hg % 2 == 0 && wg % 2 == 0 && (int64_t)n * k * hg * wg < (1ll << 40);
+}
+
+extern "C" smmd_status smmd_wino4x4s2t_filter(const float *w, int k, int c, float *u,
+                                              size_t u_bytes, smmd_stream_t stream) {
+    if (k <= 0 || c <= 0 || !w || !u) return SMMD_EINVAL;
+    if (k % 8 || c % 64) return SMMD_EUNSUPPORTED;
+    if (reinterpret_cast<uintptr_t>(u) & 15) return SMMD_EINVAL;
+    if (u_bytes < smmd_wino4x4s2_filter_bytes(k, c)) return SMMD_EWORKSPACE;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const int64_t n = (int64_t)k * c;
+    s2t_filter_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st>>>(w, k, c, u);
+    return last_launch_status();
+}
+
+extern "C" size_t smmd_wino4x4s2t_workspace_bytes(int n, int k, int c, int hg, int wg) {
+    if (!smmd_wino4x4s2t_supported(n, k, c, hg, wg)) return 0;
+    const int64_t T = (int64_t)n * (hg / 2) * (wg / 2);
+    const int S = s2t_slices(((T + S2_TB - 1) / S2_TB) * (c / 64) * 4, k / 8);
+    return S > 1 ? (size_t)S * n * c * 4 * hg * wg * sizeof(float) : 0;
+}
+
+// dx [n, c, 2 hg, 2 wg] = conv_transpose2d(gy [n, k, hg, wg], W' [k, c, 4, 4], stride 2, pad 1) + bias
+extern "C" smmd_status smmd_wino4x4s2t_conv(const float *gy, const float *u, const float *bias,
+                                            float *dx, int n, int k, int c, int hg, int wg,
+                                            void *ws, size_t ws_bytes, smmd_stream_t stream) {
+    if (n < 0 || k <= 0 || c <= 0 || hg < 0 || wg < 0) return SMMD_EINVAL;
+    if (n == 0 || hg == 0 || wg == 0) return SMMD_OK;
+    if (!gy || !u || !dx) return SMMD_EINVAL;
+    if (!smmd_wino4x4s2t_supported(n, k, c, hg, wg)) return SMMD_EUNSUPPORTED;
+    if ((reinterpret_cast<uintptr_t>(gy) | reinterpret_cast<uintptr_t>(dx) |
+         reinterpret_cast<uintptr_t>(u)) & 15)
+        return SMMD_EINVAL;
+    S2TGeom g;
+    g.N = n; g.K = k; g.C = c; g.Hg = hg; g.Wg = wg;
+    g.TW = wg / 2;
+    g.Timg = (hg / 2) * g.TW;
+    g.T = (int64_t)n * g.Timg;
+    const int64_t tb = (g.T + S2_TB - 1) / S2_TB;
+    if (tb > 0x7fffffff) return SMMD_EINVAL;
+    const int S = s2t_slices(tb * (c / 64) * 4, k / 8);
+    const int64_t total = (int64_t)n * c * 4 * hg * wg;
+    float *out = dx;
+    if (S > 1) {
+        if (!ws || ws_bytes < (size_t)S * total * sizeof(float)) return SMMD_EWORKSPACE;
+        if (reinterpret_cast<uintptr_t>(ws) & 15) return SMMD_EINVAL;
+        out = static_cast<float *>(ws);
+    }
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(s2t_conv_kernel<false>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)S2_LDS) != hipSuccess ||
+            hipFuncSetAttribute(reinterpret_cast<const void *>(s2t_conv_kernel<true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)S2_LDS) != hipSuccess)
+            return SMMD_EHIP;
+        attr = true;
+    }
+    g.slab = S > 1 ? total : 0;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const dim3 grid((unsigned)tb, (unsigned)(c / 64), (unsigned)(4 * S));
+    const float *b1 = S > 1 ? nullptr : bias;
+    if (64 % g.TW == 0)
+        s2t_conv_kernel<false><<<grid, dim3(S2_T), S2_LDS, st>>>(gy, u, b1, out, g);
+    else
+        s2t_conv_kernel<true><<<grid, dim3(S2_T), S2_LDS, st>>>(gy, u, b1, out, g);
+    smmd_status e = last_launch_status();
+    if (e != SMMD_OK || S == 1) return e;
+    const int64_t n4 = total / 4;
+    s2_reduce_kernel<<<dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st>>>(
+        out, bias, dx, n4, S, c, 4 * hg * wg);
+    return last_launch_status();
+}

@@ -17,7 +17,8 @@ import torch.nn.functional as F
 
 from . import convops
 from . import optim as _optim
-from .convops import conv2d, fold_pool_weight, fold_pool_weights, fold_up_weight, mean_pool2
+from .convops import (conv2d, conv_transpose_s2, fold_pool_weight, fold_pool_weights,
+                      fold_up_weight, mean_pool2)
 from .snops import Conv2d, Deconv2d, Linear, batch_norm, bn_relu, lrelu
 
 
@@ -86,8 +87,7 @@ class _Up(nn.Module):
             if c.k == 1:     # a 1x1 conv commutes with the nearest upsample: 4x fewer flops
                 return F.interpolate(c(x), scale_factor=2, mode='nearest')
             if c.k == 3:     # one 4x4 stride-2 transposed conv on the folded weight
-                return F.conv_transpose2d(x, self._folded(c.effective_weight()), c.bias,
-                                          stride=2, padding=1)
+                return conv_transpose_s2(x, self._folded(c.effective_weight()), c.bias)
         return c(F.interpolate(x, scale_factor=2, mode='nearest'))
 
 

@@ -155,21 +155,41 @@ def wino_applicable(x, cin, cout, k, stride, padding):
 # object at the same torch version and FlatAdam epoch (the fused optimizer
 # writes parameters without bumping versions; the SN bank's W_eff is a new
 # tensor every refresh).  Off during HIP-graph capture: a replay must
-# re-transform what it convolves.
+# re-transform what it convolves.  Shared by the 3x3 and the stride-2 kernels,
+# capped at 1 GiB (a 512 -> 1024 stride-2 filter transforms to 75 MB).
 _WINO_CACHE = {}
-_WINO_CACHE_MAX = 64
+_WINO_CACHE_MAX_BYTES = 1 << 30      # oldest entries go first past 1 GiB of HBM
+
+
+def _cache_get(key, w):
+    e = _WINO_CACHE.get(key)
+    if e is not None and e[0] is w and e[1] == w._version and e[2] == _param_epoch(w):
+        return e[3]
+    return None
+
+
+def _cache_put(key, w, u):
+    _WINO_CACHE.pop(key, None)
+    total = sum(e[3].numel() * 4 for e in _WINO_CACHE.values()) + u.numel() * 4
+    while _WINO_CACHE and total > _WINO_CACHE_MAX_BYTES:
+        old = _WINO_CACHE.pop(next(iter(_WINO_CACHE)))
+        total -= old[3].numel() * 4
+    _WINO_CACHE[key] = (w, w._version, _param_epoch(w), u)
+
+
+def _param_epoch(w):
+    from . import optim as _optim
+    return _optim.param_epoch(w)
 
 
 def _wino_filter(w, co, ci, mode):
     from . import _lib
-    from . import optim as _optim
     capturing = torch.cuda.is_current_stream_capturing()
-    key = (id(w), mode)
+    key = (id(w), 'w3', mode)
     if not capturing:
-        e = _WINO_CACHE.get(key)
-        if (e is not None and e[0] is w and e[1] == w._version
-                and e[2] == _optim.param_epoch(w)):
-            return e[3]
+        u = _cache_get(key, w)
+        if u is not None:
+            return u
     L = _lib.lib()
     u = torch.empty(L.smmd_wino3x3_filter_bytes(co, ci) // 4, dtype=w.dtype, device=w.device)
     with _lib.timed('smmd_wino3x3_filter'):
@@ -177,9 +197,7 @@ def _wino_filter(w, co, ci, mode):
                                    _lib.stream_handle(w.device))
     _lib.check(st, 'smmd_wino3x3_filter')
     if not capturing:
-        if len(_WINO_CACHE) >= _WINO_CACHE_MAX:
-            _WINO_CACHE.pop(next(iter(_WINO_CACHE)))
-        _WINO_CACHE[key] = (w, w._version, _optim.param_epoch(w), u)
+        _cache_put(key, w, u)
     return u
 
 
@@ -223,6 +241,145 @@ def _is_wino(x, w, stride, padding, mode):
     return wino_applicable(x, ci, co, 3, stride, padding)
 
 
+# ---------------------------------------------------------------------------
+# 4x4 stride-2 pad-1 convolutions (the folded ConvMeanPool layers) and their
+# transposed form (their input gradient; the generator's folded
+# UpsampleConv) on the library's polyphase Winograd F(2x2, 2x2) kernels
+# (smmd_wino4x4s2*, csrc/smmd_wino_s2.hip; SMMD_WINO_S2=0: MIOpen for them)
+# ---------------------------------------------------------------------------
+WINO_S2 = os.environ.get('SMMD_WINO_S2', '1') != '0'
+
+
+def _s2_shape_ok(x, stride, padding):
+    s = tuple(stride) if isinstance(stride, (list, tuple)) else (stride, stride)
+    p = tuple(padding) if isinstance(padding, (list, tuple)) else (padding, padding)
+    return (WINO_S2 and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
+            and x.is_contiguous() and s == (2, 2) and p == (1, 1) and x.shape[0] > 0)
+
+
+def _is_s2(x, w, stride, padding):
+    """conv(x, w [co, ci, 4, 4], stride 2, padding 1) on smmd_wino4x4s2_conv:
+    H, W % 4 == 0, ci % 2 == 0, co % 64 == 0."""
+    return (w.dim() == 4 and w.shape[2] == 4 and w.shape[3] == 4 and _s2_shape_ok(x, stride, padding)
+            and x.shape[1] == w.shape[1] and w.shape[1] % 2 == 0 and w.shape[0] % 64 == 0
+            and x.shape[2] % 4 == 0 and x.shape[3] % 4 == 0)
+
+
+def _is_s2t(g, w, stride, padding):
+    """conv_transpose(g, w [k, c, 4, 4], stride 2, padding 1) on
+    smmd_wino4x4s2t_conv: g [n, k, hg, wg] with hg, wg even, k % 8 == 0,
+    c % 64 == 0."""
+    return (w.dim() == 4 and w.shape[2] == 4 and w.shape[3] == 4 and _s2_shape_ok(g, stride, padding)
+            and g.shape[1] == w.shape[0] and w.shape[0] % 8 == 0 and w.shape[1] % 64 == 0
+            and g.shape[2] % 2 == 0 and g.shape[3] % 2 == 0)
+
+
+def _s2_filter(w, transposed):
+    from . import _lib
+    capturing = torch.cuda.is_current_stream_capturing()
+    key = (id(w), 's2', transposed)
+    if not capturing:
+        u = _cache_get(key, w)
+        if u is not None:
+            return u
+    L = _lib.lib()
+    a, b = w.shape[0], w.shape[1]
+    u = torch.empty(L.smmd_wino4x4s2_filter_bytes(a, b) // 4, dtype=w.dtype, device=w.device)
+    fn = L.smmd_wino4x4s2t_filter if transposed else L.smmd_wino4x4s2_filter
+    with _lib.timed('smmd_wino4x4s2_filter'):
+        st = fn(_lib.ptr(w), a, b, _lib.ptr(u), u.numel() * 4, _lib.stream_handle(w.device))
+    _lib.check(st, 'smmd_wino4x4s2_filter')
+    if not capturing:
+        _cache_put(key, w, u)
+    return u
+
+
+def _s2_conv(x, w, b):
+    """conv2d(x, w, b, stride 2, padding 1) on smmd_wino4x4s2_conv."""
+    from . import _lib
+    x = x.contiguous()
+    w = w.contiguous()
+    if b is not None:
+        b = b.contiguous()
+    _lib.require_cuda(x, w, b)
+    N, ci, H, W = x.shape
+    co = w.shape[0]
+    L = _lib.lib()
+    u = _s2_filter(w, False)
+    y = torch.empty((N, co, H // 2, W // 2), dtype=x.dtype, device=x.device)
+    nb = L.smmd_wino4x4s2_workspace_bytes(N, ci, co, H, W)
+    ws = _lib.workspace('wino_s2', nb, x.device) if nb else None
+    _lib.add_bytes('smmd_wino4x4s2_conv', (x.numel() + y.numel()) * 4)
+    # 9 point products per 2 x 2 output tile and (phase channel, co) pair
+    _lib.add_flops('smmd_wino4x4s2_conv', 2 * 9 * N * (H // 4) * (W // 4) * 4 * ci * co)
+    with _lib.timed('smmd_wino4x4s2_conv'):
+        st = L.smmd_wino4x4s2_conv(_lib.ptr(x), _lib.ptr(u), _lib.ptr(b), _lib.ptr(y), N, ci, co,
+                                   H, W, _lib.ptr(ws), nb, _lib.stream_handle(x.device))
+    _lib.check(st, 'smmd_wino4x4s2_conv')
+    return y
+
+
+def _s2t_conv(g, w, b):
+    """conv_transpose2d(g, w [k, c, 4, 4], b, stride 2, padding 1) on
+    smmd_wino4x4s2t_conv (the input gradient of conv(., w, stride 2))."""
+    from . import _lib
+    g = g.contiguous()
+    w = w.contiguous()
+    if b is not None:
+        b = b.contiguous()
+    _lib.require_cuda(g, w, b)
+    N, k, Hg, Wg = g.shape
+    c = w.shape[1]
+    L = _lib.lib()
+    u = _s2_filter(w, True)
+    y = torch.empty((N, c, 2 * Hg, 2 * Wg), dtype=g.dtype, device=g.device)
+    nb = L.smmd_wino4x4s2t_workspace_bytes(N, k, c, Hg, Wg)
+    ws = _lib.workspace('wino_s2t', nb, g.device) if nb else None
+    _lib.add_bytes('smmd_wino4x4s2t_conv', (g.numel() + y.numel()) * 4)
+    _lib.add_flops('smmd_wino4x4s2t_conv', 2 * 9 * N * (Hg // 2) * (Wg // 2) * 4 * k * c)
+    with _lib.timed('smmd_wino4x4s2t_conv'):
+        st = L.smmd_wino4x4s2t_conv(_lib.ptr(g), _lib.ptr(u), _lib.ptr(b), _lib.ptr(y), N, k, c,
+                                    Hg, Wg, _lib.ptr(ws), nb, _lib.stream_handle(g.device))
+    _lib.check(st, 'smmd_wino4x4s2t_conv')
+    return y
+
+
+class _ConvT2dS2(torch.autograd.Function):
+    """conv_transpose2d(x, w [cin, cout, 4, 4], b, stride 2, padding 1): the
+    generator's folded UpsampleConv.  Backward: grad_x = conv(g, w, stride 2)
+    on the forward Winograd kernel, grad_w on MIOpen, grad_b the channel sum
+    (the generator step differentiates it once)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.has_b = b is not None
+        return _s2t_conv(x, w, b)
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        gy = gy.contiguous()
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = _s2_conv(gy, w, None) if _is_s2(gy, w, 2, 1) else F.conv2d(gy, w, None, 2, 1)
+        if ctx.needs_input_grad[1]:
+            _, gw, _ = _aten.convolution_backward(gy, x, w, None, [2, 2], [1, 1], [1, 1], True,
+                                                  [0, 0], 1, [False, True, False])
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            gb = bias_grad(gy)
+        return gx, gw, gb
+
+
+def conv_transpose_s2(x, w, b=None):
+    """F.conv_transpose2d(x, w, b, stride=2, padding=1) with the Winograd
+    kernels on device tensors they tile, PyTorch otherwise."""
+    if _is_s2t(x, w, 2, 1):
+        return _ConvT2dS2.apply(x, w, b)
+    return F.conv_transpose2d(x, w, b, stride=2, padding=1)
+
+
 def _is_thin(x, w, stride, padding):
     return thin_applicable(x, w.shape[1], w.shape[0], w.shape[2], stride, padding) \
         and w.shape[2] == w.shape[3]
@@ -234,6 +391,8 @@ def _fwd(x, w, b, stride, padding):
         return _thin_conv(x, w, b, 0)
     if _is_wino(x, w, stride, padding, 0):
         return _wino_conv(x, w, b, 0)
+    if _is_s2(x, w, stride, padding):
+        return _s2_conv(x, w, b)
     return F.conv2d(x, w, b, stride, padding)
 
 
@@ -245,6 +404,14 @@ def _bwd(gy, x, w, stride, padding, mask):
         return gx, gw
     if mask[0] and _is_wino(gy, w, stride, padding, 1):
         gx = _wino_conv(gy, w, None, 1)
+        gw = None
+        if mask[1]:
+            _, gw, _ = _aten.convolution_backward(gy, x, w, None, stride, padding, [1, 1], False,
+                                                  [0, 0], 1, [False, True, False])
+        return gx, gw
+    if mask[0] and _is_s2t(gy, w, stride, padding) and tuple(x.shape[2:]) == (
+            2 * gy.shape[2], 2 * gy.shape[3]):
+        gx = _s2t_conv(gy, w, None)
         gw = None
         if mask[1]:
             _, gw, _ = _aten.convolution_backward(gy, x, w, None, stride, padding, [1, 1], False,

@@ -107,6 +107,24 @@ def test_argument_validation_without_gpu(L):
     assert need >= 2 * 64 * 512 * 64 * 4
     assert L.smmd_wino3x3_conv(x, x, None, x, 64, 512, 512, 8, 8, x, need - 1, None) == 3
     assert L.smmd_wino3x3_workspace_bytes(64, 64, 64, 64, 64) == 0
+    # polyphase 4x4 stride-2: tiling limits and argument checks before any launch
+    assert L.smmd_wino4x4s2_supported(64, 64, 128, 64, 64) == 1
+    assert L.smmd_wino4x4s2_supported(64, 3, 128, 64, 64) == 0     # ci odd
+    assert L.smmd_wino4x4s2_supported(64, 64, 96, 64, 64) == 0     # ko % 64
+    assert L.smmd_wino4x4s2_supported(64, 64, 128, 66, 64) == 0    # h % 4
+    assert L.smmd_wino4x4s2t_supported(64, 128, 64, 32, 32) == 1
+    assert L.smmd_wino4x4s2t_supported(64, 12, 64, 32, 32) == 0    # k % 8
+    assert L.smmd_wino4x4s2t_supported(64, 128, 96, 32, 32) == 0   # c % 64
+    assert L.smmd_wino4x4s2_filter_bytes(128, 64) == 36 * 128 * 64 * 4
+    assert L.smmd_wino4x4s2_filter(x, 96, 64, x, 1 << 30, None) == 4
+    assert L.smmd_wino4x4s2t_filter(x, 128, 96, x, 1 << 30, None) == 4
+    assert L.smmd_wino4x4s2_filter(x, 128, 64, x, 36 * 128 * 64 * 4 - 1, None) == 3
+    assert L.smmd_wino4x4s2_conv(None, x, None, x, 2, 8, 64, 4, 4, None, 0, None) == 1
+    assert L.smmd_wino4x4s2_conv(x, x, None, x, 2, 8, 64, 6, 4, None, 0, None) == 4
+    assert L.smmd_wino4x4s2t_conv(x, x, None, x, 2, 8, 64, 3, 4, None, 0, None) == 4
+    need = L.smmd_wino4x4s2_workspace_bytes(64, 512, 1024, 8, 8)
+    assert need >= 2 * 64 * 1024 * 16 * 4
+    assert L.smmd_wino4x4s2_conv(x, x, None, x, 64, 512, 1024, 8, 8, x, need - 1, None) == 3
 
 
 def test_product_never_imports_oracle():
