@@ -14,6 +14,16 @@ DEV = 'cuda:0'
 TOL = 2e-6
 
 
+@pytest.fixture(autouse=True)
+def s2_on():
+    """The stride-2 kernels on for these tests, whatever SMMD_WINO_S2 says."""
+    from gan.core import convops
+    saved = convops.WINO_S2
+    convops.WINO_S2 = True
+    yield
+    convops.WINO_S2 = saved
+
+
 def _rel(a, ref):
     a = a.detach().double().cpu()
     ref = ref.detach().double().cpu()
