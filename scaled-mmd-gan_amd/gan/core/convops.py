@@ -247,7 +247,7 @@ def _is_wino(x, w, stride, padding, mode):
 # UpsampleConv) on the library's polyphase Winograd F(2x2, 2x2) kernels
 # (smmd_wino4x4s2*, csrc/smmd_wino_s2.hip; SMMD_WINO_S2=0: MIOpen for them)
 # ---------------------------------------------------------------------------
-WINO_S2 = os.environ.get('SMMD_WINO_S2', '0') == '1'   # on once verified on the GPU
+WINO_S2 = os.environ.get('SMMD_WINO_S2', '1') != '0'
 
 
 def _s2_shape_ok(x, stride, padding):
