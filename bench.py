@@ -51,11 +51,11 @@ VALU_LANE_OPS = FP32_PEAK_TFS / 2 * 1e12
 TRANS_SLOTS = 4                # v_exp_f32 / v_log_f32: quarter rate (MI355X_MICROARCH.md)
 BATCH = 64
 
-PMC_TRAFFIC = os.path.join(ROOT, 'profiles', 'r07', 'pmc_traffic.json')
+PMC_TRAFFIC = os.path.join(ROOT, 'profiles', 'r09', 'pmc_traffic.json')
 # executed FLOPs per kernel class over whole 5D+1G cycles of this workload
 # (tools/gpu_step_pmc.sh -> tools/step_flops_pmc.py: rocprofv3 SQ_INSTS_VALU_*
 # and SQ_INSTS_VALU_MFMA_MOPS_F32 counters + a kernel trace)
-STEP_PMC = os.path.join(ROOT, 'profiles', 'r07', 'step_flops_pmc.json')
+STEP_PMC = os.path.join(ROOT, 'profiles', 'r09', 'step_flops_pmc.json')
 
 
 def step_counters(ms_step):

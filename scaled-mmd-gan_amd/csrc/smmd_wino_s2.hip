@@ -57,6 +57,7 @@ __global__ void s2_filter_kernel(const float *__restrict__ w, int KO, int CI,
     for (int i = 0; i < 16; ++i) f[i] = s[i];
     const int kb = ko >> 6, kl = ko & 63, cc = ci >> 1, h = ci & 1;
     const int64_t base = ((int64_t)kb * (CI >> 1) + cc) * 9;
+    float r[9][4];                    // [point][phase 2 pi + pj]
 #pragma unroll
     for (int pi = 0; pi < 2; ++pi)
 #pragma unroll
@@ -67,12 +68,16 @@ __global__ void s2_filter_kernel(const float *__restrict__ w, int KO, int CI,
             const float t[3][2] = {{g00, g01}, {g00 + g10, g01 + g11}, {g10, g11}};
 #pragma unroll
             for (int i = 0; i < 3; ++i) {
-                const float r[3] = {t[i][0], t[i][0] + t[i][1], t[i][1]};
-#pragma unroll
-                for (int j = 0; j < 3; ++j)
-                    u[(((base + i * 3 + j) * 2 + h) * 64 + kl) * 4 + 2 * pi + pj] = r[j];
+                r[i * 3 + 0][2 * pi + pj] = t[i][0];
+                r[i * 3 + 1][2 * pi + pj] = t[i][0] + t[i][1];
+                r[i * 3 + 2][2 * pi + pj] = t[i][1];
             }
         }
+    // one float4 (the four phases) per point; consecutive lanes, consecutive ko
+    float4 *u4 = reinterpret_cast<float4 *>(u);
+#pragma unroll
+    for (int p = 0; p < 9; ++p)
+        u4[((base + p) * 2 + h) * 64 + kl] = make_float4(r[p][0], r[p][1], r[p][2], r[p][3]);
 }
 
 struct S2Geom {
@@ -244,34 +249,47 @@ __global__ __launch_bounds__(S2_T, 2) void s2_conv_kernel(
 // phase (blockIdx.z & 3), 64 phase tiles x 64 output channels; as the
 // forward kernel otherwise (chunks of 8 k, 9 accumulators per wave).
 
-// U for the transposed conv: ut[q4][cb][kchunk][p9][h2][c64][k4], from W' [K][C][4][4]
+// U for the transposed conv: ut[q4][cb][kchunk][p9][h2][c64][k4], from W' [K][C][4][4];
+// a thread owns one c and four consecutive k, so each (phase, point) is one
+// float4 store and consecutive lanes (consecutive c) store consecutive 16 bytes
 __global__ void s2t_filter_kernel(const float *__restrict__ w, int K, int C,
                                   float *__restrict__ u) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= (int64_t)K * C) return;
-    const int c = (int)(idx % C), k = (int)(idx / C);
-    const float *s = w + ((int64_t)k * C + c) * 16;
-    float f[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) f[i] = s[i];
-    const int cb = c >> 6, cl = c & 63, kc = k >> 3, h = (k >> 2) & 1, k4 = k & 3;
+    if (idx >= (int64_t)(K >> 2) * C) return;
+    const int c = (int)(idx % C), kq = (int)(idx / C);
+    const int cb = c >> 6, cl = c & 63, kc = kq >> 1, h = kq & 1;
     const int64_t per_phase = (int64_t)C * K * 9;
+    float f[4][16];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const float *s = w + ((int64_t)(4 * kq + e) * C + c) * 16;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) f[e][i] = s[i];
+    }
+    float4 *u4 = reinterpret_cast<float4 *>(u);
 #pragma unroll
     for (int qi = 0; qi < 2; ++qi)
 #pragma unroll
         for (int qj = 0; qj < 2; ++qj) {
-            // g[a][b] = W'[3 - qi - 2a][3 - qj - 2b]
-            const float g00 = f[(3 - qi) * 4 + 3 - qj], g01 = f[(3 - qi) * 4 + 1 - qj];
-            const float g10 = f[(1 - qi) * 4 + 3 - qj], g11 = f[(1 - qi) * 4 + 1 - qj];
-            const float t[3][2] = {{g00, g01}, {g00 + g10, g01 + g11}, {g10, g11}};
-            const int64_t base = (qi * 2 + qj) * per_phase + ((int64_t)cb * (K >> 3) + kc) * 9 * 512;
+            float r[9][4];
 #pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                const float r[3] = {t[i][0], t[i][0] + t[i][1], t[i][1]};
+            for (int e = 0; e < 4; ++e) {
+                // g[a][b] = W'[3 - qi - 2a][3 - qj - 2b]
+                const float g00 = f[e][(3 - qi) * 4 + 3 - qj], g01 = f[e][(3 - qi) * 4 + 1 - qj];
+                const float g10 = f[e][(1 - qi) * 4 + 3 - qj], g11 = f[e][(1 - qi) * 4 + 1 - qj];
+                const float t[3][2] = {{g00, g01}, {g00 + g10, g01 + g11}, {g10, g11}};
 #pragma unroll
-                for (int j = 0; j < 3; ++j)
-                    u[base + (((i * 3 + j) * 2 + h) * 64 + cl) * 4 + k4] = r[j];
+                for (int i = 0; i < 3; ++i) {
+                    r[i * 3 + 0][e] = t[i][0];
+                    r[i * 3 + 1][e] = t[i][0] + t[i][1];
+                    r[i * 3 + 2][e] = t[i][1];
+                }
             }
+            const int64_t base =
+                ((qi * 2 + qj) * per_phase + ((int64_t)cb * (K >> 3) + kc) * 9 * 512) / 4;
+#pragma unroll
+            for (int p = 0; p < 9; ++p)
+                u4[base + (p * 2 + h) * 64 + cl] = make_float4(r[p][0], r[p][1], r[p][2], r[p][3]);
         }
 }
 
@@ -569,7 +587,7 @@ extern "C" smmd_status smmd_wino4x4s2t_filter(const float *w, int k, int c, floa
     if (reinterpret_cast<uintptr_t>(u) & 15) return SMMD_EINVAL;
     if (u_bytes < smmd_wino4x4s2_filter_bytes(k, c)) return SMMD_EWORKSPACE;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    const int64_t n = (int64_t)k * c;
+    const int64_t n = (int64_t)(k / 4) * c;
     s2t_filter_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st>>>(w, k, c, u);
     return last_launch_status();
 }

@@ -41,7 +41,11 @@ def _find(d, name):
 
 def kclass(k):
     if 'Sp3Asm' in k or 'inograd' in k:
-        return 'winograd'
+        return 'miopen_winograd'
+    if 'smmd::' in k and ('wino_' in k):
+        return 'smmd_wino3x3'
+    if 'smmd::' in k and ('s2_' in k or 's2t_' in k):
+        return 'smmd_wino_s2'
     for key, c in (('igemm_wrw', 'igemm_wrw'), ('igemm_bwd', 'igemm_bwd'),
                    ('igemm_fwd', 'igemm_fwd'), ('ransform', 'miopen_transform'),
                    ('transpose', 'transpose'), ('smmd::', 'smmd_library'),
