@@ -64,7 +64,8 @@ int smmd_abi_version(void);         /* bumped on any ABI change (2: Gram/poly,
                                        smmd_bn_relu_fwd, 7: smmd_smmd_loss_fwd/bwd,
                                        smmd_source_hash, smmd_sn_grad_stats,
                                        smmd_adam_flat_sn2, smmd_bn_relu_fwd_save / _bwd,
-                                       8: smmd_wino3x3_*, smmd_wino4x4s2*) */
+                                       8: smmd_wino3x3_*, smmd_wino4x4s2*,
+                                       smmd_wino3x3_wgrad*) */
 const char *smmd_source_hash(void); /* first 16 hex digits of the SHA-256 of the
                                        sources this binary was built from
                                        (csrc .hip and .hpp files in byte order,
@@ -638,6 +639,25 @@ smmd_status smmd_wino4x4s2_conv(const float *x, const float *u, const float *bia
 smmd_status smmd_wino4x4s2t_conv(const float *gy, const float *u, const float *bias, float *dx,
                                  int n, int k, int c, int hg, int wg, void *ws, size_t ws_bytes,
                                  smmd_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * The weight gradient of the 3x3 stride-1 SAME conv (TF's
+ * Conv2DBackpropFilter of snops.conv2d / resnet Conv2D, gan/core/snops.py:69-90,
+ * the wide layers of gan/core/resnet/block.py:38-50) as Winograd F(2x2, 3x3):
+ * dU_p = sum over 2 x 2 tiles of (A dY A^T)_p (B^T d B)_p on the f32 MFMA,
+ * then gw = G^T dU G.  gw [co, ci, 3, 3], x [n, ci, h, w_img], gy [n, co, h,
+ * w_img]; needs ci, co % 64 == 0, h even, w_img % 4 == 0
+ * (smmd_wino3x3_wgrad_supported).  The tiles are split over workgroups whose
+ * partial dU (smmd_wino3x3_wgrad_workspace_bytes) are added in slice order.
+ * Deterministic.
+ * ------------------------------------------------------------------------- */
+int smmd_wino3x3_wgrad_supported(int n, int ci, int co, int h, int w_img);
+
+size_t smmd_wino3x3_wgrad_workspace_bytes(int n, int ci, int co, int h, int w_img);
+
+smmd_status smmd_wino3x3_wgrad(const float *x, const float *gy, float *gw, int n, int ci, int co,
+                               int h, int w_img, void *ws, size_t ws_bytes,
+                               smmd_stream_t stream);
 
 #ifdef __cplusplus
 }

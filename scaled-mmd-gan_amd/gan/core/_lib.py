@@ -159,6 +159,9 @@ _SIGS = {
     'smmd_wino4x4s2t_workspace_bytes': (_SZ, [_I, _I, _I, _I, _I]),
     'smmd_wino4x4s2_conv': (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _SZ, _P]),
     'smmd_wino4x4s2t_conv': (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _SZ, _P]),
+    'smmd_wino3x3_wgrad_supported': (_I, [_I, _I, _I, _I, _I]),
+    'smmd_wino3x3_wgrad_workspace_bytes': (_SZ, [_I, _I, _I, _I, _I]),
+    'smmd_wino3x3_wgrad': (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P, _SZ, _P]),
     'smmd_poly_diff_ratio': (_I, [ctypes.POINTER(PolySums), ctypes.POINTER(PolySums),
                                   ctypes.POINTER(PolySums), ctypes.POINTER(PolySums), _I, _P,
                                   _P]),

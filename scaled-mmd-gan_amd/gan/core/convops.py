@@ -232,6 +232,36 @@ def _wino_conv(x, w, b, mode):
     return y
 
 
+# the weight gradient of those layers (SMMD_WINO_WGRAD=1: on, MIOpen otherwise)
+WINO_WGRAD = os.environ.get('SMMD_WINO_WGRAD', '0') == '1'
+
+
+def _wino_wgrad(x, gy):
+    """smmd_wino3x3_wgrad: gw [co, ci, 3, 3] of conv(x, W, stride 1, pad 1) at gy."""
+    from . import _lib
+    x = x.contiguous()
+    gy = gy.contiguous()
+    _lib.require_cuda(x, gy)
+    N, ci, H, W = x.shape
+    co = gy.shape[1]
+    L = _lib.lib()
+    nb = L.smmd_wino3x3_wgrad_workspace_bytes(N, ci, co, H, W)
+    ws = _lib.workspace('wino_wgrad', nb, x.device)
+    gw = torch.empty((co, ci, 3, 3), dtype=x.dtype, device=x.device)
+    _lib.add_bytes('smmd_wino3x3_wgrad', (x.numel() + gy.numel()) * 4)
+    _lib.add_flops('smmd_wino3x3_wgrad', 2 * 16 * N * (H // 2) * (W // 2) * ci * co)
+    with _lib.timed('smmd_wino3x3_wgrad'):
+        st = L.smmd_wino3x3_wgrad(_lib.ptr(x), _lib.ptr(gy), _lib.ptr(gw), N, ci, co, H, W,
+                                  _lib.ptr(ws), nb, _lib.stream_handle(x.device))
+    _lib.check(st, 'smmd_wino3x3_wgrad')
+    return gw
+
+
+def _wgrad_ok(x, gy, w, stride, padding):
+    return (WINO_WGRAD and _is_wino(x, w, stride, padding, 0) and gy.is_contiguous()
+            and x.shape[1] % 64 == 0 and gy.shape[1] % 64 == 0 and x.shape[3] % 4 == 0)
+
+
 def _is_wino(x, w, stride, padding, mode):
     """mode 0: conv(x, w); mode 1: its input gradient at upstream x (x has
     w.shape[0] channels, the result w.shape[1])."""
@@ -401,6 +431,14 @@ def _bwd(gy, x, w, stride, padding, mask):
     if _is_thin(x, w, stride, padding):
         gx = _thin_conv(gy, w, None, 1) if mask[0] else None
         gw = _thin_wgrad(gy, x) if mask[1] else None
+        return gx, gw
+    if mask[1] and _wgrad_ok(x, gy, w, stride, padding):
+        gw = _wino_wgrad(x, gy)
+        gx = None
+        if mask[0]:
+            gx = (_wino_conv(gy, w, None, 1) if _is_wino(gy, w, stride, padding, 1) else
+                  _aten.convolution_backward(gy, x, w, None, stride, padding, [1, 1], False,
+                                             [0, 0], 1, [True, False, False])[0])
         return gx, gw
     if mask[0] and _is_wino(gy, w, stride, padding, 1):
         gx = _wino_conv(gy, w, None, 1)

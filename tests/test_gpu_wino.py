@@ -145,3 +145,31 @@ def test_wino_off_matches_on():
     finally:
         convops.WINO = saved
     assert _rel(y1, y0) < 5e-6
+
+
+@pytest.fixture
+def wgrad_on():
+    from gan.core import convops
+    saved = convops.WINO_WGRAD
+    convops.WINO_WGRAD = True
+    yield convops
+    convops.WINO_WGRAD = saved
+
+
+@pytest.mark.parametrize('shape', [(2, 64, 64, 6, 8), (3, 64, 128, 8, 8), (4, 128, 64, 4, 12),
+                                   (2, 64, 64, 2, 4), (8, 64, 64, 64, 64), (8, 512, 512, 8, 8)])
+def test_wino_wgrad_vs_float64(wgrad_on, shape):
+    """smmd_wino3x3_wgrad against torch's float64 conv2d_weight (the sums run
+    over N*H*W terms in fp32: bound 1e-5 of max|ref|)."""
+    N, C, K, H, W = shape
+    g = torch.Generator(device=DEV).manual_seed(N + C + K + H + W)
+    x = torch.randn(N, C, H, W, device=DEV, generator=g)
+    gy = torch.randn(N, K, H, W, device=DEV, generator=g)
+    gw = wgrad_on._wino_wgrad(x, gy)
+    ref = torch.nn.grad.conv2d_weight(x.double().cpu(), (K, C, 3, 3), gy.double().cpu(),
+                                      padding=1)
+    assert _rel(gw, ref) < 1e-5
+
+
+def test_wino_wgrad_double_backward_vs_float64(wgrad_on):
+    test_convops_wino_double_backward_vs_float64((2, 64, 64, 8, 8))

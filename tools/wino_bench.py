@@ -25,6 +25,11 @@ def load(path):
         ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
     L.smmd_wino3x3_workspace_bytes.restype = ctypes.c_size_t
     L.smmd_wino3x3_workspace_bytes.argtypes = [ctypes.c_int] * 5
+    if hasattr(L, 'smmd_wino3x3_wgrad'):
+        L.smmd_wino3x3_wgrad.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int] * 5 + [
+            ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+        L.smmd_wino3x3_wgrad_workspace_bytes.restype = ctypes.c_size_t
+        L.smmd_wino3x3_wgrad_workspace_bytes.argtypes = [ctypes.c_int] * 5
     L.smmd_wino3x3_filter_bytes.restype = ctypes.c_size_t
     L.smmd_wino3x3_filter_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
     return L
@@ -116,11 +121,24 @@ def main():
         t_mi = timed(lambda: F.conv2d(x, w, b, padding=1), a.iters)
         t_mi_dx = timed(lambda: torch.nn.grad.conv2d_input(x.shape, w, gy, padding=1), a.iters)
         flops = 2.0 * N * C * K * 9 * H * H
+        wg = {}
+        if hasattr(L, 'smmd_wino3x3_wgrad'):
+            nbw = L.smmd_wino3x3_wgrad_workspace_bytes(N, C, K, H, H)
+            wsw = torch.empty(max(nbw // 4, 4), device=dev)
+            gw = torch.empty(K, C, 3, 3, device=dev)
+            fw = lambda: L.smmd_wino3x3_wgrad(x.data_ptr(), gy.data_ptr(), gw.data_ptr(), N, C, K,
+                                              H, H, wsw.data_ptr(), nbw, stream())
+            assert fw() == 0
+            refw = torch.nn.grad.conv2d_weight(x, (K, C, 3, 3), gy, padding=1)
+            wg = {'wgrad_rel_vs_miopen': ((gw - refw).abs().max() / refw.abs().max()).item(),
+                  'wgrad_wino_us': timed(fw, a.iters),
+                  'wgrad_miopen_us': timed(lambda: torch.nn.grad.conv2d_weight(
+                      x, (K, C, 3, 3), gy, padding=1), a.iters)}
         r = {'shape': [N, C, K, H, H], 'fwd_rel_vs_miopen': err, 'dgrad_rel_vs_miopen': errx,
              'wino_us': t_conv, 'filter_us': t_filt, 'miopen_fwd_us': t_mi,
              'miopen_dgrad_us': t_mi_dx, 'direct_tflops_wino': flops / t_conv / 1e6,
              'executed_tflops_wino': flops / 2.25 / t_conv / 1e6,
-             'direct_tflops_miopen': flops / t_mi / 1e6}
+             'direct_tflops_miopen': flops / t_mi / 1e6, **wg}
         res['timing'].append(r)
         print(json.dumps(r), flush=True)
     if a.out:
