@@ -476,15 +476,21 @@ __global__ void s2_reduce_kernel(const float *__restrict__ part, const float *__
 
 }  // namespace
 
+// reduction slices: one workgroup per CU at least, at least 4 (8) chunks
+// per slice.  Targets measured on the SNResNet-64 layers (conv / transposed,
+// us): 256 workgroups 115 / 120 / 119 / 112 and 132 / 118 / 124 / 129; 512:
+// 112 / 123 / 121 / 112 and 140 / 123 / 136 / 123; 1024 slower
+static int s2_target() { return 256; }
+
 static int s2t_slices(int64_t blocks, int nch) {
     int S = 1;
-    while (blocks * S < 512 && nch / (2 * S) >= 4) S *= 2;
+    while (blocks * S < s2_target() && nch / (2 * S) >= 4) S *= 2;
     return S;
 }
 
 static int s2_slices(int64_t blocks, int nch, int HWo) {
     int S = 1;
-    while (blocks * S < 512 && nch / (2 * S) >= 8 && HWo % 4 == 0) S *= 2;
+    while (blocks * S < s2_target() && nch / (2 * S) >= 8 && HWo % 4 == 0) S *= 2;
     return S;
 }
 
