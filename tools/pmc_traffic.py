@@ -36,6 +36,9 @@ GROUPS = {
                                 'thin_wgrad_final_kernel'),
     'smmd_wino3x3_conv': ('wino_conv_kernel', 'wino_reduce_kernel'),
     'smmd_wino3x3_filter': ('wino_filter_kernel',),
+    'smmd_wino4x4s2_conv': ('s2_conv_kernel',),
+    'smmd_wino4x4s2t_conv': ('s2t_conv_kernel',),
+    'smmd_wino4x4s2_filter': ('s2_filter_kernel', 's2t_filter_kernel'),
 }
 # entry points whose calls each run ONE of their kernels (fold or adjoint;
 # thin_in or thin_out):
@@ -78,7 +81,7 @@ def main():
                 if 'opt_sqsum@' not in kname:
                     calls = (calls + fetch[kname][1] if entry in SUM_CALLS
                              else max(calls, fetch[kname][1]))
-                found.append(kname.split('(')[0])
+                found.append(kname.replace('(anonymous namespace)::', '').split('(')[0])
         for kname in write:
             if any(k in kname for k in kernels):
                 wr += write[kname][0] * 1024
