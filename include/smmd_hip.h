@@ -595,6 +595,12 @@ smmd_status smmd_wino3x3_conv(const float *x, const float *u, const float *bias,
                               int ci, int ko, int h, int w_img, void *ws, size_t ws_bytes,
                               smmd_stream_t stream);
 
+/* the same with tf.nn.relu applied to the output (the critic's first conv of
+ * each down block, gan/core/resnet/block.py:44-46 with norm off): y = relu(conv + bias) */
+smmd_status smmd_wino3x3_conv_relu(const float *x, const float *u, const float *bias, float *y,
+                                   int n, int ci, int ko, int h, int w_img, void *ws,
+                                   size_t ws_bytes, smmd_stream_t stream);
+
 /* ---------------------------------------------------------------------------
  * 4x4 stride-2 padding-1 convolutions as polyphase Winograd F(2x2, 2x2) on the
  * f32 MFMA: the critics' ConvMeanPool layers (gan/core/resnet/block.py:63-66;

@@ -108,6 +108,7 @@ __global__ void wino_filter_kernel(const float *__restrict__ w, int KO, int CI, 
 struct WnGeom {
     int N, C, K, H, W, TW, Timg;
     int64_t T, slab;        // slab: floats between split-C partial outputs
+    int relu;               // 1: the output is relu(conv + bias) (not on partial slabs)
 };
 
 // raw 4 x 2 centre columns of one channel's patch rows (2ty-1 .. 2ty+2, cols
@@ -400,8 +401,12 @@ __global__ __launch_bounds__(WN_T, 1) void wino_conv_kernel(
             s1[j] = m[4 + j] - m[8 + j] - m[12 + j];
         }
         const float b = bias ? bias[k] : 0.f;
-        const float y00 = s0[0] + s0[1] + s0[2] + b, y01 = s0[1] - s0[2] - s0[3] + b;
-        const float y10 = s1[0] + s1[1] + s1[2] + b, y11 = s1[1] - s1[2] - s1[3] + b;
+        float y00 = s0[0] + s0[1] + s0[2] + b, y01 = s0[1] - s0[2] - s0[3] + b;
+        float y10 = s1[0] + s1[1] + s1[2] + b, y11 = s1[1] - s1[2] - s1[3] + b;
+        if (g.relu) {
+            y00 = fmaxf(y00, 0.f); y01 = fmaxf(y01, 0.f);
+            y10 = fmaxf(y10, 0.f); y11 = fmaxf(y11, 0.f);
+        }
         float *o = y + (((int64_t)en * g.K + k) * g.H + 2 * ety) * g.W + 2 * etx;
         if (pairs) {
             // even lanes send row 1, odd lanes row 0, to the partner lane
@@ -426,7 +431,8 @@ __global__ __launch_bounds__(WN_T, 1) void wino_conv_kernel(
 // y = bias + sum over the S partial slabs in slice order (float4 when the
 // plane size allows)
 __global__ void wino_reduce_kernel(const float *__restrict__ part, const float *__restrict__ bias,
-                                   float *__restrict__ y, int64_t n4, int S, int K, int HW) {
+                                   float *__restrict__ y, int64_t n4, int S, int K, int HW,
+                                   int relu) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n4) return;
     const float4 *p4 = reinterpret_cast<const float4 *>(part);
@@ -438,6 +444,9 @@ __global__ void wino_reduce_kernel(const float *__restrict__ part, const float *
     if (bias) {
         const float b = bias[(int)((i * 4 / HW) % K)];
         s.x += b; s.y += b; s.z += b; s.w += b;
+    }
+    if (relu) {
+        s.x = fmaxf(s.x, 0.f); s.y = fmaxf(s.y, 0.f); s.z = fmaxf(s.z, 0.f); s.w = fmaxf(s.w, 0.f);
     }
     reinterpret_cast<float4 *>(y)[i] = s;
 }
@@ -487,9 +496,9 @@ extern "C" size_t smmd_wino3x3_workspace_bytes(int n, int ci, int ko, int h, int
     return S > 1 ? (size_t)S * n * ko * h * w_img * sizeof(float) : 0;
 }
 
-extern "C" smmd_status smmd_wino3x3_conv(const float *x, const float *u, const float *bias,
-                                         float *y, int n, int ci, int ko, int h, int w_img,
-                                         void *ws, size_t ws_bytes, smmd_stream_t stream) {
+static smmd_status wino3x3_conv(const float *x, const float *u, const float *bias, float *y,
+                                int n, int ci, int ko, int h, int w_img, void *ws,
+                                size_t ws_bytes, int relu, smmd_stream_t stream) {
     if (n < 0 || ci <= 0 || ko <= 0 || h < 0 || w_img < 0) return SMMD_EINVAL;
     if (n == 0 || h == 0 || w_img == 0) return SMMD_OK;
     if (!x || !u || !y) return SMMD_EINVAL;
@@ -524,6 +533,7 @@ extern "C" smmd_status smmd_wino3x3_conv(const float *x, const float *u, const f
         attr = true;
     }
     g.slab = S > 1 ? total : 0;
+    g.relu = S > 1 ? 0 : relu;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const dim3 grid((unsigned)tb, (unsigned)(ko / WN_KB), (unsigned)S);
     const float *b1 = S > 1 ? nullptr : bias;
@@ -536,6 +546,18 @@ extern "C" smmd_status smmd_wino3x3_conv(const float *x, const float *u, const f
     if (e != SMMD_OK || S == 1) return e;
     const int64_t n4 = total / 4;
     wino_reduce_kernel<<<dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st>>>(
-        out, bias, y, n4, S, ko, h * w_img);
+        out, bias, y, n4, S, ko, h * w_img, relu);
     return last_launch_status();
+}
+
+extern "C" smmd_status smmd_wino3x3_conv(const float *x, const float *u, const float *bias,
+                                         float *y, int n, int ci, int ko, int h, int w_img,
+                                         void *ws, size_t ws_bytes, smmd_stream_t stream) {
+    return wino3x3_conv(x, u, bias, y, n, ci, ko, h, w_img, ws, ws_bytes, 0, stream);
+}
+
+extern "C" smmd_status smmd_wino3x3_conv_relu(const float *x, const float *u, const float *bias,
+                                              float *y, int n, int ci, int ko, int h, int w_img,
+                                              void *ws, size_t ws_bytes, smmd_stream_t stream) {
+    return wino3x3_conv(x, u, bias, y, n, ci, ko, h, w_img, ws, ws_bytes, 1, stream);
 }

@@ -150,6 +150,7 @@ _SIGS = {
     'smmd_wino3x3_filter': (_I, [_P, _I, _I, _I, _P, _SZ, _P]),
     'smmd_wino3x3_workspace_bytes': (_SZ, [_I, _I, _I, _I, _I]),
     'smmd_wino3x3_conv': (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _SZ, _P]),
+    'smmd_wino3x3_conv_relu': (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _SZ, _P]),
     'smmd_wino4x4s2_supported': (_I, [_I, _I, _I, _I, _I]),
     'smmd_wino4x4s2t_supported': (_I, [_I, _I, _I, _I, _I]),
     'smmd_wino4x4s2_filter_bytes': (_SZ, [_I, _I]),

@@ -234,7 +234,10 @@ class ResidualBlock(nn.Module):
         defer_bias the two convolutions leave their biases to the consumer
         (the next block's relu_pool) and return them; otherwise (None, None)."""
         r, p = convops.relu_pool(x, y, slope_p, bx, by)
-        h1 = F.relu(self.bn2(self.conv_1(r)))
+        if isinstance(self.bn2, _Identity):      # norm off: the ReLU in the conv's epilogue
+            h1 = self.conv_1(r, relu=True)
+        else:
+            h1 = F.relu(self.bn2(self.conv_1(r)))
         sc = self.shortcut.conv
         if defer_bias and self.conv_2.bias_deferrable(h1) and sc.bias is not None \
                 and self.conv_2.conv.bias is not None:

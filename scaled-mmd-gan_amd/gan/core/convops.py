@@ -205,7 +205,7 @@ def clear_wino_cache():
     _WINO_CACHE.clear()
 
 
-def _wino_conv(x, w, b, mode):
+def _wino_conv(x, w, b, mode, relu=False):
     """smmd_wino3x3_filter + smmd_wino3x3_conv: mode 0 conv(x, w) + b
     (w [co, ci, 3, 3]); mode 1 the input gradient of a conv with weight
     w [ci', co', 3, 3] at upstream x."""
@@ -225,9 +225,10 @@ def _wino_conv(x, w, b, mode):
     _lib.add_bytes('smmd_wino3x3_conv', (x.numel() + y.numel()) * 4)
     # 16 transform-point products per 2 x 2 output tile and (ci, co) pair
     _lib.add_flops('smmd_wino3x3_conv', 2 * 16 * N * (H // 2) * (W // 2) * ci * co)
+    fn = L.smmd_wino3x3_conv_relu if relu else L.smmd_wino3x3_conv
     with _lib.timed('smmd_wino3x3_conv'):
-        st = L.smmd_wino3x3_conv(_lib.ptr(x), _lib.ptr(u), _lib.ptr(b), _lib.ptr(y), N, ci, co, H,
-                                 W, _lib.ptr(ws), nb, _lib.stream_handle(x.device))
+        st = fn(_lib.ptr(x), _lib.ptr(u), _lib.ptr(b), _lib.ptr(y), N, ci, co, H, W, _lib.ptr(ws),
+                nb, _lib.stream_handle(x.device))
     _lib.check(st, 'smmd_wino3x3_conv')
     return y
 
@@ -555,6 +556,53 @@ def bias_grad(gy):
                                 ws.numel(), _lib.stream_handle(gy.device))
     _lib.check(st, 'smmd_channel_sum')
     return out
+
+
+class _Conv2dReLU(torch.autograd.Function):
+    """relu(conv(x, w) + b) with the ReLU in the Winograd kernel's epilogue (the
+    critic's first conv of each down block, block.py:44-46, norm off): no
+    pre-activation is written.  Backward: the mask (r > 0) of the output, as
+    TF's relu gradient, then the conv's backward (differentiable: the double
+    backward of the scaling regulariser)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, stride, padding):
+        r = _wino_conv(x, w, b, 0, relu=True)
+        ctx.save_for_backward(x, w, r)
+        ctx.cfg = (stride, padding, b is not None)
+        return r
+
+    @staticmethod
+    def backward(ctx, gr):
+        x, w, r = ctx.saved_tensors
+        stride, padding, has_b = ctx.cfg
+        gy = _aten.threshold_backward(gr.contiguous(), r, 0.0)
+        want_w = ctx.needs_input_grad[1] and _input_only[0] == 0
+        want_x = ctx.needs_input_grad[0] and not (_no_dx and x.data_ptr() in _no_dx)
+        if torch.is_grad_enabled():
+            gx, gw = _ConvBackward.apply(x, w, gy, stride, padding, want_w)
+            if not want_w:
+                gw = None
+        elif want_x or want_w:
+            gx, gw = _bwd(gy, x, w, stride, padding, (want_x, want_w))
+        else:
+            gx = gw = None
+        gb = (bias_grad(gy) if (has_b and ctx.needs_input_grad[2] and _input_only[0] == 0)
+              else None)
+        return gx, gw, gb, None, None
+
+
+def conv2d_relu(x, w, b=None, stride=1, padding=0):
+    """relu(conv2d(x, w, b)): one Winograd launch on the 3x3 layers it tiles
+    (SMMD_CONV_RELU=0: a separate ReLU), the two ops otherwise."""
+    s = (stride, stride) if isinstance(stride, int) else tuple(stride)
+    p = (padding, padding) if isinstance(padding, int) else tuple(padding)
+    if CONV_RELU and _is_wino(x, w, list(s), list(p), 0):
+        return _Conv2dReLU.apply(x, w, b, list(s), list(p))
+    return F.relu(conv2d(x, w, b, stride, padding))
+
+
+CONV_RELU = os.environ.get('SMMD_CONV_RELU', '1') != '0'
 
 
 def conv2d(x, w, b=None, stride=1, padding=0):

@@ -17,7 +17,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .convops import conv2d, thin_applicable
+from .convops import conv2d, conv2d_relu, thin_applicable
 
 
 def same_pad(n_in, k, s):
@@ -82,12 +82,17 @@ class Conv2d(nn.Module, _SNMixin):
         self.bias = nn.Parameter(torch.zeros(cout)) if bias else None
         self._init_sn(with_sn, with_learnable_sn_scale, scale)
 
-    def forward(self, x, with_bias=True):
-        """with_bias False: the convolution alone (a consumer adds self.bias)."""
+    def forward(self, x, with_bias=True, relu=False):
+        """with_bias False: the convolution alone (a consumer adds self.bias);
+        relu: relu(conv + bias) (convops.conv2d_relu)."""
         w = self.effective_weight()
         b = self.bias if with_bias else None
         ph = same_pad(x.shape[2], self.k, self.stride)
         pw = same_pad(x.shape[3], self.k, self.stride)
+        if relu:
+            if ph[0] == ph[1] and pw[0] == pw[1]:
+                return conv2d_relu(x, w, b, self.stride, (ph[0], pw[0]))
+            return F.relu(self.forward(x, with_bias))
         if ph[0] == ph[1] and pw[0] == pw[1]:
             return conv2d(x, w, b, self.stride, (ph[0], pw[0]))
         x = F.pad(x, (pw[0], pw[1], ph[0], ph[1]))

@@ -173,3 +173,35 @@ def test_wino_wgrad_vs_float64(wgrad_on, shape):
 
 def test_wino_wgrad_double_backward_vs_float64(wgrad_on):
     test_convops_wino_double_backward_vs_float64((2, 64, 64, 8, 8))
+
+
+@pytest.mark.parametrize('shape', [(2, 64, 64, 8, 8), (3, 512, 512, 8, 8)])
+def test_conv2d_relu_double_backward_vs_float64(shape):
+    """convops.conv2d_relu (the ReLU in the Winograd epilogue; the 512-channel
+    case takes the split-input-channel path, ReLU in the slice add) through
+    the critic's double backward against float64 relu(conv2d)."""
+    from gan.core import convops
+    N, C, K, H, W = shape
+    g = torch.Generator(device=DEV).manual_seed(31)
+    t = {k: torch.randn(*s, device=DEV, generator=g) for k, s in
+         dict(x=(N, C, H, W), w=(K, C, 3, 3), b=(K,), A=(N, K, H, W), B=(N, C, H, W),
+              D=(K, C, 3, 3)).items()}
+    t['w'] = t['w'] / (9 * C) ** 0.5
+
+    def run(dev, dtype, fn):
+        v = {k: t[k].to(dev, dtype).requires_grad_(k in ('x', 'w', 'A')) for k in t}
+        y = fn(v['x'], v['w'], v['b'])
+        loss = (y * v['A']).sum()
+        gx, gw = torch.autograd.grad(loss, (v['x'], v['w']), create_graph=True)
+        second = (gx * v['B']).sum() + (gw * v['D']).sum()
+        hx, hw, hA = torch.autograd.grad(second, (v['x'], v['w'], v['A']))
+        return y, gx, gw, hx, hw, hA
+
+    assert convops._is_wino(t['x'], t['w'], [1, 1], [1, 1], 0)
+    got = run(DEV, torch.float32, lambda x, w, b: convops.conv2d_relu(x, w, b, 1, 1))
+    # the reference takes the ReLU's mask from the fp32 output, so an
+    # activation within rounding of 0 cannot flip between the two
+    mask = (got[0] > 0).double().cpu()
+    ref = run('cpu', torch.float64, lambda x, w, b: F.conv2d(x, w, b, 1, 1) * mask)
+    for n, a, r in zip(('y', 'gx', 'gw', 'hx', 'hw', 'hA'), got, ref):
+        assert _rel(a, r) < (2e-5 if n in ('gw', 'hx', 'hw') else 1e-5), n
