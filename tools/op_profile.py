@@ -65,7 +65,8 @@ def main():
                 e.key, e.self_device_time_total, e.count, str(e.input_shapes)[:160]))
     if args.stack:
         st = prof.key_averages(group_by_stack_n=6)
-        rows = [e for e in st if e.key in ('aten::add_', 'aten::add', 'aten::fill_', 'aten::zero_',
+        rows = [e for e in st if e.key in ('aten::add_', 'aten::add', 'aten::mul', 'aten::fill_',
+                                           'aten::zero_',
                                            'aten::zeros', 'aten::zeros_like', 'aten::copy_')]
         rows.sort(key=lambda e: -e.count)
         with open(args.out.replace('.txt', '_stacks.txt'), 'w') as f:
