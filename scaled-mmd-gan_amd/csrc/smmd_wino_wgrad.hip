@@ -15,8 +15,8 @@
 // dM [p][h][k64][t4] and V [p][h][c64][t4].  Transform role: lane = channel
 // (k for dM, c for V), wave w = the chunk's tiles 2w, 2w+1 (horizontal
 // neighbours: TW is even).  Each slice writes its partial dU [K][C][16] to the
-// workspace; smmd_wino3x3_wgrad's second kernel adds the slices in order and
-// applies G^T . G.
+// workspace; smmd_wino3x3_wgrad adds the slices in order (in groups of 16 first
+// when there are more than 32) and applies G^T . G.
 #include "smmd_common.hpp"
 
 namespace smmd {
@@ -187,6 +187,24 @@ __global__ __launch_bounds__(WG_T, 1) void wino_wgrad_kernel(
     }
 }
 
+// the first level of the slice reduction: out[g] = sum of slices g*G .. g*G+G-1
+// in order, one thread per (group, float4 of dU): the many-slice layers (the
+// 64-channel layer has 512) read their partials at the full width of the chip
+__global__ void wino_wgrad_group_kernel(const float4 *__restrict__ part, int S, int G,
+                                        int64_t nf4, int ngroups, float4 *__restrict__ out) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= nf4 * ngroups) return;
+    const int gi = (int)(idx / nf4);
+    const int64_t f = idx - (int64_t)gi * nf4;
+    const int s0 = gi * G, s1 = min(S, s0 + G);
+    float4 a = part[(int64_t)s0 * nf4 + f];
+    for (int s = s0 + 1; s < s1; ++s) {
+        const float4 v = part[(int64_t)s * nf4 + f];
+        a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+    out[idx] = a;
+}
+
 // dW[k][c] = G^T (sum over slices, in order, of dU) G, G = [[1,0,0],[.5,.5,.5],[.5,-.5,.5],[0,0,1]]
 __global__ void wino_wgrad_final_kernel(const float *__restrict__ part, int S, int K, int C,
                                         float *__restrict__ dw) {
@@ -227,10 +245,14 @@ __global__ void wino_wgrad_final_kernel(const float *__restrict__ part, int S, i
 }  // namespace
 
 static int wgrad_slices(int blocks, int64_t nchunks) {
-    int64_t S = (512 + blocks - 1) / blocks;
+    int64_t S = (256 + blocks - 1) / blocks;
     S = min(S, max((int64_t)1, nchunks / 8));      // at least 8 chunks per slice
     return (int)max((int64_t)1, S);
 }
+
+constexpr int WG_GROUP = 16;                       // slices per first-level group
+
+static int wgrad_groups(int S) { return S > 2 * WG_GROUP ? (S + WG_GROUP - 1) / WG_GROUP : 0; }
 
 }  // namespace smmd
 
@@ -245,7 +267,7 @@ extern "C" size_t smmd_wino3x3_wgrad_workspace_bytes(int n, int ci, int co, int 
     if (!smmd_wino3x3_wgrad_supported(n, ci, co, h, w_img)) return 0;
     const int64_t T = (int64_t)n * (h / 2) * (w_img / 2);
     const int S = wgrad_slices((co / 64) * (ci / 64), (T + WG_TC - 1) / WG_TC);
-    return (size_t)S * co * ci * 16 * sizeof(float);
+    return (size_t)(S + wgrad_groups(S)) * co * ci * 16 * sizeof(float);
 }
 
 // gw [co, ci, 3, 3] = the weight gradient of conv(x [n, ci, h, w], W, stride 1,
@@ -270,7 +292,8 @@ extern "C" smmd_status smmd_wino3x3_wgrad(const float *x, const float *gy, float
     const int S = wgrad_slices(blocks, nchunks);
     g.chunks_per_slice = (int)((nchunks + S - 1) / S);
     const int Sused = (int)((nchunks + g.chunks_per_slice - 1) / g.chunks_per_slice);
-    if (!ws || ws_bytes < (size_t)S * co * ci * 16 * sizeof(float)) return SMMD_EWORKSPACE;
+    if (!ws || ws_bytes < (size_t)(S + wgrad_groups(S)) * co * ci * 16 * sizeof(float))
+        return SMMD_EWORKSPACE;
     if (reinterpret_cast<uintptr_t>(ws) & 15) return SMMD_EINVAL;
     static bool attr = false;
     if (!attr) {
@@ -286,7 +309,18 @@ extern "C" smmd_status smmd_wino3x3_wgrad(const float *x, const float *gy, float
     smmd_status e = last_launch_status();
     if (e != SMMD_OK) return e;
     const int64_t nkc = (int64_t)co * ci;
+    const int ng = wgrad_groups(Sused);
+    if (ng > 0) {                                  // two-level: groups of WG_GROUP slices, in order
+        float *grp = part + (size_t)S * co * ci * 16;
+        const int64_t nf4 = nkc * 4, nt = nf4 * ng;
+        wino_wgrad_group_kernel<<<dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, st>>>(
+            reinterpret_cast<const float4 *>(part), Sused, WG_GROUP, nf4, ng,
+            reinterpret_cast<float4 *>(grp));
+        e = last_launch_status();
+        if (e != SMMD_OK) return e;
+        part = grp;
+    }
     wino_wgrad_final_kernel<<<dim3((unsigned)((nkc + 255) / 256)), dim3(256), 0, st>>>(
-        part, Sused, co, ci, gw);
+        part, ng > 0 ? ng : Sused, co, ci, gw);
     return last_launch_status();
 }

@@ -233,8 +233,8 @@ def _wino_conv(x, w, b, mode, relu=False):
     return y
 
 
-# the weight gradient of those layers (SMMD_WINO_WGRAD=1: on, MIOpen otherwise)
-WINO_WGRAD = os.environ.get('SMMD_WINO_WGRAD', '0') == '1'
+# the weight gradient of those layers (SMMD_WINO_WGRAD=0: MIOpen)
+WINO_WGRAD = os.environ.get('SMMD_WINO_WGRAD', '1') == '1'
 
 
 def _wino_wgrad(x, gy):
