@@ -36,6 +36,7 @@ GROUPS = {
                                 'thin_wgrad_final_kernel'),
     'smmd_wino3x3_conv': ('wino_conv_kernel', 'wino_reduce_kernel'),
     'smmd_wino3x3_filter': ('wino_filter_kernel',),
+    'smmd_wino3x3_wgrad': ('wino_wgrad_kernel', 'wino_wgrad_group_kernel', 'wino_wgrad_final_kernel'),
     'smmd_wino4x4s2_conv': ('s2_conv_kernel',),
     'smmd_wino4x4s2t_conv': ('s2t_conv_kernel',),
     'smmd_wino4x4s2_filter': ('s2_filter_kernel', 's2t_filter_kernel'),
