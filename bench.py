@@ -51,27 +51,50 @@ VALU_LANE_OPS = FP32_PEAK_TFS / 2 * 1e12
 TRANS_SLOTS = 4                # v_exp_f32 / v_log_f32: quarter rate (MI355X_MICROARCH.md)
 BATCH = 64
 
-PMC_TRAFFIC = os.path.join(ROOT, 'profiles', 'r09', 'pmc_traffic.json')
+# committed counter evidence of this workload, each file stamped with the
+# smmd_source_hash of the library build it was measured on (tools/stamp.py);
+# embedded only when that stamp equals the running library's
+PMC_TRAFFIC = os.path.join(ROOT, 'profiles', 'r11', 'pmc_traffic.json')
 # executed FLOPs per kernel class over whole 5D+1G cycles of this workload
 # (tools/gpu_step_pmc.sh -> tools/step_flops_pmc.py: rocprofv3 SQ_INSTS_VALU_*
 # and SQ_INSTS_VALU_MFMA_MOPS_F32 counters + a kernel trace)
-STEP_PMC = os.path.join(ROOT, 'profiles', 'r09', 'step_flops_pmc.json')
+STEP_PMC = os.path.join(ROOT, 'profiles', 'r11', 'step_flops_pmc.json')
 
 
-def step_counters(ms_step):
-    """The counter-based step roofline (SURVEY 8d): executed TFLOP per step
-    from the committed PMC file, its rate over the GPU-busy time it was
-    measured with and over this run's step time, and per kernel class
-    (Winograd, implicit-GEMM fwd / bwd-data / wrw, transposes, elementwise,
-    the library) the time share, executed TFLOP/s and fraction of the fp32
-    peak."""
+def load_stamped(path, stamp):
+    """A committed profile file, only when it was measured with the library
+    build running now: (data, None), else (None, reason).  A file without a
+    stamp, or with another build's, is stale evidence and is not embedded."""
+    rel = os.path.relpath(path, ROOT)
     try:
-        with open(STEP_PMC) as f:
+        with open(path) as f:
             d = json.load(f)
-    except (OSError, ValueError):
-        return None
+    except OSError:
+        return None, 'no %s' % rel
+    except ValueError:
+        return None, '%s is not JSON' % rel
+    got = d.get('smmd_source_hash') if isinstance(d, dict) else None
+    if not got:
+        return None, '%s carries no smmd_source_hash stamp' % rel
+    if got != stamp:
+        return None, ('%s was measured on library %s, the running library is %s'
+                      % (rel, got, stamp))
+    return d, None
+
+
+def step_counters(ms_step, stamp):
+    """The counter-based step roofline (SURVEY 8d): executed TFLOP per step
+    from the committed PMC file (when its stamp is the running library's), its
+    rate over the GPU-busy time it was measured with and over this run's step
+    time, and per kernel class (Winograd, implicit-GEMM fwd / bwd-data / wrw,
+    transposes, elementwise, the library) the time share, executed TFLOP/s and
+    fraction of the fp32 peak."""
+    d, why = load_stamped(STEP_PMC, stamp)
+    if d is None:
+        return {'source': None, 'null_reason': why}
     tf_step = d['executed_tflop_per_step']
     out = {'source': os.path.relpath(STEP_PMC, ROOT),
+           'smmd_source_hash': d['smmd_source_hash'],
            'executed_tflop_per_step': tf_step,
            'executed_tflops_over_gpu_busy': d['executed_tflops_over_busy'],
            'frac_of_fp32_peak_over_gpu_busy': d['frac_of_fp32_peak_over_busy'],
@@ -83,7 +106,7 @@ def step_counters(ms_step):
                                                    'frac_of_fp32_peak')}
                        for k, v in d['classes'].items()}}
     return out
-PMC_FALLBACK = os.path.join(ROOT, 'profiles', 'r06', 'pmc_traffic.json')
+
 
 # the hot-path rows a1-a9 and the library entry points that
 # implement them (the roofline kernel is chosen among these)
@@ -93,20 +116,18 @@ HOT_PATH = ('smmd_mmd2_fwd', 'smmd_scaled_loss_fwd', 'smmd_scaled_loss_bwd',
             'smmd_adam_flat[G]', 'smmd_adam_flat_sn[D]', 'smmd_adam_flat_sn[G]')
 
 
-def pmc_traffic(entry):
+def pmc_traffic(entry, stamp):
     """HBM bytes per call of a library entry point from the committed rocprofv3
-    PMC passes (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, tools/pmc_traffic.py,
-    same kernels and sizes via tools/hipbench.py), or None when not measured.
-    Returns (bytes, source file)."""
-    for path in (PMC_TRAFFIC, PMC_FALLBACK):
-        try:
-            with open(path) as f:
-                rec = json.load(f).get(entry.split('[')[0])
-            if rec:
-                return rec['traffic_bytes'], os.path.relpath(path, ROOT)
-        except (OSError, ValueError, KeyError):
-            continue
-    return None, None
+    PMC passes (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, tools/pmc_traffic.py
+    over tools/step_cycle.py), measured on the running library build.
+    Returns (bytes, source file, None) or (None, None, reason)."""
+    d, why = load_stamped(PMC_TRAFFIC, stamp)
+    if d is None:
+        return None, None, why
+    rec = d.get(entry.split('[')[0])
+    if not rec:
+        return None, None, 'no %s group in %s' % (entry, os.path.relpath(PMC_TRAFFIC, ROOT))
+    return rec['traffic_bytes'], os.path.relpath(PMC_TRAFFIC, ROOT), None
 
 
 def imagenet_config(batch=BATCH):
@@ -697,6 +718,8 @@ def main():
         log('reference schedule: %.2f ms/step' % (dtr / args.ref_schedule_steps * 1e3))
 
     # 5. instrumented pass (separate from the headline)
+    from gan.core import _lib
+    stamp = _lib.lib().smmd_source_hash().decode()     # the running library build
     kernels, step_ms, roofline, hot = {}, {}, None, {}
     if args.instrument_cycles > 0:
         tm, tb, step_ms, n_inst = instrumented_pass(model, images, args.instrument_cycles,
@@ -767,10 +790,10 @@ def main():
                                      mfma_frac=round(tf / MFMA_F32_PEAK_TFS, 4))
         if cands:
             dom = max(cands, key=lambda k: kernels[k]['ms_per_step'])
-            traffic, src = pmc_traffic(dom)
+            traffic, src, why = pmc_traffic(dom, stamp)
             roofline = {'bound': 'hbm', 'kernel': dom, 'achieved': kernels[dom]['GB_s'],
                         'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': kernels[dom]['frac'],
-                        'traffic': traffic, 'traffic_source': src,
+                        'traffic': traffic, 'traffic_source': src, 'traffic_null_reason': why,
                         'avg_ms': kernels[dom]['avg_ms'],
                         'algorithmic_bytes': kernels[dom]['bytes']}
         # the library's dominant kernel by time per step: a Winograd
@@ -783,11 +806,15 @@ def main():
         if wk and (roofline is None
                    or kernels[wk]['ms_per_step'] > kernels[roofline['kernel']]['ms_per_step']):
             hot['hbm_roofline_kernel'] = roofline
-            traffic, src = pmc_traffic(wk)
+            traffic, src, why = pmc_traffic(wk, stamp)
             roofline = {'bound': 'mfma', 'kernel': wk, 'achieved': kernels[wk]['tflops'],
                         'peak': MFMA_F32_PEAK_TFS, 'unit': 'TFLOP/s',
                         'frac': kernels[wk]['mfma_frac'], 'traffic': traffic,
-                        'traffic_source': src, 'avg_ms': kernels[wk]['avg_ms'],
+                        'traffic_source': src, 'traffic_null_reason': why,
+                        'traffic_over_algorithmic': (
+                            round(traffic / kernels[wk]['bytes'], 3)
+                            if traffic and kernels[wk].get('bytes') else None),
+                        'avg_ms': kernels[wk]['avg_ms'],
                         'calls_per_step': round(kernels[wk]['calls'] / n_inst, 2),
                         'ms_per_step': kernels[wk]['ms_per_step'],
                         'executed_flops_per_call': kernels[wk]['mfma_flops'],
@@ -799,15 +826,19 @@ def main():
         for k in ('smmd_sn_power_iter', 'smmd_sn_weight_bwd', 'smmd_sn_grad_stats',
                   'smmd_adam_flat_sn[D]',
                   'smmd_scaled_loss_fwd', 'smmd_scaled_loss_bwd', 'smmd_smmd_loss_fwd',
-                  'smmd_smmd_loss_bwd', 'smmd_fold_pool_weights'):
+                  'smmd_smmd_loss_bwd', 'smmd_fold_pool_weights', 'smmd_wino3x3_conv',
+                  'smmd_wino3x3_wgrad', 'smmd_wino4x4s2_conv', 'smmd_wino4x4s2t_conv',
+                  'smmd_wino4x4s2_wgrad'):
             if k in kernels and 'bytes' in kernels[k]:
-                traffic, src = pmc_traffic(k)
-                hot[k] = {'avg_ms': kernels[k]['avg_ms'], 'algorithmic_bytes': kernels[k]['bytes'],
-                          'GB_s': kernels[k]['GB_s'], 'hbm_frac': kernels[k]['frac'],
-                          'pmc_traffic': traffic,
-                          'pmc_over_algorithmic': (round(traffic / kernels[k]['bytes'], 3)
-                                                   if traffic else None),
-                          'pmc_source': src}
+                traffic, src, why = pmc_traffic(k, stamp)
+                row = hot.setdefault(k, {})
+                row.update({'avg_ms': kernels[k]['avg_ms'],
+                            'algorithmic_bytes': kernels[k]['bytes'],
+                            'GB_s': kernels[k]['GB_s'], 'hbm_frac': kernels[k]['frac'],
+                            'pmc_traffic': traffic,
+                            'pmc_over_algorithmic': (round(traffic / kernels[k]['bytes'], 3)
+                                                     if traffic else None),
+                            'pmc_source': src, 'pmc_null_reason': why})
         # the loss side of a step: the fused launch and its backward (or,
         # unfused, mmd2 + scaled loss fwd + bwd), each once per step: the sum
         # of their mean HIP-event times per call
@@ -834,14 +865,17 @@ def main():
     fl_timed = (counts['D'] * fl['flops_per_D_step'] + counts['G'] * fl['flops_per_G_step']) \
         / max(counts['D'] + counts['G'], 1)
     tfs = fl_timed / (ms_step * 1e-3) / 1e12
-    hot['step'] = dict(fl, flops_per_timed_step=fl_timed, tflops=round(tfs, 2),
-                       fp32_peak_tflops=FP32_PEAK_TFS, frac=round(tfs / FP32_PEAK_TFS, 4),
-                       note='algorithmic = the reference\'s literal conv layers (no fold, '
-                            'direct-conv MAC count); the product runs Winograd and folded '
-                            'stride-2 convs, which execute fewer MACs, so this is a '
-                            'work-rate against the fp32 peak, not a utilisation counter; '
-                            '`counters` holds the executed-FLOP figures',
-                       counters=step_counters(ms_step))
+    hot['step'] = dict(fl, flops_per_timed_step=fl_timed,
+                       literal_work_rate_tflops=round(tfs, 2),
+                       literal_work_rate_over_fp32_peak=round(tfs / FP32_PEAK_TFS, 4),
+                       fp32_peak_tflops=FP32_PEAK_TFS,
+                       note='literal work rate = the reference\'s literal conv layers (no '
+                            'fold, direct-conv MAC count) per second of this run; the '
+                            'product runs Winograd and folded stride-2 convs, which execute '
+                            'fewer MACs, so this rate can exceed the peak and is not a '
+                            'utilisation; `counters` holds the executed-FLOP figures '
+                            '(rocprofv3, stamped with the library build they were measured on)',
+                       counters=step_counters(ms_step, stamp))
 
     sweep = None
     if args.mmd_sweep:
@@ -880,6 +914,7 @@ def main():
                    'miopen_db': os.environ.get('MIOPEN_USER_DB_PATH')},
         'roofline': roofline,
         'roofline_hot_path': hot,
+        'smmd_source_hash': stamp,
         'step_ms_by_kind': {k: round(v, 3) for k, v in step_ms.items()},
         'hip_kernels': kernels,
         'schedule_reference': ref_sched,

@@ -32,6 +32,7 @@ SN_MAX_FUSED = 16          # SN layers smmd_adam_flat_sn takes in one call
 ABI_VERSION = 8
 
 KIND_RBF, KIND_RQ, KIND_DISTANCE, KIND_DOT = 0, 1, 2, 3
+SMMD_EUNSUPPORTED = 4       # smmd_status (include/smmd_hip.h)
 
 
 class SmmdLibraryError(RuntimeError):

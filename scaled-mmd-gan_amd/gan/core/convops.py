@@ -18,10 +18,13 @@ with the three standard primitives on the layer's own shapes:
 so it uses MIOpen's forward, backward-data and backward-weights kernels --
 except for the thin 3x3 layers (a critic's 3-channel input conv, a
 generator's 3-channel output layer), whose three primitives run on the
-library's `smmd_conv3x3_thin*` kernels (csrc/smmd_thin.hip), and the wide 3x3
+library's `smmd_conv3x3_thin*` kernels (csrc/smmd_thin.hip), the wide 3x3
 stride-1 layers, whose forward and backward-data primitives run on the
 library's fused Winograd F(2x2, 3x3) MFMA kernel (`smmd_wino3x3_*`,
-csrc/smmd_wino.hip); their weight gradient stays on MIOpen.
+csrc/smmd_wino.hip) and whose weight gradient runs on `smmd_wino3x3_wgrad`
+(csrc/smmd_wino_wgrad.hip), and the 4x4 stride-2 layers (folded ConvMeanPool
+/ UpsampleConv), whose forward and transposed convolutions run on the
+polyphase Winograd kernels (`smmd_wino4x4s2*`, csrc/smmd_wino_s2.hip).
 """
 from __future__ import annotations
 
@@ -151,30 +154,44 @@ def wino_applicable(x, cin, cout, k, stride, padding):
 # transformed filters of the weights in use: a critic step convolves each
 # weight several times (real and fake forward, the Jacobian's and the loss's
 # input gradients, the double backward), and its transform costs 7-15 us.
-# Entries hold the weight tensor itself and are valid while it is the same
-# object at the same torch version and FlatAdam epoch (the fused optimizer
-# writes parameters without bumping versions; the SN bank's W_eff is a new
-# tensor every refresh).  Off during HIP-graph capture: a replay must
-# re-transform what it convolves.  Shared by the 3x3 and the stride-2 kernels,
-# capped at 1 GiB (a 512 -> 1024 stride-2 filter transforms to 75 MB).
-_WINO_CACHE = {}
-_WINO_CACHE_MAX_BYTES = 1 << 30      # oldest entries go first past 1 GiB of HBM
+# An entry is valid while its weight is the same live tensor at the same torch
+# version and FlatAdam epoch (the fused optimizer writes parameters without
+# bumping versions; the SN bank's W_eff is a new tensor every refresh).  The
+# entry holds the weight only through a weak reference whose finalizer drops
+# the entry when the weight is freed, so a superseded W_eff or folded filter
+# takes its transform with it instead of pinning both until an eviction.  Off
+# during HIP-graph capture: a replay must re-transform what it convolves.
+# Shared by the 3x3 and the stride-2 kernels, capped at 1 GiB of transforms
+# (a 512 -> 1024 stride-2 filter transforms to 75 MB), oldest first.
+_WINO_CACHE = {}        # key -> (weakref to w, version, epoch, u)
+_WINO_CACHE_MAX_BYTES = 1 << 30
+_wino_cache_bytes = [0]
 
 
 def _cache_get(key, w):
     e = _WINO_CACHE.get(key)
-    if e is not None and e[0] is w and e[1] == w._version and e[2] == _param_epoch(w):
+    if e is not None and e[0]() is w and e[1] == w._version and e[2] == _param_epoch(w):
         return e[3]
     return None
 
 
+def _cache_drop(key, ref=None):
+    """Remove `key` (only if it still holds `ref`, when given)."""
+    e = _WINO_CACHE.get(key)
+    if e is not None and (ref is None or e[0] is ref):
+        del _WINO_CACHE[key]
+        _wino_cache_bytes[0] -= e[3].numel() * e[3].element_size()
+
+
 def _cache_put(key, w, u):
-    _WINO_CACHE.pop(key, None)
-    total = sum(e[3].numel() * 4 for e in _WINO_CACHE.values()) + u.numel() * 4
-    while _WINO_CACHE and total > _WINO_CACHE_MAX_BYTES:
-        old = _WINO_CACHE.pop(next(iter(_WINO_CACHE)))
-        total -= old[3].numel() * 4
-    _WINO_CACHE[key] = (w, w._version, _param_epoch(w), u)
+    import weakref
+    _cache_drop(key)
+    nb = u.numel() * u.element_size()
+    while _WINO_CACHE and _wino_cache_bytes[0] + nb > _WINO_CACHE_MAX_BYTES:
+        _cache_drop(next(iter(_WINO_CACHE)))
+    ref = weakref.ref(w, lambda r, k=key: _cache_drop(k, r))
+    _WINO_CACHE[key] = (ref, w._version, _param_epoch(w), u)
+    _wino_cache_bytes[0] += nb
 
 
 def _param_epoch(w):
@@ -203,6 +220,7 @@ def _wino_filter(w, co, ci, mode):
 
 def clear_wino_cache():
     _WINO_CACHE.clear()
+    _wino_cache_bytes[0] = 0
 
 
 def _wino_conv(x, w, b, mode, relu=False):
@@ -234,7 +252,7 @@ def _wino_conv(x, w, b, mode, relu=False):
 
 
 # the weight gradient of those layers (SMMD_WINO_WGRAD=0: MIOpen)
-WINO_WGRAD = os.environ.get('SMMD_WINO_WGRAD', '1') == '1'
+WINO_WGRAD = os.environ.get('SMMD_WINO_WGRAD', '1') != '0'
 
 
 def _wino_wgrad(x, gy):

@@ -217,14 +217,26 @@ def mmd2_fused(X, Y, kernel='rbf', biased=False, process_group=None, return_sums
 TILE_MAX_ROWS = (16384 // 4 - 64) * 64      # csrc/smmd_kern.hpp TILE_MAX_RT * 64
 
 
+def _env_first(name):
+    """The first character of an environment flag, as the library reads it
+    (csrc/smmd_mmd.hip: `e && e[0] == '1'`), or '' when unset."""
+    return (os.environ.get(name) or '')[:1]
+
+
 def fused_loss_path(m, n, d):
     """smmd_smmd_loss_fwd applies: smmd_mmd2_fwd's 2-D tiled path
-    (csrc/smmd_mmd.hip use_tile) and SMMD_FUSED_LOSS not 0."""
-    if os.environ.get('SMMD_FUSED_LOSS', '1') == '0':
+    (csrc/smmd_mmd.hip use_tile, its flags parsed the same way) and
+    SMMD_FUSED_LOSS not 0.  Should the library still answer
+    SMMD_EUNSUPPORTED, _mmd2_scaled falls back to the two separate calls."""
+    if _env_first('SMMD_FUSED_LOSS') == '0':
         return False
-    if d > 8 or os.environ.get('SMMD_MMD_GRAM') == '1' or os.environ.get('SMMD_MMD_TILE') == '0':
+    if d > 8 or _env_first('SMMD_MMD_GRAM') == '1' or _env_first('SMMD_MMD_TILE') == '0':
         return False
     return m + n <= TILE_MAX_ROWS
+
+
+class _FusedUnsupported(Exception):
+    """smmd_smmd_loss_fwd returned SMMD_EUNSUPPORTED (the caller falls back)."""
 
 
 class _SMMDLoss(torch.autograd.Function):
@@ -261,6 +273,8 @@ class _SMMDLoss(torch.autograd.Function):
                 _lib.ptr(sums), _lib.ptr(mm), _lib.ptr(gx), _lib.ptr(gy), _lib.ptr(out),
                 _lib.ptr(per_sample), _lib.ptr(ws), ws.numel(), _lib.ptr(lws), lws.numel(),
                 _lib.stream_handle(dev))
+        if st == _lib.SMMD_EUNSUPPORTED:
+            raise _FusedUnsupported()
         _lib.check(st, 'smmd_smmd_loss_fwd')
         ctx.save_for_backward(gx, gy, jac, feat_c, out)
         ctx.cfg = (n_cols, b, per, dof, float(sc), variant, m, n, d)
@@ -336,7 +350,11 @@ def _mmd2_scaled(K, biased, p):
     feat = p.feat if p.variant == 1 else None
     if p.variant == 1 and feat is None:
         return None
-    val, g, _, out = _SMMDLoss.apply(X, Y, p.jac, feat, K.spec, bool(biased), p.sc, p.variant)
+    try:
+        val, g, _, out = _SMMDLoss.apply(X, Y, p.jac, feat, K.spec, bool(biased), p.sc,
+                                         p.variant)
+    except _FusedUnsupported:      # the header's contract: make the two separate calls
+        return None
     p.result = (val, g, out)
     return val
 

@@ -74,6 +74,17 @@ def _launch_refresh(bank, update_u, flags, Ws, ss):
     return outs, [bool(a.fold) for a in arr]
 
 
+def _gdirect_scales_ok(bank, ss, needs):
+    """G-direct writes dL/ds straight into each learnable scale's gradient,
+    which must therefore exist (a view of the optimizer's flat buffer, zeroed
+    before the step: the kernel OVERWRITES it, it does not accumulate).  A
+    scale that needs a gradient but has no `.grad` takes the dense backward."""
+    for e, s, need in zip(bank.entries, ss, needs):
+        if need and s is not None and s.numel() > 0 and e.scale.grad is None:
+            return False
+    return True
+
+
 class _SNBatch(torch.autograd.Function):
     @staticmethod
     def forward(ctx, bank, update_u, flags, *tensors):
@@ -91,7 +102,7 @@ class _SNBatch(torch.autograd.Function):
         n = len(bank.entries)
         saved = ctx.saved_tensors
         Ws, ss = saved[:n], saved[n:]
-        if bank._gd_armed:
+        if bank._gd_armed and _gdirect_scales_ok(bank, ss, ctx.needs_input_grad[3 + n:]):
             return _SNBatch._backward_gdirect(ctx, bank, Ws, ss, grads)
         arr = (_lib.SnLayer * n)()
         gWs, gss, keep = [], [], []
@@ -387,7 +398,11 @@ class SpectralNormBank:
         return tuple(outs_W) + tuple(outs_s)
 
     def arm_gdirect(self, on=True):
-        """Arm (or disarm) the G-direct backward for the next backward pass."""
+        """Arm (or disarm) the G-direct backward for the next backward pass.
+        Its dL/ds is WRITTEN (not accumulated) into each learnable scale's
+        `.grad`, so the caller zeroes the gradients before the backward (the
+        critic step does, right before it) and a scale without `.grad` makes
+        that backward take the dense path (`_gdirect_scales_ok`)."""
         self._gd_armed = bool(on)
         if on:
             self._gd_pending = None

@@ -156,8 +156,17 @@ def wgrad_on():
     convops.WINO_WGRAD = saved
 
 
-@pytest.mark.parametrize('shape', [(2, 64, 64, 6, 8), (3, 64, 128, 8, 8), (4, 128, 64, 4, 12),
-                                   (2, 64, 64, 2, 4), (8, 64, 64, 64, 64), (8, 512, 512, 8, 8)])
+# the r11 kernel's chunk shapes: 16-tile rows with halo columns (W 64, 128),
+# whole 16-tile rows (W 32), two 8-tile rows (W 16), four 4-tile rows (W 8);
+# shapes it does not tile (6 x 8, 4 x 12, 2 x 4, W 8 with H % 8 != 0) take the
+# first form
+WGRAD_SHAPES = [(2, 64, 64, 6, 8), (3, 64, 128, 8, 8), (4, 128, 64, 4, 12), (2, 64, 64, 2, 4),
+                (8, 64, 64, 64, 64), (8, 512, 512, 8, 8), (2, 64, 128, 32, 32),
+                (3, 128, 64, 16, 16), (1, 64, 64, 8, 128), (2, 64, 64, 12, 8),
+                (4, 128, 128, 32, 32), (16, 256, 256, 16, 16)]
+
+
+@pytest.mark.parametrize('shape', WGRAD_SHAPES)
 def test_wino_wgrad_vs_float64(wgrad_on, shape):
     """smmd_wino3x3_wgrad against torch's float64 conv2d_weight (the sums run
     over N*H*W terms in fp32: bound 1e-5 of max|ref|)."""
@@ -169,6 +178,25 @@ def test_wino_wgrad_vs_float64(wgrad_on, shape):
     ref = torch.nn.grad.conv2d_weight(x.double().cpu(), (K, C, 3, 3), gy.double().cpu(),
                                       padding=1)
     assert _rel(gw, ref) < 1e-5
+
+
+@pytest.mark.parametrize('shape', [(8, 64, 64, 64, 64), (3, 128, 64, 16, 16), (4, 128, 64, 8, 8)])
+def test_wino_wgrad_forms_agree_and_deterministic(wgrad_on, shape, monkeypatch):
+    """The coalesced form (default) and the first form (SMMD_WINO_WGRAD_V1=1,
+    read per call by the library) agree to rounding; each gives the same bits
+    run to run."""
+    N, C, K, H, W = shape
+    g = torch.Generator(device=DEV).manual_seed(7)
+    x = torch.randn(N, C, H, W, device=DEV, generator=g)
+    gy = torch.randn(N, K, H, W, device=DEV, generator=g)
+    a0 = wgrad_on._wino_wgrad(x, gy)
+    a1 = wgrad_on._wino_wgrad(x, gy)
+    monkeypatch.setenv('SMMD_WINO_WGRAD_V1', '1')
+    b0 = wgrad_on._wino_wgrad(x, gy)
+    b1 = wgrad_on._wino_wgrad(x, gy)
+    monkeypatch.delenv('SMMD_WINO_WGRAD_V1')
+    assert torch.equal(a0, a1) and torch.equal(b0, b1)
+    assert _rel(a0, b0) < 1e-5
 
 
 def test_wino_wgrad_double_backward_vs_float64(wgrad_on):

@@ -10,8 +10,12 @@ HBM section), so read bytes = 2 * FETCH_SIZE * 1024; WRITE_SIZE is exact for
 """
 import csv
 import json
+import os
 import sys
 from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from stamp import library_stamp  # noqa: E402
 
 GROUPS = {
     'smmd_sn_power_iter': ('sn_p1_kernel', 'sn_p2_kernel', 'sn_r2_kernel', 'sn_p3_kernel'),
@@ -36,7 +40,8 @@ GROUPS = {
                                 'thin_wgrad_final_kernel'),
     'smmd_wino3x3_conv': ('wino_conv_kernel', 'wino_reduce_kernel'),
     'smmd_wino3x3_filter': ('wino_filter_kernel',),
-    'smmd_wino3x3_wgrad': ('wino_wgrad_kernel', 'wino_wgrad_group_kernel', 'wino_wgrad_final_kernel'),
+    'smmd_wino3x3_wgrad': ('wino_wgrad_kernel', 'wino_wgrad2_kernel', 'wino_wgrad_group_kernel',
+                           'wino_wgrad_final_kernel', 'wino_wgrad_sum_kernel'),
     'smmd_wino4x4s2_conv': ('s2_conv_kernel',),
     'smmd_wino4x4s2t_conv': ('s2t_conv_kernel',),
     'smmd_wino4x4s2_filter': ('s2_filter_kernel', 's2t_filter_kernel'),
@@ -72,6 +77,7 @@ def main():
     write = per_kernel(sys.argv[2])
     out = {'_note': 'bytes per call; read = 2 * FETCH_SIZE(KB) * 1024 (gfx950 correction), '
                     'write = WRITE_SIZE(KB) * 1024'}
+    out.update(library_stamp())
     for entry, kernels in GROUPS.items():
         rd = wr = 0.0
         found = []

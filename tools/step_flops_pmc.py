@@ -25,6 +25,9 @@ import json
 import os
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from stamp import library_stamp  # noqa: E402
+
 FP32_PEAK_TFS = 157.3
 
 
@@ -42,6 +45,8 @@ def _find(d, name):
 def kclass(k):
     if 'Sp3Asm' in k or 'inograd' in k:
         return 'miopen_winograd'
+    if 'smmd::' in k and 'wino_wgrad' in k:
+        return 'smmd_wino3x3_wgrad'
     if 'smmd::' in k and ('wino_' in k):
         return 'smmd_wino3x3'
     if 'smmd::' in k and ('s2_' in k or 's2t_' in k):
@@ -119,6 +124,7 @@ def main():
            'executed_tflops_over_busy': round(sum(fl.values()) / busy / 1e12, 2),
            'frac_of_fp32_peak_over_busy': round(sum(fl.values()) / busy / 1e12 / FP32_PEAK_TFS, 4),
            'classes': {}}
+    out.update(library_stamp())
     if hw:
         tot = sum(hw.values()) + sum(mf.values())
         out.update(hw_executed_tflop_per_step=round(tot / steps / 1e12, 4),

@@ -131,9 +131,20 @@ def main():
             assert fw() == 0
             refw = torch.nn.grad.conv2d_weight(x, (K, C, 3, 3), gy, padding=1)
             wg = {'wgrad_rel_vs_miopen': ((gw - refw).abs().max() / refw.abs().max()).item(),
-                  'wgrad_wino_us': timed(fw, a.iters),
                   'wgrad_miopen_us': timed(lambda: torch.nn.grad.conv2d_weight(
                       x, (K, C, 3, 3), gy, padding=1), a.iters)}
+            # interleaved A/B of the two forms (the library reads
+            # SMMD_WINO_WGRAD_V1 per call): default, v1, default, v1
+            ab = {'default': [], 'v1': []}
+            for arm in ('default', 'v1', 'default', 'v1'):
+                if arm == 'v1':
+                    os.environ['SMMD_WINO_WGRAD_V1'] = '1'
+                ab[arm].append(timed(fw, a.iters))
+                os.environ.pop('SMMD_WINO_WGRAD_V1', None)
+            wg.update(wgrad_wino_us=min(ab['default']), wgrad_v1_us=min(ab['v1']),
+                      wgrad_ab_us=ab,
+                      wgrad_executed_tflops=flops / 2.25 / min(ab['default']) / 1e6,
+                      wgrad_mfma_frac=flops / 2.25 / min(ab['default']) / 1e6 / 157.3)
         r = {'shape': [N, C, K, H, H], 'fwd_rel_vs_miopen': err, 'dgrad_rel_vs_miopen': errx,
              'wino_us': t_conv, 'filter_us': t_filt, 'miopen_fwd_us': t_mi,
              'miopen_dgrad_us': t_mi_dx, 'direct_tflops_wino': flops / t_conv / 1e6,
