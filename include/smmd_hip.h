@@ -65,7 +65,7 @@ int smmd_abi_version(void);         /* bumped on any ABI change (2: Gram/poly,
                                        smmd_source_hash, smmd_sn_grad_stats,
                                        smmd_adam_flat_sn2, smmd_bn_relu_fwd_save / _bwd,
                                        8: smmd_wino3x3_*, smmd_wino4x4s2*,
-                                       smmd_wino3x3_wgrad*) */
+                                       smmd_wino3x3_wgrad*, 9: smmd_wino4x4s2_wgrad*) */
 const char *smmd_source_hash(void); /* first 16 hex digits of the SHA-256 of the
                                        sources this binary was built from
                                        (csrc .hip and .hpp files in byte order,
@@ -664,6 +664,30 @@ size_t smmd_wino3x3_wgrad_workspace_bytes(int n, int ci, int co, int h, int w_im
 smmd_status smmd_wino3x3_wgrad(const float *x, const float *gy, float *gw, int n, int ci, int co,
                                int h, int w_img, void *ws, size_t ws_bytes,
                                smmd_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * The weight gradient of the 4x4 stride-2 pad-1 conv (TF's
+ * Conv2DBackpropFilter of the folded ConvMeanPool layers, gan/core/resnet/
+ * block.py:63-66, snops.py:69-90; with x and gy swapped, of the generator's
+ * folded UpsampleConv, block.py:53-60) as polyphase Winograd F(2x2, 2x2):
+ * dU_p = sum over 2 x 2 output tiles of (A dY A^T)_p (B^T d B)_p for every
+ * (input channel, x phase) column on the f32 MFMA, then each phase's 2 x 2 tap
+ * block of gw = G^T dU G.  gw [co, ci, 4, 4], x [n, ci, h, w_img], gy [n, co,
+ * h/2, w_img/2]; needs ci % 16 == 0, co % 64 == 0 and an output tile grid
+ * (h/4) x (w_img/4) of 16 columns, 8 columns and an even row count, 4 columns
+ * and a row count divisible by 4, or 2 x 2, and n times the tiles per image
+ * divisible by 16 (smmd_wino4x4s2_wgrad_supported).
+ * The tiles are split over workgroups whose partial gw
+ * (smmd_wino4x4s2_wgrad_workspace_bytes) are added in slice order.
+ * Deterministic.
+ * ------------------------------------------------------------------------- */
+int smmd_wino4x4s2_wgrad_supported(int n, int ci, int co, int h, int w_img);
+
+size_t smmd_wino4x4s2_wgrad_workspace_bytes(int n, int ci, int co, int h, int w_img);
+
+smmd_status smmd_wino4x4s2_wgrad(const float *x, const float *gy, float *gw, int n, int ci,
+                                 int co, int h, int w_img, void *ws, size_t ws_bytes,
+                                 smmd_stream_t stream);
 
 #ifdef __cplusplus
 }

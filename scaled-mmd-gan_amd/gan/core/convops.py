@@ -393,11 +393,62 @@ def _s2t_conv(g, w, b):
     return y
 
 
+# the weight gradient of the stride-2 layers on the polyphase Winograd kernel
+# (smmd_wino4x4s2_wgrad, csrc/smmd_wino_s2_wgrad.hip; SMMD_WINO_S2_WGRAD=0: MIOpen)
+WINO_S2_WGRAD = os.environ.get('SMMD_WINO_S2_WGRAD', '1') != '0'
+
+
+def _s2_wgrad_ok(x, gy, co):
+    """gw [co, ci, 4, 4] of conv(x, ., stride 2, pad 1) at gy runs on
+    smmd_wino4x4s2_wgrad: NCHW fp32 contiguous device tensors of the shapes
+    the kernel tiles."""
+    if not (WINO_S2_WGRAD and x.is_cuda and gy.is_cuda and x.dtype == torch.float32
+            and gy.dtype == torch.float32 and x.dim() == 4 and gy.dim() == 4
+            and x.is_contiguous() and gy.is_contiguous()):
+        return False
+    n, ci, h, w = x.shape
+    if tuple(gy.shape) != (n, co, h // 2, w // 2):
+        return False
+    from . import _lib
+    return bool(_lib.lib().smmd_wino4x4s2_wgrad_supported(n, ci, co, h, w))
+
+
+def _s2_wgrad(x, gy):
+    """smmd_wino4x4s2_wgrad: gw [co, ci, 4, 4] of conv(x, W', stride 2, pad 1)
+    at gy [n, co, h/2, w/2]."""
+    from . import _lib
+    _lib.require_cuda(x, gy)
+    N, ci, H, W = x.shape
+    co = gy.shape[1]
+    L = _lib.lib()
+    nb = L.smmd_wino4x4s2_wgrad_workspace_bytes(N, ci, co, H, W)
+    ws = _lib.workspace('wino_s2_wgrad', nb, x.device)
+    gw = torch.empty((co, ci, 4, 4), dtype=x.dtype, device=x.device)
+    _lib.add_bytes('smmd_wino4x4s2_wgrad', (x.numel() + gy.numel()) * 4)
+    # 9 point products per 2 x 2 output tile and (phase column, co) pair
+    _lib.add_flops('smmd_wino4x4s2_wgrad', 2 * 9 * N * (H // 4) * (W // 4) * 4 * ci * co)
+    with _lib.timed('smmd_wino4x4s2_wgrad'):
+        st = L.smmd_wino4x4s2_wgrad(_lib.ptr(x), _lib.ptr(gy), _lib.ptr(gw), N, ci, co, H, W,
+                                    _lib.ptr(ws), nb, _lib.stream_handle(x.device))
+    _lib.check(st, 'smmd_wino4x4s2_wgrad')
+    return gw
+
+
+def _s2_weight_grad(gy, x, w, stride, padding):
+    """gw of conv(x, w [co, ci, 4, 4], stride 2, pad 1) at gy: the library's
+    polyphase kernel where it tiles the shapes, MIOpen otherwise."""
+    if _s2_wgrad_ok(x, gy, w.shape[0]):
+        return _s2_wgrad(x.contiguous(), gy.contiguous())
+    return _aten.convolution_backward(gy, x, w, None, stride, padding, [1, 1], False,
+                                      [0, 0], 1, [False, True, False])[1]
+
+
 class _ConvT2dS2(torch.autograd.Function):
     """conv_transpose2d(x, w [cin, cout, 4, 4], b, stride 2, padding 1): the
     generator's folded UpsampleConv.  Backward: grad_x = conv(g, w, stride 2)
-    on the forward Winograd kernel, grad_w on MIOpen, grad_b the channel sum
-    (the generator step differentiates it once)."""
+    on the forward Winograd kernel, grad_w on the stride-2 weight-gradient
+    kernel (x and g in swapped roles), grad_b the channel sum (the generator
+    step differentiates it once)."""
 
     @staticmethod
     def forward(ctx, x, w, b):
@@ -414,8 +465,13 @@ class _ConvT2dS2(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             gx = _s2_conv(gy, w, None) if _is_s2(gy, w, 2, 1) else F.conv2d(gy, w, None, 2, 1)
         if ctx.needs_input_grad[1]:
-            _, gw, _ = _aten.convolution_backward(gy, x, w, None, [2, 2], [1, 1], [1, 1], True,
-                                                  [0, 0], 1, [False, True, False])
+            # conv_transpose(x, w) = Dx of conv(., w): its weight gradient is
+            # the stride-2 conv's weight gradient at input gy, upstream x
+            if _s2_wgrad_ok(gy, x.contiguous(), w.shape[0]):
+                gw = _s2_wgrad(gy, x.contiguous())
+            else:
+                _, gw, _ = _aten.convolution_backward(gy, x, w, None, [2, 2], [1, 1], [1, 1], True,
+                                                      [0, 0], 1, [False, True, False])
         if ctx.has_b and ctx.needs_input_grad[2]:
             gb = bias_grad(gy)
         return gx, gw, gb
@@ -466,13 +522,16 @@ def _bwd(gy, x, w, stride, padding, mask):
             _, gw, _ = _aten.convolution_backward(gy, x, w, None, stride, padding, [1, 1], False,
                                                   [0, 0], 1, [False, True, False])
         return gx, gw
-    if mask[0] and _is_s2t(gy, w, stride, padding) and tuple(x.shape[2:]) == (
-            2 * gy.shape[2], 2 * gy.shape[3]):
-        gx = _s2t_conv(gy, w, None)
-        gw = None
+    s2 = (w.dim() == 4 and tuple(w.shape[2:]) == (4, 4) and _s2_shape_ok(x, stride, padding)
+          and tuple(x.shape[2:]) == (2 * gy.shape[2], 2 * gy.shape[3]))
+    if s2 and (mask[1] or _is_s2t(gy, w, stride, padding)):
+        gx = gw = None
+        if mask[0]:
+            gx = (_s2t_conv(gy, w, None) if _is_s2t(gy, w, stride, padding) else
+                  _aten.convolution_backward(gy, x, w, None, stride, padding, [1, 1], False,
+                                             [0, 0], 1, [True, False, False])[0])
         if mask[1]:
-            _, gw, _ = _aten.convolution_backward(gy, x, w, None, stride, padding, [1, 1], False,
-                                                  [0, 0], 1, [False, True, False])
+            gw = _s2_weight_grad(gy, x, w, stride, padding)
         return gx, gw
     gx, gw, _ = _aten.convolution_backward(gy, x, w, None, stride, padding, [1, 1], False,
                                            [0, 0], 1, [mask[0], mask[1], False])

@@ -59,7 +59,8 @@ def test_s2_conv_and_transposed_vs_float64(shape):
         assert _rel(gx, refx) < TOL
 
 
-@pytest.mark.parametrize('shape', [(2, 64, 64, 8, 8), (3, 128, 64, 12, 4)])
+@pytest.mark.parametrize('shape', [(2, 64, 64, 8, 8), (3, 128, 64, 12, 4), (4, 64, 64, 8, 8),
+                                   (2, 32, 64, 32, 32)])
 def test_s2_double_backward_vs_float64(shape):
     """The critic's ConvMeanPool conv through the double backward: conv, Dx,
     Dw and their second-order terms against float64 autograd."""
@@ -104,6 +105,49 @@ def test_conv_transpose_s2_autograd_vs_float64():
         outs.append((y, gx, gw, gb))
     for n, a, r in zip(('y', 'gx', 'gw', 'gb'), *outs):
         assert _rel(a, r) < (2e-5 if n in ('gw', 'gb') else TOL), n
+
+
+# the critic's four folded ConvMeanPool layers (SNResNet-64: 64 -> 128 at 64 x 64
+# ... 512 -> 1024 at 8 x 8) at small batches, other tile grids, and shapes the
+# kernel does not tile (MIOpen then): (x [n, ci, h, w], co)
+S2_WGRAD_SHAPES = [(2, 64, 128, 64, 64), (2, 128, 256, 32, 32), (4, 256, 512, 16, 16),
+                   (4, 512, 1024, 8, 8), (3, 16, 64, 32, 64), (2, 32, 64, 16, 32),
+                   (8, 16, 64, 16, 16), (2, 64, 64, 8, 8), (1, 16, 64, 12, 20)]
+
+
+@pytest.mark.parametrize('shape', S2_WGRAD_SHAPES)
+def test_s2_wgrad_vs_float64(shape):
+    """smmd_wino4x4s2_wgrad (through convops' dispatch) against torch's float64
+    conv2d_weight: sums over N * H/2 * W/2 terms in fp32, bound 1e-5 of
+    max|ref|; deterministic."""
+    from gan.core import _lib, convops
+    N, C, K, H, W = shape
+    g = torch.Generator(device=DEV).manual_seed(N + C + K + H + W)
+    x = torch.randn(N, C, H, W, device=DEV, generator=g)
+    gy = torch.randn(N, K, H // 2, W // 2, device=DEV, generator=g)
+    w = torch.empty(K, C, 4, 4, device=DEV)
+    tiled = convops._s2_wgrad_ok(x, gy, K)
+    assert tiled == bool(_lib.lib().smmd_wino4x4s2_wgrad_supported(N, C, K, H, W))
+    gw = convops._s2_weight_grad(gy, x, w, [2, 2], [1, 1])
+    ref = torch.nn.grad.conv2d_weight(x.double().cpu(), (K, C, 4, 4), gy.double().cpu(),
+                                      stride=2, padding=1)
+    assert _rel(gw, ref) < 1e-5
+    if tiled:
+        assert torch.equal(gw, convops._s2_weight_grad(gy, x, w, [2, 2], [1, 1]))
+
+
+def test_s2_wgrad_routes_to_library():
+    from gan.core import _lib, convops
+    x = torch.randn(2, 64, 32, 32, device=DEV)
+    gy = torch.randn(2, 128, 16, 16, device=DEV)
+    _lib.reset_timing()
+    _lib.enable_timing(True)
+    try:
+        convops._s2_weight_grad(gy, x, torch.empty(128, 64, 4, 4, device=DEV), [2, 2], [1, 1])
+        assert 'smmd_wino4x4s2_wgrad' in _lib.timing_ms()
+    finally:
+        _lib.enable_timing(False)
+        _lib.reset_timing()
 
 
 def test_s2_off_matches_on():
