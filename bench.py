@@ -216,10 +216,25 @@ def cpu_threads():
     """Threads for the CPU baseline: the process's CPU affinity, capped at the
     GPU box's CPU share for one GPU (the harness sets OMP_NUM_THREADS to that
     share, 16, and asks worker pools to stay within it; the box's affinity
-    mask lists the whole host)."""
+    mask lists the whole host, whose other CPUs belong to other jobs)."""
     affinity = len(os.sched_getaffinity(0))
     share = int(os.environ.get('OMP_NUM_THREADS', affinity) or affinity)
     return affinity, max(1, min(affinity, share))
+
+
+def cpu_thread_scan(threads, steps=3):
+    """The mirror's ImageNet step at half the thread count beside the
+    headline's: whether more threads still pay.  The full
+    affinity (256 host CPUs on the GPU box) is outside the job's CPU share and
+    is not timed.  Returns {threads: median step s}."""
+    out = {}
+    for n in sorted({max(1, threads // 2), threads}):
+        torch.set_num_threads(n)
+        tr, imgs = _mirror_trainer(imagenet_config(BATCH), BATCH)
+        times, _ = _time_steps(tr, imgs, steps, warm=1)
+        out[n] = round(_pct(times, .5), 4)
+    torch.set_num_threads(threads)
+    return out
 
 
 def cpu_baseline(steps=24, cifar_steps=24):
@@ -249,6 +264,14 @@ def cpu_baseline(steps=24, cifar_steps=24):
         'value': round(32 / mean, 3), 'unit': 'images/s', 'steps': len(times), 'warmup': 3,
         'schedule': ''.join(kinds), 'step_s': _stats(times)}
     out['components'] = cpu_components()
+    scan = cpu_thread_scan(threads)
+    out['thread_scan_median_step_s'] = scan
+    best = min(scan, key=scan.get)
+    out['thread_scan_note'] = ('median ImageNet mirror step over 3 steps per thread count; the '
+                               'headline uses %d threads (the fastest of the scan is %d); the '
+                               'host affinity of %d CPUs exceeds the job\'s CPU share (%s) and '
+                               'is not used' % (threads, best, affinity,
+                                                os.environ.get('OMP_NUM_THREADS')))
     return out
 
 

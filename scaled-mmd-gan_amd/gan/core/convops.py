@@ -731,6 +731,21 @@ def _fold_launch(srcs, adjoint):
     return tuple(dsts)
 
 
+def _fold_launch_into(srcs, dsts, adjoint):
+    """smmd_fold_pool_weights from ``srcs`` into the existing contiguous
+    ``dsts`` (e.g. gradient views of a flat buffer), ONE launch."""
+    from . import _lib
+    import ctypes
+    n = len(srcs)
+    P = ctypes.c_void_p * n
+    nf = (ctypes.c_int64 * n)(*[t.numel() // (16 if adjoint else 9) for t in srcs])
+    with _lib.timed('smmd_fold_pool_weights'):
+        st = _lib.lib().smmd_fold_pool_weights(P(*[t.data_ptr() for t in srcs]),
+                                               P(*[t.data_ptr() for t in dsts]), nf, n,
+                                               int(adjoint), _lib.stream_handle(srcs[0].device))
+    _lib.check(st, 'smmd_fold_pool_weights')
+
+
 def _fold_torch(w):
     return F.avg_pool2d(F.pad(w, (1, 1, 1, 1)), 2, stride=1)
 

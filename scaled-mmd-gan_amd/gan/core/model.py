@@ -413,6 +413,9 @@ class MMD_GAN:
             return
         # buckets not already issued from the backward's hooks go now; wait all
         self._bucket_for(opt).finish()
+        if getattr(self, '_dpgd', False) and opt is self.d_optim:
+            # the buckets summed G: its stats and dL/ds, then the fused update
+            self.sn_D.dp_gdirect_finish()
         if self.dp_mode == 'tower':
             # per-tower clip done per bucket; the tower mean (model.py:257-258)
             opt.step(grad_scale=1.0 / self.world, clip=False)
@@ -434,8 +437,11 @@ class MMD_GAN:
         if ref:       # the generator's gradient set, computed and discarded
             torch.autograd.grad(g_loss, self.g_vars, retain_graph=True)
         gd = self._gdirect()
-        self.sn_D.arm_gdirect(gd)
+        dpgd = gd and self.world > 1
+        self.sn_D.arm_gdirect(gd and not dpgd)
         self.sn_D.arm_direct(self.world > 1)        # the grouped SN nodes' direct writes
+        self.sn_D.arm_dp_gdirect(dpgd)
+        self._dpgd = dpgd
         try:
             if ref:
                 d_loss.backward(inputs=self.d_vars)
@@ -447,18 +453,28 @@ class MMD_GAN:
         finally:
             self.sn_D.arm_gdirect(False)
             self.sn_D.arm_direct(False)
+            self.sn_D.arm_dp_gdirect(False)
         self._exchange(self.d_optim)
+        self._dpgd = False
         return self._detach_step_state()
 
     def _gdirect(self):
         """The critic's SN weight gradients go straight from G into the
-        fused update (sn._SNBatch._backward_gdirect, smmd_adam_flat_sn2):
-        one process, an SN-fused optimizer, SMMD_SN_GDIRECT not 0.  With
-        several ranks the flat gradient is what the buckets all-reduce, so
-        dL/dW is formed as before."""
+        fused update (smmd_adam_flat_sn2 forms dL/dW from G): an SN-fused
+        optimizer, SMMD_SN_GDIRECT not 0; one process (sn._SNBatch.
+        _backward_gdirect), or several ranks in global mode with the grouped SN
+        nodes (the buckets all-reduce G itself: sn.arm_dp_gdirect).  Tower mode
+        clips each rank's dL/dW before the mean, so there dL/dW is formed per
+        rank (smmd_sn_weight_bwd) as before."""
         import os
-        return (self.world == 1 and self.d_optim._sn is not None and bool(self.sn_D.entries)
-                and os.environ.get('SMMD_SN_GDIRECT', '1') != '0')
+        if not (self.d_optim._sn is not None and bool(self.sn_D.entries)
+                and os.environ.get('SMMD_SN_GDIRECT', '1') != '0'):
+            return False
+        if self.world == 1:
+            return True
+        return (self.dp_mode == 'global' and self.sn_D.groups is not None
+                and self.sn_D._direct is not None
+                and os.environ.get('SMMD_SN_DP_GDIRECT', '1') != '0')
 
     def _detach_step_state(self):
         """After a step's backward: keep the reference attributes (self.g_loss,

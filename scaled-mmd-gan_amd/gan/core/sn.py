@@ -266,6 +266,11 @@ class SpectralNormBank:
         self.groups = None
         self._direct = None
         self._direct_armed = False
+        # data parallel G-direct (global mode): while armed, a group's backward
+        # writes G (the adjoint fold of G' for ConvMeanPool layers) into the
+        # SN weights' .grad views instead of dL/dW, the buckets sum G over the
+        # ranks, and dp_gdirect_finish runs the stats on the sum
+        self._dpgd_armed = False
         self._fresh = None
         self._folds = None
         self._alloc_ws()
@@ -352,9 +357,78 @@ class SpectralNormBank:
         """Arm the direct-write group backward for the next backward pass."""
         self._direct_armed = bool(on) and self._direct is not None
 
+    def arm_dp_gdirect(self, on=True):
+        """Arm the data-parallel G-direct backward (with arm_direct) for the
+        next backward pass.  dL/dW = (s/sigma) G - (s <G, W> / sigma^2) u' v^T is
+        linear in G given the replicated W, u', v, sigma and s, so the sum over
+        ranks of dL/dW is that of the summed G: the buckets all-reduce G and
+        the fused update forms dL/dW once (smmd_adam_flat_sn2)."""
+        self._dpgd_armed = bool(on) and self._direct is not None
+
+    def _group_write_g(self, members, Ws, ss, grads):
+        """The data-parallel G-direct group backward: G into each SN weight's
+        .grad view (fold layers: the adjoint fold of G', one launch for the
+        group), the scale's .grad left zero (dp_gdirect_finish writes dL/ds
+        from the summed G)."""
+        folds_src, folds_dst = [], []
+        for j, i in enumerate(members):
+            e, W, G = self.entries[i], Ws[j], grads[j]
+            gW = e.weight.grad
+            if G is None:
+                gW.zero_()
+                continue
+            if self._folds[i]:
+                folds_src.append(G.contiguous())
+                folds_dst.append(gW)
+            else:
+                gW.copy_(G.reshape(gW.shape))
+        if folds_src:
+            from .convops import _fold_launch_into
+            _fold_launch_into(folds_src, folds_dst, adjoint=True)
+        self._direct(members)
+        return (None,) * (2 * len(members))
+
+    def _grad_stats(self, Ws, ss, Gs, folds):
+        """smmd_sn_grad_stats over every layer: the record {coef, ||dL/dW||^2,
+        sigma, s} the G-direct update reads, and dL/ds written into each
+        learnable scale's .grad."""
+        n = len(self.entries)
+        arr = (_lib.SnLayer * n)()
+        for i, (e, W, s, G) in enumerate(zip(self.entries, Ws, ss, Gs)):
+            L = arr[i]
+            L.W = W.data_ptr()
+            L.u = e.u.data_ptr()
+            L.v = e.v.data_ptr()
+            L.sigma = e.sigma.data_ptr()
+            has_s = s is not None and s.numel() > 0
+            L.s = s.data_ptr() if has_s else None
+            sg = e.scale.grad if has_s else None
+            L.gs = sg.data_ptr() if sg is not None else None
+            L.G = G.data_ptr()
+            L.N, L.K = e.N, e.K
+            L.fold = 1 if folds[i] else 0
+        args = (arr, n, _lib.ptr(self.ws), self.ws.numel(), _lib.stream_handle(Ws[0].device))
+        with _lib.timed('smmd_sn_grad_stats'):
+            st = _lib.lib().smmd_sn_grad_stats(*args)
+        _lib.check(st, 'smmd_sn_grad_stats')
+
+    def dp_gdirect_finish(self):
+        """After the buckets' all-reduce (global mode): the stats of the summed
+        G (in the SN weights' .grad views) and dL/ds, then G pending for the
+        fused update, which forms dL/dW, clips it with the analytic norm and
+        applies Adam."""
+        Ws = [e.weight for e in self.entries]
+        ss = [e.scale if e.scale is not None else None for e in self.entries]
+        Gs = [e.weight.grad for e in self.entries]
+        folds = [False] * len(self.entries)
+        self._grad_stats(Ws, ss, Gs, folds)
+        self._gd_pending = (Gs, folds)
+
     def _group_backward(self, members, Ws, ss, grads):
         """smmd_sn_weight_bwd for the group's layers (the full layer array with
         the others' G NULL: the workspace is carved by the whole array)."""
+        if self._direct_armed and self._dpgd_armed:
+            return self._group_write_g(members, Ws, ss, grads)
         n = len(self.entries)
         arr = (_lib.SnLayer * n)()
         direct = self._direct_armed

@@ -178,6 +178,50 @@ class FakeLib:
                 _arr(L.gs, 1)[0] = gs
         return 0
 
+    # G-direct: smmd_sn_grad_stats keeps the layer's dL/dW (the "record") per
+    # workspace for the fused update, and writes dL/ds
+    _gd = {}
+
+    def smmd_sn_grad_stats(self, arr, n, ws, wsb, stream):
+        key = ws.value if isinstance(ws, ctypes.c_void_p) else int(ws or 0)
+        for i in range(n):
+            L = arr[i]
+            assert not L.fold, 'fake_lib: fold layers are GPU-only'
+            N, K, W, s = self._layer(L)
+            G = _arr(L.G, N * K).reshape(N, K).astype(np.float64)
+            sigma = float(_arr(L.sigma, 1)[0])
+            gW, gs = O.sn_weight_backward(W, s, sigma, self._ucur[(key, i)],
+                                          _arr(L.v, K).astype(np.float64), G)
+            self._gd[(key, i)] = gW.ravel()
+            if L.gs:
+                _arr(L.gs, 1)[0] = gs
+        return 0
+
+    def smmd_adam_flat_sn2(self, param, grad, m, v, offs, n, gscale, clip, lr, b1, b2, eps, step,
+                           lr_dev, ws, wsb, layers, idx, nl, snws, snwsb, flags, stream):
+        """The fused update: with SMMD_ADAM_SN_GDIRECT the SN weights' gradient
+        is the dL/dW smmd_sn_grad_stats formed from G; the P1 pass is not
+        modelled (the fake refresh ignores SN_P1_READY)."""
+        key = snws.value if isinstance(snws, ctypes.c_void_p) else int(snws or 0)
+        tot = offs[n]
+        P, G, M, V = (_arr(x, tot) for x in (param, grad, m, v))
+        sn_of = {int(idx[k]): k for k in range(nl)} if flags & 1 else {}
+        for i, (a, b) in enumerate(self._tensors(offs, n)):
+            if b == a:
+                continue
+            g = G[a:b].astype(np.float64)
+            if i in sn_of:                # dL/dW of the record (offsets are padded)
+                d = self._gd[(key, sn_of[i])]
+                g = np.zeros(b - a)
+                g[:d.size] = d
+            g = g * gscale
+            if clip > 0:
+                g = O.clip_by_norm(g, clip)
+            p, mm, vv = O.adam_step(P[a:b].astype(np.float64), M[a:b].astype(np.float64),
+                                    V[a:b].astype(np.float64), g, step, lr, b1, b2, eps)
+            P[a:b], M[a:b], V[a:b] = p, mm, vv
+        return 0
+
     def smmd_opt_workspace_bytes(self, offs, n):
         return 256
 

@@ -431,3 +431,72 @@ def test_sn_buckets_issued_inside_backward(mode, world, monkeypatch):
         assert nb >= 3 and issued == nb and order == list(range(nb)) and n_ar == nb
         assert len(fired) >= 2                   # several SN groups, each from the backward
         np.testing.assert_allclose(flat, np.concatenate(expect), rtol=2e-5, atol=1e-7)
+
+
+def _worker_sn_dp_gdirect(rank, world, port, mode, q):
+    """Global mode with the data-parallel G-direct backward: the SN groups
+    write G into the flat gradient, the buckets sum it, the stats of the sum
+    and the fused update form dL/dW once."""
+    _init(rank, world, port)
+    from gan.core.collectives import GradBuckets
+    from gan.core.model import MMD_GAN
+    net, bank, opt = _sn_setup()
+    assert opt.attach_sn(bank)
+    m = MMD_GAN.__new__(MMD_GAN)
+    m.world, m.group, m.dp_mode = world, dist.group.WORLD, 'global'
+    m.d_optim, m.sn_D = opt, bank
+    m._buckets = {id(opt): GradBuckets(opt, m.group, bucket_bytes=64, clip_norm=0.0)}
+    m._group_sn(bank, opt)
+    assert bank.groups is not None and len(bank.groups) >= 2
+    opt.zero_grad()
+    m._arm(opt)
+    loss = _sn_loss(net, bank, rank)
+    bank.arm_direct(True)
+    bank.arm_dp_gdirect(True)
+    m._dpgd = True
+    cnt = _Count()
+    loss.backward()
+    bank.arm_direct(False)
+    bank.arm_dp_gdirect(False)
+    bk = m._buckets[id(opt)]
+    issued = len(bk.launch_log)
+    # what the buckets carried for the SN weights: G, not dL/dW
+    m._exchange(opt)
+    q.put((rank, np.concatenate([p.detach().numpy().ravel() for p in net.parameters()]),
+           issued, len(bk.buckets), cnt.n['all_reduce']))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world', [2, 4, 8])
+def test_sn_dp_gdirect_matches_dense_exchange(world, monkeypatch):
+    """with several ranks in global mode the buckets
+    all-reduce G (the gradient of the effective weight) instead of dL/dW, and
+    the update forms dL/dW = (s/sigma)(sum G) - (s <sum G, W>/sigma^2) u' v^T
+    once: the updated parameters equal the reference exchange (sum of the
+    ranks' dL/dW, clip_by_norm, Adam; model.py:233-266, :444-456) on the
+    per-rank gradients of the single-node SN backward."""
+    import fake_lib
+    from gan.core import _lib
+    f = fake_lib.FakeLib()
+    monkeypatch.setattr(_lib, '_lib', f)
+    monkeypatch.setattr(_lib, 'lib', lambda: f)
+    monkeypatch.setattr(_lib, 'require_cuda', lambda *t: None)
+    monkeypatch.setattr(_lib, 'stream_handle', lambda device=None: None)
+    monkeypatch.setattr(_lib, 'workspace', lambda tag, nbytes, device: torch.zeros(
+        max(int(nbytes), 256), dtype=torch.uint8))
+    grads, params = [], None
+    for r in range(world):
+        net, bank, opt = _sn_setup()
+        opt.zero_grad()
+        _sn_loss(net, bank, r).backward()
+        grads.append([p.grad.detach().numpy().astype(np.float64).ravel().copy()
+                      for p in net.parameters()])
+        params = [p.detach().numpy().astype(np.float64).ravel().copy()
+                  for p in net.parameters()]
+    expect = [O.adam_step(params[i], 0, 0, O.clip_by_norm(sum(g[i] for g in grads), 1.0),
+                          1, 1e-3)[0] for i in range(len(params))]
+    res = _run(_worker_sn_dp_gdirect, 'global', world=world)
+    for rank, flat, issued, nb, n_ar in res:
+        assert issued == nb and n_ar == nb          # every bucket from inside the backward
+        np.testing.assert_allclose(flat, np.concatenate(expect), rtol=2e-5, atol=1e-7)

@@ -6,6 +6,7 @@ every counter over its dispatches, plus the derived MFMA busy fraction
 import collections
 import csv
 import glob
+import gzip
 import os
 import sys
 
@@ -14,9 +15,10 @@ def main():
     dirs, sub = sys.argv[1:-1], sys.argv[-1]
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
     for d in dirs:
-        for path in glob.glob(os.path.join(d, '**', '*counter_collection.csv'), recursive=True):
+        for path in glob.glob(os.path.join(d, '**', '*counter_collection.csv*'), recursive=True):
             disp = collections.defaultdict(dict)
-            for r in csv.DictReader(open(path)):
+            fh = gzip.open(path, 'rt') if path.endswith('.gz') else open(path)
+            for r in csv.DictReader(fh):
                 if sub not in r['Kernel_Name']:
                     continue
                 key = (r['Kernel_Name'].replace('(anonymous namespace)::', '').split('(')[0],
