@@ -65,7 +65,9 @@ int smmd_abi_version(void);         /* bumped on any ABI change (2: Gram/poly,
                                        smmd_source_hash, smmd_sn_grad_stats,
                                        smmd_adam_flat_sn2, smmd_bn_relu_fwd_save / _bwd,
                                        8: smmd_wino3x3_*, smmd_wino4x4s2*,
-                                       smmd_wino3x3_wgrad*, 9: smmd_wino4x4s2_wgrad*) */
+                                       smmd_wino3x3_wgrad*, 9: smmd_wino4x4s2_wgrad*,
+                                       smmd_wino3x3_filter_sn, smmd_wino4x4s2(t)_filter_sn,
+                                       smmd_sn_clip_g) */
 const char *smmd_source_hash(void); /* first 16 hex digits of the SHA-256 of the
                                        sources this binary was built from
                                        (csrc .hip and .hpp files in byte order,
@@ -286,9 +288,19 @@ smmd_status smmd_sn_weight_bwd(const smmd_sn_layer *layers, int n_layers,
  * layer in ws the record {coef = s d / sigma^2, ||dL/dW||^2 (analytic:
  * (s/sigma)^2 ||G||^2 - 2 (s/sigma) coef u'^T G v + coef^2 ||u'||^2 ||v||^2),
  * sigma, s} that smmd_adam_flat_sn2 with SMMD_ADAM_SN_GDIRECT reads.  G must
- * stay alive (unchanged) until that update has run. */
+ * stay alive (unchanged) until that update has run.  A layer whose G is NULL
+ * is skipped (its record untouched): one gradient bucket's layers. */
 smmd_status smmd_sn_grad_stats(const smmd_sn_layer *layers, int n_layers,
                                void *ws, size_t ws_bytes, smmd_stream_t stream);
+
+/* The per-rank clip of the data-parallel G-direct tower mode: for each layer
+ * with G (non-fold: G has W's shape) G *= clip / max(||dL/dW||, clip), the
+ * norm from its smmd_sn_grad_stats record (dL/dW is linear in G: this is
+ * tf.clip_by_norm of the rank's dL/dW, gan/core/model.py:449-455), and
+ * gs *= clip / max(|gs|, clip) (the scale's own clip).  Layers with G NULL
+ * are skipped (smmd_sn_grad_stats skips them too). */
+smmd_status smmd_sn_clip_g(const smmd_sn_layer *layers, int n_layers, float clip, void *ws,
+                           size_t ws_bytes, smmd_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * Materialised kernel matrix K(A, B) [na, nb] (row-major) and its backward
@@ -647,6 +659,29 @@ smmd_status smmd_wino4x4s2t_conv(const float *gy, const float *u, const float *b
                                  smmd_stream_t stream);
 
 /* ---------------------------------------------------------------------------
+ * Filter transforms straight from a spectrally normalised layer's raw weight
+ * W and its device scalars sigma (smmd_sn_power_iter's output) and s (NULL:
+ * 1): the filter is W_eff = (W / sigma) * s (sn.py:43, snops.py:84), and with
+ * fold = 1 the ConvMeanPool fold of it from the raw 3 x 3 W [ko, ci, 3, 3]
+ * (block.py:63-66), computed with the refresh's own arithmetic (no
+ * contraction), so u is bit-identical to smmd_wino3x3_filter /
+ * smmd_wino4x4s2(t)_filter of the W_eff the refresh would have written --
+ * which it then need not write (smmd_sn_layer.W_eff = NULL).  Layouts, modes
+ * and requirements as the plain transforms; fold = 0 takes W [.., .., 4, 4].
+ * ------------------------------------------------------------------------- */
+smmd_status smmd_wino3x3_filter_sn(const float *w, const float *sigma, const float *s, int ko,
+                                   int ci, int mode, float *u, size_t u_bytes,
+                                   smmd_stream_t stream);
+
+smmd_status smmd_wino4x4s2_filter_sn(const float *w, const float *sigma, const float *s, int fold,
+                                     int ko, int ci, float *u, size_t u_bytes,
+                                     smmd_stream_t stream);
+
+smmd_status smmd_wino4x4s2t_filter_sn(const float *w, const float *sigma, const float *s,
+                                      int fold, int k, int c, float *u, size_t u_bytes,
+                                      smmd_stream_t stream);
+
+/* ---------------------------------------------------------------------------
  * The weight gradient of the 3x3 stride-1 SAME conv (TF's
  * Conv2DBackpropFilter of snops.conv2d / resnet Conv2D, gan/core/snops.py:69-90,
  * the wide layers of gan/core/resnet/block.py:38-50) as Winograd F(2x2, 3x3):
@@ -658,6 +693,7 @@ smmd_status smmd_wino4x4s2t_conv(const float *gy, const float *u, const float *b
  * Deterministic.
  * ------------------------------------------------------------------------- */
 int smmd_wino3x3_wgrad_supported(int n, int ci, int co, int h, int w_img);
+
 
 size_t smmd_wino3x3_wgrad_workspace_bytes(int n, int ci, int co, int h, int w_img);
 

@@ -594,6 +594,7 @@ __global__ __launch_bounds__(256) void sn_bwd_b_kernel(SnTable t) {
 __global__ __launch_bounds__(256) void sn_gstat_a_kernel(SnTable t) {
     const int unit = blockIdx.x;
     const SnLayerDev L = t.L[find_unit_layer(t, unit)];
+    if (!L.G) return;                            // this call skips the layer
     const int lt = unit - L.unit_begin;
     __shared__ float red[4];
     float ad = 0.f, ag = 0.f, au = 0.f;
@@ -670,6 +671,7 @@ __global__ __launch_bounds__(256) void sn_gstat_a_kernel(SnTable t) {
 // record {coef, ||dL/dW||^2, sigma, s} and gs
 __global__ __launch_bounds__(256) void sn_gstat_r_kernel(SnTable t) {
     const SnLayerDev L = t.L[blockIdx.x];
+    if (!L.G) return;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int units = layer_units(L);
     double dd = 0.0, gg = 0.0, ug = 0.0;
@@ -905,11 +907,65 @@ smmd_status smmd_sn_power_iter_ex(const smmd_sn_layer *layers, int n_layers, int
     return SMMD_OK;
 }
 
+// The per-rank clip of the G-direct data-parallel tower mode
+// (smmd_sn_clip_g): G *= c / max(||dL/dW||, c) with the norm of the layer's
+// smmd_sn_grad_stats record (dL/dW is linear in G, so this is clip_by_norm of
+// the rank's dL/dW, model.py:449-455) and gs *= c / max(|gs|, c).
+// Grid (element blocks, layer); float4 over the layer's contiguous G.
+__global__ __launch_bounds__(256) void sn_clip_g_kernel(SnTable t, float clip) {
+    const SnLayerDev L = t.L[blockIdx.y];
+    if (!L.G) return;
+    const float ss = L.stats[1];
+    const float inv = (ss > 0.f) ? rsqrtf(ss) : INFINITY;
+    const float f = clip * fminf(inv, 1.f / clip);
+    float *G = const_cast<float *>(L.G);
+    const int64_t n = (int64_t)L.N * L.K;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (L.vec) {
+        float4 *G4 = reinterpret_cast<float4 *>(G);
+        for (; i < n / 4; i += stride) {
+            float4 v = G4[i];
+            v.x *= f; v.y *= f; v.z *= f; v.w *= f;
+            G4[i] = v;
+        }
+    } else {
+        for (; i < n; i += stride) G[i] *= f;
+    }
+    if (L.gs && blockIdx.x == 0 && threadIdx.x == 0) {
+        const float g = L.gs[0], a = fabsf(g);
+        L.gs[0] = g * (clip * fminf(a > 0.f ? 1.f / a : INFINITY, 1.f / clip));
+    }
+}
+
+smmd_status smmd_sn_clip_g(const smmd_sn_layer *layers, int n_layers, float clip, void *ws,
+                           size_t ws_bytes, smmd_stream_t stream) {
+    if (!layers || n_layers < 1 || n_layers > SMMD_SN_MAX_LAYERS || !(clip > 0.f))
+        return SMMD_EINVAL;
+    for (int i = 0; i < n_layers; ++i)
+        if (layers[i].G && layers[i].fold) return SMMD_EINVAL;    // W-shaped G only
+    if (!ws || ws_bytes < smmd_sn_workspace_bytes(layers, n_layers)) return SMMD_EWORKSPACE;
+    hipStream_t s = (hipStream_t)stream;
+    for (int first = 0; first < n_layers; first += SN_CHUNK) {
+        const int count = (n_layers - first < SN_CHUNK) ? n_layers - first : SN_CHUNK;
+        SnTable t;
+        if (!build_table(layers, first, count, (char *)ws + 256, t)) return SMMD_EINVAL;
+        hipLaunchKernelGGL(sn_clip_g_kernel, dim3(64, t.n_layers), dim3(256), 0, s, t, clip);
+        smmd_status st = last_launch_status();
+        if (st != SMMD_OK) return st;
+    }
+    return SMMD_OK;
+}
+
 smmd_status smmd_sn_grad_stats(const smmd_sn_layer *layers, int n_layers, void *ws,
                                size_t ws_bytes, smmd_stream_t stream) {
     if (!layers || n_layers < 1 || n_layers > SMMD_SN_MAX_LAYERS) return SMMD_EINVAL;
-    for (int i = 0; i < n_layers; ++i)
-        if (!layers[i].G || !layers[i].v || !layers[i].sigma) return SMMD_EINVAL;
+    int any = 0;
+    for (int i = 0; i < n_layers; ++i) {
+        if (!layers[i].v || !layers[i].sigma) return SMMD_EINVAL;
+        any |= layers[i].G != nullptr;       // a layer with G NULL is skipped
+    }
+    if (!any) return SMMD_EINVAL;
     if (!ws || ws_bytes < smmd_sn_workspace_bytes(layers, n_layers)) return SMMD_EWORKSPACE;
     hipStream_t s = (hipStream_t)stream;
     for (int first = 0; first < n_layers; first += SN_CHUNK) {

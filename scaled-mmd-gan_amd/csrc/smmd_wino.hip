@@ -58,11 +58,20 @@ __device__ __forceinline__ float wn_from_right(float v) {  // lane l gets lane l
 // chunk of 8): a thread owns one ko and four consecutive ci, so each point's
 // four values are one float4 store and consecutive lanes (consecutive ko)
 // store consecutive 16 bytes
+//
+// sig != NULL (smmd_wino3x3_filter_sn): w is the raw weight W of a spectrally
+// normalised layer and the filter is W_eff = (W / sigma) * s, formed here with
+// the SN refresh's own arithmetic (sn.py:43, snops.py:84; smmd_sn.hip P3, no
+// contraction), so U is bit-identical to the transform of a stored W_eff and
+// the refresh need not write W_eff at all.
 __global__ void wino_filter_kernel(const float *__restrict__ w, int KO, int CI, int mode,
-                                   float *__restrict__ u) {
+                                   float *__restrict__ u, const float *__restrict__ sig,
+                                   const float *__restrict__ sc) {
+#pragma clang fp contract(off)
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= (int64_t)KO * (CI >> 2)) return;
     const int ko = (int)(idx % KO), q = (int)(idx / KO);
+    const float sigma = sig ? sig[0] : 1.f, scale = sc ? sc[0] : 1.f;
     float r[16][4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -80,6 +89,12 @@ __global__ void wino_filter_kernel(const float *__restrict__ w, int KO, int CI, 
             for (int i = 0; i < 3; ++i)
 #pragma unroll
                 for (int j = 0; j < 3; ++j) g[i][j] = s[(2 - i) * 3 + (2 - j)];
+        }
+        if (sig) {
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) g[i][j] = (g[i][j] / sigma) * scale;
         }
         float t[4][3];
 #pragma unroll
@@ -485,7 +500,22 @@ extern "C" smmd_status smmd_wino3x3_filter(const float *w, int ko, int ci, int m
     if (u_bytes < smmd_wino3x3_filter_bytes(ko, ci)) return SMMD_EWORKSPACE;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const int64_t n = (int64_t)ko * (ci / 4);
-    wino_filter_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st>>>(w, ko, ci, mode, u);
+    wino_filter_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st>>>(w, ko, ci, mode, u,
+                                                                               nullptr, nullptr);
+    return last_launch_status();
+}
+
+extern "C" smmd_status smmd_wino3x3_filter_sn(const float *w, const float *sigma, const float *s,
+                                              int ko, int ci, int mode, float *u, size_t u_bytes,
+                                              smmd_stream_t stream) {
+    if (ko <= 0 || ci <= 0 || (mode != 0 && mode != 1) || !w || !u || !sigma) return SMMD_EINVAL;
+    if (ko % WN_KB || ci % WN_CC) return SMMD_EUNSUPPORTED;
+    if (reinterpret_cast<uintptr_t>(u) & 15) return SMMD_EINVAL;
+    if (u_bytes < smmd_wino3x3_filter_bytes(ko, ci)) return SMMD_EWORKSPACE;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const int64_t n = (int64_t)ko * (ci / 4);
+    wino_filter_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st>>>(w, ko, ci, mode, u,
+                                                                               sigma, s);
     return last_launch_status();
 }
 

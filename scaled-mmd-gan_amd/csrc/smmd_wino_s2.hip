@@ -44,17 +44,60 @@ __device__ __forceinline__ float s2_from_right(float v) {
                                                                  0x130, 0xf, 0xf, false));
 }
 
+// The 16 taps of filter q of W': with sig NULL read from w [q][16]; else w is
+// the raw weight of a spectrally normalised layer and the taps are those of
+// W_eff = (W / sigma) * s (sn.py:43, snops.py:84), pool-folded from the raw
+// 3 x 3 filter w [q][9] when fold (ConvMeanPool, block.py:63-66):
+// W'[a][b] = 1/4 sum_{i,j in 0..1} W_eff[a-i][b-j] -- the SN refresh's P3
+// arithmetic (smmd_sn.hip snf_p3, no contraction), so U is bit-identical to
+// the transform of the W_eff / W' that P3 would have written.
+__device__ __forceinline__ void s2_taps(const float *__restrict__ w, int64_t q, int fold,
+                                        const float *__restrict__ sig,
+                                        const float *__restrict__ sc, float (&f)[16]) {
+#pragma clang fp contract(off)
+    if (!sig) {
+        const float *s = w + q * 16;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) f[i] = s[i];
+        return;
+    }
+    const float sigma = sig[0], scale = sc ? sc[0] : 1.f;
+    if (!fold) {
+        const float *s = w + q * 16;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) f[i] = (s[i] / sigma) * scale;
+        return;
+    }
+    const float *s = w + q * 9;
+    float k[9];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) k[j] = (s[j] / sigma) * scale;
+#pragma unroll
+    for (int si = 0; si < 4; ++si)
+#pragma unroll
+        for (int ti = 0; ti < 4; ++ti) {
+            float acc = 0.f;
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b) {
+                    const int uu = si - a, vv = ti - b;
+                    if (uu >= 0 && uu < 3 && vv >= 0 && vv < 3) acc += k[uu * 3 + vv];
+                }
+            f[si * 4 + ti] = acc * 0.25f;
+        }
+}
+
 // U for (ko, ci): 4 phases x 9 points, stored u[kb][chunk][p9][h2][k64][c4]
 // with phase channel pc = 4 (ci & 1) + 2 pi + pj = 4 h + c4
 __global__ void s2_filter_kernel(const float *__restrict__ w, int KO, int CI,
-                                 float *__restrict__ u) {
+                                 float *__restrict__ u, const float *__restrict__ sig,
+                                 const float *__restrict__ sc, int fold) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= (int64_t)KO * CI) return;
     const int ko = (int)(idx % KO), ci = (int)(idx / KO);
-    const float *s = w + ((int64_t)ko * CI + ci) * 16;
     float f[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) f[i] = s[i];
+    s2_taps(w, (int64_t)ko * CI + ci, fold, sig, sc, f);
     const int kb = ko >> 6, kl = ko & 63, cc = ci >> 1, h = ci & 1;
     const int64_t base = ((int64_t)kb * (CI >> 1) + cc) * 9;
     float r[9][4];                    // [point][phase 2 pi + pj]
@@ -253,7 +296,8 @@ __global__ __launch_bounds__(S2_T, 2) void s2_conv_kernel(
 // a thread owns one c and four consecutive k, so each (phase, point) is one
 // float4 store and consecutive lanes (consecutive c) store consecutive 16 bytes
 __global__ void s2t_filter_kernel(const float *__restrict__ w, int K, int C,
-                                  float *__restrict__ u) {
+                                  float *__restrict__ u, const float *__restrict__ sig,
+                                  const float *__restrict__ sc, int fold) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= (int64_t)(K >> 2) * C) return;
     const int c = (int)(idx % C), kq = (int)(idx / C);
@@ -261,11 +305,7 @@ __global__ void s2t_filter_kernel(const float *__restrict__ w, int K, int C,
     const int64_t per_phase = (int64_t)C * K * 9;
     float f[4][16];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        const float *s = w + ((int64_t)(4 * kq + e) * C + c) * 16;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) f[e][i] = s[i];
-    }
+    for (int e = 0; e < 4; ++e) s2_taps(w, (int64_t)(4 * kq + e) * C + c, fold, sig, sc, f[e]);
     float4 *u4 = reinterpret_cast<float4 *>(u);
 #pragma unroll
     for (int qi = 0; qi < 2; ++qi)
@@ -516,7 +556,22 @@ extern "C" smmd_status smmd_wino4x4s2_filter(const float *w, int ko, int ci, flo
     if (u_bytes < smmd_wino4x4s2_filter_bytes(ko, ci)) return SMMD_EWORKSPACE;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const int64_t n = (int64_t)ko * ci;
-    s2_filter_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st>>>(w, ko, ci, u);
+    s2_filter_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st>>>(w, ko, ci, u,
+                                                                             nullptr, nullptr, 0);
+    return last_launch_status();
+}
+
+extern "C" smmd_status smmd_wino4x4s2_filter_sn(const float *w, const float *sigma,
+                                                const float *s, int fold, int ko, int ci,
+                                                float *u, size_t u_bytes, smmd_stream_t stream) {
+    if (ko <= 0 || ci <= 0 || !w || !u || !sigma || (fold != 0 && fold != 1)) return SMMD_EINVAL;
+    if (ko % S2_KB || ci % S2_CC) return SMMD_EUNSUPPORTED;
+    if (reinterpret_cast<uintptr_t>(u) & 15) return SMMD_EINVAL;
+    if (u_bytes < smmd_wino4x4s2_filter_bytes(ko, ci)) return SMMD_EWORKSPACE;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const int64_t n = (int64_t)ko * ci;
+    s2_filter_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st>>>(w, ko, ci, u,
+                                                                             sigma, s, fold);
     return last_launch_status();
 }
 
@@ -594,7 +649,22 @@ extern "C" smmd_status smmd_wino4x4s2t_filter(const float *w, int k, int c, floa
     if (u_bytes < smmd_wino4x4s2_filter_bytes(k, c)) return SMMD_EWORKSPACE;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const int64_t n = (int64_t)(k / 4) * c;
-    s2t_filter_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st>>>(w, k, c, u);
+    s2t_filter_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st>>>(w, k, c, u,
+                                                                              nullptr, nullptr, 0);
+    return last_launch_status();
+}
+
+extern "C" smmd_status smmd_wino4x4s2t_filter_sn(const float *w, const float *sigma,
+                                                 const float *s, int fold, int k, int c,
+                                                 float *u, size_t u_bytes, smmd_stream_t stream) {
+    if (k <= 0 || c <= 0 || !w || !u || !sigma || (fold != 0 && fold != 1)) return SMMD_EINVAL;
+    if (k % 8 || c % 64) return SMMD_EUNSUPPORTED;
+    if (reinterpret_cast<uintptr_t>(u) & 15) return SMMD_EINVAL;
+    if (u_bytes < smmd_wino4x4s2_filter_bytes(k, c)) return SMMD_EWORKSPACE;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const int64_t n = (int64_t)(k / 4) * c;
+    s2t_filter_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st>>>(w, k, c, u,
+                                                                              sigma, s, fold);
     return last_launch_status();
 }
 

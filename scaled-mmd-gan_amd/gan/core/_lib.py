@@ -114,6 +114,7 @@ _SIGS = {
     'smmd_sn_power_iter_ex': (_I, [ctypes.POINTER(SnLayer), _I, _I, _F, _I, _I, _P, _SZ, _P]),
     'smmd_sn_weight_bwd': (_I, [ctypes.POINTER(SnLayer), _I, _P, _SZ, _P]),
     'smmd_sn_grad_stats': (_I, [ctypes.POINTER(SnLayer), _I, _P, _SZ, _P]),
+    'smmd_sn_clip_g': (_I, [ctypes.POINTER(SnLayer), _I, _F, _P, _SZ, _P]),
     'smmd_adam_flat_sn2': (_I, [_P, _P, _P, _P, ctypes.POINTER(ctypes.c_int64), _I, _F, _F, _F,
                                 _F, _F, _F, _I64, _P, _P, _SZ, ctypes.POINTER(SnLayer),
                                 ctypes.POINTER(ctypes.c_int32), _I, _P, _SZ, _I, _P]),
@@ -164,6 +165,9 @@ _SIGS = {
     'smmd_wino3x3_wgrad_supported': (_I, [_I, _I, _I, _I, _I]),
     'smmd_wino3x3_wgrad_workspace_bytes': (_SZ, [_I, _I, _I, _I, _I]),
     'smmd_wino3x3_wgrad': (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P, _SZ, _P]),
+    'smmd_wino3x3_filter_sn': (_I, [_P, _P, _P, _I, _I, _I, _P, _SZ, _P]),
+    'smmd_wino4x4s2_filter_sn': (_I, [_P, _P, _P, _I, _I, _I, _P, _SZ, _P]),
+    'smmd_wino4x4s2t_filter_sn': (_I, [_P, _P, _P, _I, _I, _I, _P, _SZ, _P]),
     'smmd_wino4x4s2_wgrad_supported': (_I, [_I, _I, _I, _I, _I]),
     'smmd_wino4x4s2_wgrad_workspace_bytes': (_SZ, [_I, _I, _I, _I, _I]),
     'smmd_wino4x4s2_wgrad': (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P, _SZ, _P]),

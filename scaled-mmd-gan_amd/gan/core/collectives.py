@@ -160,6 +160,9 @@ class GradBuckets:
         self._hooks = [p.register_post_accumulate_grad_hook(self._hook(i))
                        for i, p in enumerate(opt.params)]
         self.launch_log = []      # bucket ids in issue order of the last step (tests)
+        # tensors the bucket clip leaves alone (their owner clipped them: the
+        # SN weights and scales under the tower-mode G-direct backward)
+        self.clip_exclude = frozenset()
 
     def arm(self):
         """Call before the backward whose gradients this step exchanges."""
@@ -188,7 +191,16 @@ class GradBuckets:
         self.next = b + 1
         self.launch_log.append(b)
         if self.clip_norm > 0:
-            self.opt.clip_range_(lo, hi, self.clip_norm)
+            i = lo
+            while i < hi:                 # runs of tensors not excluded
+                if i in self.clip_exclude:
+                    i += 1
+                    continue
+                j = i
+                while j < hi and j not in self.clip_exclude:
+                    j += 1
+                self.opt.clip_range_(i, j, self.clip_norm)
+                i = j
         w = all_reduce_async(self.opt.flat_grad[self._offs[lo]:self._offs[hi]], self.group)
         if w is not None:
             self.works.append(w)

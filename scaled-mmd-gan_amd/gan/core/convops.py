@@ -194,6 +194,49 @@ def _cache_put(key, w, u):
     _wino_cache_bytes[0] += nb
 
 
+# Effective SN weights the refresh did not write (sn.SpectralNormBank.lazy):
+# the Winograd filter transforms form them from the raw W and the device
+# sigma and s (smmd_wino3x3_filter_sn, smmd_wino4x4s2(t)_filter_sn, bit-identical
+# to transforming a written W_eff), and every other consumer materialises the
+# values first (`materialize`).  id(tensor) -> [weakref, SN entry, fold, done].
+_LAZY = {}
+
+
+def register_lazy(w, entry, fold):
+    import weakref
+    key = id(w)
+    ref = weakref.ref(w, lambda r, k=key: _LAZY.pop(k, None) if (
+        _LAZY.get(k) is not None and _LAZY[k][0] is r) else None)
+    _LAZY[key] = [ref, entry, bool(fold), False]
+
+
+def _lazy(w):
+    rec = _LAZY.get(id(w))
+    return rec if rec is not None and rec[0]() is w and not rec[3] else None
+
+
+def materialize(w):
+    """Write the values of a lazily refreshed SN weight (W_eff = (W / sigma) s,
+    or its ConvMeanPool fold) into ``w`` before a consumer reads them directly
+    (MIOpen, the thin kernels, an unfold); a no-op for any other tensor."""
+    rec = _lazy(w)
+    if rec is None:
+        return w
+    e, fold = rec[1], rec[2]
+    with torch.no_grad():
+        W = e.weight
+        s = e.scale
+        weff = torch.div(W, e.sigma)
+        if s is not None and s.numel() > 0:
+            weff = weff.mul_(s)
+        if fold:
+            _fold_launch_into([weff.contiguous()], [w], adjoint=False)
+        else:
+            w.copy_(weff.view_as(w))
+    rec[3] = True
+    return w
+
+
 def _param_epoch(w):
     from . import optim as _optim
     return _optim.param_epoch(w)
@@ -209,9 +252,17 @@ def _wino_filter(w, co, ci, mode):
             return u
     L = _lib.lib()
     u = torch.empty(L.smmd_wino3x3_filter_bytes(co, ci) // 4, dtype=w.dtype, device=w.device)
+    lz = _lazy(w)
     with _lib.timed('smmd_wino3x3_filter'):
-        st = L.smmd_wino3x3_filter(_lib.ptr(w), co, ci, int(mode), _lib.ptr(u), u.numel() * 4,
-                                   _lib.stream_handle(w.device))
+        if lz is not None:      # from the raw SN weight: W_eff was never written
+            e = lz[1]
+            sc = e.scale if e.scale is not None and e.scale.numel() > 0 else None
+            st = L.smmd_wino3x3_filter_sn(_lib.ptr(e.weight), _lib.ptr(e.sigma), _lib.ptr(sc), co,
+                                          ci, int(mode), _lib.ptr(u), u.numel() * 4,
+                                          _lib.stream_handle(w.device))
+        else:
+            st = L.smmd_wino3x3_filter(_lib.ptr(w), co, ci, int(mode), _lib.ptr(u), u.numel() * 4,
+                                       _lib.stream_handle(w.device))
     _lib.check(st, 'smmd_wino3x3_filter')
     if not capturing:
         _cache_put(key, w, u)
@@ -334,9 +385,17 @@ def _s2_filter(w, transposed):
     L = _lib.lib()
     a, b = w.shape[0], w.shape[1]
     u = torch.empty(L.smmd_wino4x4s2_filter_bytes(a, b) // 4, dtype=w.dtype, device=w.device)
-    fn = L.smmd_wino4x4s2t_filter if transposed else L.smmd_wino4x4s2_filter
+    lz = _lazy(w)
     with _lib.timed('smmd_wino4x4s2_filter'):
-        st = fn(_lib.ptr(w), a, b, _lib.ptr(u), u.numel() * 4, _lib.stream_handle(w.device))
+        if lz is not None:      # from the raw SN weight (and its fold): W' was never written
+            e = lz[1]
+            sc = e.scale if e.scale is not None and e.scale.numel() > 0 else None
+            fn = L.smmd_wino4x4s2t_filter_sn if transposed else L.smmd_wino4x4s2_filter_sn
+            st = fn(_lib.ptr(e.weight), _lib.ptr(e.sigma), _lib.ptr(sc), int(lz[2]), a, b,
+                    _lib.ptr(u), u.numel() * 4, _lib.stream_handle(w.device))
+        else:
+            fn = L.smmd_wino4x4s2t_filter if transposed else L.smmd_wino4x4s2_filter
+            st = fn(_lib.ptr(w), a, b, _lib.ptr(u), u.numel() * 4, _lib.stream_handle(w.device))
     _lib.check(st, 'smmd_wino4x4s2_filter')
     if not capturing:
         _cache_put(key, w, u)
@@ -493,16 +552,18 @@ def _is_thin(x, w, stride, padding):
 def _fwd(x, w, b, stride, padding):
     """conv(x, w) + b: the library's thin kernel or MIOpen."""
     if _is_thin(x, w, stride, padding):
-        return _thin_conv(x, w, b, 0)
+        return _thin_conv(x, materialize(w), b, 0)
     if _is_wino(x, w, stride, padding, 0):
         return _wino_conv(x, w, b, 0)
     if _is_s2(x, w, stride, padding):
         return _s2_conv(x, w, b)
-    return F.conv2d(x, w, b, stride, padding)
+    return F.conv2d(x, materialize(w), b, stride, padding)
 
 
 def _bwd(gy, x, w, stride, padding, mask):
     """(Dx, Dw) of conv(x, w) at upstream gy via the native backward kernels."""
+    if mask[0] and not (_is_wino(gy, w, stride, padding, 1) or _is_s2t(gy, w, stride, padding)):
+        materialize(w)          # a direct reader of w's values below
     if _is_thin(x, w, stride, padding):
         gx = _thin_conv(gy, w, None, 1) if mask[0] else None
         gw = _thin_wgrad(gy, x) if mask[1] else None
@@ -551,9 +612,8 @@ class _ConvBackward(torch.autograd.Function):
         # double backward ran conv(x, 0) and Dx(gy, 0) on it
         ctx.set_materialize_grads(False)
         gx, gw = _bwd(gy, x, w, stride, padding, (True, want_w))
-        if gw is None:          # placeholder, discarded by the caller: no allocation
-            gw = w.new_zeros(()).expand_as(w)
-            ctx.mark_non_differentiable(gw)
+        # gw None (the input-only pass): a non-tensor output, discarded by the
+        # caller -- no placeholder tensor, so no fill kernel per call
         return gx, gw
 
     @staticmethod
@@ -717,7 +777,7 @@ def _fold_launch(srcs, adjoint):
     from . import _lib
     import ctypes
     _lib.require_cuda(*srcs)
-    srcs = [t.contiguous() for t in srcs]
+    srcs = [materialize(t).contiguous() for t in srcs]
     dsts = [torch.empty(t.shape[:2] + ((3, 3) if adjoint else (4, 4)), dtype=t.dtype,
                         device=t.device) for t in srcs]
     n = len(srcs)

@@ -61,6 +61,30 @@ class Timer:
         return msg
 
 
+def _winograd_fed(bank):
+    """Indices of the SN layers whose convolutions run on the library's
+    Winograd kernels in both directions (forward and input gradient) at any
+    even input size: 3x3 stride-1 convs with 64-multiple channel counts, and
+    4x4 stride-2 convs (the ConvMeanPool folds) whose transposed form tiles
+    (smmd_wino3x3_*, smmd_wino4x4s2(t)_*).  Their W_eff is never read
+    directly, so the refresh need not write it (SpectralNormBank.set_lazy)."""
+    from . import snops
+    out = []
+    for i, e in enumerate(bank.entries):
+        m = e.module
+        if not isinstance(m, snops.Conv2d) or m.weight.dim() != 4:
+            continue
+        co, ci = m.weight.shape[0], m.weight.shape[1]
+        if ci % 64 or co % 64:
+            continue
+        if e.fold and tuple(m.weight.shape[2:]) == (3, 3):
+            out.append(i)
+        elif (tuple(m.weight.shape[2:]) == (3, 3) and getattr(m, 'stride', 1) == 1
+              and convops.WINO):
+            out.append(i)
+    return out
+
+
 class MMD_GAN:
     """Base model: loss = mmd2 of the configured kernel (model.py:313-325),
     optional witness gradient penalty (:327-350) and L2 critic penalty
@@ -106,6 +130,7 @@ class MMD_GAN:
             self.generator.to(memory_format=torch.channels_last)
             self.discriminator.to(memory_format=torch.channels_last)
         self.sn_D = SpectralNormBank(sn_modules(self.discriminator))
+        self.sn_D.set_lazy(_winograd_fed(self.sn_D))
         self.sn_G = SpectralNormBank(sn_modules(self.generator))
         self.spec = mmd.get_kernel_spec(c.kernel) if c.kernel else None
         self.g_vars = [p for p in self.generator.parameters() if p.requires_grad]
@@ -414,8 +439,9 @@ class MMD_GAN:
         # buckets not already issued from the backward's hooks go now; wait all
         self._bucket_for(opt).finish()
         if getattr(self, '_dpgd', False) and opt is self.d_optim:
-            # the buckets summed G: its stats and dL/ds, then the fused update
-            self.sn_D.dp_gdirect_finish()
+            # the buckets summed G: its stats (global: and dL/ds), then the
+            # fused update
+            self.sn_D.dp_gdirect_finish(write_gs=self.dp_mode == 'global')
         if self.dp_mode == 'tower':
             # per-tower clip done per bucket; the tower mean (model.py:257-258)
             opt.step(grad_scale=1.0 / self.world, clip=False)
@@ -440,7 +466,11 @@ class MMD_GAN:
         dpgd = gd and self.world > 1
         self.sn_D.arm_gdirect(gd and not dpgd)
         self.sn_D.arm_direct(self.world > 1)        # the grouped SN nodes' direct writes
-        self.sn_D.arm_dp_gdirect(dpgd)
+        tower_clip = self.d_optim.clip_norm if (dpgd and self.dp_mode == 'tower') else 0.0
+        self.sn_D.arm_dp_gdirect(dpgd, clip=tower_clip)
+        if self.world > 1:
+            bk = self._bucket_for(self.d_optim)
+            bk.clip_exclude = self._sn_tensor_ids() if tower_clip > 0 else frozenset()
         self._dpgd = dpgd
         try:
             if ref:
@@ -458,22 +488,31 @@ class MMD_GAN:
         self._dpgd = False
         return self._detach_step_state()
 
+    def _sn_tensor_ids(self):
+        """Flat-buffer tensor indices of the critic's SN weights and scales."""
+        index = {id(p): i for i, p in enumerate(self.d_optim.params)}
+        out = set()
+        for e in self.sn_D.entries:
+            for p in (e.weight, e.scale):
+                if p is not None and id(p) in index:
+                    out.add(index[id(p)])
+        return frozenset(out)
+
     def _gdirect(self):
         """The critic's SN weight gradients go straight from G into the
         fused update (smmd_adam_flat_sn2 forms dL/dW from G): an SN-fused
         optimizer, SMMD_SN_GDIRECT not 0; one process (sn._SNBatch.
-        _backward_gdirect), or several ranks in global mode with the grouped SN
-        nodes (the buckets all-reduce G itself: sn.arm_dp_gdirect).  Tower mode
-        clips each rank's dL/dW before the mean, so there dL/dW is formed per
-        rank (smmd_sn_weight_bwd) as before."""
+        _backward_gdirect), or several ranks (either mode) with the grouped SN
+        nodes (the buckets all-reduce G itself: sn.arm_dp_gdirect; in tower
+        mode each rank's G is first scaled by its own clip factor).
+        SMMD_SN_DP_GDIRECT=0 keeps the dense dL/dW exchange for several ranks."""
         import os
         if not (self.d_optim._sn is not None and bool(self.sn_D.entries)
                 and os.environ.get('SMMD_SN_GDIRECT', '1') != '0'):
             return False
         if self.world == 1:
             return True
-        return (self.dp_mode == 'global' and self.sn_D.groups is not None
-                and self.sn_D._direct is not None
+        return (self.sn_D.groups is not None and self.sn_D._direct is not None
                 and os.environ.get('SMMD_SN_DP_GDIRECT', '1') != '0')
 
     def _detach_step_state(self):
@@ -495,13 +534,15 @@ class MMD_GAN:
         self.aux = aux
         # the SN layers' effective weights are outputs of the step's SN node
         # (whose backward holds the weights' accumulation nodes): keep values
+        # (an unwritten lazy one is dropped: after the update its W, sigma and
+        # s no longer define it; every step refreshes before using the critic)
         for bank in (self.sn_D, self.sn_G):
             for e in bank.entries:
                 mod = e.module
-                if torch.is_tensor(getattr(mod, 'w_eff', None)):
-                    mod.w_eff = mod.w_eff.detach()
-                if torch.is_tensor(getattr(mod, 'w_fold', None)):
-                    mod.w_fold = mod.w_fold.detach()
+                for name in ('w_eff', 'w_fold'):
+                    t = getattr(mod, name, None)
+                    if torch.is_tensor(t):
+                        setattr(mod, name, None if convops._lazy(t) is not None else t.detach())
         for net in (self.discriminator, self.generator):
             if getattr(net, '_fold_cache', None) is not None:
                 net._fold_cache = None

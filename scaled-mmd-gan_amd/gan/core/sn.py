@@ -45,6 +45,7 @@ def _launch_refresh(bank, update_u, flags, Ws, ss):
     n = len(bank.entries)
     outs = []
     arr = (_lib.SnLayer * n)()
+    lazy = bank.lazy if (bank.lazy and not torch.cuda.is_current_stream_capturing()) else ()
     for i, (e, W, s) in enumerate(zip(bank.entries, Ws, ss)):
         # each output channel's K values must be contiguous: true for the
         # default and the channels_last layouts (SN is invariant to the
@@ -58,7 +59,14 @@ def _launch_refresh(bank, update_u, flags, Ws, ss):
         L = arr[i]
         L.fold = 1 if fold else 0
         L.W = W.data_ptr()
-        L.W_eff = W_eff.data_ptr()
+        if i in lazy and bool(fold) == bool(e.fold):
+            # consumed only through the Winograd filter transforms, which form
+            # it from W, sigma and s (convops.register_lazy): P3 skips it
+            from .convops import register_lazy
+            register_lazy(W_eff, e, fold)
+            L.W_eff = None
+        else:
+            L.W_eff = W_eff.data_ptr()
         L.u = e.u.data_ptr()
         L.v = e.v.data_ptr()
         L.sigma = e.sigma.data_ptr()
@@ -271,6 +279,8 @@ class SpectralNormBank:
         # SN weights' .grad views instead of dL/dW, the buckets sum G over the
         # ranks, and dp_gdirect_finish runs the stats on the sum
         self._dpgd_armed = False
+        # layers whose W_eff the refresh does not write (set_lazy)
+        self.lazy = set()
         self._fresh = None
         self._folds = None
         self._alloc_ws()
@@ -357,13 +367,52 @@ class SpectralNormBank:
         """Arm the direct-write group backward for the next backward pass."""
         self._direct_armed = bool(on) and self._direct is not None
 
-    def arm_dp_gdirect(self, on=True):
+    def set_lazy(self, indices):
+        """Layers (bank indices) whose W_eff / W' the refresh leaves unwritten:
+        their consumers are the Winograd convolutions, whose filter transforms
+        read W, sigma and s directly (smmd_wino3x3_filter_sn,
+        smmd_wino4x4s2(t)_filter_sn); any other reader materialises it
+        (convops.materialize).  SMMD_SN_LAZY=0: none."""
+        self.lazy = set(indices) if os.environ.get('SMMD_SN_LAZY', '1') != '0' else set()
+
+    def arm_dp_gdirect(self, on=True, clip=0.0):
+        """See below; clip > 0 (tower mode): each rank's dL/dW and dL/ds are
+        clipped (model.py:449-455) before the sum, by scaling its G by the
+        clip factor of the analytic norm (smmd_sn_grad_stats on the rank's G,
+        then smmd_sn_clip_g)."""
+        self._dpgd_clip = float(clip)
+        self._arm_dp_gdirect(on)
+
+    def _arm_dp_gdirect(self, on=True):
         """Arm the data-parallel G-direct backward (with arm_direct) for the
         next backward pass.  dL/dW = (s/sigma) G - (s <G, W> / sigma^2) u' v^T is
         linear in G given the replicated W, u', v, sigma and s, so the sum over
         ranks of dL/dW is that of the summed G: the buckets all-reduce G and
         the fused update forms dL/dW once (smmd_adam_flat_sn2)."""
         self._dpgd_armed = bool(on) and self._direct is not None
+
+    def _layers(self, Gs, gss, folds):
+        """The full SnLayer array (the workspace is carved by all layers) with
+        G / gs only where given (None: the layer is skipped)."""
+        n = len(self.entries)
+        arr = (_lib.SnLayer * n)()
+        for i, e in enumerate(self.entries):
+            L = arr[i]
+            L.W = e.weight.data_ptr()
+            L.u = e.u.data_ptr()
+            L.v = e.v.data_ptr()
+            L.sigma = e.sigma.data_ptr()
+            s = e.scale
+            L.s = s.data_ptr() if s is not None and s.numel() > 0 else None
+            L.G = Gs[i].data_ptr() if Gs[i] is not None else None
+            L.gs = gss[i].data_ptr() if gss[i] is not None else None
+            L.N, L.K = e.N, e.K
+            L.fold = 1 if folds[i] else 0
+        return arr
+
+    def _scale_grad(self, e):
+        s = e.scale
+        return s.grad if (s is not None and s.numel() > 0 and s.requires_grad) else None
 
     def _group_write_g(self, members, Ws, ss, grads):
         """The data-parallel G-direct group backward: G into each SN weight's
@@ -385,43 +434,41 @@ class SpectralNormBank:
         if folds_src:
             from .convops import _fold_launch_into
             _fold_launch_into(folds_src, folds_dst, adjoint=True)
+        clip = getattr(self, '_dpgd_clip', 0.0)
+        if clip > 0:
+            # tower mode: this rank's clip_by_norm of dL/dW (and of dL/ds)
+            # before the sum, through the analytic norm of its own G
+            n = len(self.entries)
+            Gs = [self.entries[i].weight.grad if i in members else None for i in range(n)]
+            gss = [self._scale_grad(self.entries[i]) if i in members else None
+                   for i in range(n)]
+            arr = self._layers(Gs, gss, [False] * n)
+            stream = _lib.stream_handle(Ws[0].device)
+            with _lib.timed('smmd_sn_grad_stats'):
+                st = _lib.lib().smmd_sn_grad_stats(arr, n, _lib.ptr(self.ws), self.ws.numel(),
+                                                   stream)
+            _lib.check(st, 'smmd_sn_grad_stats')
+            st = _lib.lib().smmd_sn_clip_g(arr, n, float(clip), _lib.ptr(self.ws),
+                                           self.ws.numel(), stream)
+            _lib.check(st, 'smmd_sn_clip_g')
         self._direct(members)
         return (None,) * (2 * len(members))
 
-    def _grad_stats(self, Ws, ss, Gs, folds):
-        """smmd_sn_grad_stats over every layer: the record {coef, ||dL/dW||^2,
-        sigma, s} the G-direct update reads, and dL/ds written into each
-        learnable scale's .grad."""
+    def dp_gdirect_finish(self, write_gs=True):
+        """After the buckets' all-reduce: the stats of the summed G (in the SN
+        weights' .grad views), then G pending for the fused update, which
+        forms dL/dW (global mode: clips it with the analytic norm) and applies
+        Adam.  write_gs: dL/ds from the summed G (global mode); tower mode
+        keeps the all-reduced sum of the ranks' clipped dL/ds."""
         n = len(self.entries)
-        arr = (_lib.SnLayer * n)()
-        for i, (e, W, s, G) in enumerate(zip(self.entries, Ws, ss, Gs)):
-            L = arr[i]
-            L.W = W.data_ptr()
-            L.u = e.u.data_ptr()
-            L.v = e.v.data_ptr()
-            L.sigma = e.sigma.data_ptr()
-            has_s = s is not None and s.numel() > 0
-            L.s = s.data_ptr() if has_s else None
-            sg = e.scale.grad if has_s else None
-            L.gs = sg.data_ptr() if sg is not None else None
-            L.G = G.data_ptr()
-            L.N, L.K = e.N, e.K
-            L.fold = 1 if folds[i] else 0
-        args = (arr, n, _lib.ptr(self.ws), self.ws.numel(), _lib.stream_handle(Ws[0].device))
-        with _lib.timed('smmd_sn_grad_stats'):
-            st = _lib.lib().smmd_sn_grad_stats(*args)
-        _lib.check(st, 'smmd_sn_grad_stats')
-
-    def dp_gdirect_finish(self):
-        """After the buckets' all-reduce (global mode): the stats of the summed
-        G (in the SN weights' .grad views) and dL/ds, then G pending for the
-        fused update, which forms dL/dW, clips it with the analytic norm and
-        applies Adam."""
-        Ws = [e.weight for e in self.entries]
-        ss = [e.scale if e.scale is not None else None for e in self.entries]
         Gs = [e.weight.grad for e in self.entries]
-        folds = [False] * len(self.entries)
-        self._grad_stats(Ws, ss, Gs, folds)
+        gss = [self._scale_grad(e) if write_gs else None for e in self.entries]
+        folds = [False] * n
+        arr = self._layers(Gs, gss, folds)
+        with _lib.timed('smmd_sn_grad_stats'):
+            st = _lib.lib().smmd_sn_grad_stats(arr, n, _lib.ptr(self.ws), self.ws.numel(),
+                                               _lib.stream_handle(Gs[0].device))
+        _lib.check(st, 'smmd_sn_grad_stats')
         self._gd_pending = (Gs, folds)
 
     def _group_backward(self, members, Ws, ss, grads):

@@ -58,8 +58,8 @@ class _SNMixin:
             return self.weight
         if self.w_eff is None:
             if getattr(self, 'w_fold', None) is not None:
-                from .convops import unfold_pool_weight
-                self.w_eff = unfold_pool_weight(self.w_fold)
+                from .convops import materialize, unfold_pool_weight
+                self.w_eff = unfold_pool_weight(materialize(self.w_fold))
                 return self.w_eff
             raise RuntimeError('SN layer used before its SpectralNormBank.refresh()')
         return self.w_eff

@@ -186,6 +186,8 @@ class FakeLib:
         key = ws.value if isinstance(ws, ctypes.c_void_p) else int(ws or 0)
         for i in range(n):
             L = arr[i]
+            if not L.G:
+                continue
             assert not L.fold, 'fake_lib: fold layers are GPU-only'
             N, K, W, s = self._layer(L)
             G = _arr(L.G, N * K).reshape(N, K).astype(np.float64)
@@ -195,6 +197,22 @@ class FakeLib:
             self._gd[(key, i)] = gW.ravel()
             if L.gs:
                 _arr(L.gs, 1)[0] = gs
+        return 0
+
+    def smmd_sn_clip_g(self, arr, n, clip, ws, wsb, stream):
+        key = ws.value if isinstance(ws, ctypes.c_void_p) else int(ws or 0)
+        for i in range(n):
+            L = arr[i]
+            if not L.G:
+                continue
+            N, K = L.N, L.K
+            gW = self._gd[(key, i)]
+            f = clip / max(float(np.sqrt((gW ** 2).sum())), clip)
+            G = _arr(L.G, N * K)
+            G[:] = (G.astype(np.float64) * f).astype(np.float32)
+            if L.gs:
+                g = float(_arr(L.gs, 1)[0])
+                _arr(L.gs, 1)[0] = g * clip / max(abs(g), clip)
         return 0
 
     def smmd_adam_flat_sn2(self, param, grad, m, v, offs, n, gscale, clip, lr, b1, b2, eps, step,

@@ -434,25 +434,28 @@ def test_sn_buckets_issued_inside_backward(mode, world, monkeypatch):
 
 
 def _worker_sn_dp_gdirect(rank, world, port, mode, q):
-    """Global mode with the data-parallel G-direct backward: the SN groups
-    write G into the flat gradient, the buckets sum it, the stats of the sum
-    and the fused update form dL/dW once."""
+    """The data-parallel G-direct backward: the SN groups write G into the
+    flat gradient (tower: scaled by the rank's clip factor), the buckets sum
+    it, the stats of the sum and the fused update form dL/dW once."""
     _init(rank, world, port)
     from gan.core.collectives import GradBuckets
     from gan.core.model import MMD_GAN
     net, bank, opt = _sn_setup()
     assert opt.attach_sn(bank)
     m = MMD_GAN.__new__(MMD_GAN)
-    m.world, m.group, m.dp_mode = world, dist.group.WORLD, 'global'
+    m.world, m.group, m.dp_mode = world, dist.group.WORLD, mode
     m.d_optim, m.sn_D = opt, bank
-    m._buckets = {id(opt): GradBuckets(opt, m.group, bucket_bytes=64, clip_norm=0.0)}
+    clip = opt.clip_norm if mode == 'tower' else 0.0
+    m._buckets = {id(opt): GradBuckets(opt, m.group, bucket_bytes=64, clip_norm=clip)}
     m._group_sn(bank, opt)
     assert bank.groups is not None and len(bank.groups) >= 2
+    if mode == 'tower':
+        m._buckets[id(opt)].clip_exclude = m._sn_tensor_ids()
     opt.zero_grad()
     m._arm(opt)
     loss = _sn_loss(net, bank, rank)
     bank.arm_direct(True)
-    bank.arm_dp_gdirect(True)
+    bank.arm_dp_gdirect(True, clip=clip)
     m._dpgd = True
     cnt = _Count()
     loss.backward()
@@ -469,13 +472,16 @@ def _worker_sn_dp_gdirect(rank, world, port, mode, q):
 
 
 @pytest.mark.parametrize('world', [2, 4, 8])
-def test_sn_dp_gdirect_matches_dense_exchange(world, monkeypatch):
-    """with several ranks in global mode the buckets
-    all-reduce G (the gradient of the effective weight) instead of dL/dW, and
-    the update forms dL/dW = (s/sigma)(sum G) - (s <sum G, W>/sigma^2) u' v^T
-    once: the updated parameters equal the reference exchange (sum of the
-    ranks' dL/dW, clip_by_norm, Adam; model.py:233-266, :444-456) on the
-    per-rank gradients of the single-node SN backward."""
+@pytest.mark.parametrize('mode', ['global', 'tower'])
+def test_sn_dp_gdirect_matches_dense_exchange(mode, world, monkeypatch):
+    """with several ranks the buckets all-reduce G (the
+    gradient of the effective weight) instead of dL/dW, and the update forms
+    dL/dW = (s/sigma)(sum G) - (s <sum G, W>/sigma^2) u' v^T once; in tower
+    mode each rank's G (and dL/ds) is first scaled by the clip factor of its
+    own dL/dW.  The updated parameters equal the reference exchange (global:
+    sum, clip_by_norm, Adam; tower: per-rank clip_by_norm, mean, Adam;
+    model.py:233-266, :444-456) on the per-rank gradients of the single-node
+    SN backward."""
     import fake_lib
     from gan.core import _lib
     f = fake_lib.FakeLib()
@@ -494,9 +500,13 @@ def test_sn_dp_gdirect_matches_dense_exchange(world, monkeypatch):
                       for p in net.parameters()])
         params = [p.detach().numpy().astype(np.float64).ravel().copy()
                   for p in net.parameters()]
-    expect = [O.adam_step(params[i], 0, 0, O.clip_by_norm(sum(g[i] for g in grads), 1.0),
-                          1, 1e-3)[0] for i in range(len(params))]
-    res = _run(_worker_sn_dp_gdirect, 'global', world=world)
+    if mode == 'global':
+        gsum = [O.clip_by_norm(sum(g[i] for g in grads), 1.0) for i in range(len(params))]
+    else:
+        gsum = [np.mean([O.clip_by_norm(g[i], 1.0) for g in grads], axis=0)
+                for i in range(len(params))]
+    expect = [O.adam_step(params[i], 0, 0, gsum[i], 1, 1e-3)[0] for i in range(len(params))]
+    res = _run(_worker_sn_dp_gdirect, mode, world=world)
     for rank, flat, issued, nb, n_ar in res:
         assert issued == nb and n_ar == nb          # every bucket from inside the backward
         np.testing.assert_allclose(flat, np.concatenate(expect), rtol=2e-5, atol=1e-7)

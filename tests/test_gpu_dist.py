@@ -68,7 +68,7 @@ def _critic_update(model, images, z):
             model.d_optim.flat_param.detach().cpu().numpy())
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, mode='global', dp_gdirect='1'):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     for p in (root, os.path.join(root, 'scaled-mmd-gan_amd')):
@@ -76,12 +76,14 @@ def _worker(rank, world, port, q):
             sys.path.insert(0, p)
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
+    os.environ['SMMD_SN_DP_GDIRECT'] = dp_gdirect
     torch.cuda.set_device(0)
     dev = torch.device('cuda:0')
     dist.init_process_group('gloo', rank=rank, world_size=world)
     from gan.core.smmd import SMMD
     torch.manual_seed(0)
-    model = SMMD(_cfg(), device=dev, process_group=dist.group.WORLD, dp_mode='global')
+    model = SMMD(_cfg(), device=dev, process_group=dist.group.WORLD, dp_mode=mode)
+    assert model._gdirect() == (dp_gdirect != '0')
     images, z = _inputs(world)
     sl = slice(rank * N_PER_RANK, (rank + 1) * N_PER_RANK)
     res = _critic_update(model, images[sl].to(dev), z[sl].to(dev))
@@ -117,3 +119,38 @@ def test_global_mode_two_ranks_equal_one_process(dev):
         np.testing.assert_allclose(grad, ref[2], rtol=1e-3, atol=2e-3 * scale)
     # every rank applied the same update
     np.testing.assert_array_equal(outs[0][4], outs[1][4])
+
+
+def _run_ranks(world, mode, dp_gdirect):
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, mode, dp_gdirect))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = sorted([q.get(timeout=300) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return outs
+
+
+def test_tower_mode_gdirect_equals_dense_exchange(dev):
+    """Tower mode, two ranks: the G-direct exchange (each rank's G and dL/ds
+    scaled by the clip factor of its own dL/dW, the buckets average G, the
+    fused update forms dL/dW once) gives the parameters of the dense exchange
+    (per-rank dL/dW, per-tensor clip_by_norm, mean, Adam; model.py:244-266).
+    Adam's first step, lr * g / (|g| + eps), turns a rounding difference of a
+    near-zero gradient into up to 2 lr: the applied gradients are compared to
+    1e-4 of their max, the parameters to 2 lr."""
+    world = 2
+    dense = _run_ranks(world, 'tower', '0')
+    gd = _run_ranks(world, 'tower', '1')
+    lr = _cfg().learning_rate
+    for a, b in zip(dense, gd):
+        assert a[1] == b[1]                                   # same losses
+        scale = np.abs(a[3]).max()
+        np.testing.assert_allclose(b[3], a[3], rtol=1e-4, atol=1e-4 * scale)
+        assert np.abs(b[4] - a[4]).max() <= 2.0001 * lr
+    np.testing.assert_array_equal(gd[0][4], gd[1][4])
