@@ -38,7 +38,9 @@ constexpr int WN_TB = 64;                 // tiles per block
 constexpr int WN_KB = 64;                 // output channels per block
 constexpr int WN_CC = 8;                  // input channels per chunk
 constexpr int WN_STAGE = 16 * WN_CC * 64; // floats per V (and per U) stage
-constexpr size_t WN_LDS = 2 * 2 * WN_STAGE * sizeof(float);   // 128 KB
+// + the block's 64 biases: the epilogue reads them from LDS, so its rows never
+// wait on a global load (a load there waits, in order, for every earlier store)
+constexpr size_t WN_LDS = 2 * 2 * WN_STAGE * sizeof(float) + WN_KB * sizeof(float);
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f4v __attribute__((ext_vector_type(4)));
@@ -217,6 +219,40 @@ __device__ __forceinline__ void wn_b_row(const float (&t)[4][4], int i, float (&
     v[i][3] = t[i][1] - t[i][3];
 }
 
+// LDS byte offset of a shared-memory pointer
+__device__ __forceinline__ uint32_t wn_lds_addr(const void *p) {
+    return (uint32_t)reinterpret_cast<uintptr_t>(
+        (const __attribute__((address_space(3))) void *)p);
+}
+
+// one 1-KiB LDS-DMA piece: 64 lanes x 16 bytes from per-lane sources into LDS
+// at the wave-uniform byte offset lds_dst (lane l at + 16 l).  Written as asm
+// because the compiler's own form would make every later LDS read wait for it;
+// its completion is the explicit waits below, then a barrier
+__device__ __forceinline__ void wn_glds16(const void *gsrc, uint32_t lds_dst) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_dst)
+                 : "memory");
+}
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float2 wn_f2(f2v v) { return make_float2(v.x, v.y); }
+
+// one patch row (two floats per lane), asm: the loop counts its loads itself
+// (its data is only read after a wait statement naming the register)
+__device__ __forceinline__ void wn_ld2(f2v &r, const float *p) {
+    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
+}
+__device__ __forceinline__ void wn_wait_vm8() { asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); }
+__device__ __forceinline__ void wn_wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+#ifdef WN_CLOCK        // diagnostic build only (-DWN_CLOCK): per-block clock stamps
+                       // (tools/wino_pmc.py reads them through smmd_diag_wino_clock)
+__device__ unsigned long long wn_clk[4096][4];
+#endif
+
 template <bool EDGE>
 __global__ __launch_bounds__(WN_T, 1) void wino_conv_kernel(
     const float *__restrict__ x, const float *__restrict__ u, const float *__restrict__ bias,
@@ -224,11 +260,16 @@ __global__ __launch_bounds__(WN_T, 1) void wino_conv_kernel(
     extern __shared__ float4 wn_lds[];
     float4 *const Vs = wn_lds;                         // [2][p][h][t64]  (float4 = c4)
     float4 *const Us = wn_lds + 2 * (WN_STAGE / 4);    // [2][p][h][k64]
+    float *const Bs = reinterpret_cast<float *>(wn_lds + 4 * (WN_STAGE / 4));   // [k64]
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int kb = blockIdx.y;
     const int64_t tile0 = (int64_t)blockIdx.x * WN_TB;
     const int nch = g.C / WN_CC;
+#ifdef WN_CLOCK
+    const unsigned long long clk_t0 = __builtin_amdgcn_s_memtime();
+    const unsigned long long clk_r0 = __builtin_amdgcn_s_memrealtime();
+#endif
     // input-channel slice blockIdx.z of gridDim.z: chunks [c0, c0 + nchunk)
     const int c0 = (int)((int64_t)nch * blockIdx.z / gridDim.z);
     const int nchunk = (int)((int64_t)nch * (blockIdx.z + 1) / gridDim.z) - c0;
@@ -250,32 +291,40 @@ __global__ __launch_bounds__(WN_T, 1) void wino_conv_kernel(
         reinterpret_cast<const float4 *>(u) + ((int64_t)kb * nch + c0) * (WN_STAGE / 4);
     xn += (int64_t)c0 * WN_CC * HW;
 
-    float2 raw[2][4];
-    // the filter stage goes through registers (an LDS-DMA load would make
-    // the compiler wait for it before every ds_read of the MFMA phase)
-    f4v ur[8];
-#define WN_LOAD_CHUNK(CC_)                                                                   \
-    do {                                                                                     \
-        _Pragma("unroll") for (int e = 0; e < 2; ++e)                                        \
-            wn_load_rows(xn + (int64_t)((CC_) * WN_CC + 2 * w + e) * HW, tty, ttx, tok, g,    \
-                         raw[e]);                                                            \
-        const float4 *src_ = ub + (int64_t)(CC_) * (WN_STAGE / 4) + w * 512 + lane;          \
-        _Pragma("unroll") for (int i = 0; i < 8; ++i)                                        \
-            ur[i] = *reinterpret_cast<const f4v *>(src_ + i * 64);                            \
-    } while (0)
-#define WN_STORE_CHUNK(CC_, BUF_)                                                            \
-    do {                                                                                     \
-        f4v *U_ = reinterpret_cast<f4v *>(Us + (BUF_) * (WN_STAGE / 4) + w * 512 + lane);    \
-        _Pragma("unroll") for (int i = 0; i < 8; ++i) U_[i * 64] = ur[i];                    \
-        float v_[2][16];                                                                     \
-        _Pragma("unroll") for (int e = 0; e < 2; ++e)                                        \
-            wn_transform<EDGE>(raw[e], xn + (int64_t)((CC_) * WN_CC + 2 * w + e) * HW, tty,  \
-                               ttx, tok, g, lane, v_[e]);                                    \
-        float2 *V2_ = reinterpret_cast<float2 *>(Vs + (BUF_) * (WN_STAGE / 4));              \
-        _Pragma("unroll") for (int p = 0; p < 16; ++p)                                       \
-            V2_[((p * 2 + (w >> 1)) * 64 + lane) * 2 + (w & 1)] =                            \
-                make_float2(v_[0][p], v_[1][p]);                                             \
-    } while (0)
+    // The loop's global loads are asm, counted by hand (two waits per chunk):
+    //   top of chunk c:       chunk c+1's filter stage, LDS-DMA (8 pieces)
+    //   second half, K 8-15:  chunk c+2's patch rows into `raw` (8 loads),
+    //                         right after chunk c+1's rows were consumed
+    //   before K 0:           vmcnt(8) -- chunk c+1's rows (older than the 8
+    //                         stage pieces) have landed
+    //   before the barrier:   vmcnt(8) -- the stage has landed (only chunk
+    //                         c+2's rows may be in flight)
+    // so a chunk's rows have ~1.5 chunks and its stage one chunk of cover.
+    f2v raw[2][4];
+    const float *xrow[2][4];            // chunk 0's row pointers, clamped rows
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int yc = min(max(2 * tty - 1 + i, 0), g.H - 1);
+            xrow[e][i] = xn + (int64_t)(2 * w + e) * HW + (int64_t)yc * g.W + 2 * ttx;
+        }
+    auto load_row = [&](int cc, int e, int i) {
+        wn_ld2(raw[e][i], xrow[e][i] + (int64_t)cc * WN_CC * HW);
+    };
+    const uint32_t us_lds = wn_lds_addr(Us) + (uint32_t)__builtin_amdgcn_readfirstlane(w) * 8192u;
+    auto load_u = [&](int cc) {
+        const float4 *src = ub + (int64_t)cc * (WN_STAGE / 4) + w * 512 + lane;
+        const uint32_t dst = us_lds + (uint32_t)(cc & 1) * (WN_STAGE * 4);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) wn_glds16(src + i * 64, dst + i * 1024);
+    };
+#define WN_WAIT_ROWS(N_)                                                                     \
+    asm volatile("s_waitcnt vmcnt(" #N_ ")"                                                  \
+                 : "+v"(raw[0][0]), "+v"(raw[0][1]), "+v"(raw[0][2]), "+v"(raw[0][3]),       \
+                   "+v"(raw[1][0]), "+v"(raw[1][1]), "+v"(raw[1][2]), "+v"(raw[1][3])         \
+                 :                                                                           \
+                 : "memory")
 
     f32x16 acc[16];
 #pragma unroll
@@ -283,8 +332,8 @@ __global__ __launch_bounds__(WN_T, 1) void wino_conv_kernel(
 
     const int th = w & 1, kh = w >> 1, hl = lane >> 5, l32 = lane & 31;
 // 64 MFMAs per wave per chunk, the points taken in pairs so consecutive
-// MFMAs never share an accumulator; the next pair's fragments are read while
-// this pair's MFMAs run
+// MFMAs never share an accumulator; the next pair's fragments are read right
+// after each pair's first MFMA (seven MFMAs of cover for the LDS latency)
 #define WN_MFMA_CHUNK(BUF_)                                                                  \
     do {                                                                                     \
         const float4 *V_ = Vs + (BUF_) * (WN_STAGE / 4);                                     \
@@ -294,83 +343,118 @@ __global__ __launch_bounds__(WN_T, 1) void wino_conv_kernel(
         _Pragma("unroll") for (int pp = 0; pp < 8; ++pp) {                                   \
             const int p = 2 * pp;                                                            \
             const float4 ca0 = a0, cb0 = b0, ca1 = a1, cb1 = b1;                             \
-            if (pp < 7) {                                                                    \
-                a0 = U_[((p + 2) * 2 + hl) * 64 + kh * 32 + l32];                            \
-                b0 = V_[((p + 2) * 2 + hl) * 64 + th * 32 + l32];                            \
-                a1 = U_[((p + 3) * 2 + hl) * 64 + kh * 32 + l32];                            \
-                b1 = V_[((p + 3) * 2 + hl) * 64 + th * 32 + l32];                            \
+            _Pragma("unroll") for (int m = 0; m < 8; ++m) {                                  \
+                const int s4 = m >> 1;                                                       \
+                if ((m & 1) == 0)                                                            \
+                    acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca0[s4], cb0[s4], acc[p], 0, 0, 0); \
+                else                                                                         \
+                    acc[p + 1] =                                                             \
+                        __builtin_amdgcn_mfma_f32_32x32x2f32(ca1[s4], cb1[s4], acc[p + 1], 0, 0, 0); \
+                if (m == 0 && pp < 7) {                                                      \
+                    a0 = U_[((p + 2) * 2 + hl) * 64 + kh * 32 + l32];                        \
+                    b0 = V_[((p + 2) * 2 + hl) * 64 + th * 32 + l32];                        \
+                    a1 = U_[((p + 3) * 2 + hl) * 64 + kh * 32 + l32];                        \
+                    b1 = V_[((p + 3) * 2 + hl) * 64 + th * 32 + l32];                        \
+                }                                                                            \
+                __builtin_amdgcn_sched_barrier(0);                                           \
             }                                                                                \
-            acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca0.x, cb0.x, acc[p], 0, 0, 0);    \
-            acc[p + 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca1.x, cb1.x, acc[p + 1], 0, 0, 0); \
-            acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca0.y, cb0.y, acc[p], 0, 0, 0);    \
-            acc[p + 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca1.y, cb1.y, acc[p + 1], 0, 0, 0); \
-            acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca0.z, cb0.z, acc[p], 0, 0, 0);    \
-            acc[p + 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca1.z, cb1.z, acc[p + 1], 0, 0, 0); \
-            acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca0.w, cb0.w, acc[p], 0, 0, 0);    \
-            acc[p + 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca1.w, cb1.w, acc[p + 1], 0, 0, 0); \
         }                                                                                    \
     } while (0)
 
-    WN_LOAD_CHUNK(0);
-    WN_STORE_CHUNK(0, 0);
+    // chunk 0 staged before the loop (everything waited for), chunk 1's rows
+    // then issued
+    const float bias_k = (bias && tid < WN_KB) ? bias[kb * WN_KB + tid] : 0.f;
+    load_u(0);
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) load_row(0, e, i);
+    WN_WAIT_ROWS(0);
+    {
+        float v_[2][16];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const float2 r_[4] = {wn_f2(raw[e][0]), wn_f2(raw[e][1]), wn_f2(raw[e][2]),
+                                  wn_f2(raw[e][3])};
+            wn_transform<EDGE>(r_, xn + (int64_t)(2 * w + e) * HW, tty, ttx, tok, g, lane, v_[e]);
+        }
+        float2 *V2 = reinterpret_cast<float2 *>(Vs);
+#pragma unroll
+        for (int p = 0; p < 16; ++p)
+            V2[((p * 2 + (w >> 1)) * 64 + lane) * 2 + (w & 1)] = make_float2(v_[0][p], v_[1][p]);
+    }
+    if (tid < WN_KB) Bs[tid] = bias_k;
+    const int c1 = min(1, nchunk - 1);      // (a spare reload when there is one chunk)
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) load_row(c1, e, i);
     __syncthreads();
+
     for (int cc = 0; cc + 1 < nchunk; ++cc) {
         const int buf = cc & 1, nbuf = buf ^ 1;
-        WN_LOAD_CHUNK(cc + 1);          // in flight during this chunk's MFMAs
+        const int cn = min(cc + 2, nchunk - 1);     // (a spare reload at the end)
+        load_u(cc + 1);
         __builtin_amdgcn_sched_barrier(0);
         const float4 *V_ = Vs + buf * (WN_STAGE / 4);
         const float4 *U_ = Us + buf * (WN_STAGE / 4);
         float4 a0 = U_[hl * 64 + kh * 32 + l32], b0 = V_[hl * 64 + th * 32 + l32];
         float4 a1 = U_[(2 + hl) * 64 + kh * 32 + l32], b1 = V_[(2 + hl) * 64 + th * 32 + l32];
-        // first half: 32 MFMAs, the loads' cover
+        // first half: 32 MFMAs
 #pragma unroll
         for (int pp = 0; pp < 4; ++pp) {
             const int p = 2 * pp;
             const float4 ca0 = a0, cb0 = b0, ca1 = a1, cb1 = b1;
-            a0 = U_[((p + 2) * 2 + hl) * 64 + kh * 32 + l32];
-            b0 = V_[((p + 2) * 2 + hl) * 64 + th * 32 + l32];
-            a1 = U_[((p + 3) * 2 + hl) * 64 + kh * 32 + l32];
-            b1 = V_[((p + 3) * 2 + hl) * 64 + th * 32 + l32];
 #pragma unroll
-            for (int s4 = 0; s4 < 4; ++s4) {
-                acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca0[s4], cb0[s4], acc[p], 0, 0, 0);
-                acc[p + 1] =
-                    __builtin_amdgcn_mfma_f32_32x32x2f32(ca1[s4], cb1[s4], acc[p + 1], 0, 0, 0);
+            for (int m = 0; m < 8; ++m) {
+                const int s4 = m >> 1;
+                if ((m & 1) == 0)
+                    acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca0[s4], cb0[s4], acc[p], 0, 0, 0);
+                else
+                    acc[p + 1] =
+                        __builtin_amdgcn_mfma_f32_32x32x2f32(ca1[s4], cb1[s4], acc[p + 1], 0, 0, 0);
+                if (m == 0) {
+                    a0 = U_[((p + 2) * 2 + hl) * 64 + kh * 32 + l32];
+                    b0 = V_[((p + 2) * 2 + hl) * 64 + th * 32 + l32];
+                    a1 = U_[((p + 3) * 2 + hl) * 64 + kh * 32 + l32];
+                    b1 = V_[((p + 3) * 2 + hl) * 64 + th * 32 + l32];
+                }
+                __builtin_amdgcn_sched_barrier(0);
             }
         }
-        __builtin_amdgcn_sched_barrier(0);
         // second half: after each MFMA one slice of the next chunk's
-        // transform and LDS stores (the other buffer), issued in the MFMA's
-        // shadow; sched_barrier pins the order
+        // transform and LDS stores (the other buffer) or of chunk cc + 2's
+        // row loads, issued in the MFMA's shadow; sched_barrier pins the order
+        WN_WAIT_ROWS(8);
+        __builtin_amdgcn_sched_barrier(0);
         float d0[4][4], d1[4][4], t0[4][4], t1[4][4], v0[4][4], v1[4][4];
         const float *xc0 = xn + (int64_t)((cc + 1) * WN_CC + 2 * w) * HW;
-        f4v *Un = reinterpret_cast<f4v *>(Us + nbuf * (WN_STAGE / 4) + w * 512 + lane);
         float2 *Vn = reinterpret_cast<float2 *>(Vs + nbuf * (WN_STAGE / 4));
 #pragma unroll
         for (int pp = 4; pp < 8; ++pp) {
             const int p = 2 * pp;
             const float4 ca0 = a0, cb0 = b0, ca1 = a1, cb1 = b1;
-            if (pp < 7) {
-                a0 = U_[((p + 2) * 2 + hl) * 64 + kh * 32 + l32];
-                b0 = V_[((p + 2) * 2 + hl) * 64 + th * 32 + l32];
-                a1 = U_[((p + 3) * 2 + hl) * 64 + kh * 32 + l32];
-                b1 = V_[((p + 3) * 2 + hl) * 64 + th * 32 + l32];
-            }
 #pragma unroll
             for (int m = 0; m < 8; ++m) {
-                const int s4 = m >> 1, q = m & 1;
-                if (q == 0)
+                const int s4 = m >> 1;
+                if ((m & 1) == 0)
                     acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca0[s4], cb0[s4], acc[p], 0, 0, 0);
                 else
                     acc[p + 1] =
                         __builtin_amdgcn_mfma_f32_32x32x2f32(ca1[s4], cb1[s4], acc[p + 1], 0, 0, 0);
+                if (m == 0 && pp < 7) {
+                    a0 = U_[((p + 2) * 2 + hl) * 64 + kh * 32 + l32];
+                    b0 = V_[((p + 2) * 2 + hl) * 64 + th * 32 + l32];
+                    a1 = U_[((p + 3) * 2 + hl) * 64 + kh * 32 + l32];
+                    b1 = V_[((p + 3) * 2 + hl) * 64 + th * 32 + l32];
+                }
                 const int K = (pp - 4) * 8 + m;
                 if (K < 8) {                         // patch rows of channel K / 4
                     const int e = K >> 2, i = K & 3;
-                    wn_row<EDGE>(raw[e][i], xc0 + e * HW, tty, ttx, tok, g, lane, i,
+                    wn_row<EDGE>(wn_f2(raw[e][i]), xc0 + e * HW, tty, ttx, tok, g, lane, i,
                                  e ? d1[i] : d0[i]);
-                } else if (K < 16) {                 // the filter stage
-                    Un[(K - 8) * 64] = ur[K - 8];
+                } else if (K < 16) {                 // chunk cc + 2's row, same register
+                    load_row(cn, (K - 8) >> 2, (K - 8) & 3);
                 } else if (K < 20) {                 // B^T d, column j, channel 0
                     wn_bt_col(d0, K - 16, t0);
                 } else if (K < 24) {                 // (B^T d) B, row i, channel 0
@@ -388,9 +472,13 @@ __global__ __launch_bounds__(WN_T, 1) void wino_conv_kernel(
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
+        // chunk cc + 1's filter stage landed (chunk cc + 2's rows may not have)
+        wn_wait_vm8();
         __syncthreads();
     }
     WN_MFMA_CHUNK((nchunk - 1) & 1);
+    WN_WAIT_ROWS(0);                        // nothing of ours left in flight
+#undef WN_WAIT_ROWS
 
     // epilogue: C_p[k][tile], k = (r & 3) + 8 (r >> 2) + 4 hl, tile = l32.
     // With an even tile-row width the lane pair (2i, 2i+1) holds two
@@ -415,7 +503,7 @@ __global__ __launch_bounds__(WN_T, 1) void wino_conv_kernel(
             s0[j] = m[j] + m[4 + j] + m[8 + j];
             s1[j] = m[4 + j] - m[8 + j] - m[12 + j];
         }
-        const float b = bias ? bias[k] : 0.f;
+        const float b = Bs[k - kb * WN_KB];
         float y00 = s0[0] + s0[1] + s0[2] + b, y01 = s0[1] - s0[2] - s0[3] + b;
         float y10 = s1[0] + s1[1] + s1[2] + b, y11 = s1[1] - s1[2] - s1[3] + b;
         if (g.relu) {
@@ -441,6 +529,14 @@ __global__ __launch_bounds__(WN_T, 1) void wino_conv_kernel(
             *reinterpret_cast<float2 *>(o + g.W) = make_float2(y10, y11);
         }
     }
+#ifdef WN_CLOCK
+    if (tid == 0 && blockIdx.z == 0) {
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+        const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+        const unsigned b = (blockIdx.y * gridDim.x + blockIdx.x) & 4095;
+        wn_clk[b][0] = clk_t0; wn_clk[b][1] = t1; wn_clk[b][2] = clk_r0; wn_clk[b][3] = r1;
+    }
+#endif
 }
 
 // y = bias + sum over the S partial slabs in slice order (float4 when the
@@ -481,6 +577,13 @@ static int wino_slices(int64_t blocks, int nch, int HW) {
 }  // namespace smmd
 
 using namespace smmd;
+
+#ifdef WN_CLOCK
+extern "C" int smmd_diag_wino_clock(unsigned long long *host, int n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(wn_clk), sizeof(unsigned long long) * 4 * n) ==
+                   hipSuccess ? 0 : 1;
+}
+#endif
 
 extern "C" size_t smmd_wino3x3_filter_bytes(int ko, int ci) {
     if (ko <= 0 || ci <= 0) return 0;

@@ -29,7 +29,9 @@ constexpr int S2_TB = 64;
 constexpr int S2_KB = 64;
 constexpr int S2_CC = 2;                     // input channels per chunk (8 phase channels)
 constexpr int S2_STAGE = 9 * 8 * 64;         // floats per V (and per U) stage
-constexpr size_t S2_LDS = 2 * 2 * S2_STAGE * sizeof(float);   // 72 KB
+// + the block's 64 biases (the epilogue reads them from LDS: a global load
+// there would wait, in order, for every earlier store)
+constexpr size_t S2_LDS = 2 * 2 * S2_STAGE * sizeof(float) + S2_KB * sizeof(float);
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f4v __attribute__((ext_vector_type(4)));
@@ -135,6 +137,7 @@ __global__ __launch_bounds__(S2_T, 2) void s2_conv_kernel(
     extern __shared__ float4 s2_lds[];
     float4 *const Vs = s2_lds;                         // [2][p9][h2][t64]  (float4 = c4)
     float4 *const Us = s2_lds + 2 * (S2_STAGE / 4);    // [2][p9][h2][k64]
+    float *const Bs = reinterpret_cast<float *>(s2_lds + 4 * (S2_STAGE / 4));   // [k64]
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int kb = blockIdx.y;
@@ -244,7 +247,9 @@ __global__ __launch_bounds__(S2_T, 2) void s2_conv_kernel(
     };
 
     load(0);
+    const float bias_k = (bias && tid < S2_KB) ? bias[kb * S2_KB + tid] : 0.f;
     store(0, 0);
+    if (tid < S2_KB) Bs[tid] = bias_k;
     __syncthreads();
     for (int cc = 0; cc + 1 < nchunk; ++cc) {
         load(cc + 1);
@@ -276,7 +281,7 @@ __global__ __launch_bounds__(S2_T, 2) void s2_conv_kernel(
             s0[j] = m[j] + m[3 + j];
             s1[j] = m[3 + j] + m[6 + j];
         }
-        const float b = bias ? bias[k] : 0.f;
+        const float b = Bs[k - kb * S2_KB];
         float *o = y + (((int64_t)en * g.K + k) * Ho + 2 * ety) * Wo + 2 * etx;
         *reinterpret_cast<float2 *>(o) = make_float2(s0[0] + s0[1] + b, s0[1] + s0[2] + b);
         *reinterpret_cast<float2 *>(o + Wo) = make_float2(s1[0] + s1[1] + b, s1[1] + s1[2] + b);
@@ -345,6 +350,7 @@ __global__ __launch_bounds__(S2_T, 2) void s2t_conv_kernel(
     extern __shared__ float4 s2_lds[];
     float4 *const Vs = s2_lds;
     float4 *const Us = s2_lds + 2 * (S2_STAGE / 4);
+    float *const Bs = reinterpret_cast<float *>(s2_lds + 4 * (S2_STAGE / 4));   // [c64]
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int cb = blockIdx.y;
@@ -457,7 +463,9 @@ __global__ __launch_bounds__(S2_T, 2) void s2t_conv_kernel(
     };
 
     load(0);
+    const float bias_c = (bias && tid < 64) ? bias[cb * 64 + tid] : 0.f;
     store(0, 0);
+    if (tid < 64) Bs[tid] = bias_c;
     __syncthreads();
     for (int cc = 0; cc + 1 < nchunk; ++cc) {
         load(cc + 1);
@@ -488,7 +496,7 @@ __global__ __launch_bounds__(S2_T, 2) void s2t_conv_kernel(
             s0[j] = m[j] + m[3 + j];
             s1[j] = m[3 + j] + m[6 + j];
         }
-        const float b = bias ? bias[c] : 0.f;
+        const float b = Bs[c - cb * 64];
         float *o = dx + (((int64_t)en * g.C + c) * Hx + 4 * ety + qi) * Wx + 4 * etx + qj;
         o[0] = s0[0] + s0[1] + b;
         o[2] = s0[1] + s0[2] + b;

@@ -260,7 +260,10 @@ class SpectralNormBank:
     reference's u read/assign race."""
 
     def __init__(self, modules, num_iters=1):
-        self.entries = [SNEntry(m) for m in modules]
+        self._init_state([SNEntry(m) for m in modules], num_iters)
+
+    def _init_state(self, entries, num_iters):
+        self.entries = entries
         self.num_iters = num_iters
         self.ws = None
         self._p1_token = None
@@ -274,7 +277,7 @@ class SpectralNormBank:
         self.groups = None
         self._direct = None
         self._direct_armed = False
-        # data parallel G-direct (global mode): while armed, a group's backward
+        # data parallel G-direct (either mode): while armed, a group's backward
         # writes G (the adjoint fold of G' for ConvMeanPool layers) into the
         # SN weights' .grad views instead of dL/dW, the buckets sum G over the
         # ranks, and dp_gdirect_finish runs the stats on the sum
@@ -564,8 +567,7 @@ def spectral_normed_weight(W, u=None, num_iters=1, update_collection=None, with_
     e.u = u.reshape(N).detach().clone().contiguous()
     e.v = torch.zeros(e.K, device=W.device, dtype=torch.float32)
     e.sigma = torch.ones(1, device=W.device, dtype=torch.float32)
-    bank.entries, bank.num_iters, bank.ws = [e], num_iters, None
-    bank._alloc_ws()
+    bank._init_state([e], num_iters)
     W_eff_t, = _SNBatch.apply(bank, True, 0, Wt, torch.empty(0, device=W.device))
     if update_collection is None:
         with torch.no_grad():
