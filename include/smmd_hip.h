@@ -67,7 +67,8 @@ int smmd_abi_version(void);         /* bumped on any ABI change (2: Gram/poly,
                                        8: smmd_wino3x3_*, smmd_wino4x4s2*,
                                        smmd_wino3x3_wgrad*, 9: smmd_wino4x4s2_wgrad*,
                                        smmd_wino3x3_filter_sn, smmd_wino4x4s2(t)_filter_sn,
-                                       smmd_sn_clip_g) */
+                                       smmd_sn_clip_g, 10: smmd_wino3x3_conv2*,
+                                       smmd_wino4x4s2_conv2*) */
 const char *smmd_source_hash(void); /* first 16 hex digits of the SHA-256 of the
                                        sources this binary was built from
                                        (csrc .hip and .hpp files in byte order,
@@ -613,6 +614,18 @@ smmd_status smmd_wino3x3_conv_relu(const float *x, const float *u, const float *
                                    int n, int ci, int ko, int h, int w_img, void *ws,
                                    size_t ws_bytes, smmd_stream_t stream);
 
+/* the pair form: y = conv(x, u) + conv(x2, u2) + bias, both inputs [n, ci, h,
+ * w_img] and both filters from smmd_wino3x3_filter at the same (ko, ci), in
+ * ONE launch whose input-channel loop runs over both (the double backward's
+ * gradient of a conv's upstream, conv(ggx, w) + conv(x, ggw),
+ * gan/core/convops._ConvBackward: one output instead of two and their sum).
+ * Workspace: smmd_wino3x3_conv2_workspace_bytes. */
+size_t smmd_wino3x3_conv2_workspace_bytes(int n, int ci, int ko, int h, int w_img);
+
+smmd_status smmd_wino3x3_conv2(const float *x, const float *u, const float *x2, const float *u2,
+                               const float *bias, float *y, int n, int ci, int ko, int h,
+                               int w_img, void *ws, size_t ws_bytes, smmd_stream_t stream);
+
 /* ---------------------------------------------------------------------------
  * 4x4 stride-2 padding-1 convolutions as polyphase Winograd F(2x2, 2x2) on the
  * f32 MFMA: the critics' ConvMeanPool layers (gan/core/resnet/block.py:63-66;
@@ -656,6 +669,15 @@ smmd_status smmd_wino4x4s2_conv(const float *x, const float *u, const float *bia
 
 smmd_status smmd_wino4x4s2t_conv(const float *gy, const float *u, const float *bias, float *dx,
                                  int n, int k, int c, int hg, int wg, void *ws, size_t ws_bytes,
+                                 smmd_stream_t stream);
+
+/* the pair form of smmd_wino4x4s2_conv: y = conv(x, u) + conv(x2, u2) + bias
+ * in one launch (as smmd_wino3x3_conv2). */
+size_t smmd_wino4x4s2_conv2_workspace_bytes(int n, int ci, int ko, int h, int w_img);
+
+smmd_status smmd_wino4x4s2_conv2(const float *x, const float *u, const float *x2,
+                                 const float *u2, const float *bias, float *y, int n, int ci,
+                                 int ko, int h, int w_img, void *ws, size_t ws_bytes,
                                  smmd_stream_t stream);
 
 /* ---------------------------------------------------------------------------

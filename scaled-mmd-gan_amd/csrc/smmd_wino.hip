@@ -44,15 +44,18 @@ constexpr size_t WN_LDS = 2 * 2 * WN_STAGE * sizeof(float) + WN_KB * sizeof(floa
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f4v __attribute__((ext_vector_type(4)));
+typedef float f2v __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ float wn_from_left(float v) {   // lane l gets lane l-1's v (lane 0: 0)
-    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
-                                                                 0x138, 0xf, 0xf, false));
+// neighbour lanes' values, 0 where the source lane is outside the wave
+// (bound_ctrl: no preset of the destination)
+__device__ __forceinline__ float wn_dpp_left(float v) {    // lane l gets lane l-1's v
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x138,
+                                                              0xf, 0xf, true));
 }
 
-__device__ __forceinline__ float wn_from_right(float v) {  // lane l gets lane l+1's v (lane 63: 0)
-    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
-                                                                 0x130, 0xf, 0xf, false));
+__device__ __forceinline__ float wn_dpp_right(float v) {   // lane l gets lane l+1's v
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x130,
+                                                              0xf, 0xf, true));
 }
 
 // U = G g G^T for the filters (ko, 4 q .. 4 q + 3), stored in the conv
@@ -126,97 +129,86 @@ struct WnGeom {
     int N, C, K, H, W, TW, Timg;
     int64_t T, slab;        // slab: floats between split-C partial outputs
     int relu;               // 1: the output is relu(conv + bias) (not on partial slabs)
+    // the pair form (smmd_wino3x3_conv2): a second input and filter, the
+    // input-channel loop running over both (chunks nch1 .. 2 nch1 - 1 from
+    // them), so y = conv(x, U) + conv(x2, U2) in one set of accumulators
+    const float *x2, *u2;
 };
 
-// raw 4 x 2 centre columns of one channel's patch rows (2ty-1 .. 2ty+2, cols
-// 2tx, 2tx+1): a row outside the image loads the clamped row, which the
-// transform replaces by zero (so nothing waits on the loads before it)
-__device__ __forceinline__ void wn_load_rows(const float *__restrict__ xc, int ty, int tx, bool ok,
-                                             const WnGeom &g, float2 (&r)[4]) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int yy = 2 * ty - 1 + i;
-        const int yc = min(max(yy, 0), g.H - 1);
-        r[i] = *reinterpret_cast<const float2 *>(xc + (int64_t)yc * g.W + 2 * tx);
-    }
+// The input transform V = B^T d B of one tile's 4 x 4 patch d (rows 2ty-1 ..
+// 2ty+2, columns 2tx-1 .. 2tx+2), factored by columns: t = B^T d column by
+// column, v = t B row by row.  A lane loads only its two centre columns
+// (2tx, 2tx+1); t's outer columns are the neighbouring tiles' centre columns,
+// so they come transformed from the neighbour lanes (t[.][0] = the left
+// tile's t of its column 2tx-1, t[.][3] = the right tile's t of 2tx+2):
+// 8 column ops instead of 16 and no raw neighbour values.  Rows 1 and 2 are
+// always inside the image (H even); rows 0 and 3 are zero at its top and
+// bottom, columns 0 and 3 at its left and right edges.  The arithmetic is
+// the column-then-row form, term for term.
+
+// B^T of one column of the patch
+__device__ __forceinline__ void wn_bt(float a0, float a1, float a2, float a3, float (&t)[4]) {
+    t[0] = a0 - a2;
+    t[1] = a1 + a2;
+    t[2] = a2 - a1;
+    t[3] = a1 - a3;
 }
 
-// V = B^T d B of one channel's patch; d's outer columns come from the
-// neighbouring tiles' lanes (the tile to the left holds column 2tx-1 as its
-// .y, the one to the right column 2tx+2 as its .x), or from memory at a wave
-// edge inside a tile row
-template <bool EDGE>
-__device__ __forceinline__ void wn_transform(const float2 (&r)[4], const float *__restrict__ xc,
-                                             int ty, int tx, bool ok, const WnGeom &g, int lane,
-                                             float (&v)[16]) {
-    float d[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int yy = 2 * ty - 1 + i;
-        const bool row = ok && yy >= 0 && yy < g.H;
-        const float cx = row ? r[i].x : 0.f, cy = row ? r[i].y : 0.f;
-        float L = wn_from_left(cy), R = wn_from_right(cx);
-        if (EDGE) {        // a tile row wider than a wave: its wave edges load
-            if (tx > 0 && lane == 0) L = row ? xc[(int64_t)yy * g.W + 2 * tx - 1] : 0.f;
-            if (tx < g.TW - 1 && lane == 63) R = row ? xc[(int64_t)yy * g.W + 2 * tx + 2] : 0.f;
-        }
-        L = tx == 0 ? 0.f : L;
-        R = tx == g.TW - 1 ? 0.f : R;
-        d[i][0] = L;
-        d[i][1] = cx;
-        d[i][2] = cy;
-        d[i][3] = R;
-    }
-    float t[4][4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        t[0][j] = d[0][j] - d[2][j];
-        t[1][j] = d[1][j] + d[2][j];
-        t[2][j] = d[2][j] - d[1][j];
-        t[3][j] = d[1][j] - d[3][j];
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        v[i * 4 + 0] = t[i][0] - t[i][2];
-        v[i * 4 + 1] = t[i][1] + t[i][2];
-        v[i * 4 + 2] = t[i][2] - t[i][1];
-        v[i * 4 + 3] = t[i][1] - t[i][3];
-    }
+// the lane's own columns' B^T from its rows r (rows 0 / 3 masked)
+__device__ __forceinline__ void wn_own(const f2v (&r)[4], bool r0ok, bool r3ok, float (&tx)[4],
+                                       float (&ty)[4]) {
+    wn_bt(r0ok ? r[0].x : 0.f, r[1].x, r[2].x, r3ok ? r[3].x : 0.f, tx);
+    wn_bt(r0ok ? r[0].y : 0.f, r[1].y, r[2].y, r3ok ? r[3].y : 0.f, ty);
 }
 
-// one patch row of V's input: d[i][0..3] = (left neighbour, 2tx, 2tx+1,
-// right neighbour), zero outside the image
+// the outer columns from the neighbour lanes (EDGE: a tile row wider than a
+// wave, whose wave-edge lanes transform the neighbour column from memory)
 template <bool EDGE>
-__device__ __forceinline__ void wn_row(float2 r, const float *__restrict__ xc, int ty, int tx,
-                                       bool ok, const WnGeom &g, int lane, int i, float (&d)[4]) {
-    const int yy = 2 * ty - 1 + i;
-    const bool row = ok && yy >= 0 && yy < g.H;
-    const float cx = row ? r.x : 0.f, cy = row ? r.y : 0.f;
-    float L = wn_from_left(cy), R = wn_from_right(cx);
+__device__ __forceinline__ void wn_outer(const float (&tx)[4], const float (&ty)[4],
+                                         const float *__restrict__ xc, int ty_, int tx_,
+                                         bool r0ok, bool r3ok, int lane, int TW, int H, int W,
+                                         float (&tl)[4], float (&tr)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        tl[i] = wn_dpp_left(ty[i]);
+        tr[i] = wn_dpp_right(tx[i]);
+    }
     if (EDGE) {
-        if (tx > 0 && lane == 0) L = row ? xc[(int64_t)yy * g.W + 2 * tx - 1] : 0.f;
-        if (tx < g.TW - 1 && lane == 63) R = row ? xc[(int64_t)yy * g.W + 2 * tx + 2] : 0.f;
+        if (lane == 0 && tx_ > 0) {
+            float c[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int yy = 2 * ty_ - 1 + i;
+                c[i] = (yy >= 0 && yy < H) ? xc[(int64_t)yy * W + 2 * tx_ - 1] : 0.f;
+            }
+            wn_bt(c[0], c[1], c[2], c[3], tl);
+        }
+        if (lane == 63 && tx_ < TW - 1) {
+            float c[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int yy = 2 * ty_ - 1 + i;
+                c[i] = (yy >= 0 && yy < H) ? xc[(int64_t)yy * W + 2 * tx_ + 2] : 0.f;
+            }
+            wn_bt(c[0], c[1], c[2], c[3], tr);
+        }
     }
-    d[0] = tx == 0 ? 0.f : L;
-    d[1] = cx;
-    d[2] = cy;
-    d[3] = tx == g.TW - 1 ? 0.f : R;
+    (void)r0ok; (void)r3ok;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        tl[i] = tx_ == 0 ? 0.f : tl[i];
+        tr[i] = tx_ == TW - 1 ? 0.f : tr[i];
+    }
 }
 
-// column j of t = B^T d
-__device__ __forceinline__ void wn_bt_col(const float (&d)[4][4], int j, float (&t)[4][4]) {
-    t[0][j] = d[0][j] - d[2][j];
-    t[1][j] = d[1][j] + d[2][j];
-    t[2][j] = d[2][j] - d[1][j];
-    t[3][j] = d[1][j] - d[3][j];
-}
-
-// row i of v = t B
-__device__ __forceinline__ void wn_b_row(const float (&t)[4][4], int i, float (&v)[4][4]) {
-    v[i][0] = t[i][0] - t[i][2];
-    v[i][1] = t[i][1] + t[i][2];
-    v[i][2] = t[i][2] - t[i][1];
-    v[i][3] = t[i][1] - t[i][3];
+// row i of v = t B, t's columns (tl, tx, ty, tr)
+__device__ __forceinline__ void wn_vrow(const float (&tl)[4], const float (&tx)[4],
+                                        const float (&ty)[4], const float (&tr)[4], int i,
+                                        float (&v)[4]) {
+    v[0] = tl[i] - ty[i];
+    v[1] = tx[i] + ty[i];
+    v[2] = ty[i] - tx[i];
+    v[3] = tx[i] - tr[i];
 }
 
 // LDS byte offset of a shared-memory pointer
@@ -225,25 +217,26 @@ __device__ __forceinline__ uint32_t wn_lds_addr(const void *p) {
         (const __attribute__((address_space(3))) void *)p);
 }
 
-// one 1-KiB LDS-DMA piece: 64 lanes x 16 bytes from per-lane sources into LDS
-// at the wave-uniform byte offset lds_dst (lane l at + 16 l).  Written as asm
-// because the compiler's own form would make every later LDS read wait for it;
-// its completion is the explicit waits below, then a barrier
-__device__ __forceinline__ void wn_glds16(const void *gsrc, uint32_t lds_dst) {
+// one 1-KiB LDS-DMA piece: 64 lanes x 16 bytes from sbase + voff
+// into LDS at the wave-uniform byte offset lds_dst (lane l at + 16 l).
+// Written as asm because the compiler's own form would make every later LDS
+// read wait for it; its completion is the explicit waits below, then a
+// barrier.  The address is a uniform SGPR base plus a fixed per-lane offset,
+// so a chunk's pieces cost no vector arithmetic
+__device__ __forceinline__ void wn_glds16(uint32_t voff, const void *sbase, uint32_t lds_dst) {
     unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-                 "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep)
-                 : "v"(gsrc), "s"(lds_dst)
+                 : "v"(voff), "s"(sbase), "s"(lds_dst)
                  : "memory");
 }
-typedef float f2v __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ float2 wn_f2(f2v v) { return make_float2(v.x, v.y); }
 
-// one patch row (two floats per lane), asm: the loop counts its loads itself
-// (its data is only read after a wait statement naming the register)
-__device__ __forceinline__ void wn_ld2(f2v &r, const float *p) {
-    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
+// one patch row (two floats per lane) at sbase + voff, asm: the loop counts
+// its loads itself (the data is only read after a wait statement naming the
+// register)
+__device__ __forceinline__ void wn_ld2(f2v &r, uint32_t voff, const float *sbase) {
+    asm volatile("global_load_dwordx2 %0, %1, %2" : "=v"(r) : "v"(voff), "s"(sbase) : "memory");
 }
 __device__ __forceinline__ void wn_wait_vm8() { asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); }
 __device__ __forceinline__ void wn_wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
@@ -265,7 +258,8 @@ __global__ __launch_bounds__(WN_T, 1) void wino_conv_kernel(
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int kb = blockIdx.y;
     const int64_t tile0 = (int64_t)blockIdx.x * WN_TB;
-    const int nch = g.C / WN_CC;
+    const int nch1 = g.C / WN_CC;                       // chunks per input
+    const int nch = g.x2 ? 2 * nch1 : nch1;             // over both inputs
 #ifdef WN_CLOCK
     const unsigned long long clk_t0 = __builtin_amdgcn_s_memtime();
     const unsigned long long clk_r0 = __builtin_amdgcn_s_memrealtime();
@@ -286,38 +280,58 @@ __global__ __launch_bounds__(WN_T, 1) void wino_conv_kernel(
         ttx = r - tty * g.TW;
     }
     const int64_t HW = (int64_t)g.H * g.W;
-    const float *xn = x + (int64_t)tn * g.C * HW;
-    const float4 *ub =
-        reinterpret_cast<const float4 *>(u) + ((int64_t)kb * nch + c0) * (WN_STAGE / 4);
-    xn += (int64_t)c0 * WN_CC * HW;
 
     // The loop's global loads are asm, counted by hand (two waits per chunk):
     //   top of chunk c:       chunk c+1's filter stage, LDS-DMA (8 pieces)
-    //   second half, K 8-15:  chunk c+2's patch rows into `raw` (8 loads),
+    //   second half:          chunk c+2's patch rows into `raw` (8 loads),
     //                         right after chunk c+1's rows were consumed
-    //   before K 0:           vmcnt(8) -- chunk c+1's rows (older than the 8
-    //                         stage pieces) have landed
+    //   before the second half: vmcnt(8) -- chunk c+1's rows (older than the
+    //                         8 stage pieces) have landed
     //   before the barrier:   vmcnt(8) -- the stage has landed (only chunk
     //                         c+2's rows may be in flight)
     // so a chunk's rows have ~1.5 chunks and its stage one chunk of cover.
+    // Addresses: a uniform SGPR base per chunk plus fixed per-lane byte
+    // offsets (x is under 4 GiB: smmd_wino3x3_supported).
     f2v raw[2][4];
-    const float *xrow[2][4];            // chunk 0's row pointers, clamped rows
+    uint32_t xoff[2][4];                // byte offsets of the rows from the chunk base
+    const int TH = g.H >> 1;
+    const bool r0ok = tty > 0, r3ok = tty < TH - 1;
 #pragma unroll
     for (int e = 0; e < 2; ++e)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int yc = min(max(2 * tty - 1 + i, 0), g.H - 1);
-            xrow[e][i] = xn + (int64_t)(2 * w + e) * HW + (int64_t)yc * g.W + 2 * ttx;
+            xoff[e][i] = (uint32_t)((((int64_t)tn * g.C + 2 * w + e) * HW + (int64_t)yc * g.W +
+                                     2 * ttx) * 4);
         }
-    auto load_row = [&](int cc, int e, int i) {
-        wn_ld2(raw[e][i], xrow[e][i] + (int64_t)cc * WN_CC * HW);
+    // chunk cc of this slice: its input and filter stage (wave-uniform)
+    auto xbase = [&](int cc) -> const float * {
+        const int c = c0 + cc;
+        return c < nch1 ? x + (int64_t)c * WN_CC * HW : g.x2 + (int64_t)(c - nch1) * WN_CC * HW;
+    };
+    auto ubase = [&](int cc) -> const float4 * {
+        const int c = c0 + cc;
+        return reinterpret_cast<const float4 *>(c < nch1 ? u : g.u2) +
+               ((int64_t)kb * nch1 + (c < nch1 ? c : c - nch1)) * (WN_STAGE / 4);
+    };
+    auto load_rows = [&](int cc) {
+        const float *sb = xbase(cc);
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) wn_ld2(raw[e][i], xoff[e][i], sb);
     };
     const uint32_t us_lds = wn_lds_addr(Us) + (uint32_t)__builtin_amdgcn_readfirstlane(w) * 8192u;
+    // (per-piece lane offsets, no instruction offset: an LDS-DMA's immediate
+    // offset would move its LDS destination too)
+    uint32_t uoff[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) uoff[i] = (uint32_t)((w * 512 + i * 64 + lane) * 16);
     auto load_u = [&](int cc) {
-        const float4 *src = ub + (int64_t)cc * (WN_STAGE / 4) + w * 512 + lane;
+        const float4 *sb = ubase(cc);
         const uint32_t dst = us_lds + (uint32_t)(cc & 1) * (WN_STAGE * 4);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) wn_glds16(src + i * 64, dst + i * 1024);
+        for (int i = 0; i < 8; ++i) wn_glds16(uoff[i], sb, dst + i * 1024);
     };
 #define WN_WAIT_ROWS(N_)                                                                     \
     asm volatile("s_waitcnt vmcnt(" #N_ ")"                                                  \
@@ -365,30 +379,28 @@ __global__ __launch_bounds__(WN_T, 1) void wino_conv_kernel(
     // then issued
     const float bias_k = (bias && tid < WN_KB) ? bias[kb * WN_KB + tid] : 0.f;
     load_u(0);
-#pragma unroll
-    for (int e = 0; e < 2; ++e)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) load_row(0, e, i);
+    load_rows(0);
     WN_WAIT_ROWS(0);
     {
-        float v_[2][16];
+        float tx[2][4], ty[2][4], tl[4], tr[4], v[2][4][4];
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
-            const float2 r_[4] = {wn_f2(raw[e][0]), wn_f2(raw[e][1]), wn_f2(raw[e][2]),
-                                  wn_f2(raw[e][3])};
-            wn_transform<EDGE>(r_, xn + (int64_t)(2 * w + e) * HW, tty, ttx, tok, g, lane, v_[e]);
+            wn_own(raw[e], r0ok, r3ok, tx[e], ty[e]);
+            wn_outer<EDGE>(tx[e], ty[e], xbase(0) + ((int64_t)tn * g.C + 2 * w + e) * HW, tty, ttx,
+                           r0ok, r3ok, lane, g.TW, g.H, g.W, tl, tr);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) wn_vrow(tl, tx[e], ty[e], tr, i, v[e][i]);
         }
         float2 *V2 = reinterpret_cast<float2 *>(Vs);
 #pragma unroll
-        for (int p = 0; p < 16; ++p)
-            V2[((p * 2 + (w >> 1)) * 64 + lane) * 2 + (w & 1)] = make_float2(v_[0][p], v_[1][p]);
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                V2[(((i * 4 + j) * 2 + (w >> 1)) * 64 + lane) * 2 + (w & 1)] =
+                    make_float2(v[0][i][j], v[1][i][j]);
     }
     if (tid < WN_KB) Bs[tid] = bias_k;
-    const int c1 = min(1, nchunk - 1);      // (a spare reload when there is one chunk)
-#pragma unroll
-    for (int e = 0; e < 2; ++e)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) load_row(c1, e, i);
+    load_rows(min(1, nchunk - 1));          // (a spare reload when there is one chunk)
     __syncthreads();
 
     for (int cc = 0; cc + 1 < nchunk; ++cc) {
@@ -422,14 +434,16 @@ __global__ __launch_bounds__(WN_T, 1) void wino_conv_kernel(
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
-        // second half: after each MFMA one slice of the next chunk's
-        // transform and LDS stores (the other buffer) or of chunk cc + 2's
-        // row loads, issued in the MFMA's shadow; sched_barrier pins the order
+        // second half: after each MFMA one slice of chunk cc + 1's transform
+        // and V stores (the other buffer) or of chunk cc + 2's row loads,
+        // issued in the MFMA's slot (the f32 MFMA holds the SIMD's VALU, so
+        // each slice costs its own issue time); sched_barrier pins the order
         WN_WAIT_ROWS(8);
         __builtin_amdgcn_sched_barrier(0);
-        float d0[4][4], d1[4][4], t0[4][4], t1[4][4], v0[4][4], v1[4][4];
-        const float *xc0 = xn + (int64_t)((cc + 1) * WN_CC + 2 * w) * HW;
+        float tx0[4], ty0[4], tx1[4], ty1[4], tl0[4], tr0[4], tl1[4], tr1[4], v0[4], v1[4];
+        const float *xc = xbase(cc + 1) + ((int64_t)tn * g.C + 2 * w) * HW;
         float2 *Vn = reinterpret_cast<float2 *>(Vs + nbuf * (WN_STAGE / 4));
+        const float *rb = xbase(cn);
 #pragma unroll
         for (int pp = 4; pp < 8; ++pp) {
             const int p = 2 * pp;
@@ -449,25 +463,27 @@ __global__ __launch_bounds__(WN_T, 1) void wino_conv_kernel(
                     b1 = V_[((p + 3) * 2 + hl) * 64 + th * 32 + l32];
                 }
                 const int K = (pp - 4) * 8 + m;
-                if (K < 8) {                         // patch rows of channel K / 4
-                    const int e = K >> 2, i = K & 3;
-                    wn_row<EDGE>(wn_f2(raw[e][i]), xc0 + e * HW, tty, ttx, tok, g, lane, i,
-                                 e ? d1[i] : d0[i]);
-                } else if (K < 16) {                 // chunk cc + 2's row, same register
-                    load_row(cn, (K - 8) >> 2, (K - 8) & 3);
-                } else if (K < 20) {                 // B^T d, column j, channel 0
-                    wn_bt_col(d0, K - 16, t0);
-                } else if (K < 24) {                 // (B^T d) B, row i, channel 0
-                    wn_b_row(t0, K - 20, v0);
-                } else if (K < 28) {
-                    wn_bt_col(d1, K - 24, t1);
-                } else {                             // channel 1's row i, both stored
-                    const int i = K - 28;
-                    wn_b_row(t1, i, v1);
+                if (K == 0) {                        // own columns, channel 0
+                    wn_own(raw[0], r0ok, r3ok, tx0, ty0);
+                } else if (K == 1) {                 // own columns, channel 1
+                    wn_own(raw[1], r0ok, r3ok, tx1, ty1);
+                } else if (K >= 2 && K < 10) {       // chunk cc + 2's rows, same registers
+                    const int e = (K - 2) >> 2, i = (K - 2) & 3;
+                    wn_ld2(raw[e][i], xoff[e][i], rb);
+                    if (K == 3)
+                        wn_outer<EDGE>(tx0, ty0, xc, tty, ttx, r0ok, r3ok, lane, g.TW, g.H, g.W,
+                                       tl0, tr0);
+                    else if (K == 5)
+                        wn_outer<EDGE>(tx1, ty1, xc + HW, tty, ttx, r0ok, r3ok, lane, g.TW, g.H,
+                                       g.W, tl1, tr1);
+                } else if (K >= 10 && K < 14) {      // row i of V, both channels, stored
+                    const int i = K - 10;
+                    wn_vrow(tl0, tx0, ty0, tr0, i, v0);
+                    wn_vrow(tl1, tx1, ty1, tr1, i, v1);
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
                         Vn[(((i * 4 + j) * 2 + (w >> 1)) * 64 + lane) * 2 + (w & 1)] =
-                            make_float2(v0[i][j], v1[i][j]);
+                            make_float2(v0[j], v1[j]);
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
@@ -590,9 +606,10 @@ extern "C" size_t smmd_wino3x3_filter_bytes(int ko, int ci) {
     return (size_t)16 * ko * ci * sizeof(float);
 }
 
+// (x under 4 GiB: the conv kernel addresses it by 32-bit byte offsets)
 extern "C" int smmd_wino3x3_supported(int n, int ci, int ko, int h, int w_img) {
     return n > 0 && ci > 0 && ko > 0 && ci % WN_CC == 0 && ko % WN_KB == 0 && h > 0 &&
-           w_img > 0 && h % 2 == 0 && w_img % 2 == 0 && (int64_t)n * ci * h * w_img < (1ll << 40);
+           w_img > 0 && h % 2 == 0 && w_img % 2 == 0 && (int64_t)n * ci * h * w_img < (1ll << 30);
 }
 
 extern "C" smmd_status smmd_wino3x3_filter(const float *w, int ko, int ci, int mode, float *u,
@@ -629,24 +646,29 @@ extern "C" size_t smmd_wino3x3_workspace_bytes(int n, int ci, int ko, int h, int
     return S > 1 ? (size_t)S * n * ko * h * w_img * sizeof(float) : 0;
 }
 
-static smmd_status wino3x3_conv(const float *x, const float *u, const float *bias, float *y,
-                                int n, int ci, int ko, int h, int w_img, void *ws,
-                                size_t ws_bytes, int relu, smmd_stream_t stream) {
+static smmd_status wino3x3_conv(const float *x, const float *u, const float *x2,
+                                const float *u2, const float *bias, float *y, int n, int ci,
+                                int ko, int h, int w_img, void *ws, size_t ws_bytes, int relu,
+                                smmd_stream_t stream) {
     if (n < 0 || ci <= 0 || ko <= 0 || h < 0 || w_img < 0) return SMMD_EINVAL;
     if (n == 0 || h == 0 || w_img == 0) return SMMD_OK;
-    if (!x || !u || !y) return SMMD_EINVAL;
+    if (!x || !u || !y || (!x2 != !u2)) return SMMD_EINVAL;
     if (!smmd_wino3x3_supported(n, ci, ko, h, w_img)) return SMMD_EUNSUPPORTED;
     if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y) |
-         reinterpret_cast<uintptr_t>(u)) & 15)
+         reinterpret_cast<uintptr_t>(u) | reinterpret_cast<uintptr_t>(x2) |
+         reinterpret_cast<uintptr_t>(u2)) & 15)
         return SMMD_EINVAL;
+    const int pair = x2 ? 2 : 1;
     WnGeom g;
+    g.x2 = x2;
+    g.u2 = u2;
     g.N = n; g.C = ci; g.K = ko; g.H = h; g.W = w_img;
     g.TW = w_img / 2;
     g.Timg = (h / 2) * g.TW;
     g.T = (int64_t)n * g.Timg;
     const int64_t tb = (g.T + WN_TB - 1) / WN_TB;
     if (tb > 0x7fffffff) return SMMD_EINVAL;
-    const int S = wino_slices(tb * (ko / WN_KB), ci / WN_CC, h * w_img);
+    const int S = wino_slices(tb * (ko / WN_KB), pair * ci / WN_CC, h * w_img);
     const int64_t total = (int64_t)n * ko * h * w_img;
     float *out = y;
     if (S > 1) {
@@ -686,11 +708,28 @@ static smmd_status wino3x3_conv(const float *x, const float *u, const float *bia
 extern "C" smmd_status smmd_wino3x3_conv(const float *x, const float *u, const float *bias,
                                          float *y, int n, int ci, int ko, int h, int w_img,
                                          void *ws, size_t ws_bytes, smmd_stream_t stream) {
-    return wino3x3_conv(x, u, bias, y, n, ci, ko, h, w_img, ws, ws_bytes, 0, stream);
+    return wino3x3_conv(x, u, nullptr, nullptr, bias, y, n, ci, ko, h, w_img, ws, ws_bytes, 0,
+                        stream);
+}
+
+extern "C" size_t smmd_wino3x3_conv2_workspace_bytes(int n, int ci, int ko, int h, int w_img) {
+    if (!smmd_wino3x3_supported(n, ci, ko, h, w_img)) return 0;
+    const int64_t T = (int64_t)n * (h / 2) * (w_img / 2);
+    const int S = wino_slices(((T + WN_TB - 1) / WN_TB) * (ko / WN_KB), 2 * ci / WN_CC, h * w_img);
+    return S > 1 ? (size_t)S * n * ko * h * w_img * sizeof(float) : 0;
+}
+
+extern "C" smmd_status smmd_wino3x3_conv2(const float *x, const float *u, const float *x2,
+                                          const float *u2, const float *bias, float *y, int n,
+                                          int ci, int ko, int h, int w_img, void *ws,
+                                          size_t ws_bytes, smmd_stream_t stream) {
+    if (!x2 || !u2) return SMMD_EINVAL;
+    return wino3x3_conv(x, u, x2, u2, bias, y, n, ci, ko, h, w_img, ws, ws_bytes, 0, stream);
 }
 
 extern "C" smmd_status smmd_wino3x3_conv_relu(const float *x, const float *u, const float *bias,
                                               float *y, int n, int ci, int ko, int h, int w_img,
                                               void *ws, size_t ws_bytes, smmd_stream_t stream) {
-    return wino3x3_conv(x, u, bias, y, n, ci, ko, h, w_img, ws, ws_bytes, 1, stream);
+    return wino3x3_conv(x, u, nullptr, nullptr, bias, y, n, ci, ko, h, w_img, ws, ws_bytes, 1,
+                        stream);
 }

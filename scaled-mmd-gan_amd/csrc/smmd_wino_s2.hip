@@ -36,14 +36,17 @@ constexpr size_t S2_LDS = 2 * 2 * S2_STAGE * sizeof(float) + S2_KB * sizeof(floa
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f4v __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ float s2_from_left(float v) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
-                                                                 0x138, 0xf, 0xf, false));
+// neighbour lanes' values, 0 where the source lane is outside the wave
+// (bound_ctrl: no preset of the destination; every VALU instruction costs
+// SIMD time beside the f32 MFMA, profiles/r12/mfma_valu_coissue.txt)
+__device__ __forceinline__ float s2_from_left(float v) {    // lane l gets lane l-1's v
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x138,
+                                                              0xf, 0xf, true));
 }
 
-__device__ __forceinline__ float s2_from_right(float v) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
-                                                                 0x130, 0xf, 0xf, false));
+__device__ __forceinline__ float s2_from_right(float v) {   // lane l gets lane l+1's v
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x130,
+                                                              0xf, 0xf, true));
 }
 
 // The 16 taps of filter q of W': with sig NULL read from w [q][16]; else w is
@@ -128,6 +131,9 @@ __global__ void s2_filter_kernel(const float *__restrict__ w, int KO, int CI,
 struct S2Geom {
     int N, C, K, H, W, TW, Timg;   // H, W: the input's; output H/2 x W/2
     int64_t T, slab;
+    // the pair form (smmd_wino4x4s2_conv2): y = conv(x, U) + conv(x2, U2),
+    // the input-channel loop running over both inputs
+    const float *x2, *u2;
 };
 
 template <bool EDGE>
@@ -142,7 +148,8 @@ __global__ __launch_bounds__(S2_T, 2) void s2_conv_kernel(
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int kb = blockIdx.y;
     const int64_t tile0 = (int64_t)blockIdx.x * S2_TB;
-    const int nch = g.C / S2_CC;
+    const int nch1 = g.C / S2_CC;                       // chunks per input
+    const int nch = g.x2 ? 2 * nch1 : nch1;             // over both inputs
     const int c0 = (int)((int64_t)nch * blockIdx.z / gridDim.z);
     const int nchunk = (int)((int64_t)nch * (blockIdx.z + 1) / gridDim.z) - c0;
     y += (int64_t)blockIdx.z * g.slab;
@@ -160,21 +167,40 @@ __global__ __launch_bounds__(S2_T, 2) void s2_conv_kernel(
         ttx = r - tty * g.TW;
     }
     const int64_t HW = (int64_t)g.H * g.W;
-    const float *xn = x + ((int64_t)tn * g.C + (int64_t)c0 * S2_CC + e) * HW;
-    const float4 *ub =
-        reinterpret_cast<const float4 *>(u) + ((int64_t)kb * nch + c0) * (S2_STAGE / 4);
+    // the lane's three patch rows in chunk 0 of input 1 (clamped rows), and
+    // chunk cc's wave-uniform byte shift from there (input 2: the distance
+    // between the two tensors; integer arithmetic, no per-lane select)
+    const float *xrow[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const int yc = min(max(4 * tty - 1 + pi + 2 * a, 0), g.H - 1);
+        xrow[a] = x + ((int64_t)tn * g.C + e) * HW + (int64_t)yc * g.W + 4 * ttx;
+    }
+    const int64_t x2shift = g.x2 ? (int64_t)(reinterpret_cast<uintptr_t>(g.x2) -
+                                             reinterpret_cast<uintptr_t>(x)) : 0;
+    auto xshift = [&](int cc) -> int64_t {      // bytes from chunk 0 of input 1
+        const int c = c0 + cc;
+        return c < nch1 ? (int64_t)c * S2_CC * HW * 4
+                        : x2shift + (int64_t)(c - nch1) * S2_CC * HW * 4;
+    };
+    auto xchunk = [&](int cc) -> const float * {   // the lane's image and channel (EDGE)
+        return reinterpret_cast<const float *>(
+            reinterpret_cast<const char *>(x + ((int64_t)tn * g.C + e) * HW) + xshift(cc));
+    };
+    auto uchunk = [&](int cc) -> const float4 * {
+        const int c = c0 + cc;
+        return reinterpret_cast<const float4 *>(c < nch1 ? u : g.u2) +
+               ((int64_t)kb * nch1 + (c < nch1 ? c : c - nch1)) * (S2_STAGE / 4);
+    };
 
     float4 raw[3];
     f4v ur[5];
     auto load = [&](int cc) {
-        const float *xc = xn + (int64_t)cc * S2_CC * HW;
+        const int64_t sh = xshift(cc);
 #pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            const int yy = 4 * tty - 1 + pi + 2 * a;
-            const int yc = min(max(yy, 0), g.H - 1);
-            raw[a] = *reinterpret_cast<const float4 *>(xc + (int64_t)yc * g.W + 4 * ttx);
-        }
-        const float4 *src = ub + (int64_t)cc * (S2_STAGE / 4) + tid;
+        for (int a = 0; a < 3; ++a)
+            raw[a] = *reinterpret_cast<const float4 *>(reinterpret_cast<const char *>(xrow[a]) + sh);
+        const float4 *src = uchunk(cc) + tid;
 #pragma unroll
         for (int i = 0; i < 5; ++i)
             if (i * S2_T + tid < S2_STAGE / 4)
@@ -185,7 +211,7 @@ __global__ __launch_bounds__(S2_T, 2) void s2_conv_kernel(
 #pragma unroll
         for (int i = 0; i < 5; ++i)
             if (i * S2_T + tid < S2_STAGE / 4) U[i * S2_T] = ur[i];
-        const float *xc = xn + (int64_t)cc * S2_CC * HW;
+        const float *xc = xchunk(cc);
         // rows: columns 4tx-1 .. 4tx+4; pj = 0 takes (-1, 1, 3), pj = 1 (0, 2, 4)
         float d0[3][3], d1[3][3];
 #pragma unroll
@@ -343,10 +369,13 @@ struct S2TGeom {
     int64_t T, slab;
 };
 
-template <bool EDGE>
-__global__ __launch_bounds__(S2_T, 2) void s2t_conv_kernel(
-    const float *__restrict__ gy, const float *__restrict__ u, const float *__restrict__ bias,
-    float *__restrict__ dx, S2TGeom g) {
+// the body for output phase (QI, QJ): the phase is a compile-time constant, so
+// its row and column picks cost no per-lane selects (every VALU instruction
+// costs SIMD time beside the f32 MFMA, profiles/r12/mfma_valu_coissue.txt)
+template <bool EDGE, int QI, int QJ>
+__device__ __forceinline__ void s2t_body(const float *__restrict__ gy, const float *__restrict__ u,
+                                         const float *__restrict__ bias, float *__restrict__ dx,
+                                         const S2TGeom &g) {
     extern __shared__ float4 s2_lds[];
     float4 *const Vs = s2_lds;
     float4 *const Us = s2_lds + 2 * (S2_STAGE / 4);
@@ -354,7 +383,8 @@ __global__ __launch_bounds__(S2_T, 2) void s2t_conv_kernel(
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int cb = blockIdx.y;
-    const int q = blockIdx.z & 3, qi = q >> 1, qj = q & 1;
+    constexpr int q = QI * 2 + QJ, qi = QI, qj = QJ;
+    const int THg = g.Hg >> 1;           // phase tile rows per image
     const int sl = blockIdx.z >> 2, S = gridDim.z >> 2;
     const int64_t tile0 = (int64_t)blockIdx.x * S2_TB;
     const int nch = g.K / 8;
@@ -409,7 +439,10 @@ __global__ __launch_bounds__(S2_T, 2) void s2t_conv_kernel(
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
                 const int yy = 2 * tty - 1 + qi + a;
-                const bool row = tok && yy >= 0 && yy < g.Hg;
+                // rows 2ty - 1 (phase row 0) and 2ty + 2 (phase row 1) can be
+                // outside the image; a tile past the end is never stored
+                const bool row = (a == 0 && qi == 0) ? tty > 0
+                                 : (a == 2 && qi == 1) ? tty < THg - 1 : true;
                 const float cx = row ? raw[e][a].x : 0.f, cy = row ? raw[e][a].y : 0.f;
                 float L = s2_from_left(cy), R = s2_from_right(cx);
                 if (EDGE) {
@@ -505,6 +538,18 @@ __global__ __launch_bounds__(S2_T, 2) void s2t_conv_kernel(
     }
 }
 
+template <bool EDGE>
+__global__ __launch_bounds__(S2_T, 2) void s2t_conv_kernel(
+    const float *__restrict__ gy, const float *__restrict__ u, const float *__restrict__ bias,
+    float *__restrict__ dx, S2TGeom g) {
+    switch (blockIdx.z & 3) {           // the block's output phase (wave-uniform)
+    case 0: s2t_body<EDGE, 0, 0>(gy, u, bias, dx, g); break;
+    case 1: s2t_body<EDGE, 0, 1>(gy, u, bias, dx, g); break;
+    case 2: s2t_body<EDGE, 1, 0>(gy, u, bias, dx, g); break;
+    default: s2t_body<EDGE, 1, 1>(gy, u, bias, dx, g); break;
+    }
+}
+
 __global__ void s2_reduce_kernel(const float *__restrict__ part, const float *__restrict__ bias,
                                  float *__restrict__ y, int64_t n4, int S, int K, int HW) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -591,17 +636,21 @@ extern "C" size_t smmd_wino4x4s2_workspace_bytes(int n, int ci, int ko, int h, i
     return S > 1 ? (size_t)S * n * ko * (h / 2) * (w_img / 2) * sizeof(float) : 0;
 }
 
-extern "C" smmd_status smmd_wino4x4s2_conv(const float *x, const float *u, const float *bias,
-                                           float *y, int n, int ci, int ko, int h, int w_img,
-                                           void *ws, size_t ws_bytes, smmd_stream_t stream) {
+static smmd_status s2_conv(const float *x, const float *u, const float *x2, const float *u2,
+                           const float *bias, float *y, int n, int ci, int ko, int h, int w_img,
+                           void *ws, size_t ws_bytes, smmd_stream_t stream) {
     if (n < 0 || ci <= 0 || ko <= 0 || h < 0 || w_img < 0) return SMMD_EINVAL;
     if (n == 0 || h == 0 || w_img == 0) return SMMD_OK;
-    if (!x || !u || !y) return SMMD_EINVAL;
+    if (!x || !u || !y || (!x2 != !u2)) return SMMD_EINVAL;
     if (!smmd_wino4x4s2_supported(n, ci, ko, h, w_img)) return SMMD_EUNSUPPORTED;
     if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y) |
-         reinterpret_cast<uintptr_t>(u)) & 15)
+         reinterpret_cast<uintptr_t>(u) | reinterpret_cast<uintptr_t>(x2) |
+         reinterpret_cast<uintptr_t>(u2)) & 15)
         return SMMD_EINVAL;
+    const int pair = x2 ? 2 : 1;
     S2Geom g;
+    g.x2 = x2;
+    g.u2 = u2;
     g.N = n; g.C = ci; g.K = ko; g.H = h; g.W = w_img;
     g.TW = w_img / 4;
     g.Timg = (h / 4) * g.TW;
@@ -609,7 +658,7 @@ extern "C" smmd_status smmd_wino4x4s2_conv(const float *x, const float *u, const
     const int64_t tb = (g.T + S2_TB - 1) / S2_TB;
     if (tb > 0x7fffffff) return SMMD_EINVAL;
     const int HWo = (h / 2) * (w_img / 2);
-    const int S = s2_slices(tb * (ko / S2_KB), ci / S2_CC, HWo);
+    const int S = s2_slices(tb * (ko / S2_KB), pair * ci / S2_CC, HWo);
     const int64_t total = (int64_t)n * ko * HWo;
     float *out = y;
     if (S > 1) {
@@ -642,6 +691,28 @@ extern "C" smmd_status smmd_wino4x4s2_conv(const float *x, const float *u, const
     s2_reduce_kernel<<<dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st>>>(out, bias, y, n4,
                                                                               S, ko, HWo);
     return last_launch_status();
+}
+
+extern "C" smmd_status smmd_wino4x4s2_conv(const float *x, const float *u, const float *bias,
+                                           float *y, int n, int ci, int ko, int h, int w_img,
+                                           void *ws, size_t ws_bytes, smmd_stream_t stream) {
+    return s2_conv(x, u, nullptr, nullptr, bias, y, n, ci, ko, h, w_img, ws, ws_bytes, stream);
+}
+
+extern "C" size_t smmd_wino4x4s2_conv2_workspace_bytes(int n, int ci, int ko, int h, int w_img) {
+    if (!smmd_wino4x4s2_supported(n, ci, ko, h, w_img)) return 0;
+    const int64_t T = (int64_t)n * (h / 4) * (w_img / 4);
+    const int S = s2_slices(((T + S2_TB - 1) / S2_TB) * (ko / S2_KB), 2 * ci / S2_CC,
+                            (h / 2) * (w_img / 2));
+    return S > 1 ? (size_t)S * n * ko * (h / 2) * (w_img / 2) * sizeof(float) : 0;
+}
+
+extern "C" smmd_status smmd_wino4x4s2_conv2(const float *x, const float *u, const float *x2,
+                                            const float *u2, const float *bias, float *y, int n,
+                                            int ci, int ko, int h, int w_img, void *ws,
+                                            size_t ws_bytes, smmd_stream_t stream) {
+    if (!x2 || !u2) return SMMD_EINVAL;
+    return s2_conv(x, u, x2, u2, bias, y, n, ci, ko, h, w_img, ws, ws_bytes, stream);
 }
 
 extern "C" int smmd_wino4x4s2t_supported(int n, int k, int c, int hg, int wg) {

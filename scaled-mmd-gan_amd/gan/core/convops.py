@@ -302,6 +302,31 @@ def _wino_conv(x, w, b, mode, relu=False):
     return y
 
 
+def _wino_conv2(x, w, x2, w2):
+    """conv(x, w) + conv(x2, w2) (3x3 stride 1 SAME, same shapes) in ONE
+    smmd_wino3x3_conv2 launch: the input-channel loop runs over both pairs."""
+    from . import _lib
+    x, x2 = x.contiguous(), x2.contiguous()
+    w, w2 = w.contiguous(), w2.contiguous()
+    _lib.require_cuda(x, w, x2, w2)
+    N, ci, H, W = x.shape
+    co = w.shape[0]
+    L = _lib.lib()
+    u = _wino_filter(w, co, ci, 0)
+    u2 = _wino_filter(w2, co, ci, 0)
+    y = torch.empty((N, co, H, W), dtype=x.dtype, device=x.device)
+    nb = L.smmd_wino3x3_conv2_workspace_bytes(N, ci, co, H, W)
+    ws = _lib.workspace('wino', nb, x.device) if nb else None
+    _lib.add_bytes('smmd_wino3x3_conv', (2 * x.numel() + y.numel()) * 4)
+    _lib.add_flops('smmd_wino3x3_conv', 2 * 2 * 16 * N * (H // 2) * (W // 2) * ci * co)
+    with _lib.timed('smmd_wino3x3_conv'):
+        st = L.smmd_wino3x3_conv2(_lib.ptr(x), _lib.ptr(u), _lib.ptr(x2), _lib.ptr(u2), None,
+                                  _lib.ptr(y), N, ci, co, H, W, _lib.ptr(ws), nb,
+                                  _lib.stream_handle(x.device))
+    _lib.check(st, 'smmd_wino3x3_conv2')
+    return y
+
+
 # the weight gradient of those layers (SMMD_WINO_WGRAD=0: MIOpen)
 WINO_WGRAD = os.environ.get('SMMD_WINO_WGRAD', '1') != '0'
 
@@ -424,6 +449,31 @@ def _s2_conv(x, w, b):
         st = L.smmd_wino4x4s2_conv(_lib.ptr(x), _lib.ptr(u), _lib.ptr(b), _lib.ptr(y), N, ci, co,
                                    H, W, _lib.ptr(ws), nb, _lib.stream_handle(x.device))
     _lib.check(st, 'smmd_wino4x4s2_conv')
+    return y
+
+
+def _s2_conv2(x, w, x2, w2):
+    """conv(x, w) + conv(x2, w2) (4x4 stride 2 pad 1, same shapes) in ONE
+    smmd_wino4x4s2_conv2 launch."""
+    from . import _lib
+    x, x2 = x.contiguous(), x2.contiguous()
+    w, w2 = w.contiguous(), w2.contiguous()
+    _lib.require_cuda(x, w, x2, w2)
+    N, ci, H, W = x.shape
+    co = w.shape[0]
+    L = _lib.lib()
+    u = _s2_filter(w, False)
+    u2 = _s2_filter(w2, False)
+    y = torch.empty((N, co, H // 2, W // 2), dtype=x.dtype, device=x.device)
+    nb = L.smmd_wino4x4s2_conv2_workspace_bytes(N, ci, co, H, W)
+    ws = _lib.workspace('wino_s2', nb, x.device) if nb else None
+    _lib.add_bytes('smmd_wino4x4s2_conv', (2 * x.numel() + y.numel()) * 4)
+    _lib.add_flops('smmd_wino4x4s2_conv', 2 * 2 * 9 * N * (H // 4) * (W // 4) * 4 * ci * co)
+    with _lib.timed('smmd_wino4x4s2_conv'):
+        st = L.smmd_wino4x4s2_conv2(_lib.ptr(x), _lib.ptr(u), _lib.ptr(x2), _lib.ptr(u2), None,
+                                    _lib.ptr(y), N, ci, co, H, W, _lib.ptr(ws), nb,
+                                    _lib.stream_handle(x.device))
+    _lib.check(st, 'smmd_wino4x4s2_conv2')
     return y
 
 
@@ -560,6 +610,23 @@ def _fwd(x, w, b, stride, padding):
     return F.conv2d(x, materialize(w), b, stride, padding)
 
 
+# conv(x, w) + conv(x2, w2) as one pair launch (SMMD_CONV_PAIR=0: two
+# launches and an add)
+CONV_PAIR = os.environ.get('SMMD_CONV_PAIR', '1') != '0'
+
+
+def _fwd2(x, w, x2, w2, stride, padding):
+    """conv(x, w) + conv(x2, w2) on one library launch when both convs take
+    the same Winograd path; None otherwise."""
+    if not (CONV_PAIR and x.shape == x2.shape and w.shape == w2.shape):
+        return None
+    if _is_wino(x, w, stride, padding, 0) and _is_wino(x2, w2, stride, padding, 0):
+        return _wino_conv2(x, w, x2, w2)
+    if _is_s2(x, w, stride, padding) and _is_s2(x2, w2, stride, padding):
+        return _s2_conv2(x, w, x2, w2)
+    return None
+
+
 def _bwd(gy, x, w, stride, padding, mask):
     """(Dx, Dw) of conv(x, w) at upstream gy via the native backward kernels."""
     if mask[0] and not (_is_wino(gy, w, stride, padding, 1) or _is_s2t(gy, w, stride, padding)):
@@ -624,16 +691,24 @@ class _ConvBackward(torch.autograd.Function):
         g_x = g_w = g_gy = None
         if ggx is not None:
             ggx = ggx.contiguous(memory_format=_fmt(x))
-            if need_gy:
+        # the upstream's gradient conv(ggx, w) + conv(x, ggw): one pair launch
+        # when both take the same Winograd path, else two convs and their sum
+        pair = None
+        if need_gy and ggx is not None and ggw is not None:
+            pair = _fwd2(ggx, w, x, ggw, stride, padding)
+        if ggx is not None:
+            if need_gy and pair is None:
                 g_gy = _fwd(ggx, w, None, stride, padding)
             if need_w:
                 _, g_w = _bwd(gy, ggx, w, stride, padding, (False, True))
         if ggw is not None:
-            if need_gy:
+            if need_gy and pair is None:
                 t = _fwd(x, ggw, None, stride, padding)
                 g_gy = t if g_gy is None else g_gy + t
             if need_x:
                 g_x, _ = _bwd(gy, x, ggw, stride, padding, (True, False))
+        if pair is not None:
+            g_gy = pair
         return g_x, g_w, g_gy, None, None, None
 
 

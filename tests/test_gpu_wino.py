@@ -130,6 +130,50 @@ def test_convops_wino_double_backward_vs_float64(shape):
         assert _rel(a, r) < (2e-5 if n in ('gw', 'hx', 'hw') else TOL), n
 
 
+# the pair form: odd tiles, the edge kernel, split reductions over the two
+# inputs (512 -> 64 at 8 x 8; 64 -> 64 at batch 1), the critic's layers
+PAIR_SHAPES = [(2, 8, 64, 6, 6), (1, 8, 64, 4, 130), (4, 512, 64, 8, 8), (1, 64, 64, 8, 8),
+               (3, 128, 128, 32, 32), (2, 256, 256, 16, 16)]
+
+
+@pytest.mark.parametrize('shape', PAIR_SHAPES)
+def test_wino_pair_conv_vs_float64(shape):
+    """smmd_wino3x3_conv2: conv(x, w) + conv(x2, w2) in one launch against the
+    float64 sum of the two convolutions, through convops (the double
+    backward's conv(ggx, w) + conv(x, ggw))."""
+    from gan.core import convops
+    N, C, K, H, W = shape
+    g = torch.Generator(device=DEV).manual_seed(N + C + K + H + W)
+    x, x2 = (torch.randn(N, C, H, W, device=DEV, generator=g) for _ in range(2))
+    w, w2 = (torch.randn(K, C, 3, 3, device=DEV, generator=g) for _ in range(2))
+    y = convops._fwd2(x, w, x2, w2, [1, 1], [1, 1])
+    assert y is not None
+    ref = (F.conv2d(x.double().cpu(), w.double().cpu(), padding=1) +
+           F.conv2d(x2.double().cpu(), w2.double().cpu(), padding=1))
+    assert _rel(y, ref) < TOL
+    assert torch.equal(y, convops._fwd2(x, w, x2, w2, [1, 1], [1, 1]))    # deterministic
+
+
+def test_wino_pair_off_matches_on(monkeypatch):
+    """SMMD_CONV_PAIR=0 (two launches and an add) agrees with the pair launch
+    through a critic-shaped double backward."""
+    from gan.core import convops
+    g = torch.Generator(device=DEV).manual_seed(3)
+    x = torch.randn(4, 128, 16, 16, device=DEV, generator=g, requires_grad=True)
+    w = (torch.randn(128, 128, 3, 3, device=DEV, generator=g) / 34.0).requires_grad_(True)
+    A = torch.randn(4, 128, 16, 16, device=DEV, generator=g, requires_grad=True)
+    B = torch.randn(4, 128, 16, 16, device=DEV, generator=g)
+    D = torch.randn(128, 128, 3, 3, device=DEV, generator=g)
+    res = []
+    for on in (True, False):
+        monkeypatch.setattr(convops, 'CONV_PAIR', on)
+        y = convops.conv2d(x, w, None, 1, 1)
+        gx, gw = torch.autograd.grad((y * A).sum(), (x, w), create_graph=True)
+        hA, = torch.autograd.grad((gx * B).sum() + (gw * D).sum(), (A,))
+        res.append(hA)
+    assert _rel(res[0], res[1]) < 1e-6
+
+
 def test_wino_off_matches_on():
     """SMMD_WINO=0 (MIOpen) and the Winograd path agree on a critic-shaped layer."""
     from gan.core import convops

@@ -59,6 +59,23 @@ def test_s2_conv_and_transposed_vs_float64(shape):
         assert _rel(gx, refx) < TOL
 
 
+@pytest.mark.parametrize('shape', [(2, 2, 64, 4, 4), (1, 64, 64, 4, 264), (4, 512, 64, 8, 8),
+                                   (4, 64, 128, 64, 64), (4, 512, 1024, 8, 8)])
+def test_s2_pair_conv_vs_float64(shape):
+    """smmd_wino4x4s2_conv2: conv(x, w) + conv(x2, w2) (stride 2) in one launch
+    against the float64 sum (edge kernel, split reductions over both inputs)."""
+    from gan.core import convops
+    N, C, K, H, W = shape
+    g = torch.Generator(device=DEV).manual_seed(N + C + K + H + W)
+    x, x2 = (torch.randn(N, C, H, W, device=DEV, generator=g) for _ in range(2))
+    w, w2 = (torch.randn(K, C, 4, 4, device=DEV, generator=g) for _ in range(2))
+    y = convops._fwd2(x, w, x2, w2, [2, 2], [1, 1])
+    assert y is not None
+    ref = (F.conv2d(x.double().cpu(), w.double().cpu(), stride=2, padding=1) +
+           F.conv2d(x2.double().cpu(), w2.double().cpu(), stride=2, padding=1))
+    assert _rel(y, ref) < TOL
+
+
 @pytest.mark.parametrize('shape', [(2, 64, 64, 8, 8), (3, 128, 64, 12, 4), (4, 64, 64, 8, 8),
                                    (2, 32, 64, 32, 32)])
 def test_s2_double_backward_vs_float64(shape):
