@@ -295,9 +295,14 @@ static_assert(Wg2<16>::LDS <= 160 * 1024 && Wg2<4>::LDS <= 160 * 1024, "LDS budg
 static_assert(Wg2<16>::LDS >= 4 * 64 * 64 * sizeof(float), "epilogue hand-off fits");
 static_assert(Wg2<16>::NH * WG2_T == 64 * Wg2<16>::XR * 2, "halo split");
 
-template <int CT>
-__global__ __launch_bounds__(WG2_T, 1) void wino_wgrad2_kernel(
-    const float *__restrict__ x, const float *__restrict__ gy, float *__restrict__ part, WgGeom g) {
+// the body for the waves of transform half PH (rows 2 PH, 2 PH + 1 of the
+// 4 x 4 transforms): a compile-time constant, so the half's picks cost no
+// per-lane selects (every VALU instruction costs SIMD time beside the f32
+// MFMA, profiles/r12/mfma_valu_coissue.txt)
+template <int CT, int PH>
+__device__ __forceinline__ void wgrad2_body(const float *__restrict__ x,
+                                            const float *__restrict__ gy,
+                                            float *__restrict__ part, const WgGeom &g) {
     using P = Wg2<CT>;
     extern __shared__ float4 wg2_lds4[];
     float *const lds = reinterpret_cast<float *>(wg2_lds4);
@@ -396,7 +401,8 @@ __global__ __launch_bounds__(WG2_T, 1) void wino_wgrad2_kernel(
         }
     };
 
-    const int ph = w >> 2, kh = (w >> 1) & 1, ch = w & 1, hl = lane >> 5, l32 = lane & 31;
+    constexpr int ph = PH;
+    const int kh = (w >> 1) & 1, ch = w & 1, hl = lane >> 5, l32 = lane & 31;
     // the lane's raw inputs of k-step s from buffer buf: x rows 2 ty + ph ..
     // 2 ty + ph + 2 of the 4 x 4 patch (channel c = ch 32 + l32) and the 2 x 2
     // gy tile (k = kh 32 + l32) of tile tau = 2 s + hl
@@ -541,6 +547,16 @@ __global__ __launch_bounds__(WG2_T, 1) void wino_wgrad2_kernel(
         }
         __syncthreads();
     }
+}
+
+template <int CT>
+__global__ __launch_bounds__(WG2_T, 1) void wino_wgrad2_kernel(
+    const float *__restrict__ x, const float *__restrict__ gy, float *__restrict__ part, WgGeom g) {
+    // waves 4..7 are half 1 (a wave-uniform, scalar branch)
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 8))
+        wgrad2_body<CT, 1>(x, gy, part, g);
+    else
+        wgrad2_body<CT, 0>(x, gy, part, g);
 }
 
 // out[i] = sum of the S slabs of n4 float4 each, in slab order (the last

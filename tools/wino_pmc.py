@@ -4,7 +4,7 @@ stride-2 layers (smmd_wino4x4s2_conv) at batch 64, random data, --iters
 launches each, through the stamped library.  Prints per-shape HIP-event
 times (no profiler: run it bare for times, under rocprofv3 --pmc for counters).
 
-python tools/wino_pmc.py [--iters N] [--only 3x3|s2|s2t] [--lib PATH]
+python tools/wino_pmc.py [--iters N] [--only 3x3|s2|s2t|wgrad] [--lib PATH]
 (--lib: another build of the library, unstamped, for interleaved A/B runs)
 """
 import argparse
@@ -143,6 +143,24 @@ def main():
                                                'executed_tflops': round(fl / us / 1e6, 1),
                                                'mfma_frac': round(fl / us / 1e6 / 157.3, 3)}
             print(json.dumps(out['s2t_%d_%d_%d' % (C, K, H)]), flush=True)
+    if a.only in ('', 'wgrad'):
+        for (N, C, K, H) in SHAPES_3X3:
+            x = torch.randn(N, C, H, H, device=dev)
+            gy = torch.randn(N, K, H, H, device=dev)
+            gw = torch.empty(K, C, 3, 3, device=dev)
+            nb = L.smmd_wino3x3_wgrad_workspace_bytes(N, C, K, H, H)
+            ws = torch.empty(max(nb // 4, 4), device=dev)
+
+            def f():
+                s = L.smmd_wino3x3_wgrad(_lib.ptr(x), _lib.ptr(gy), _lib.ptr(gw), N, C, K, H, H,
+                                         _lib.ptr(ws), nb, st)
+                assert s == 0
+            us = timed(f, a.iters)
+            fl = 2.0 * 16 * N * (H // 2) ** 2 * C * K
+            out['wgrad_%d_%d_%d' % (C, K, H)] = {'us': round(us, 2),
+                                                 'executed_tflops': round(fl / us / 1e6, 1),
+                                                 'mfma_frac': round(fl / us / 1e6 / 157.3, 3)}
+            print(json.dumps(out['wgrad_%d_%d_%d' % (C, K, H)]), flush=True)
     print(json.dumps(out))
 
 
