@@ -232,11 +232,18 @@ __device__ __forceinline__ void wn_glds16(uint32_t voff, const void *sbase, uint
                  : "memory");
 }
 
-// one patch row (two floats per lane) at sbase + voff, asm: the loop counts
-// its loads itself (the data is only read after a wait statement naming the
-// register)
-__device__ __forceinline__ void wn_ld2(f2v &r, uint32_t voff, const float *sbase) {
-    asm volatile("global_load_dwordx2 %0, %1, %2" : "=v"(r) : "v"(voff), "s"(sbase) : "memory");
+// one patch row (two floats per lane) at sbase + voff: an ordinary load, so
+// the compiler tracks it (an asm load's destination would count as written
+// at once, and the compiler may copy or reuse the register before the data
+// lands).  Its waits also retire the older filter-stage LDS-DMA (vmcnt is
+// in order): safe, at worst early.
+// (a buffer load: the base in a uniform descriptor, the lane's 32-bit byte
+// offset in one VGPR -- no 64-bit address arithmetic per load)
+__device__ __forceinline__ f2v wn_ld2(uint32_t voff, __amdgpu_buffer_rsrc_t rs) {
+    return __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, 0, 0));
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wn_rsrc(const float *base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(base), 0, 0x7fffffff, 0x00020000);
 }
 __device__ __forceinline__ void wn_wait_vm8() { asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); }
 __device__ __forceinline__ void wn_wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
@@ -281,15 +288,13 @@ __global__ __launch_bounds__(WN_T, 1) void wino_conv_kernel(
     }
     const int64_t HW = (int64_t)g.H * g.W;
 
-    // The loop's global loads are asm, counted by hand (two waits per chunk):
-    //   top of chunk c:       chunk c+1's filter stage, LDS-DMA (8 pieces)
-    //   second half:          chunk c+2's patch rows into `raw` (8 loads),
-    //                         right after chunk c+1's rows were consumed
-    //   before the second half: vmcnt(8) -- chunk c+1's rows (older than the
-    //                         8 stage pieces) have landed
-    //   before the barrier:   vmcnt(8) -- the stage has landed (only chunk
-    //                         c+2's rows may be in flight)
-    // so a chunk's rows have ~1.5 chunks and its stage one chunk of cover.
+    // The loop's global loads, all issued at the top of chunk c for chunk
+    // c + 1: its filter stage by LDS-DMA (8 asm pieces, no VGPR destination;
+    // the compiler does not count them), then its patch rows into `raw` (8
+    // ordinary loads, used in this chunk's second half: loaded and used in one
+    // iteration, so no loop-carried copy of a register still loading).  The
+    // compiler's waits for the rows also retire the older stage pieces (vmcnt
+    // is in order); a vmcnt(0) before the barrier makes that explicit.
     // Addresses: a uniform SGPR base per chunk plus fixed per-lane byte
     // offsets (x is under 4 GiB: smmd_wino3x3_supported).
     f2v raw[2][4];
@@ -315,11 +320,11 @@ __global__ __launch_bounds__(WN_T, 1) void wino_conv_kernel(
                ((int64_t)kb * nch1 + (c < nch1 ? c : c - nch1)) * (WN_STAGE / 4);
     };
     auto load_rows = [&](int cc) {
-        const float *sb = xbase(cc);
+        const __amdgpu_buffer_rsrc_t rs = wn_rsrc(xbase(cc));
 #pragma unroll
         for (int e = 0; e < 2; ++e)
 #pragma unroll
-            for (int i = 0; i < 4; ++i) wn_ld2(raw[e][i], xoff[e][i], sb);
+            for (int i = 0; i < 4; ++i) raw[e][i] = wn_ld2(xoff[e][i], rs);
     };
     const uint32_t us_lds = wn_lds_addr(Us) + (uint32_t)__builtin_amdgcn_readfirstlane(w) * 8192u;
     // (per-piece lane offsets, no instruction offset: an LDS-DMA's immediate
@@ -333,13 +338,6 @@ __global__ __launch_bounds__(WN_T, 1) void wino_conv_kernel(
 #pragma unroll
         for (int i = 0; i < 8; ++i) wn_glds16(uoff[i], sb, dst + i * 1024);
     };
-#define WN_WAIT_ROWS(N_)                                                                     \
-    asm volatile("s_waitcnt vmcnt(" #N_ ")"                                                  \
-                 : "+v"(raw[0][0]), "+v"(raw[0][1]), "+v"(raw[0][2]), "+v"(raw[0][3]),       \
-                   "+v"(raw[1][0]), "+v"(raw[1][1]), "+v"(raw[1][2]), "+v"(raw[1][3])         \
-                 :                                                                           \
-                 : "memory")
-
     f32x16 acc[16];
 #pragma unroll
     for (int p = 0; p < 16; ++p) acc[p] = f32x16{};
@@ -380,7 +378,6 @@ __global__ __launch_bounds__(WN_T, 1) void wino_conv_kernel(
     const float bias_k = (bias && tid < WN_KB) ? bias[kb * WN_KB + tid] : 0.f;
     load_u(0);
     load_rows(0);
-    WN_WAIT_ROWS(0);
     {
         float tx[2][4], ty[2][4], tl[4], tr[4], v[2][4][4];
 #pragma unroll
@@ -400,13 +397,14 @@ __global__ __launch_bounds__(WN_T, 1) void wino_conv_kernel(
                     make_float2(v[0][i][j], v[1][i][j]);
     }
     if (tid < WN_KB) Bs[tid] = bias_k;
-    load_rows(min(1, nchunk - 1));          // (a spare reload when there is one chunk)
+    wn_wait_vm0();                          // chunk 0's stage landed (the rows' waits did it)
     __syncthreads();
 
     for (int cc = 0; cc + 1 < nchunk; ++cc) {
         const int buf = cc & 1, nbuf = buf ^ 1;
-        const int cn = min(cc + 2, nchunk - 1);     // (a spare reload at the end)
         load_u(cc + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        load_rows(cc + 1);
         __builtin_amdgcn_sched_barrier(0);
         const float4 *V_ = Vs + buf * (WN_STAGE / 4);
         const float4 *U_ = Us + buf * (WN_STAGE / 4);
@@ -435,15 +433,12 @@ __global__ __launch_bounds__(WN_T, 1) void wino_conv_kernel(
             }
         }
         // second half: after each MFMA one slice of chunk cc + 1's transform
-        // and V stores (the other buffer) or of chunk cc + 2's row loads,
-        // issued in the MFMA's slot (the f32 MFMA holds the SIMD's VALU, so
+        // and V stores (the other buffer), issued in the MFMA's slot (the f32 MFMA holds the SIMD's VALU, so
         // each slice costs its own issue time); sched_barrier pins the order
-        WN_WAIT_ROWS(8);
         __builtin_amdgcn_sched_barrier(0);
         float tx0[4], ty0[4], tx1[4], ty1[4], tl0[4], tr0[4], tl1[4], tr1[4], v0[4], v1[4];
         const float *xc = xbase(cc + 1) + ((int64_t)tn * g.C + 2 * w) * HW;
         float2 *Vn = reinterpret_cast<float2 *>(Vs + nbuf * (WN_STAGE / 4));
-        const float *rb = xbase(cn);
 #pragma unroll
         for (int pp = 4; pp < 8; ++pp) {
             const int p = 2 * pp;
@@ -463,21 +458,25 @@ __global__ __launch_bounds__(WN_T, 1) void wino_conv_kernel(
                     b1 = V_[((p + 3) * 2 + hl) * 64 + th * 32 + l32];
                 }
                 const int K = (pp - 4) * 8 + m;
-                if (K == 0) {                        // own columns, channel 0
+                // (the rows are first used at slice 8: 40 MFMAs after their
+                // loads went out)
+                if (K == 8) {                        // own columns, channel 0
+                    // (an empty asm on the rows: their arithmetic cannot be
+                    // hoisted above this slot, so their wait lands here)
+                    asm volatile("" : "+v"(raw[0][0]), "+v"(raw[0][1]), "+v"(raw[0][2]),
+                                 "+v"(raw[0][3]), "+v"(raw[1][0]), "+v"(raw[1][1]),
+                                 "+v"(raw[1][2]), "+v"(raw[1][3]));
                     wn_own(raw[0], r0ok, r3ok, tx0, ty0);
-                } else if (K == 1) {                 // own columns, channel 1
+                } else if (K == 9) {                 // own columns, channel 1
                     wn_own(raw[1], r0ok, r3ok, tx1, ty1);
-                } else if (K >= 2 && K < 10) {       // chunk cc + 2's rows, same registers
-                    const int e = (K - 2) >> 2, i = (K - 2) & 3;
-                    wn_ld2(raw[e][i], xoff[e][i], rb);
-                    if (K == 3)
-                        wn_outer<EDGE>(tx0, ty0, xc, tty, ttx, r0ok, r3ok, lane, g.TW, g.H, g.W,
-                                       tl0, tr0);
-                    else if (K == 5)
-                        wn_outer<EDGE>(tx1, ty1, xc + HW, tty, ttx, r0ok, r3ok, lane, g.TW, g.H,
-                                       g.W, tl1, tr1);
-                } else if (K >= 10 && K < 14) {      // row i of V, both channels, stored
-                    const int i = K - 10;
+                } else if (K == 11) {
+                    wn_outer<EDGE>(tx0, ty0, xc, tty, ttx, r0ok, r3ok, lane, g.TW, g.H, g.W,
+                                   tl0, tr0);
+                } else if (K == 13) {
+                    wn_outer<EDGE>(tx1, ty1, xc + HW, tty, ttx, r0ok, r3ok, lane, g.TW, g.H, g.W,
+                                   tl1, tr1);
+                } else if (K >= 16 && K < 20) {      // row i of V, both channels, stored
+                    const int i = K - 16;
                     wn_vrow(tl0, tx0, ty0, tr0, i, v0);
                     wn_vrow(tl1, tx1, ty1, tr1, i, v1);
 #pragma unroll
@@ -488,13 +487,10 @@ __global__ __launch_bounds__(WN_T, 1) void wino_conv_kernel(
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
-        // chunk cc + 1's filter stage landed (chunk cc + 2's rows may not have)
-        wn_wait_vm8();
+        wn_wait_vm0();                      // chunk cc + 1's filter stage landed
         __syncthreads();
     }
     WN_MFMA_CHUNK((nchunk - 1) & 1);
-    WN_WAIT_ROWS(0);                        // nothing of ours left in flight
-#undef WN_WAIT_ROWS
 
     // epilogue: C_p[k][tile], k = (r & 3) + 8 (r >> 2) + 4 hl, tile = l32.
     // With an even tile-row width the lane pair (2i, 2i+1) holds two
