@@ -45,6 +45,8 @@ GROUPS = {
     'smmd_wino4x4s2_conv': ('s2_conv_kernel',),
     'smmd_wino4x4s2t_conv': ('s2t_conv_kernel',),
     'smmd_wino4x4s2_filter': ('s2_filter_kernel', 's2t_filter_kernel'),
+    'smmd_wino4x4s2_wgrad': ('s2_wgrad_kernel', 's2w_sum_kernel', 's2w_group_kernel'),
+    'smmd_sn_clip_g': ('sn_clip_g_kernel',),
 }
 # entry points whose calls each run ONE of their kernels (fold or adjoint;
 # thin_in or thin_out):
