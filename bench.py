@@ -752,6 +752,11 @@ def main():
         # the SN output per layer: W_eff [N, K], or for a ConvMeanPool conv the
         # pool-folded 4 x 4 filter the bank writes directly (16 floats per 9)
         sn_out = sum(e.N * e.K * 16 // 9 if e.fold else e.N * e.K for e in model.sn_D.entries)
+        # the refresh writes W_eff / W' only for the layers that are not lazy
+        # (the Winograd-fed ones' filters are formed from W, sigma, s: sn.set_lazy)
+        lazy = getattr(model.sn_D, 'lazy', set())
+        sn_out_written = sum(e.N * e.K * 16 // 9 if e.fold else e.N * e.K
+                             for i, e in enumerate(model.sn_D.entries) if i not in lazy)
         per_img = 3 * size * size
         gdirect = model._gdirect()
         adam_sn_d = model.d_optim.numel * 4 * 8
@@ -771,8 +776,9 @@ def main():
             # the G-direct backward: one read of G and of W
             'smmd_sn_grad_stats': (sn_out + sn_kn) * 4,
             # one read of W + one write of W_eff (2 K N 4 B per
-            # iteration; the folded filters' 16 / 9 larger output for ConvMeanPool)
-            'smmd_sn_power_iter': (sn_kn + sn_out) * 4,
+            # iteration; the folded filters' 16 / 9 larger output for
+            # ConvMeanPool), the write only for the layers that are not lazy
+            'smmd_sn_power_iter': (sn_kn + sn_out_written) * 4,
             # one read of G (W_eff's shape) and W, one write of gW
             'smmd_sn_weight_bwd': (sn_out + 2 * sn_kn) * 4,
             # X, Y rows read, unit gradients written, sums
