@@ -251,6 +251,9 @@ __device__ __forceinline__ void wn_wait_vm0() { asm volatile("s_waitcnt vmcnt(0)
 #ifdef WN_CLOCK        // diagnostic build only (-DWN_CLOCK): per-block clock stamps
                        // (tools/wino_pmc.py reads them through smmd_diag_wino_clock)
 __device__ unsigned long long wn_clk[4096][4];
+// the 8-wave kernel's phases, waves 0 and 4: memtime at entry, after the
+// prologue's barrier, after the chunk loop, at exit; realtime at entry, exit
+__device__ unsigned long long wn_clk8[4096][2][6];
 #endif
 
 template <bool EDGE>
@@ -551,6 +554,332 @@ __global__ __launch_bounds__(WN_T, 1) void wino_conv_kernel(
 #endif
 }
 
+// The same block tile (64 tiles x 64 output channels, chunks of 8 input
+// channels, the same LDS stages) with 8 waves, two per SIMD: waves w and
+// w + 4 share a SIMD and the (k, tile) quadrant q = w & 3, and split the 16
+// points (PH = w >> 2: points 8 PH .. 8 PH + 7, 128 accumulator registers).
+// The f32 MFMA holds its own wave's VALU issue, but the partner wave's VALU
+// work goes out beside it (profiles/r12/mfma_valu_coissue.txt: two waves per
+// SIMD, the MFMA wave keeps its 64 cycles a slot), so the input transform --
+// one channel per wave now -- and the chunk-boundary waits of one wave are
+// covered by the other's MFMAs.  Each point's accumulation order over the
+// channels is that of wino_conv_kernel and the output transform is its
+// arithmetic term for term (the partners swap the halves of their
+// accumulators through LDS and each finishes 8 of the 16 rows), so the two
+// kernels' outputs are bit-identical.
+constexpr int W8_T = 512;
+
+// The 8-wave kernel's transform of one channel where tile rows are whole lane
+// groups (no edge loads) and the rows outside the image were loaded as zeros
+// (w8 row offsets past the descriptor's range): the column ops on both
+// columns packed, and the neighbour columns masked at the SOURCE (a lane at
+// its image row's right edge passes 0 to the right neighbour's left column,
+// one at the left edge 0 to the left neighbour's right column), so each DPP
+// move folds into its subtraction.  Term for term wn_own / wn_outer / wn_vrow.
+__device__ __forceinline__ void w8_cols(const f2v (&r)[4], f2v (&t)[4]) {
+    t[0] = r[0] - r[2];
+    t[1] = r[1] + r[2];
+    t[2] = r[2] - r[1];
+    t[3] = r[1] - r[3];
+}
+__device__ __forceinline__ void w8_row(const f2v &t, bool eL, bool eR, float (&v)[4]) {
+    const float ys = eR ? 0.f : t.y, xs = eL ? 0.f : t.x;
+    v[0] = wn_dpp_left(ys) - t.y;
+    v[3] = t.x - wn_dpp_right(xs);
+    // (tx + ty, ty - tx) in one packed add: the low result takes (t.lo,
+    // t.hi), the high one (t.hi, -t.lo)
+    f2v s;
+    asm("v_pk_add_f32 %0, %1, %1 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(s) : "v"(t));
+    v[1] = s.x;
+    v[2] = s.y;
+}
+#ifndef W8_SLOT
+#define W8_SLOT 16      // first MFMA slot of the transform slices (rows issued at the chunk top)
+#endif
+#ifndef W8_SLOT1
+#define W8_SLOT1 W8_SLOT  // the same for the PH = 1 waves
+#endif
+
+template <bool EDGE, int PH>
+__device__ __forceinline__ void wino8_body(const float *__restrict__ x, const float *__restrict__ u,
+                                           const float *__restrict__ bias, float *__restrict__ y,
+                                           const WnGeom &g) {
+    extern __shared__ float4 wn_lds[];
+    float4 *const Vs = wn_lds;                         // [2][p][h][t64]  (float4 = c4)
+    float4 *const Us = wn_lds + 2 * (WN_STAGE / 4);    // [2][p][h][k64]
+    float *const Bs = reinterpret_cast<float *>(wn_lds + 4 * (WN_STAGE / 4));   // [k64]
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int kb = blockIdx.y;
+    const int64_t tile0 = (int64_t)blockIdx.x * WN_TB;
+    const int nch1 = g.C / WN_CC;
+    const int nch = g.x2 ? 2 * nch1 : nch1;
+    const int c0 = (int)((int64_t)nch * blockIdx.z / gridDim.z);
+    const int nchunk = (int)((int64_t)nch * (blockIdx.z + 1) / gridDim.z) - c0;
+    y += (int64_t)blockIdx.z * g.slab;
+#ifdef WN_CLOCK
+    unsigned long long ck[6];
+    ck[0] = __builtin_amdgcn_s_memtime();
+    ck[4] = __builtin_amdgcn_s_memrealtime();
+#endif
+
+    // transform role: lane = tile, wave w = channel w of each chunk
+    const int64_t gt = tile0 + lane;
+    const bool tok = gt < g.T;
+    int tn = 0, tty = 0, ttx = 0;
+    if (tok) {
+        tn = (int)(gt / g.Timg);
+        const int r = (int)(gt - (int64_t)tn * g.Timg);
+        tty = r / g.TW;
+        ttx = r - tty * g.TW;
+    }
+    const int64_t HW = (int64_t)g.H * g.W;
+    f2v raw[4];
+    uint32_t xoff[4];
+    const int TH = g.H >> 1;
+    const bool r0ok = tty > 0, r3ok = tty < TH - 1;
+    // (a row outside the image: an offset past the descriptor's range, so
+    // the load returns zeros)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int yy = 2 * tty - 1 + i;
+        xoff[i] = (yy < 0 || yy >= g.H)
+                      ? 0x80000000u
+                      : (uint32_t)((((int64_t)tn * g.C + w) * HW + (int64_t)yy * g.W + 2 * ttx) * 4);
+    }
+    const bool eL = ttx == 0, eR = ttx == g.TW - 1;
+    auto xbase = [&](int cc) -> const float * {
+        const int c = c0 + cc;
+        return c < nch1 ? x + (int64_t)c * WN_CC * HW : g.x2 + (int64_t)(c - nch1) * WN_CC * HW;
+    };
+    auto ubase = [&](int cc) -> const float4 * {
+        const int c = c0 + cc;
+        return reinterpret_cast<const float4 *>(c < nch1 ? u : g.u2) +
+               ((int64_t)kb * nch1 + (c < nch1 ? c : c - nch1)) * (WN_STAGE / 4);
+    };
+    auto load_rows = [&](int cc) {
+        const __amdgpu_buffer_rsrc_t rs = wn_rsrc(xbase(cc));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) raw[i] = wn_ld2(xoff[i], rs);
+    };
+    // filter stage: 4 LDS-DMA pieces per wave
+    const uint32_t us_lds = wn_lds_addr(Us) + (uint32_t)__builtin_amdgcn_readfirstlane(w) * 4096u;
+    uint32_t uoff[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) uoff[i] = (uint32_t)((w * 256 + i * 64 + lane) * 16);
+    auto load_u = [&](int cc) {
+        const float4 *sb = ubase(cc);
+        const uint32_t dst = us_lds + (uint32_t)(cc & 1) * (WN_STAGE * 4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) wn_glds16(uoff[i], sb, dst + i * 1024);
+    };
+    // V of this wave's channel: float index ((p h t) c4) with h = w >> 2, c4 = w & 3
+    auto store_vrow = [&](float *Vf, int i, const float (&v)[4]) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            Vf[(((i * 4 + j) * 2 + (w >> 2)) * 64 + lane) * 4 + (w & 3)] = v[j];
+    };
+    f32x16 acc[8];
+#pragma unroll
+    for (int p = 0; p < 8; ++p) acc[p] = f32x16{};
+
+    const int q = w & 3, th = q & 1, kh = q >> 1, hl = lane >> 5, l32 = lane & 31;
+    constexpr int P0 = 8 * PH;
+    constexpr int SL = PH ? W8_SLOT1 : W8_SLOT;
+    const float bias_k = (bias && tid < WN_KB) ? bias[kb * WN_KB + tid] : 0.f;
+    load_u(0);
+    load_rows(0);
+    if constexpr (EDGE) {
+        float tx[4], ty[4], tl[4], tr[4], v[4];
+        wn_own(raw, r0ok, r3ok, tx, ty);
+        wn_outer<EDGE>(tx, ty, xbase(0) + ((int64_t)tn * g.C + w) * HW, tty, ttx, r0ok, r3ok, lane,
+                       g.TW, g.H, g.W, tl, tr);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            wn_vrow(tl, tx, ty, tr, i, v);
+            store_vrow(reinterpret_cast<float *>(Vs), i, v);
+        }
+    } else {
+        f2v t[4];
+        float v[4];
+        w8_cols(raw, t);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            w8_row(t[i], eL, eR, v);
+            store_vrow(reinterpret_cast<float *>(Vs), i, v);
+        }
+    }
+    if (tid < WN_KB) Bs[tid] = bias_k;
+    wn_wait_vm0();
+    __syncthreads();
+#ifdef WN_CLOCK
+    ck[1] = __builtin_amdgcn_s_memtime();
+#endif
+
+    for (int cc = 0;; ++cc) {
+        const bool more = cc + 1 < nchunk;
+        const int buf = cc & 1, nbuf = buf ^ 1;
+        if (more) {
+#ifndef W8_NO_DMA         // (W8_NO_*: timing-only diagnostic builds, wrong results)
+            load_u(cc + 1);
+#endif
+            __builtin_amdgcn_sched_barrier(0);
+#ifndef W8_NO_ROWS
+            load_rows(cc + 1);
+#endif
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        const float4 *V_ = Vs + buf * (WN_STAGE / 4);
+        const float4 *U_ = Us + buf * (WN_STAGE / 4);
+        float4 a0 = U_[(P0 * 2 + hl) * 64 + kh * 32 + l32], b0 = V_[(P0 * 2 + hl) * 64 + th * 32 + l32];
+        float4 a1 = U_[((P0 + 1) * 2 + hl) * 64 + kh * 32 + l32],
+               b1 = V_[((P0 + 1) * 2 + hl) * 64 + th * 32 + l32];
+        float tx[4], ty[4], tl[4], tr[4], v[4];
+        f2v t[4];
+        const float *xc = more ? xbase(cc + 1) + ((int64_t)tn * g.C + w) * HW : x;
+        float *Vn = reinterpret_cast<float *>(Vs + nbuf * (WN_STAGE / 4));
+#pragma unroll
+        for (int pp = 0; pp < 4; ++pp) {
+            const int p = P0 + 2 * pp;
+            const float4 ca0 = a0, cb0 = b0, ca1 = a1, cb1 = b1;
+#pragma unroll
+            for (int m = 0; m < 8; ++m) {
+                const int s4 = m >> 1;
+                if ((m & 1) == 0)
+                    acc[2 * pp] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca0[s4], cb0[s4], acc[2 * pp], 0, 0, 0);
+                else
+                    acc[2 * pp + 1] =
+                        __builtin_amdgcn_mfma_f32_32x32x2f32(ca1[s4], cb1[s4], acc[2 * pp + 1], 0, 0, 0);
+                if (m == 0 && pp < 3) {
+                    a0 = U_[((p + 2) * 2 + hl) * 64 + kh * 32 + l32];
+                    b0 = V_[((p + 2) * 2 + hl) * 64 + th * 32 + l32];
+                    a1 = U_[((p + 3) * 2 + hl) * 64 + kh * 32 + l32];
+                    b1 = V_[((p + 3) * 2 + hl) * 64 + th * 32 + l32];
+                }
+                const int K = pp * 8 + m;
+#ifdef W8_NO_XFORM
+                if (false) {
+#else
+                if (more) {
+#endif
+                    if (K == SL) {
+                        asm volatile("" : "+v"(raw[0]), "+v"(raw[1]), "+v"(raw[2]), "+v"(raw[3]));
+                        if constexpr (EDGE)
+                            wn_own(raw, r0ok, r3ok, tx, ty);
+                        else
+                            w8_cols(raw, t);
+                    } else if (EDGE && K == SL + 2) {
+                        wn_outer<EDGE>(tx, ty, xc, tty, ttx, r0ok, r3ok, lane, g.TW, g.H, g.W, tl,
+                                       tr);
+                    } else if (K >= SL + 4 && K < SL + 8) {
+                        if constexpr (EDGE)
+                            wn_vrow(tl, tx, ty, tr, K - SL - 4, v);
+                        else
+                            w8_row(t[K - SL - 4], eL, eR, v);
+                        store_vrow(Vn, K - SL - 4, v);
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        if (!more) break;
+        wn_wait_vm0();
+        __syncthreads();
+    }
+#ifdef WN_CLOCK
+    ck[2] = __builtin_amdgcn_s_memtime();
+#endif
+
+    // epilogue: the partners swap accumulator halves (rows 8 (1 - PH) ..
+    // through LDS, the stages being free once every wave is past its last
+    // MFMA), then each finishes rows 8 PH .. 8 PH + 7 of the quadrant with all
+    // 16 points.  X[w][p local][r4][lane] float4 (16 KB per wave).
+    __syncthreads();
+    float4 *const X = wn_lds;
+    constexpr int RO = 8 * (1 - PH);       // rows handed to the partner
+#pragma unroll
+    for (int p = 0; p < 8; ++p)
+#pragma unroll
+        for (int r4 = 0; r4 < 2; ++r4)
+            X[((w * 8 + p) * 2 + r4) * 64 + lane] =
+                make_float4(acc[p][RO + 4 * r4], acc[p][RO + 4 * r4 + 1], acc[p][RO + 4 * r4 + 2],
+                            acc[p][RO + 4 * r4 + 3]);
+    __syncthreads();
+    const int partner = w ^ 4;
+    const int64_t et = tile0 + th * 32 + l32;
+    const bool eok = et < g.T;
+    const int en = eok ? (int)(et / g.Timg) : 0;
+    const int er = (int)(et - (int64_t)en * g.Timg);
+    const int ety = er / g.TW, etx = er - ety * g.TW;
+    const bool pairs = (g.TW & 1) == 0;
+    const bool odd = lane & 1;
+#pragma unroll
+    for (int r4 = 0; r4 < 2; ++r4) {
+        float4 o4[8];
+#pragma unroll
+        for (int p = 0; p < 8; ++p) o4[p] = X[((partner * 8 + p) * 2 + r4) * 64 + lane];
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            const int r = 8 * PH + 4 * r4 + rr;
+            const int k = kb * WN_KB + kh * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+            float m[16];
+#pragma unroll
+            for (int p = 0; p < 8; ++p) {
+                m[P0 + p] = acc[p][r];
+                m[8 - P0 + p] = o4[p][rr];
+            }
+            float s0[4], s1[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                s0[j] = m[j] + m[4 + j] + m[8 + j];
+                s1[j] = m[4 + j] - m[8 + j] - m[12 + j];
+            }
+            const float b = Bs[k - kb * WN_KB];
+            float y00 = s0[0] + s0[1] + s0[2] + b, y01 = s0[1] - s0[2] - s0[3] + b;
+            float y10 = s1[0] + s1[1] + s1[2] + b, y11 = s1[1] - s1[2] - s1[3] + b;
+            if (g.relu) {
+                y00 = fmaxf(y00, 0.f); y01 = fmaxf(y01, 0.f);
+                y10 = fmaxf(y10, 0.f); y11 = fmaxf(y11, 0.f);
+            }
+            float *o = y + (((int64_t)en * g.K + k) * g.H + 2 * ety) * g.W + 2 * etx;
+            if (pairs) {
+                const float sx = odd ? y00 : y10, sy = odd ? y01 : y11;
+                const float rx = __builtin_bit_cast(
+                    float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, sx), 0xb1, 0xf, 0xf, false));
+                const float ry = __builtin_bit_cast(
+                    float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, sy), 0xb1, 0xf, 0xf, false));
+                if (eok) {
+                    if (!odd)
+                        *reinterpret_cast<float4 *>(o) = make_float4(y00, y01, rx, ry);
+                    else
+                        *reinterpret_cast<float4 *>(o + g.W - 2) = make_float4(rx, ry, y10, y11);
+                }
+            } else if (eok) {
+                *reinterpret_cast<float2 *>(o) = make_float2(y00, y01);
+                *reinterpret_cast<float2 *>(o + g.W) = make_float2(y10, y11);
+            }
+        }
+    }
+#ifdef WN_CLOCK
+    ck[3] = __builtin_amdgcn_s_memtime();
+    ck[5] = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0 && (w & 3) == 0 && blockIdx.z == 0) {
+        const unsigned b = (blockIdx.y * gridDim.x + blockIdx.x) & 4095;
+        for (int i = 0; i < 6; ++i) wn_clk8[b][PH][i] = ck[i];
+    }
+#endif
+}
+
+template <bool EDGE>
+__global__ __launch_bounds__(W8_T, 1) void wino_conv8_kernel(
+    const float *__restrict__ x, const float *__restrict__ u, const float *__restrict__ bias,
+    float *__restrict__ y, WnGeom g) {
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 8))
+        wino8_body<EDGE, 1>(x, u, bias, y, g);
+    else
+        wino8_body<EDGE, 0>(x, u, bias, y, g);
+}
+
 // y = bias + sum over the S partial slabs in slice order (float4 when the
 // plane size allows)
 __global__ void wino_reduce_kernel(const float *__restrict__ part, const float *__restrict__ bias,
@@ -586,6 +915,12 @@ static int wino_slices(int64_t blocks, int nch, int HW) {
     return S;
 }
 
+// SMMD_WINO8=0: the 4-wave form (A/B and tests; the two are bit-identical)
+static bool wino8_enabled() {
+    const char *e = getenv("SMMD_WINO8");
+    return !(e && e[0] == '0');
+}
+
 }  // namespace smmd
 
 using namespace smmd;
@@ -593,6 +928,10 @@ using namespace smmd;
 #ifdef WN_CLOCK
 extern "C" int smmd_diag_wino_clock(unsigned long long *host, int n) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(wn_clk), sizeof(unsigned long long) * 4 * n) ==
+                   hipSuccess ? 0 : 1;
+}
+extern "C" int smmd_diag_wino8_clock(unsigned long long *host, int n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(wn_clk8), sizeof(unsigned long long) * 12 * n) ==
                    hipSuccess ? 0 : 1;
 }
 #endif
@@ -674,13 +1013,14 @@ static smmd_status wino3x3_conv(const float *x, const float *u, const float *x2,
     }
     static bool attr = false;
     if (!attr) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void *>(wino_conv_kernel<false>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)WN_LDS) != hipSuccess ||
-            hipFuncSetAttribute(reinterpret_cast<const void *>(wino_conv_kernel<true>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)WN_LDS) != hipSuccess)
-            return SMMD_EHIP;
+        const void *ks[4] = {reinterpret_cast<const void *>(wino_conv_kernel<false>),
+                             reinterpret_cast<const void *>(wino_conv_kernel<true>),
+                             reinterpret_cast<const void *>(wino_conv8_kernel<false>),
+                             reinterpret_cast<const void *>(wino_conv8_kernel<true>)};
+        for (const void *k : ks)
+            if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)WN_LDS) !=
+                hipSuccess)
+                return SMMD_EHIP;
         attr = true;
     }
     g.slab = S > 1 ? total : 0;
@@ -689,10 +1029,17 @@ static smmd_status wino3x3_conv(const float *x, const float *u, const float *x2,
     const dim3 grid((unsigned)tb, (unsigned)(ko / WN_KB), (unsigned)S);
     const float *b1 = S > 1 ? nullptr : bias;
     // tile rows that are whole lane groups of a wave need no edge loads
-    if (64 % g.TW == 0)
+    const bool edge = 64 % g.TW != 0;
+    if (wino8_enabled()) {
+        if (!edge)
+            wino_conv8_kernel<false><<<grid, dim3(W8_T), WN_LDS, st>>>(x, u, b1, out, g);
+        else
+            wino_conv8_kernel<true><<<grid, dim3(W8_T), WN_LDS, st>>>(x, u, b1, out, g);
+    } else if (!edge) {
         wino_conv_kernel<false><<<grid, dim3(WN_T), WN_LDS, st>>>(x, u, b1, out, g);
-    else
+    } else {
         wino_conv_kernel<true><<<grid, dim3(WN_T), WN_LDS, st>>>(x, u, b1, out, g);
+    }
     smmd_status e = last_launch_status();
     if (e != SMMD_OK || S == 1) return e;
     const int64_t n4 = total / 4;

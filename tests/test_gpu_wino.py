@@ -69,6 +69,40 @@ def test_wino_forward_and_input_grad_vs_float64(shape):
     assert _rel(gx, ref1) < TOL
 
 
+@pytest.mark.parametrize('shape', SHAPES)
+def test_wino_eight_wave_form_bit_identical(shape, monkeypatch):
+    """The 8-wave kernel (two waves per SIMD splitting the 16 points) and the
+    4-wave one accumulate every point in the same order and share the output
+    transform's arithmetic: the same bits, both modes, relu too."""
+    from gan.core import _lib
+    N, C, K, H, W = shape
+    g = torch.Generator(device=DEV).manual_seed(N * 31 + C + K + H + W)
+    x = torch.randn(N, C, H, W, device=DEV, generator=g)
+    w = torch.randn(K, C, 3, 3, device=DEV, generator=g)
+    b = torch.randn(K, device=DEV, generator=g)
+    out = {}
+    for form in ('0', '1'):
+        monkeypatch.setenv('SMMD_WINO8', form)
+        y0, _ = _abi_conv(x, w, b, 0)
+        y1, _ = _abi_conv(x, w.transpose(0, 1).contiguous(), None, 1) if C == K else (None, 0)
+        L = _lib.lib()
+        u = torch.empty(L.smmd_wino3x3_filter_bytes(K, C) // 4, device=DEV)
+        assert L.smmd_wino3x3_filter(_lib.ptr(w), K, C, 0, _lib.ptr(u), u.numel() * 4,
+                                     _lib.stream_handle()) == 0
+        yr = torch.empty(N, K, H, W, device=DEV)
+        nb = L.smmd_wino3x3_workspace_bytes(N, C, K, H, W)
+        ws = torch.empty(max(nb // 4, 1), device=DEV)
+        assert L.smmd_wino3x3_conv_relu(_lib.ptr(x), _lib.ptr(u), _lib.ptr(b), _lib.ptr(yr), N, C,
+                                        K, H, W, _lib.ptr(ws) if nb else None, nb,
+                                        _lib.stream_handle()) == 0
+        out[form] = (y0, y1, yr)
+    monkeypatch.delenv('SMMD_WINO8')
+    for a, c in zip(out['0'], out['1']):
+        if a is not None:
+            assert torch.equal(a, c)
+    assert (out['1'][2] >= 0).all()
+
+
 def test_wino_split_channels_deterministic():
     """The split-input-channel path (workspace + fixed-order add) gives the
     same bits run to run."""
