@@ -252,8 +252,9 @@ __device__ __forceinline__ void wn_wait_vm0() { asm volatile("s_waitcnt vmcnt(0)
                        // (tools/wino_pmc.py reads them through smmd_diag_wino_clock)
 __device__ unsigned long long wn_clk[4096][4];
 // the 8-wave kernel's phases, waves 0 and 4: memtime at entry, after the
-// prologue's barrier, after the chunk loop, at exit; realtime at entry, exit
-__device__ unsigned long long wn_clk8[4096][2][6];
+// prologue's barrier, after the chunk loop, after the epilogue's two
+// barriers, at exit; realtime at entry, exit
+__device__ unsigned long long wn_clk8[4096][2][8];
 #endif
 
 template <bool EDGE>
@@ -600,7 +601,7 @@ __device__ __forceinline__ void w8_row(const f2v &t, bool eL, bool eR, float (&v
 #define W8_SLOT1 W8_SLOT  // the same for the PH = 1 waves
 #endif
 
-template <bool EDGE, int PH>
+template <bool EDGE, int PH, bool RELU>
 __device__ __forceinline__ void wino8_body(const float *__restrict__ x, const float *__restrict__ u,
                                            const float *__restrict__ bias, float *__restrict__ y,
                                            const WnGeom &g) {
@@ -618,9 +619,9 @@ __device__ __forceinline__ void wino8_body(const float *__restrict__ x, const fl
     const int nchunk = (int)((int64_t)nch * (blockIdx.z + 1) / gridDim.z) - c0;
     y += (int64_t)blockIdx.z * g.slab;
 #ifdef WN_CLOCK
-    unsigned long long ck[6];
+    unsigned long long ck[8];
     ck[0] = __builtin_amdgcn_s_memtime();
-    ck[4] = __builtin_amdgcn_s_memrealtime();
+    ck[6] = __builtin_amdgcn_s_memrealtime();
 #endif
 
     // transform role: lane = tile, wave w = channel w of each chunk
@@ -795,6 +796,9 @@ __device__ __forceinline__ void wino8_body(const float *__restrict__ x, const fl
     // MFMA), then each finishes rows 8 PH .. 8 PH + 7 of the quadrant with all
     // 16 points.  X[w][p local][r4][lane] float4 (16 KB per wave).
     __syncthreads();
+#ifdef WN_CLOCK
+    ck[3] = __builtin_amdgcn_s_memtime();
+#endif
     float4 *const X = wn_lds;
     constexpr int RO = 8 * (1 - PH);       // rows handed to the partner
 #pragma unroll
@@ -805,79 +809,88 @@ __device__ __forceinline__ void wino8_body(const float *__restrict__ x, const fl
                 make_float4(acc[p][RO + 4 * r4], acc[p][RO + 4 * r4 + 1], acc[p][RO + 4 * r4 + 2],
                             acc[p][RO + 4 * r4 + 3]);
     __syncthreads();
+#ifdef WN_CLOCK
+    ck[4] = __builtin_amdgcn_s_memtime();
+#endif
     const int partner = w ^ 4;
     const int64_t et = tile0 + th * 32 + l32;
     const bool eok = et < g.T;
     const int en = eok ? (int)(et / g.Timg) : 0;
     const int er = (int)(et - (int64_t)en * g.Timg);
     const int ety = er / g.TW, etx = er - ety * g.TW;
-    const bool pairs = (g.TW & 1) == 0;
-    const bool odd = lane & 1;
+    // stores: a uniform descriptor on this slab, the lane's byte offset of
+    // its row-0 channel (k0) fixed, each row adding a uniform multiple of H W
+    // (y under 4 GiB: smmd_wino3x3_supported); each lane stores its own
+    // tile's two output rows (8 bytes each, 32 tiles of a row contiguous)
+    const int k0 = kb * WN_KB + kh * 32 + 4 * hl;
+    const uint32_t yo =
+        (uint32_t)(((((int64_t)en * g.K + k0) * g.H + 2 * ety) * g.W + 2 * etx) * 4);
+    const __amdgpu_buffer_rsrc_t ys = wn_rsrc(y);
+    const uint32_t hw4 = (uint32_t)(HW * 4), yo1 = yo + (uint32_t)g.W * 4;
+    typedef unsigned u2v __attribute__((ext_vector_type(2)));
+    // the output transform on row pairs (r, r + 1): both rows' values of a
+    // point sit in adjacent registers (acc[p][r], acc[p][r + 1]; the
+    // partner's float4), so every add is one packed op on the pair
 #pragma unroll
     for (int r4 = 0; r4 < 2; ++r4) {
         float4 o4[8];
 #pragma unroll
         for (int p = 0; p < 8; ++p) o4[p] = X[((partner * 8 + p) * 2 + r4) * 64 + lane];
 #pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-            const int r = 8 * PH + 4 * r4 + rr;
-            const int k = kb * WN_KB + kh * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-            float m[16];
+        for (int rp = 0; rp < 2; ++rp) {
+            const int r = 8 * PH + 4 * r4 + 2 * rp;           // even: rows r, r + 1 -> k, k + 1
+            const int kr = (r & 3) + 8 * (r >> 2);            // k - k0 of row r
+            f2v m[16];
 #pragma unroll
             for (int p = 0; p < 8; ++p) {
-                m[P0 + p] = acc[p][r];
-                m[8 - P0 + p] = o4[p][rr];
+                m[P0 + p] = f2v{acc[p][r], acc[p][r + 1]};
+                m[8 - P0 + p] = rp ? f2v{o4[p].z, o4[p].w} : f2v{o4[p].x, o4[p].y};
             }
-            float s0[4], s1[4];
+            f2v s0[4], s1[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 s0[j] = m[j] + m[4 + j] + m[8 + j];
                 s1[j] = m[4 + j] - m[8 + j] - m[12 + j];
             }
-            const float b = Bs[k - kb * WN_KB];
-            float y00 = s0[0] + s0[1] + s0[2] + b, y01 = s0[1] - s0[2] - s0[3] + b;
-            float y10 = s1[0] + s1[1] + s1[2] + b, y11 = s1[1] - s1[2] - s1[3] + b;
-            if (g.relu) {
-                y00 = fmaxf(y00, 0.f); y01 = fmaxf(y01, 0.f);
-                y10 = fmaxf(y10, 0.f); y11 = fmaxf(y11, 0.f);
+            const f2v b = *reinterpret_cast<const f2v *>(Bs + (k0 - kb * WN_KB) + kr);
+            f2v y00 = s0[0] + s0[1] + s0[2] + b, y01 = s0[1] - s0[2] - s0[3] + b;
+            f2v y10 = s1[0] + s1[1] + s1[2] + b, y11 = s1[1] - s1[2] - s1[3] + b;
+            if constexpr (RELU) {
+                y00 = __builtin_elementwise_max(y00, f2v{0.f, 0.f});
+                y01 = __builtin_elementwise_max(y01, f2v{0.f, 0.f});
+                y10 = __builtin_elementwise_max(y10, f2v{0.f, 0.f});
+                y11 = __builtin_elementwise_max(y11, f2v{0.f, 0.f});
             }
-            float *o = y + (((int64_t)en * g.K + k) * g.H + 2 * ety) * g.W + 2 * etx;
-            if (pairs) {
-                const float sx = odd ? y00 : y10, sy = odd ? y01 : y11;
-                const float rx = __builtin_bit_cast(
-                    float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, sx), 0xb1, 0xf, 0xf, false));
-                const float ry = __builtin_bit_cast(
-                    float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, sy), 0xb1, 0xf, 0xf, false));
-                if (eok) {
-                    if (!odd)
-                        *reinterpret_cast<float4 *>(o) = make_float4(y00, y01, rx, ry);
-                    else
-                        *reinterpret_cast<float4 *>(o + g.W - 2) = make_float4(rx, ry, y10, y11);
+            if (eok) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const uint32_t so = (uint32_t)(kr + h) * hw4;
+                    __builtin_amdgcn_raw_buffer_store_b64(
+                        __builtin_bit_cast(u2v, f2v{y00[h], y01[h]}), ys, yo, so, 0);
+                    __builtin_amdgcn_raw_buffer_store_b64(
+                        __builtin_bit_cast(u2v, f2v{y10[h], y11[h]}), ys, yo1, so, 0);
                 }
-            } else if (eok) {
-                *reinterpret_cast<float2 *>(o) = make_float2(y00, y01);
-                *reinterpret_cast<float2 *>(o + g.W) = make_float2(y10, y11);
             }
         }
     }
 #ifdef WN_CLOCK
-    ck[3] = __builtin_amdgcn_s_memtime();
-    ck[5] = __builtin_amdgcn_s_memrealtime();
+    ck[5] = __builtin_amdgcn_s_memtime();
+    ck[7] = __builtin_amdgcn_s_memrealtime();
     if (lane == 0 && (w & 3) == 0 && blockIdx.z == 0) {
         const unsigned b = (blockIdx.y * gridDim.x + blockIdx.x) & 4095;
-        for (int i = 0; i < 6; ++i) wn_clk8[b][PH][i] = ck[i];
+        for (int i = 0; i < 8; ++i) wn_clk8[b][PH][i] = ck[i];
     }
 #endif
 }
 
-template <bool EDGE>
+template <bool EDGE, bool RELU>
 __global__ __launch_bounds__(W8_T, 1) void wino_conv8_kernel(
     const float *__restrict__ x, const float *__restrict__ u, const float *__restrict__ bias,
     float *__restrict__ y, WnGeom g) {
     if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 8))
-        wino8_body<EDGE, 1>(x, u, bias, y, g);
+        wino8_body<EDGE, 1, RELU>(x, u, bias, y, g);
     else
-        wino8_body<EDGE, 0>(x, u, bias, y, g);
+        wino8_body<EDGE, 0, RELU>(x, u, bias, y, g);
 }
 
 // y = bias + sum over the S partial slabs in slice order (float4 when the
@@ -931,7 +944,7 @@ extern "C" int smmd_diag_wino_clock(unsigned long long *host, int n) {
                    hipSuccess ? 0 : 1;
 }
 extern "C" int smmd_diag_wino8_clock(unsigned long long *host, int n) {
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(wn_clk8), sizeof(unsigned long long) * 12 * n) ==
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(wn_clk8), sizeof(unsigned long long) * 16 * n) ==
                    hipSuccess ? 0 : 1;
 }
 #endif
@@ -941,10 +954,11 @@ extern "C" size_t smmd_wino3x3_filter_bytes(int ko, int ci) {
     return (size_t)16 * ko * ci * sizeof(float);
 }
 
-// (x under 4 GiB: the conv kernel addresses it by 32-bit byte offsets)
+// (x and y under 4 GiB: the conv kernels address them by 32-bit byte offsets)
 extern "C" int smmd_wino3x3_supported(int n, int ci, int ko, int h, int w_img) {
     return n > 0 && ci > 0 && ko > 0 && ci % WN_CC == 0 && ko % WN_KB == 0 && h > 0 &&
-           w_img > 0 && h % 2 == 0 && w_img % 2 == 0 && (int64_t)n * ci * h * w_img < (1ll << 30);
+           w_img > 0 && h % 2 == 0 && w_img % 2 == 0 && (int64_t)n * ci * h * w_img < (1ll << 30) &&
+           (int64_t)n * ko * h * w_img < (1ll << 30);
 }
 
 extern "C" smmd_status smmd_wino3x3_filter(const float *w, int ko, int ci, int mode, float *u,
@@ -1013,10 +1027,12 @@ static smmd_status wino3x3_conv(const float *x, const float *u, const float *x2,
     }
     static bool attr = false;
     if (!attr) {
-        const void *ks[4] = {reinterpret_cast<const void *>(wino_conv_kernel<false>),
+        const void *ks[6] = {reinterpret_cast<const void *>(wino_conv_kernel<false>),
                              reinterpret_cast<const void *>(wino_conv_kernel<true>),
-                             reinterpret_cast<const void *>(wino_conv8_kernel<false>),
-                             reinterpret_cast<const void *>(wino_conv8_kernel<true>)};
+                             reinterpret_cast<const void *>(wino_conv8_kernel<false, false>),
+                             reinterpret_cast<const void *>(wino_conv8_kernel<true, false>),
+                             reinterpret_cast<const void *>(wino_conv8_kernel<false, true>),
+                             reinterpret_cast<const void *>(wino_conv8_kernel<true, true>)};
         for (const void *k : ks)
             if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)WN_LDS) !=
                 hipSuccess)
@@ -1031,10 +1047,9 @@ static smmd_status wino3x3_conv(const float *x, const float *u, const float *x2,
     // tile rows that are whole lane groups of a wave need no edge loads
     const bool edge = 64 % g.TW != 0;
     if (wino8_enabled()) {
-        if (!edge)
-            wino_conv8_kernel<false><<<grid, dim3(W8_T), WN_LDS, st>>>(x, u, b1, out, g);
-        else
-            wino_conv8_kernel<true><<<grid, dim3(W8_T), WN_LDS, st>>>(x, u, b1, out, g);
+        auto k8 = edge ? (g.relu ? wino_conv8_kernel<true, true> : wino_conv8_kernel<true, false>)
+                       : (g.relu ? wino_conv8_kernel<false, true> : wino_conv8_kernel<false, false>);
+        k8<<<grid, dim3(W8_T), WN_LDS, st>>>(x, u, b1, out, g);
     } else if (!edge) {
         wino_conv_kernel<false><<<grid, dim3(WN_T), WN_LDS, st>>>(x, u, b1, out, g);
     } else {

@@ -51,26 +51,29 @@ def main():
                                        H, H, _lib.ptr(ws), nb, st) == 0
         torch.cuda.synchronize()
         blocks = min(N * (H // 2) ** 2 // 64 * (K // 64), 4096)
-        buf = (ctypes.c_ulonglong * (12 * blocks))()
+        buf = (ctypes.c_ulonglong * (16 * blocks))()
         assert L.smmd_diag_wino8_clock(buf, blocks) == 0
         res = {}
         starts = []
         for ph in (0, 1):
-            ghz, pro, loop, epi, tot = [], [], [], [], []
+            ghz, pro, loop, b1, b2, epi, tot = [], [], [], [], [], [], []
             for bk in range(blocks):
-                t0, t1, t2, t3, r0, r1 = buf[12 * bk + 6 * ph:12 * bk + 6 * ph + 6]
-                if r1 <= r0 or t3 <= t0:
+                t0, t1, t2, t3, t4, t5, r0, r1 = buf[16 * bk + 8 * ph:16 * bk + 8 * ph + 8]
+                if r1 <= r0 or t5 <= t0:
                     continue
-                g = (t3 - t0) / (r1 - r0) * 0.1
+                g = (t5 - t0) / (r1 - r0) * 0.1
                 ghz.append(g)
                 pro.append((t1 - t0) / g / 1e3)
                 loop.append((t2 - t1) / g / 1e3)
-                epi.append((t3 - t2) / g / 1e3)
+                b1.append((t3 - t2) / g / 1e3)
+                b2.append((t4 - t3) / g / 1e3)
+                epi.append((t5 - t4) / g / 1e3)
                 tot.append((r1 - r0) / 100.0)
                 if ph == 0:
                     starts.append(r0)
             res['ph%d' % ph] = {'ghz': round(med(ghz), 3), 'prologue_us': round(med(pro), 2),
-                                'loop_us': round(med(loop), 2), 'epilogue_us': round(med(epi), 2),
+                                'loop_us': round(med(loop), 2), 'to_barrier1_us': round(med(b1), 2),
+                                'swap_us': round(med(b2), 2), 'rows_us': round(med(epi), 2),
                                 'block_us': round(med(tot), 2)}
         starts.sort()
         res['start_spread_us'] = round((starts[-1] - starts[0]) / 100.0, 2)
