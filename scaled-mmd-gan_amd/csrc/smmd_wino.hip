@@ -720,6 +720,14 @@ __device__ __forceinline__ void wino8_body(const float *__restrict__ x, const fl
     for (int cc = 0;; ++cc) {
         const bool more = cc + 1 < nchunk;
         const int buf = cc & 1, nbuf = buf ^ 1;
+        // the first fragments' LDS reads go out first, so their latency runs
+        // under the next chunk's load issue
+        const float4 *V_ = Vs + buf * (WN_STAGE / 4);
+        const float4 *U_ = Us + buf * (WN_STAGE / 4);
+        float4 a0 = U_[(P0 * 2 + hl) * 64 + kh * 32 + l32], b0 = V_[(P0 * 2 + hl) * 64 + th * 32 + l32];
+        float4 a1 = U_[((P0 + 1) * 2 + hl) * 64 + kh * 32 + l32],
+               b1 = V_[((P0 + 1) * 2 + hl) * 64 + th * 32 + l32];
+        __builtin_amdgcn_sched_barrier(0);
         if (more) {
 #ifndef W8_NO_DMA         // (W8_NO_*: timing-only diagnostic builds, wrong results)
             load_u(cc + 1);
@@ -730,11 +738,6 @@ __device__ __forceinline__ void wino8_body(const float *__restrict__ x, const fl
 #endif
             __builtin_amdgcn_sched_barrier(0);
         }
-        const float4 *V_ = Vs + buf * (WN_STAGE / 4);
-        const float4 *U_ = Us + buf * (WN_STAGE / 4);
-        float4 a0 = U_[(P0 * 2 + hl) * 64 + kh * 32 + l32], b0 = V_[(P0 * 2 + hl) * 64 + th * 32 + l32];
-        float4 a1 = U_[((P0 + 1) * 2 + hl) * 64 + kh * 32 + l32],
-               b1 = V_[((P0 + 1) * 2 + hl) * 64 + th * 32 + l32];
         float tx[4], ty[4], tl[4], tr[4], v[4];
         f2v t[4];
         const float *xc = more ? xbase(cc + 1) + ((int64_t)tn * g.C + w) * HW : x;
