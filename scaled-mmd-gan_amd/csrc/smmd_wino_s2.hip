@@ -49,6 +49,14 @@ __device__ __forceinline__ float s2_from_right(float v) {   // lane l gets lane 
                                                               0xf, 0xf, true));
 }
 
+// buffer access: a wave-uniform base in the descriptor, the lane's 32-bit
+// byte offset in one VGPR (no 64-bit address arithmetic per access; tensors
+// under 4 GiB, the *_supported checks); an offset past the range reads zeros
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t s2_rsrc(const void *base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, 0x7fffffff, 0x00020000);
+}
+constexpr uint32_t S2_OOB = 0x80000000u;
+
 // The 16 taps of filter q of W': with sig NULL read from w [q][16]; else w is
 // the raw weight of a spectrally normalised layer and the taps are those of
 // W_eff = (W / sigma) * s (sn.py:43, snops.py:84), pool-folded from the raw
@@ -167,14 +175,16 @@ __global__ __launch_bounds__(S2_T, 2) void s2_conv_kernel(
         ttx = r - tty * g.TW;
     }
     const int64_t HW = (int64_t)g.H * g.W;
-    // the lane's three patch rows in chunk 0 of input 1 (clamped rows), and
-    // chunk cc's wave-uniform byte shift from there (input 2: the distance
-    // between the two tensors; integer arithmetic, no per-lane select)
-    const float *xrow[3];
+    // the lane's three patch rows: byte offsets from chunk cc's wave-uniform
+    // base (input 2: the distance between the two tensors), a row outside the
+    // image past the buffer range (reads zeros)
+    uint32_t xo[3];
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-        const int yc = min(max(4 * tty - 1 + pi + 2 * a, 0), g.H - 1);
-        xrow[a] = x + ((int64_t)tn * g.C + e) * HW + (int64_t)yc * g.W + 4 * ttx;
+        const int yy = 4 * tty - 1 + pi + 2 * a;
+        xo[a] = (yy < 0 || yy >= g.H)
+                    ? S2_OOB
+                    : (uint32_t)((((int64_t)tn * g.C + e) * HW + (int64_t)yy * g.W + 4 * ttx) * 4);
     }
     const int64_t x2shift = g.x2 ? (int64_t)(reinterpret_cast<uintptr_t>(g.x2) -
                                              reinterpret_cast<uintptr_t>(x)) : 0;
@@ -193,33 +203,41 @@ __global__ __launch_bounds__(S2_T, 2) void s2_conv_kernel(
                ((int64_t)kb * nch1 + (c < nch1 ? c : c - nch1)) * (S2_STAGE / 4);
     };
 
-    float4 raw[3];
+    f4v raw[3];
     f4v ur[5];
     auto load = [&](int cc) {
-        const int64_t sh = xshift(cc);
+        const __amdgpu_buffer_rsrc_t rs =
+            s2_rsrc(reinterpret_cast<const char *>(x) + xshift(cc));
+#ifndef S2_NO_ROWS      // (S2_NO_*: timing-only diagnostic builds, wrong results)
 #pragma unroll
         for (int a = 0; a < 3; ++a)
-            raw[a] = *reinterpret_cast<const float4 *>(reinterpret_cast<const char *>(xrow[a]) + sh);
-        const float4 *src = uchunk(cc) + tid;
+            raw[a] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, xo[a], 0, 0));
+#else
+        (void)rs;
+#endif
+        const __amdgpu_buffer_rsrc_t us = s2_rsrc(uchunk(cc));
 #pragma unroll
         for (int i = 0; i < 5; ++i)
             if (i * S2_T + tid < S2_STAGE / 4)
-                ur[i] = *reinterpret_cast<const f4v *>(src + i * S2_T);
+                ur[i] = __builtin_bit_cast(
+                    f4v, __builtin_amdgcn_raw_buffer_load_b128(us, (uint32_t)(i * S2_T + tid) * 16, 0, 0));
     };
     auto store = [&](int cc, int buf) {
         f4v *U = reinterpret_cast<f4v *>(Us + buf * (S2_STAGE / 4)) + tid;
 #pragma unroll
         for (int i = 0; i < 5; ++i)
             if (i * S2_T + tid < S2_STAGE / 4) U[i * S2_T] = ur[i];
+#ifdef S2_NO_XFORM
+        return;
+#endif
         const float *xc = xchunk(cc);
         // rows: columns 4tx-1 .. 4tx+4; pj = 0 takes (-1, 1, 3), pj = 1 (0, 2, 4)
         float d0[3][3], d1[3][3];
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
             const int yy = 4 * tty - 1 + pi + 2 * a;
-            const bool row = tok && yy >= 0 && yy < g.H;
-            const float c0v = row ? raw[a].x : 0.f, c1v = row ? raw[a].y : 0.f;
-            const float c2v = row ? raw[a].z : 0.f, c3v = row ? raw[a].w : 0.f;
+            const bool row = yy >= 0 && yy < g.H;     // (outside: loaded as zeros)
+            const float c0v = raw[a].x, c1v = raw[a].y, c2v = raw[a].z, c3v = raw[a].w;
             float L = s2_from_left(c3v), R = s2_from_right(c0v);
             if (EDGE) {
                 if (ttx > 0 && lane == 0) L = row ? xc[(int64_t)yy * g.W + 4 * ttx - 1] : 0.f;
@@ -287,30 +305,50 @@ __global__ __launch_bounds__(S2_T, 2) void s2_conv_kernel(
     }
     mfma_chunk((nchunk - 1) & 1);
 
-    // epilogue: C_p[k][tile]; output tile (2ty, 2tx) of y [N, K, H/2, W/2]
+    // epilogue: C_p[k][tile]; output tile (2ty, 2tx) of y [N, K, H/2, W/2];
+    // rows in pairs (r, r + 1: channels k, k + 1, adjacent registers) for
+    // packed adds, buffer stores at the lane's fixed offsets plus a uniform
+    // per-channel offset
     const int64_t et = tile0 + th * 32 + l32;
     if (et >= g.T) return;
     const int en = (int)(et / g.Timg);
     const int er = (int)(et - (int64_t)en * g.Timg);
     const int ety = er / g.TW, etx = er - ety * g.TW;
     const int Ho = g.H / 2, Wo = g.W / 2;
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    typedef unsigned u2v __attribute__((ext_vector_type(2)));
+    const int kl0 = kh * 32 + 4 * hl;                       // k - 64 kb of row 0
+    const uint32_t o0 = (uint32_t)(((((int64_t)en * g.K + kb * S2_KB + kl0) * Ho + 2 * ety) * Wo +
+                                     2 * etx) * 4);
+    const uint32_t o1 = o0 + (uint32_t)Wo * 4;
+    const uint32_t hw4 = (uint32_t)Ho * (uint32_t)Wo * 4;
+    const __amdgpu_buffer_rsrc_t ys = s2_rsrc(y);
+#ifdef S2_NO_EPI
+    for (int r = 0; r < 2; r += 2) {
+#else
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int k = kb * S2_KB + kh * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-        float m[9];
+    for (int r = 0; r < 16; r += 2) {
+#endif
+        const int kr = (r & 3) + 8 * (r >> 2);
+        f2v m[9];
 #pragma unroll
-        for (int p = 0; p < 9; ++p) m[p] = acc[p][r];
+        for (int p = 0; p < 9; ++p) m[p] = f2v{acc[p][r], acc[p][r + 1]};
         // rows: s_a[j] = m[a][j] + m[a+1][j]
-        float s0[3], s1[3];
+        f2v s0[3], s1[3];
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
             s0[j] = m[j] + m[3 + j];
             s1[j] = m[3 + j] + m[6 + j];
         }
-        const float b = Bs[k - kb * S2_KB];
-        float *o = y + (((int64_t)en * g.K + k) * Ho + 2 * ety) * Wo + 2 * etx;
-        *reinterpret_cast<float2 *>(o) = make_float2(s0[0] + s0[1] + b, s0[1] + s0[2] + b);
-        *reinterpret_cast<float2 *>(o + Wo) = make_float2(s1[0] + s1[1] + b, s1[1] + s1[2] + b);
+        const f2v b = *reinterpret_cast<const f2v *>(Bs + kl0 + kr);
+        const f2v y00 = s0[0] + s0[1] + b, y01 = s0[1] + s0[2] + b;
+        const f2v y10 = s1[0] + s1[1] + b, y11 = s1[1] + s1[2] + b;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t so = (uint32_t)(kr + h) * hw4;
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, f2v{y00[h], y01[h]}), ys, o0, so, 0);
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, f2v{y10[h], y11[h]}), ys, o1, so, 0);
+        }
     }
 }
 
@@ -320,7 +358,7 @@ __global__ __launch_bounds__(S2_T, 2) void s2_conv_kernel(
 // (qi, qj) of dx is a 2 x 2 stride-1 correlation of gy: dx[2r+qi][2s+qj] =
 // sum_k sum_{a,b in 0..1} gy[k][r-1+qi+a][s-1+qj+b] W'[k][c][3-qi-2a][3-qj-2b],
 // one F(2x2, 2x2) problem per phase with K reduction channels.  Block: one
-// phase (blockIdx.z & 3), 64 phase tiles x 64 output channels; as the
+// phase (s2_xcd_order), 64 phase tiles x 64 output channels; as the
 // forward kernel otherwise (chunks of 8 k, 9 accumulators per wave).
 
 // U for the transposed conv: ut[q4][cb][kchunk][p9][h2][c64][k4], from W' [K][C][4][4];
@@ -367,7 +405,25 @@ __global__ void s2t_filter_kernel(const float *__restrict__ w, int K, int C,
 struct S2TGeom {
     int N, K, C, Hg, Wg, TW, Timg;  // gy [N, K, Hg, Wg]; dx [N, C, 2Hg, 2Wg]; tiles of a phase
     int64_t T, slab;
+    int CB, S;                      // channel blocks (C / 64), K slices
 };
+
+// The block's work from its 1-D id, XCD-aware: blocks b and b + 8 share an
+// XCD and its L2 (MI355X_MICROARCH.md, dispatch; for speed only, any
+// placement is correct), so XCD x takes the x-th contiguous range of a
+// logical order.  Tile-major ((tile block, slice, channel block), phase): the
+// four phase blocks and the channel blocks of one tile block -- which read
+// the same gy rows and write interleaved columns of the same dx lines -- run
+// together on one L2 (a phase writes every other 4-byte column; on separate
+// L2s each line went to HBM up to four times, each partial write read back
+// first: 128 -> 64 MB written on the 64-channel fold layer at batch 64).
+// (Measured and not kept: filter-major, (phase, channel block, slice) outer
+// and tile blocks inner, 1-6 % slower on all four fold layers even where the
+// filter outweighs gy and dx.)
+__device__ __forceinline__ uint32_t s2_xcd_order(uint32_t L, uint32_t n) {
+    const uint32_t q = n >> 3, r = n & 7, x = L & 7, j = L >> 3;
+    return x < r ? x * (q + 1) + j : r * (q + 1) + (x - r) * q + j;
+}
 
 // the body for output phase (QI, QJ): the phase is a compile-time constant, so
 // its row and column picks cost no per-lane selects (every VALU instruction
@@ -375,18 +431,17 @@ struct S2TGeom {
 template <bool EDGE, int QI, int QJ>
 __device__ __forceinline__ void s2t_body(const float *__restrict__ gy, const float *__restrict__ u,
                                          const float *__restrict__ bias, float *__restrict__ dx,
-                                         const S2TGeom &g) {
+                                         const S2TGeom &g, int64_t tb, int cb, int sl) {
     extern __shared__ float4 s2_lds[];
     float4 *const Vs = s2_lds;
     float4 *const Us = s2_lds + 2 * (S2_STAGE / 4);
     float *const Bs = reinterpret_cast<float *>(s2_lds + 4 * (S2_STAGE / 4));   // [c64]
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int cb = blockIdx.y;
     constexpr int q = QI * 2 + QJ, qi = QI, qj = QJ;
     const int THg = g.Hg >> 1;           // phase tile rows per image
-    const int sl = blockIdx.z >> 2, S = gridDim.z >> 2;
-    const int64_t tile0 = (int64_t)blockIdx.x * S2_TB;
+    const int S = g.S;
+    const int64_t tile0 = tb * S2_TB;
     const int nch = g.K / 8;
     const int c0 = (int)((int64_t)nch * sl / S);
     const int nchunk = (int)((int64_t)nch * (sl + 1) / S) - c0;
@@ -407,30 +462,48 @@ __device__ __forceinline__ void s2t_body(const float *__restrict__ gy, const flo
     const float4 *ub = reinterpret_cast<const float4 *>(u) + (int64_t)q * g.C * g.K * 9 / 4 +
                        ((int64_t)cb * nch + c0) * (S2_STAGE / 4);
 
-    float2 raw[2][3];
+    // the rows by buffer loads: chunk cc's base (k = 8 (c0 + cc)) uniform, the
+    // lane's offsets fixed; a row outside the image reads zeros
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    f2v raw[2][3];
     f4v ur[5];
-    auto load = [&](int cc) {
+    uint32_t roff[2][3];
 #pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            const float *gc = gn + ((int64_t)cc * 8 + e) * HW;
+    for (int e = 0; e < 2; ++e)
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const int yy = 2 * tty - 1 + qi + a;
+            roff[e][a] = (yy < 0 || yy >= g.Hg)
+                             ? S2_OOB
+                             : (uint32_t)((((int64_t)tn * g.K + 2 * w + e) * HW +
+                                           (int64_t)yy * g.Wg + 2 * ttx) * 4);
+        }
+    auto load = [&](int cc) {
+        const __amdgpu_buffer_rsrc_t rs = s2_rsrc(gy + ((int64_t)c0 + cc) * 8 * HW);
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
-                const int yy = 2 * tty - 1 + qi + a;
-                const int yc = min(max(yy, 0), g.Hg - 1);
-                raw[e][a] = *reinterpret_cast<const float2 *>(gc + (int64_t)yc * g.Wg + 2 * ttx);
+#ifndef S2_NO_ROWS
+                raw[e][a] = __builtin_bit_cast(
+                    f2v, __builtin_amdgcn_raw_buffer_load_b64(rs, roff[e][a], 0, 0));
+#endif
             }
-        }
-        const float4 *src = ub + (int64_t)cc * (S2_STAGE / 4) + tid;
+        const __amdgpu_buffer_rsrc_t us = s2_rsrc(ub + (int64_t)cc * (S2_STAGE / 4));
 #pragma unroll
         for (int i = 0; i < 5; ++i)
             if (i * S2_T + tid < S2_STAGE / 4)
-                ur[i] = *reinterpret_cast<const f4v *>(src + i * S2_T);
+                ur[i] = __builtin_bit_cast(
+                    f4v, __builtin_amdgcn_raw_buffer_load_b128(us, (uint32_t)(i * S2_T + tid) * 16, 0, 0));
     };
     auto store = [&](int cc, int buf) {
         f4v *U = reinterpret_cast<f4v *>(Us + buf * (S2_STAGE / 4)) + tid;
 #pragma unroll
         for (int i = 0; i < 5; ++i)
             if (i * S2_T + tid < S2_STAGE / 4) U[i * S2_T] = ur[i];
+#ifdef S2_NO_XFORM
+        return;
+#endif
         float v[2][9];
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
@@ -440,10 +513,11 @@ __device__ __forceinline__ void s2t_body(const float *__restrict__ gy, const flo
             for (int a = 0; a < 3; ++a) {
                 const int yy = 2 * tty - 1 + qi + a;
                 // rows 2ty - 1 (phase row 0) and 2ty + 2 (phase row 1) can be
-                // outside the image; a tile past the end is never stored
+                // outside the image (loaded as zeros); a tile past the end is
+                // never stored
                 const bool row = (a == 0 && qi == 0) ? tty > 0
                                  : (a == 2 && qi == 1) ? tty < THg - 1 : true;
-                const float cx = row ? raw[e][a].x : 0.f, cy = row ? raw[e][a].y : 0.f;
+                const float cx = raw[e][a].x, cy = raw[e][a].y;
                 float L = s2_from_left(cy), R = s2_from_right(cx);
                 if (EDGE) {
                     if (ttx > 0 && lane == 0) L = row ? gc[(int64_t)yy * g.Wg + 2 * ttx - 1] : 0.f;
@@ -510,31 +584,46 @@ __device__ __forceinline__ void s2t_body(const float *__restrict__ gy, const flo
     }
     mfma_chunk((nchunk - 1) & 1);
 
-    // epilogue: phase tile (ty, tx) -> dx rows 2 (2ty + a) + qi, cols 2 (2tx + b) + qj
+    // epilogue: phase tile (ty, tx) -> dx rows 2 (2ty + a) + qi, cols 2 (2tx + b) + qj;
+    // buffer stores at the lane's fixed offsets plus a uniform per-channel
+    // offset
     const int64_t et = tile0 + th * 32 + l32;
     if (et >= g.T) return;
     const int en = (int)(et / g.Timg);
     const int er = (int)(et - (int64_t)en * g.Timg);
     const int ety = er / g.TW, etx = er - ety * g.TW;
     const int Hx = 2 * g.Hg, Wx = 2 * g.Wg;
+    const int cl0 = kh * 32 + 4 * hl;                       // c - 64 cb of row 0
+    const uint32_t o0 = (uint32_t)(((((int64_t)en * g.C + cb * 64 + cl0) * Hx + 4 * ety + qi) * Wx +
+                                     4 * etx + qj) * 4);
+    const uint32_t o1 = o0 + (uint32_t)Wx * 8;            // output row + 2
+    const uint32_t hw4 = (uint32_t)Hx * (uint32_t)Wx * 4;
+    const __amdgpu_buffer_rsrc_t ds = s2_rsrc(dx);
+#ifdef S2_NO_EPI
+    for (int r = 0; r < 2; r += 2) {
+#else
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int c = cb * 64 + kh * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-        float m[9];
+    for (int r = 0; r < 16; r += 2) {
+#endif
+        const int cr = (r & 3) + 8 * (r >> 2);              // c - c of row 0
 #pragma unroll
-        for (int p = 0; p < 9; ++p) m[p] = acc[p][r];
-        float s0[3], s1[3];
+        for (int h = 0; h < 2; ++h) {
+            float m[9];
 #pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            s0[j] = m[j] + m[3 + j];
-            s1[j] = m[3 + j] + m[6 + j];
+            for (int p = 0; p < 9; ++p) m[p] = acc[p][r + h];
+            float s0[3], s1[3];
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                s0[j] = m[j] + m[3 + j];
+                s1[j] = m[3 + j] + m[6 + j];
+            }
+            const float b = Bs[cl0 + cr + h];
+            const uint32_t so = (uint32_t)(cr + h) * hw4;
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, s0[0] + s0[1] + b), ds, o0, so, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, s0[1] + s0[2] + b), ds, o0 + 8, so, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, s1[0] + s1[1] + b), ds, o1, so, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, s1[1] + s1[2] + b), ds, o1 + 8, so, 0);
         }
-        const float b = Bs[c - cb * 64];
-        float *o = dx + (((int64_t)en * g.C + c) * Hx + 4 * ety + qi) * Wx + 4 * etx + qj;
-        o[0] = s0[0] + s0[1] + b;
-        o[2] = s0[1] + s0[2] + b;
-        o[2 * Wx] = s1[0] + s1[1] + b;
-        o[2 * Wx + 2] = s1[1] + s1[2] + b;
     }
 }
 
@@ -542,11 +631,18 @@ template <bool EDGE>
 __global__ __launch_bounds__(S2_T, 2) void s2t_conv_kernel(
     const float *__restrict__ gy, const float *__restrict__ u, const float *__restrict__ bias,
     float *__restrict__ dx, S2TGeom g) {
-    switch (blockIdx.z & 3) {           // the block's output phase (wave-uniform)
-    case 0: s2t_body<EDGE, 0, 0>(gy, u, bias, dx, g); break;
-    case 1: s2t_body<EDGE, 0, 1>(gy, u, bias, dx, g); break;
-    case 2: s2t_body<EDGE, 1, 0>(gy, u, bias, dx, g); break;
-    default: s2t_body<EDGE, 1, 1>(gy, u, bias, dx, g); break;
+    uint32_t W = s2_xcd_order(blockIdx.x, gridDim.x);
+    const int q = (int)(W & 3);         // the block's output phase (wave-uniform)
+    W >>= 2;
+    const int cb = (int)(W % (uint32_t)g.CB);
+    W /= (uint32_t)g.CB;
+    const int sl = (int)(W % (uint32_t)g.S);
+    const int64_t tb = W / (uint32_t)g.S;
+    switch (q) {
+    case 0: s2t_body<EDGE, 0, 0>(gy, u, bias, dx, g, tb, cb, sl); break;
+    case 1: s2t_body<EDGE, 0, 1>(gy, u, bias, dx, g, tb, cb, sl); break;
+    case 2: s2t_body<EDGE, 1, 0>(gy, u, bias, dx, g, tb, cb, sl); break;
+    default: s2t_body<EDGE, 1, 1>(gy, u, bias, dx, g, tb, cb, sl); break;
     }
 }
 
@@ -593,7 +689,8 @@ using namespace smmd;
 
 extern "C" int smmd_wino4x4s2_supported(int n, int ci, int ko, int h, int w_img) {
     return n > 0 && ci > 0 && ko > 0 && ci % S2_CC == 0 && ko % S2_KB == 0 && h > 0 &&
-           w_img > 0 && h % 4 == 0 && w_img % 4 == 0 && (int64_t)n * ci * h * w_img < (1ll << 40);
+           w_img > 0 && h % 4 == 0 && w_img % 4 == 0 && (int64_t)n * ci * h * w_img < (1ll << 30) &&
+           (int64_t)n * ko * h * w_img < (1ll << 32);   // x, y under 4 GiB (buffer offsets)
 }
 
 extern "C" size_t smmd_wino4x4s2_filter_bytes(int ko, int ci) {
@@ -717,7 +814,8 @@ extern "C" smmd_status smmd_wino4x4s2_conv2(const float *x, const float *u, cons
 
 extern "C" int smmd_wino4x4s2t_supported(int n, int k, int c, int hg, int wg) {
     return n > 0 && k > 0 && c > 0 && k % 8 == 0 && c % 64 == 0 && hg > 0 && wg > 0 &&
-           hg % 2 == 0 && wg % 2 == 0 && (int64_t)n * k * hg * wg < (1ll << 40);
+           hg % 2 == 0 && wg % 2 == 0 && (int64_t)n * k * hg * wg < (1ll << 30) &&
+           (int64_t)n * c * 4 * hg * wg < (1ll << 30);   // gy, dx under 4 GiB (buffer offsets)
 }
 
 extern "C" smmd_status smmd_wino4x4s2t_filter(const float *w, int k, int c, float *u,
@@ -792,8 +890,13 @@ extern "C" smmd_status smmd_wino4x4s2t_conv(const float *gy, const float *u, con
         attr = true;
     }
     g.slab = S > 1 ? total : 0;
+    g.CB = c / 64;
+    g.S = S;
+
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    const dim3 grid((unsigned)tb, (unsigned)(c / 64), (unsigned)(4 * S));
+    const int64_t nblk = tb * (c / 64) * 4 * S;
+    if (nblk > 0x7fffffff) return SMMD_EINVAL;
+    const dim3 grid((unsigned)nblk);
     const float *b1 = S > 1 ? nullptr : bias;
     if (64 % g.TW == 0)
         s2t_conv_kernel<false><<<grid, dim3(S2_T), S2_LDS, st>>>(gy, u, b1, out, g);

@@ -138,6 +138,14 @@ def _thin_wgrad(gy, x):
 WINO = os.environ.get('SMMD_WINO', '1') != '0'
 
 
+def _under_4g(x, out_per_in_channel):
+    """The Winograd kernels address their input and output by 32-bit byte
+    offsets: both under 2^30 floats (out_per_in_channel: output elements per
+    input element of one channel plane, e.g. cout for a same-size conv)."""
+    plane = x.shape[0] * x.shape[2] * x.shape[3]
+    return x.numel() < (1 << 30) and plane * out_per_in_channel < (1 << 30)
+
+
 def wino_applicable(x, cin, cout, k, stride, padding):
     """True when conv(x, [cout, cin, 3, 3], stride 1, padding 1) runs on
     `smmd_wino3x3_conv`: an NCHW fp32 contiguous device tensor with even height
@@ -148,7 +156,7 @@ def wino_applicable(x, cin, cout, k, stride, padding):
             and x.is_contiguous() and k == 3 and s == (1, 1) and p == (1, 1)
             and x.shape[1] == cin and cin % 8 == 0 and cout % 64 == 0
             and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0 and x.shape[2] > 0
-            and x.shape[3] > 0 and x.shape[0] > 0)
+            and x.shape[3] > 0 and x.shape[0] > 0 and _under_4g(x, cout))
 
 
 # transformed filters of the weights in use: a critic step convolves each
@@ -387,7 +395,7 @@ def _is_s2(x, w, stride, padding):
     H, W % 4 == 0, ci % 2 == 0, co % 64 == 0."""
     return (w.dim() == 4 and w.shape[2] == 4 and w.shape[3] == 4 and _s2_shape_ok(x, stride, padding)
             and x.shape[1] == w.shape[1] and w.shape[1] % 2 == 0 and w.shape[0] % 64 == 0
-            and x.shape[2] % 4 == 0 and x.shape[3] % 4 == 0)
+            and x.shape[2] % 4 == 0 and x.shape[3] % 4 == 0 and _under_4g(x, w.shape[0] / 4))
 
 
 def _is_s2t(g, w, stride, padding):
@@ -396,7 +404,7 @@ def _is_s2t(g, w, stride, padding):
     c % 64 == 0."""
     return (w.dim() == 4 and w.shape[2] == 4 and w.shape[3] == 4 and _s2_shape_ok(g, stride, padding)
             and g.shape[1] == w.shape[0] and w.shape[0] % 8 == 0 and w.shape[1] % 64 == 0
-            and g.shape[2] % 2 == 0 and g.shape[3] % 2 == 0)
+            and g.shape[2] % 2 == 0 and g.shape[3] % 2 == 0 and _under_4g(g, w.shape[1] * 4))
 
 
 def _s2_filter(w, transposed):
