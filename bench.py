@@ -54,11 +54,11 @@ BATCH = 64
 # committed counter evidence of this workload, each file stamped with the
 # smmd_source_hash of the library build it was measured on (tools/stamp.py);
 # embedded only when that stamp equals the running library's
-PMC_TRAFFIC = os.path.join(ROOT, 'profiles', 'r12', 'pmc_traffic.json')
+PMC_TRAFFIC = os.path.join(ROOT, 'profiles', 'r13', 'pmc_traffic.json')
 # executed FLOPs per kernel class over whole 5D+1G cycles of this workload
 # (tools/gpu_step_pmc.sh -> tools/step_flops_pmc.py: rocprofv3 SQ_INSTS_VALU_*
 # and SQ_INSTS_VALU_MFMA_MOPS_F32 counters + a kernel trace)
-STEP_PMC = os.path.join(ROOT, 'profiles', 'r12', 'step_flops_pmc.json')
+STEP_PMC = os.path.join(ROOT, 'profiles', 'r13', 'step_flops_pmc.json')
 
 
 def load_stamped(path, stamp):
@@ -200,10 +200,12 @@ def _time_steps(tr, imgs, steps, warm=3):
         tr.train_step(imgs)                   # allocator, threads, first-touch
     tr.d_counter = tr.g_counter = 0           # cycle start
     times, kinds = [], []
-    for _ in range(steps):
+    for i in range(steps):
         t0 = time.perf_counter()
         kinds.append(tr.train_step(imgs))
         times.append(time.perf_counter() - t0)
+        print('[bench] cpu baseline step %d/%d: %.2f s' % (i + 1, steps, times[-1]),
+              file=sys.stderr, flush=True)
     return times, kinds
 
 
@@ -378,6 +380,8 @@ def mmd_sweep(world, rank, dev, group, quick=False):
             torch.autograd.grad(v, (Xl, Yl))
             return v
 
+        if rank == 0:
+            print('[bench] mmd sweep %s N=%d D=%d' % (kern, N, D), file=sys.stderr, flush=True)
         for _ in range(3):
             once()
         iters = 20 if D < 1024 else 8

@@ -1,0 +1,20 @@
+# Round-4 (r13, after the 8-wave Winograd kernel) evidence on the final tree, every file stamped with the
+# library's smmd_source_hash: PMC traffic and executed-FLOP passes (written
+# into profiles/r13/ on the box so the bench line embeds them), then the
+# default bench line and a kernel trace of the same workload.
+# bash tools/gpu_evidence_r13.sh [skip_pmc]
+set -o pipefail
+mkdir -p gpurun_out profiles/r13
+export TMPDIR=/tmp
+if [ "${1:-0}" != "1" ]; then
+bash tools/gpu_pmc.sh ev13 > gpurun_out/ev13_pmc.log 2>&1 || { echo "pmc failed"; tail -20 gpurun_out/ev13_pmc.log; exit 1; }
+cp gpurun_out/ev13_traffic.json profiles/r13/pmc_traffic.json
+bash tools/gpu_step_pmc.sh ev13s --cycles 2 > gpurun_out/ev13_step.log 2>&1 || { echo "step pmc failed"; tail -20 gpurun_out/ev13_step.log; exit 1; }
+python -c "import json;json.load(open('gpurun_out/ev13s_step_flops.json'))" && cp gpurun_out/ev13s_step_flops.json profiles/r13/step_flops_pmc.json
+cp profiles/r13/pmc_traffic.json profiles/r13/step_flops_pmc.json gpurun_out/
+fi
+timeout -k 10 900 python bench.py > gpurun_out/ev13_bench_default.json 2> gpurun_out/ev13_bench_default.err || { echo "bench rc=$?"; tail -20 gpurun_out/ev13_bench_default.err; exit 1; }
+python -c "import json;d=json.load(open('gpurun_out/ev13_bench_default.json'));print(d['value'],d['ms_per_step'],d['roofline']['kernel'],d['roofline']['frac'],d['roofline']['traffic'],d['roofline']['traffic_null_reason'],d['roofline_hot_path']['step']['counters'].get('source'))"
+timeout -s KILL 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/ev13_trace -o run -- python tools/step_cycle.py --cycles 2 > gpurun_out/ev13_trace.log 2>&1 || { echo "trace rc=$?"; exit 1; }
+find gpurun_out/ev13_trace -name "*kernel_trace.csv" -exec gzip -f {} \;
+echo done
