@@ -38,7 +38,7 @@ GROUPS = {
     'smmd_conv3x3_thin': ('thin_in_kernel', 'thin_out_kernel'),
     'smmd_conv3x3_thin_wgrad': ('thin_wgrad_mfma_kernel', 'thin_wgrad_kernel',
                                 'thin_wgrad_final_kernel'),
-    'smmd_wino3x3_conv': ('wino_conv_kernel', 'wino_reduce_kernel'),
+    'smmd_wino3x3_conv': ('wino_conv_kernel', 'wino_conv8_kernel', 'wino_reduce_kernel'),
     'smmd_wino3x3_filter': ('wino_filter_kernel',),
     'smmd_wino3x3_wgrad': ('wino_wgrad_kernel', 'wino_wgrad2_kernel', 'wino_wgrad_group_kernel',
                            'wino_wgrad_final_kernel', 'wino_wgrad_sum_kernel'),
@@ -83,14 +83,18 @@ def main():
     for entry, kernels in GROUPS.items():
         rd = wr = 0.0
         found = []
-        calls = 0
+        by_base = defaultdict(int)      # launches per kernel, template instances summed
         for kname in fetch:
             if any(k in kname for k in kernels):
                 rd += 2 * fetch[kname][0] * 1024
                 if 'opt_sqsum@' not in kname:
-                    calls = (calls + fetch[kname][1] if entry in SUM_CALLS
-                             else max(calls, fetch[kname][1]))
+                    by_base[next(k for k in kernels if k in kname)] += fetch[kname][1]
                 found.append(kname.replace('(anonymous namespace)::', '').split('(')[0])
+        # one call launches one instance of each of its kernels (e.g. the 3x3
+        # conv's relu / plain and edge forms, the stride-2 weight gradient's
+        # four tilings): instances add up, distinct kernels of a call do not
+        calls = (sum(by_base.values()) if entry in SUM_CALLS
+                 else max(by_base.values(), default=0))
         for kname in write:
             if any(k in kname for k in kernels):
                 wr += write[kname][0] * 1024
