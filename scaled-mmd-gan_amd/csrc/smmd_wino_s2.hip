@@ -230,6 +230,28 @@ __global__ __launch_bounds__(S2_T, 2) void s2_conv_kernel(
 #ifdef S2_NO_XFORM
         return;
 #endif
+        float v0[9], v1[9];
+        if constexpr (!EDGE) {
+            // column-factored: Bᵀ over the rows on the lane's own four columns
+            // (packed), the outer columns' from the neighbour lanes by DPP
+            // folded into the subtraction, the image-edge zero applied at the
+            // source lane; term for term the form below
+            const bool eL = ttx == 0, eR = ttx == g.TW - 1;
+            f4v t[3];
+            t[0] = raw[0] - raw[1];
+            t[1] = raw[1];
+            t[2] = raw[2] - raw[1];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                const float ws = eR ? 0.f : t[i].w, xs = eL ? 0.f : t[i].x;
+                v0[i * 3 + 0] = s2_from_left(ws) - t[i].y;      // columns (L, 1, 3)
+                v0[i * 3 + 1] = t[i].y;
+                v0[i * 3 + 2] = t[i].w - t[i].y;
+                v1[i * 3 + 0] = t[i].x - t[i].z;                // columns (0, 2, R)
+                v1[i * 3 + 1] = t[i].z;
+                v1[i * 3 + 2] = s2_from_right(xs) - t[i].z;
+            }
+        } else {
         const float *xc = xchunk(cc);
         // rows: columns 4tx-1 .. 4tx+4; pj = 0 takes (-1, 1, 3), pj = 1 (0, 2, 4)
         float d0[3][3], d1[3][3];
@@ -248,7 +270,6 @@ __global__ __launch_bounds__(S2_T, 2) void s2_conv_kernel(
             d0[a][0] = L;   d0[a][1] = c1v; d0[a][2] = c3v;
             d1[a][0] = c0v; d1[a][1] = c2v; d1[a][2] = R;
         }
-        float v0[9], v1[9];
 #pragma unroll
         for (int b = 0; b < 3; ++b) {      // B^T d per column
             const float t00 = d0[0][b] - d0[1][b], t01 = d0[1][b], t02 = d0[2][b] - d0[1][b];
@@ -265,10 +286,12 @@ __global__ __launch_bounds__(S2_T, 2) void s2_conv_kernel(
             v1[i * 3 + 1] = d1[i][1];
             v1[i * 3 + 2] = d1[i][2] - d1[i][1];
         }
-        float2 *V2 = reinterpret_cast<float2 *>(Vs + buf * (S2_STAGE / 4));
+        }
+        float2 *const Vl = reinterpret_cast<float2 *>(Vs + buf * (S2_STAGE / 4)) +
+                           (e * 64 + lane) * 2 + pi;
 #pragma unroll
         for (int p = 0; p < 9; ++p)
-            V2[((p * 2 + e) * 64 + lane) * 2 + pi] = make_float2(v0[p], v1[p]);
+            Vl[p * 256] = make_float2(v0[p], v1[p]);      // point p: + p * 2 KB
     };
 
     f32x16 acc[9];
@@ -505,6 +528,36 @@ __device__ __forceinline__ void s2t_body(const float *__restrict__ gy, const flo
         return;
 #endif
         float v[2][9];
+        if constexpr (!EDGE) {
+            // column-factored: Bᵀ over the rows on the lane's own two columns
+            // (packed), the outer column's from the neighbour lane by DPP
+            // folded into the subtraction, its image-edge zero applied at the
+            // source lane (a lane at its row's right edge passes 0 to the
+            // right, one at the left edge 0 to the left); term for term the
+            // form below
+            const bool eL = ttx == 0, eR = ttx == g.TW - 1;
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                f2v t[3];
+                t[0] = raw[e][0] - raw[e][1];
+                t[1] = raw[e][1];
+                t[2] = raw[e][2] - raw[e][1];
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    if (qj == 0) {          // columns (L, x, y)
+                        const float ys = eR ? 0.f : t[i].y;
+                        v[e][i * 3 + 0] = s2_from_left(ys) - t[i].x;
+                        v[e][i * 3 + 1] = t[i].x;
+                        v[e][i * 3 + 2] = t[i].y - t[i].x;
+                    } else {                // columns (x, y, R)
+                        const float xs = eL ? 0.f : t[i].x;
+                        v[e][i * 3 + 0] = t[i].x - t[i].y;
+                        v[e][i * 3 + 1] = t[i].y;
+                        v[e][i * 3 + 2] = s2_from_right(xs) - t[i].y;
+                    }
+                }
+            }
+        } else
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
             const float *gc = gn + ((int64_t)cc * 8 + e) * HW;
@@ -544,10 +597,11 @@ __device__ __forceinline__ void s2t_body(const float *__restrict__ gy, const flo
                 v[e][i * 3 + 2] = d[i][2] - d[i][1];
             }
         }
-        float2 *V2 = reinterpret_cast<float2 *>(Vs + buf * (S2_STAGE / 4));
+        float2 *const Vl = reinterpret_cast<float2 *>(Vs + buf * (S2_STAGE / 4)) +
+                           ((w >> 1) * 64 + lane) * 2 + (w & 1);
 #pragma unroll
         for (int p = 0; p < 9; ++p)
-            V2[((p * 2 + (w >> 1)) * 64 + lane) * 2 + (w & 1)] = make_float2(v[0][p], v[1][p]);
+            Vl[p * 256] = make_float2(v[0][p], v[1][p]);  // point p: + p * 2 KB
     };
 
     f32x16 acc[9];
