@@ -2,7 +2,12 @@
 # library's smmd_source_hash: PMC traffic and executed-FLOP passes (written
 # into profiles/r13/ on the box so the bench line embeds them), then the
 # default bench line and a kernel trace of the same workload.
-# bash tools/gpu_evidence_r13.sh [skip_pmc]
+# bash tools/gpu_evidence_r13.sh [1 | pmc]
+#   pmc: the counter passes only; 1: the bench and the trace only.
+# Run them as two gpurun calls (pmc, copy the two JSON files into
+# profiles/r13/, then 1): a bench after rocprofv3 --pmc passes in the same
+# call ran ~10 % slower on every box tried (5298 / 5304 against 5956 / 5980
+# images/s on the same tree), its kernels at the same speed.
 set -o pipefail
 mkdir -p gpurun_out profiles/r13
 export TMPDIR=/tmp
@@ -13,6 +18,7 @@ bash tools/gpu_step_pmc.sh ev13s --cycles 2 > gpurun_out/ev13_step.log 2>&1 || {
 python -c "import json;json.load(open('gpurun_out/ev13s_step_flops.json'))" && cp gpurun_out/ev13s_step_flops.json profiles/r13/step_flops_pmc.json
 cp profiles/r13/pmc_traffic.json profiles/r13/step_flops_pmc.json gpurun_out/
 fi
+if [ "${1:-0}" = "pmc" ]; then echo done; exit 0; fi
 timeout -k 10 900 python bench.py > gpurun_out/ev13_bench_default.json 2> gpurun_out/ev13_bench_default.err || { echo "bench rc=$?"; tail -20 gpurun_out/ev13_bench_default.err; exit 1; }
 python -c "import json;d=json.load(open('gpurun_out/ev13_bench_default.json'));print(d['value'],d['ms_per_step'],d['roofline']['kernel'],d['roofline']['frac'],d['roofline']['traffic'],d['roofline']['traffic_null_reason'],d['roofline_hot_path']['step']['counters'].get('source'))"
 timeout -s KILL 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/ev13_trace -o run -- python tools/step_cycle.py --cycles 2 > gpurun_out/ev13_trace.log 2>&1 || { echo "trace rc=$?"; exit 1; }
