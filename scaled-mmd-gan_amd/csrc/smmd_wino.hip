@@ -133,6 +133,9 @@ struct WnGeom {
     // input-channel loop running over both (chunks nch1 .. 2 nch1 - 1 from
     // them), so y = conv(x, U) + conv(x2, U2) in one set of accumulators
     const float *x2, *u2;
+    // the 8-wave kernel's 1-D grid: tile blocks, output-channel blocks,
+    // input-channel slices (w8_block)
+    int TB, KB, S;
 };
 
 // The input transform V = B^T d B of one tile's 4 x 4 patch d (rows 2ty-1 ..
@@ -601,6 +604,32 @@ __device__ __forceinline__ void w8_row(const f2v &t, bool eL, bool eR, float (&v
 #define W8_SLOT1 W8_SLOT  // the same for the PH = 1 waves
 #endif
 
+// The 8-wave kernel's block (tile block, output-channel block, slice) from
+// its 1-D id, XCD-aware: blocks b and b + 8 share an XCD and its L2
+// (MI355X_MICROARCH.md, dispatch; for speed only, any placement is correct),
+// so XCD x takes the x-th contiguous range of the tile-major order ((tile
+// block, slice), output-channel block): the output-channel blocks of one
+// tile block run together on one L2 and read its x rows once (the 3-D grid
+// dealt them to the XCDs round-robin, and each read x again).  Measured and
+// not kept: filter-major ((output-channel block, slice), tile block), equal
+// on the 512-channel layer, 1-2 % slower on the others
+// (profiles/r13/wino8_order_ab.txt).
+struct W8Block {
+    int64_t tb;
+    int kb, sl;
+};
+__device__ __forceinline__ W8Block w8_block(const WnGeom &g) {
+    const uint32_t n = gridDim.x, L = blockIdx.x;
+    const uint32_t q = n >> 3, r = n & 7, xc = L & 7, j = L >> 3;
+    uint32_t W = xc < r ? xc * (q + 1) + j : r * (q + 1) + (xc - r) * q + j;
+    W8Block b;
+    b.kb = (int)(W % (uint32_t)g.KB);
+    W /= (uint32_t)g.KB;
+    b.sl = (int)(W % (uint32_t)g.S);
+    b.tb = W / (uint32_t)g.S;
+    return b;
+}
+
 template <bool EDGE, int PH, bool RELU>
 __device__ __forceinline__ void wino8_body(const float *__restrict__ x, const float *__restrict__ u,
                                            const float *__restrict__ bias, float *__restrict__ y,
@@ -611,13 +640,14 @@ __device__ __forceinline__ void wino8_body(const float *__restrict__ x, const fl
     float *const Bs = reinterpret_cast<float *>(wn_lds + 4 * (WN_STAGE / 4));   // [k64]
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int kb = blockIdx.y;
-    const int64_t tile0 = (int64_t)blockIdx.x * WN_TB;
+    const W8Block blk = w8_block(g);
+    const int kb = blk.kb;
+    const int64_t tile0 = blk.tb * WN_TB;
     const int nch1 = g.C / WN_CC;
     const int nch = g.x2 ? 2 * nch1 : nch1;
-    const int c0 = (int)((int64_t)nch * blockIdx.z / gridDim.z);
-    const int nchunk = (int)((int64_t)nch * (blockIdx.z + 1) / gridDim.z) - c0;
-    y += (int64_t)blockIdx.z * g.slab;
+    const int c0 = (int)((int64_t)nch * blk.sl / g.S);
+    const int nchunk = (int)((int64_t)nch * (blk.sl + 1) / g.S) - c0;
+    y += (int64_t)blk.sl * g.slab;
 #ifdef WN_CLOCK
     unsigned long long ck[8];
     ck[0] = __builtin_amdgcn_s_memtime();
@@ -879,8 +909,8 @@ __device__ __forceinline__ void wino8_body(const float *__restrict__ x, const fl
 #ifdef WN_CLOCK
     ck[5] = __builtin_amdgcn_s_memtime();
     ck[7] = __builtin_amdgcn_s_memrealtime();
-    if (lane == 0 && (w & 3) == 0 && blockIdx.z == 0) {
-        const unsigned b = (blockIdx.y * gridDim.x + blockIdx.x) & 4095;
+    if (lane == 0 && (w & 3) == 0 && blk.sl == 0) {
+        const unsigned b = (unsigned)(kb * g.TB + blk.tb) & 4095;
         for (int i = 0; i < 8; ++i) wn_clk8[b][PH][i] = ck[i];
     }
 #endif
@@ -1050,9 +1080,14 @@ static smmd_status wino3x3_conv(const float *x, const float *u, const float *x2,
     // tile rows that are whole lane groups of a wave need no edge loads
     const bool edge = 64 % g.TW != 0;
     if (wino8_enabled()) {
+        g.TB = (int)tb;
+        g.KB = ko / WN_KB;
+        g.S = S;
+        const int64_t nblk = tb * g.KB * S;
+        if (nblk > 0x7fffffff) return SMMD_EINVAL;
         auto k8 = edge ? (g.relu ? wino_conv8_kernel<true, true> : wino_conv8_kernel<true, false>)
                        : (g.relu ? wino_conv8_kernel<false, true> : wino_conv8_kernel<false, false>);
-        k8<<<grid, dim3(W8_T), WN_LDS, st>>>(x, u, b1, out, g);
+        k8<<<dim3((unsigned)nblk), dim3(W8_T), WN_LDS, st>>>(x, u, b1, out, g);
     } else if (!edge) {
         wino_conv_kernel<false><<<grid, dim3(WN_T), WN_LDS, st>>>(x, u, b1, out, g);
     } else {
