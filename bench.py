@@ -661,7 +661,16 @@ def main():
         local = 0
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
-    if world > 1:
+    # SMMD_DP_FORCE=1 at N = 1: a world-size-1 group whose rank takes the
+    # data-parallel path (collectives.force_dp), so the RCCL device branches
+    # run on one GPU; the line says so in config.dp_forced
+    dp_forced = world == 1 and os.environ.get('SMMD_DP_FORCE', '0') != '0'
+    if dp_forced:
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        os.environ.setdefault('MASTER_PORT', str(_free_port()))
+        os.environ.setdefault('RANK', '0')
+        os.environ.setdefault('WORLD_SIZE', '1')
+    if world > 1 or dp_forced:
         if backend == 'nccl':
             dist.init_process_group('nccl', device_id=dev)
         else:
@@ -678,7 +687,8 @@ def main():
     cfg = CONFIGS[args.config][0](BATCH)
     size = int(cfg.output_size)
     torch.manual_seed(2 + rank)
-    model = SMMD(cfg, device=dev, process_group=dist.group.WORLD if world > 1 else None,
+    model = SMMD(cfg, device=dev,
+                 process_group=dist.group.WORLD if (world > 1 or dp_forced) else None,
                  dp_mode=args.dp_mode, channels_last=bool(args.channels_last))
     gen = torch.Generator(device=dev).manual_seed(0 + rank)
     images = [torch.rand(BATCH, 3, size, size, device=dev, generator=gen) for _ in range(4)]
@@ -938,6 +948,7 @@ def main():
                                                                        BATCH),
                    'model': cfg.architecture, 'global_batch': BATCH * world, 'seq_len': None,
                    'parallelism': 'dp%d' % world, 'dp_mode': args.dp_mode,
+                   'dp_forced': dp_forced,
                    'memory_format': 'channels_last' if args.channels_last else 'nchw',
                    'miopen_winograd': bool(args.miopen_winograd),
                    'miopen_find': bool(args.miopen_find),
@@ -955,8 +966,13 @@ def main():
         'losses': {'g_loss': g_loss, 'd_loss': d_loss},
     }
     if step_ms.get('D') and step_ms.get('G'):
-        result['cycle_value'] = round(world * BATCH * 6 / ((5 * step_ms['D'] + step_ms['G'])
-                                                           * 1e-3), 2)
+        # from the instrumented pass (HIP events around every library call and
+        # every step: ~10 % slower than the timed region), so not a clean
+        # timing; the timed region itself covers whole 5D+1G cycles when
+        # `steps` is a multiple of 6 (whole_cycles_timed)
+        result['instrumented_cycle_value'] = round(
+            world * BATCH * 6 / ((5 * step_ms['D'] + step_ms['G']) * 1e-3), 2)
+    result['whole_cycles_timed'] = (counts['G'] if counts['D'] == 5 * counts['G'] else None)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             result['cpu_baseline'] = cpu_baseline(args.cpu_steps)
@@ -964,7 +980,7 @@ def main():
             result['cpu_baseline'] = {'error': repr(e)}
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if world > 1 or dp_forced:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -226,10 +226,21 @@ __device__ __forceinline__ uint32_t wn_lds_addr(const void *p) {
 // read wait for it; its completion is the explicit waits below, then a
 // barrier.  The address is a uniform SGPR base plus a fixed per-lane offset,
 // so a chunk's pieces cost no vector arithmetic
+// Every piece's completion is a vmcnt(0) wait by its issuing wave before the
+// stage barrier (wn_wait_vm0 below; no partial counts).  The compiler does
+// not count these loads, which can only make its own vmcnt(N) waits for the
+// row loads wait longer, never shorter.  WN_DMA_SYNC (the `conservative` make
+// target, checked bit for bit against the shipped build by
+// tools/lib_bitexact.py) waits for each piece right after its issue.
+#ifdef WN_DMA_SYNC
+#define WN_DMA_WAIT "\n\ts_waitcnt vmcnt(0)"
+#else
+#define WN_DMA_WAIT ""
+#endif
 __device__ __forceinline__ void wn_glds16(uint32_t voff, const void *sbase, uint32_t lds_dst) {
     unsigned keep;
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
-                 "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0" WN_DMA_WAIT
                  : "=&s"(keep)
                  : "v"(voff), "s"(sbase), "s"(lds_dst)
                  : "memory");
@@ -248,7 +259,6 @@ __device__ __forceinline__ f2v wn_ld2(uint32_t voff, __amdgpu_buffer_rsrc_t rs) 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t wn_rsrc(const float *base) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(base), 0, 0x7fffffff, 0x00020000);
 }
-__device__ __forceinline__ void wn_wait_vm8() { asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); }
 __device__ __forceinline__ void wn_wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 #ifdef WN_CLOCK        // diagnostic build only (-DWN_CLOCK): per-block clock stamps
@@ -303,7 +313,7 @@ __global__ __launch_bounds__(WN_T, 1) void wino_conv_kernel(
     // compiler's waits for the rows also retire the older stage pieces (vmcnt
     // is in order); a vmcnt(0) before the barrier makes that explicit.
     // Addresses: a uniform SGPR base per chunk plus fixed per-lane byte
-    // offsets (x is under 4 GiB: smmd_wino3x3_supported).
+    // offsets (x is under 2 GiB: smmd_wino3x3_supported).
     f2v raw[2][4];
     uint32_t xoff[2][4];                // byte offsets of the rows from the chunk base
     const int TH = g.H >> 1;
@@ -853,7 +863,7 @@ __device__ __forceinline__ void wino8_body(const float *__restrict__ x, const fl
     const int ety = er / g.TW, etx = er - ety * g.TW;
     // stores: a uniform descriptor on this slab, the lane's byte offset of
     // its row-0 channel (k0) fixed, each row adding a uniform multiple of H W
-    // (y under 4 GiB: smmd_wino3x3_supported); each lane stores its own
+    // (y under 2 GiB: smmd_wino3x3_supported); each lane stores its own
     // tile's two output rows (8 bytes each, 32 tiles of a row contiguous)
     const int k0 = kb * WN_KB + kh * 32 + 4 * hl;
     const uint32_t yo =
@@ -987,11 +997,13 @@ extern "C" size_t smmd_wino3x3_filter_bytes(int ko, int ci) {
     return (size_t)16 * ko * ci * sizeof(float);
 }
 
-// (x and y under 4 GiB: the conv kernels address them by 32-bit byte offsets)
+// (x and y under 2 GiB: the conv kernels address them by 32-bit byte offsets
+// into a buffer range of 0x7fffffff bytes, and an offset at or past 2^31 is
+// the out-of-range sentinel that reads zeros)
 extern "C" int smmd_wino3x3_supported(int n, int ci, int ko, int h, int w_img) {
     return n > 0 && ci > 0 && ko > 0 && ci % WN_CC == 0 && ko % WN_KB == 0 && h > 0 &&
-           w_img > 0 && h % 2 == 0 && w_img % 2 == 0 && (int64_t)n * ci * h * w_img < (1ll << 30) &&
-           (int64_t)n * ko * h * w_img < (1ll << 30);
+           w_img > 0 && h % 2 == 0 && w_img % 2 == 0 && (int64_t)n * ci * h * w_img < (1ll << 29) &&
+           (int64_t)n * ko * h * w_img < (1ll << 29);
 }
 
 extern "C" smmd_status smmd_wino3x3_filter(const float *w, int ko, int ci, int mode, float *u,

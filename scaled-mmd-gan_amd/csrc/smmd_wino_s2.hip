@@ -51,7 +51,8 @@ __device__ __forceinline__ float s2_from_right(float v) {   // lane l gets lane 
 
 // buffer access: a wave-uniform base in the descriptor, the lane's 32-bit
 // byte offset in one VGPR (no 64-bit address arithmetic per access; tensors
-// under 4 GiB, the *_supported checks); an offset past the range reads zeros
+// under 2 GiB, the *_supported checks: the range is 0x7fffffff bytes and
+// S2_OOB = 2^31 its out-of-range sentinel); an offset past the range reads zeros
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t s2_rsrc(const void *base) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, 0x7fffffff, 0x00020000);
 }
@@ -743,8 +744,8 @@ using namespace smmd;
 
 extern "C" int smmd_wino4x4s2_supported(int n, int ci, int ko, int h, int w_img) {
     return n > 0 && ci > 0 && ko > 0 && ci % S2_CC == 0 && ko % S2_KB == 0 && h > 0 &&
-           w_img > 0 && h % 4 == 0 && w_img % 4 == 0 && (int64_t)n * ci * h * w_img < (1ll << 30) &&
-           (int64_t)n * ko * h * w_img < (1ll << 32);   // x, y under 4 GiB (buffer offsets)
+           w_img > 0 && h % 4 == 0 && w_img % 4 == 0 && (int64_t)n * ci * h * w_img < (1ll << 29) &&
+           (int64_t)n * ko * h * w_img < (1ll << 31);   // x, y (n ko h w / 4) under 2 GiB (buffer offsets)
 }
 
 extern "C" size_t smmd_wino4x4s2_filter_bytes(int ko, int ci) {
@@ -868,8 +869,8 @@ extern "C" smmd_status smmd_wino4x4s2_conv2(const float *x, const float *u, cons
 
 extern "C" int smmd_wino4x4s2t_supported(int n, int k, int c, int hg, int wg) {
     return n > 0 && k > 0 && c > 0 && k % 8 == 0 && c % 64 == 0 && hg > 0 && wg > 0 &&
-           hg % 2 == 0 && wg % 2 == 0 && (int64_t)n * k * hg * wg < (1ll << 30) &&
-           (int64_t)n * c * 4 * hg * wg < (1ll << 30);   // gy, dx under 4 GiB (buffer offsets)
+           hg % 2 == 0 && wg % 2 == 0 && (int64_t)n * k * hg * wg < (1ll << 29) &&
+           (int64_t)n * c * 4 * hg * wg < (1ll << 29);   // gy, dx under 2 GiB (buffer offsets)
 }
 
 extern "C" smmd_status smmd_wino4x4s2t_filter(const float *w, int k, int c, float *u,

@@ -613,7 +613,8 @@ using namespace smmd;
 
 extern "C" int smmd_wino3x3_wgrad_supported(int n, int ci, int co, int h, int w_img) {
     return n > 0 && ci > 0 && co > 0 && ci % 64 == 0 && co % 64 == 0 && h > 0 && w_img > 0 &&
-           h % 2 == 0 && w_img % 4 == 0 && (int64_t)n * (ci + co) * h * w_img < (1ll << 40);
+           h % 2 == 0 && w_img % 4 == 0 && (int64_t)n * (ci + co) * h * w_img < (1ll << 40) &&
+           (int64_t)h * w_img < (1ll << 23);   // a 64-channel range of one image under 2 GiB
 }
 
 static size_t wgrad_v1_ws(int n, int ci, int co, int h, int w_img) {

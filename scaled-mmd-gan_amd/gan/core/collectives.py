@@ -12,6 +12,23 @@ import torch
 import torch.distributed as dist
 
 
+def force_dp():
+    """SMMD_DP_FORCE=1: a world-size-1 group takes the data-parallel path
+    (packed all-gather, bucketed in-backward all-reduce, parameter broadcast)
+    instead of the one-process shortcuts, so the RCCL device branches below
+    run on a one-GPU box (tests/test_gpu_dist.py::test_rccl_world1_*)."""
+    import os
+    return os.environ.get('SMMD_DP_FORCE', '0') != '0'
+
+
+def is_dp(group):
+    """True when ``group`` takes the data-parallel path: more than one rank,
+    or any initialised group under SMMD_DP_FORCE=1."""
+    if group is None:
+        return False
+    return dist.get_world_size(group) > 1 or force_dp()
+
+
 def _host_staged(t, group):
     return t.is_cuda and dist.get_backend(group) == 'gloo'
 

@@ -138,12 +138,14 @@ def _thin_wgrad(gy, x):
 WINO = os.environ.get('SMMD_WINO', '1') != '0'
 
 
-def _under_4g(x, out_per_in_channel):
+def _under_2g(x, out_per_in_channel):
     """The Winograd kernels address their input and output by 32-bit byte
-    offsets: both under 2^30 floats (out_per_in_channel: output elements per
-    input element of one channel plane, e.g. cout for a same-size conv)."""
+    offsets into a 0x7fffffff-byte buffer range (2^31 is the out-of-range
+    sentinel): both under 2^29 floats = 2 GiB (out_per_in_channel: output
+    elements per input element of one channel plane, e.g. cout for a same-size
+    conv).  The library's *_supported checks hold the same bound."""
     plane = x.shape[0] * x.shape[2] * x.shape[3]
-    return x.numel() < (1 << 30) and plane * out_per_in_channel < (1 << 30)
+    return x.numel() < (1 << 29) and plane * out_per_in_channel < (1 << 29)
 
 
 def wino_applicable(x, cin, cout, k, stride, padding):
@@ -156,7 +158,7 @@ def wino_applicable(x, cin, cout, k, stride, padding):
             and x.is_contiguous() and k == 3 and s == (1, 1) and p == (1, 1)
             and x.shape[1] == cin and cin % 8 == 0 and cout % 64 == 0
             and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0 and x.shape[2] > 0
-            and x.shape[3] > 0 and x.shape[0] > 0 and _under_4g(x, cout))
+            and x.shape[3] > 0 and x.shape[0] > 0 and _under_2g(x, cout))
 
 
 # transformed filters of the weights in use: a critic step convolves each
@@ -206,8 +208,23 @@ def _cache_put(key, w, u):
 # the Winograd filter transforms form them from the raw W and the device
 # sigma and s (smmd_wino3x3_filter_sn, smmd_wino4x4s2(t)_filter_sn, bit-identical
 # to transforming a written W_eff), and every other consumer materialises the
-# values first (`materialize`).  id(tensor) -> [weakref, SN entry, fold, done].
+# values first (`materialize`).  id(tensor) -> [weakref, SN entry, fold, done,
+# stamp].  The values are formed from the entry's CURRENT W, sigma and s, so a
+# record is valid only while they are the ones of its refresh: `stamp` holds
+# the entry's refresh generation and the weight's FlatAdam epoch and version,
+# and a reader after a later refresh or update gets an error instead of the
+# values of another W (model._detach_step_state drops lazy tensors at the end
+# of every step, so the training loop never holds one that long).
 _LAZY = {}
+
+
+class StaleLazyWeight(RuntimeError):
+    pass
+
+
+def _lazy_stamp(entry):
+    W = entry.weight
+    return (getattr(entry, 'refresh_gen', 0), _param_epoch(W), W._version)
 
 
 def register_lazy(w, entry, fold):
@@ -215,12 +232,25 @@ def register_lazy(w, entry, fold):
     key = id(w)
     ref = weakref.ref(w, lambda r, k=key: _LAZY.pop(k, None) if (
         _LAZY.get(k) is not None and _LAZY[k][0] is r) else None)
-    _LAZY[key] = [ref, entry, bool(fold), False]
+    _LAZY[key] = [ref, entry, bool(fold), False, _lazy_stamp(entry)]
+
+
+def is_lazy(w):
+    """True for an unwritten lazy W_eff, current or stale."""
+    rec = _LAZY.get(id(w))
+    return rec is not None and rec[0]() is w and not rec[3]
 
 
 def _lazy(w):
     rec = _LAZY.get(id(w))
-    return rec if rec is not None and rec[0]() is w and not rec[3] else None
+    if rec is None or rec[0]() is not w or rec[3]:
+        return None
+    if rec[4] != _lazy_stamp(rec[1]):
+        raise StaleLazyWeight(
+            'an unwritten spectrally normalised weight (W_eff) of an earlier refresh was '
+            'read after its layer was refreshed or updated; its values can no longer be '
+            'formed (materialize it before the update, or use the current W_eff)')
+    return rec
 
 
 def materialize(w):
@@ -395,7 +425,7 @@ def _is_s2(x, w, stride, padding):
     H, W % 4 == 0, ci % 2 == 0, co % 64 == 0."""
     return (w.dim() == 4 and w.shape[2] == 4 and w.shape[3] == 4 and _s2_shape_ok(x, stride, padding)
             and x.shape[1] == w.shape[1] and w.shape[1] % 2 == 0 and w.shape[0] % 64 == 0
-            and x.shape[2] % 4 == 0 and x.shape[3] % 4 == 0 and _under_4g(x, w.shape[0] / 4))
+            and x.shape[2] % 4 == 0 and x.shape[3] % 4 == 0 and _under_2g(x, w.shape[0] / 4))
 
 
 def _is_s2t(g, w, stride, padding):
@@ -404,7 +434,7 @@ def _is_s2t(g, w, stride, padding):
     c % 64 == 0."""
     return (w.dim() == 4 and w.shape[2] == 4 and w.shape[3] == 4 and _s2_shape_ok(g, stride, padding)
             and g.shape[1] == w.shape[0] and w.shape[0] % 8 == 0 and w.shape[1] % 64 == 0
-            and g.shape[2] % 2 == 0 and g.shape[3] % 2 == 0 and _under_4g(g, w.shape[1] * 4))
+            and g.shape[2] % 2 == 0 and g.shape[3] % 2 == 0 and _under_2g(g, w.shape[1] * 4))
 
 
 def _s2_filter(w, transposed):

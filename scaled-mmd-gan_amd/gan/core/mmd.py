@@ -26,7 +26,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from .collectives import all_reduce_, gather_rows
+from .collectives import all_reduce_, gather_rows, is_dp
 from . import _lib
 
 _eps = 1.0e-5   # gan/core/mmd.py:6
@@ -138,7 +138,7 @@ class _MMD2Fused(torch.autograd.Function):
         d = X.shape[1]
         ml, nl = X.shape[0], Y.shape[0]
         shard = False
-        if group is not None and dist.get_world_size(group) > 1:
+        if is_dp(group):
             world, rank = dist.get_world_size(group), dist.get_rank(group)
             if exchange is not None and exchange.group is group and not exchange.used:
                 Xa, Ya = exchange.gather(X, Y)     # the step's one packed all-gather
@@ -512,7 +512,7 @@ class loss_group:
     all-gather together with the step's other small messages."""
 
     def __init__(self, group, exchange=None):
-        self.group = group if (group is not None and dist.get_world_size(group) > 1) else None
+        self.group = group if is_dp(group) else None
         self.exchange = exchange if self.group is not None else None
 
     def __enter__(self):

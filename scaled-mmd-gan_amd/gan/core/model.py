@@ -32,7 +32,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from . import convops, mmd, ops
+from . import collectives, convops, mmd, ops
 from .architecture import get_networks
 from .collectives import GradBuckets, StepExchange
 from .optim import FlatAdam
@@ -107,8 +107,9 @@ class MMD_GAN:
         self.config = c
         self.device = device or torch.device('cuda', torch.cuda.current_device())
         self.group = process_group
-        self.world = dist.get_world_size(process_group) if (
-            process_group is not None or (dist.is_available() and dist.is_initialized())) else 1
+        grouped = process_group is not None or (dist.is_available() and dist.is_initialized())
+        self.world = dist.get_world_size(process_group) if grouped else 1
+        self._dp_forced = bool(grouped and collectives.force_dp())
         if dp_mode not in ('tower', 'global'):
             raise ValueError(dp_mode)
         self.dp_mode = dp_mode
@@ -154,15 +155,22 @@ class MMD_GAN:
         self.last = {}
         self._ex = None
         self._buckets = {}
-        if self.world > 1:
+        if self.dp:
             self._broadcast_params()
             for opt in (self.d_optim, self.g_optim):
                 self._bucket_for(opt)
             self._group_sn(self.sn_D, self.d_optim)
 
     # ------------------------------------------------------------------
+    @property
+    def dp(self):
+        """The data-parallel path: several ranks, or (SMMD_DP_FORCE=1) the one
+        rank of an initialised group, which then runs the collectives on one
+        GPU (collectives.force_dp)."""
+        return self.world > 1 or getattr(self, '_dp_forced', False)
+
     def _dist_group(self):
-        return self.group if self.world > 1 else None
+        return self.group if self.dp else None
 
     def _broadcast_params(self):
         for opt in (self.g_optim, self.d_optim):
@@ -429,11 +437,11 @@ class MMD_GAN:
         bank.set_groups(groups, direct)
 
     def _arm(self, opt):
-        if self.world > 1:
+        if self.dp:
             self._bucket_for(opt).arm()
 
     def _exchange(self, opt):
-        if self.world == 1:
+        if not self.dp:
             opt.step()
             return
         # buckets not already issued from the backward's hooks go now; wait all
@@ -463,12 +471,12 @@ class MMD_GAN:
         if ref:       # the generator's gradient set, computed and discarded
             torch.autograd.grad(g_loss, self.g_vars, retain_graph=True)
         gd = self._gdirect()
-        dpgd = gd and self.world > 1
+        dpgd = gd and self.dp
         self.sn_D.arm_gdirect(gd and not dpgd)
-        self.sn_D.arm_direct(self.world > 1)        # the grouped SN nodes' direct writes
+        self.sn_D.arm_direct(self.dp)        # the grouped SN nodes' direct writes
         tower_clip = self.d_optim.clip_norm if (dpgd and self.dp_mode == 'tower') else 0.0
         self.sn_D.arm_dp_gdirect(dpgd, clip=tower_clip)
-        if self.world > 1:
+        if self.dp:
             bk = self._bucket_for(self.d_optim)
             bk.clip_exclude = self._sn_tensor_ids() if tower_clip > 0 else frozenset()
         self._dpgd = dpgd
@@ -510,7 +518,7 @@ class MMD_GAN:
         if not (self.d_optim._sn is not None and bool(self.sn_D.entries)
                 and os.environ.get('SMMD_SN_GDIRECT', '1') != '0'):
             return False
-        if self.world == 1:
+        if not self.dp:
             return True
         return (self.sn_D.groups is not None and self.sn_D._direct is not None
                 and os.environ.get('SMMD_SN_DP_GDIRECT', '1') != '0')
@@ -542,7 +550,7 @@ class MMD_GAN:
                 for name in ('w_eff', 'w_fold'):
                     t = getattr(mod, name, None)
                     if torch.is_tensor(t):
-                        setattr(mod, name, None if convops._lazy(t) is not None else t.detach())
+                        setattr(mod, name, None if convops.is_lazy(t) else t.detach())
         for net in (self.discriminator, self.generator):
             if getattr(net, '_fold_cache', None) is not None:
                 net._fold_cache = None
@@ -597,7 +605,7 @@ class MMD_GAN:
                 self._graphs.close()
             self._graphs = None
             return
-        if self.world > 1:
+        if self.dp:
             raise NotImplementedError('step graphs are single-GPU (the collectives run eagerly)')
         if self.schedule != 'lean':
             raise NotImplementedError("step graphs capture the lean schedule")

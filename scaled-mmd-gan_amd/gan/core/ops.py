@@ -124,8 +124,8 @@ class _ScaledLoss(torch.autograd.Function):
 
 
 def _b_total(jac, process_group):
-    group = process_group if (process_group is not None and
-                              dist.get_world_size(process_group) > 1) else None
+    from .collectives import is_dp
+    group = process_group if is_dp(process_group) else None
     return group, jac.shape[1] * (dist.get_world_size(group) if group is not None else 1)
 
 

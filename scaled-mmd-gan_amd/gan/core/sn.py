@@ -59,9 +59,15 @@ def _launch_refresh(bank, update_u, flags, Ws, ss):
         L = arr[i]
         L.fold = 1 if fold else 0
         L.W = W.data_ptr()
-        if i in lazy and bool(fold) == bool(e.fold):
+        # every refresh rewrites the entry's sigma (and u): a lazy W_eff of an
+        # earlier refresh can no longer be formed (convops._lazy raises)
+        e.refresh_gen = getattr(e, 'refresh_gen', 0) + 1
+        if i in lazy and bool(fold) == bool(e.fold) and W.is_contiguous():
             # consumed only through the Winograd filter transforms, which form
-            # it from W, sigma and s (convops.register_lazy): P3 skips it
+            # it from W, sigma and s (convops.register_lazy): P3 skips it.
+            # Only an OIHW-contiguous W: the _filter_sn kernels read it as
+            # OIHW, and a channels_last W_eff placeholder copied by a
+            # .contiguous() would escape the registry unwritten
             from .convops import register_lazy
             register_lazy(W_eff, e, fold)
             L.W_eff = None

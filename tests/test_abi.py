@@ -127,6 +127,54 @@ def test_argument_validation_without_gpu(L):
     assert L.smmd_wino4x4s2_conv(x, x, None, x, 64, 512, 1024, 8, 8, x, need - 1, None) == 3
 
 
+def test_conservative_variant_exports_every_symbol():
+    """The conservative LDS-DMA build (`make conservative`, built by
+    __graft_entry__.build(); tools/lib_bitexact.py compares it with the
+    shipped one bit for bit on the GPU) loads and exports the same ABI."""
+    path = os.path.join(ROOT, 'scaled-mmd-gan_amd', 'lib', 'libsmmd_hip_dmasync.so')
+    if not os.path.exists(path):
+        pytest.skip('conservative variant not built (make -C scaled-mmd-gan_amd/csrc conservative)')
+    C = ctypes.CDLL(path)
+    for name in _declared():
+        assert hasattr(C, name), name
+
+
+def test_wino_supported_2gib_boundary(L):
+    """The Winograd kernels address x and y through buffer descriptors whose
+    range is 0x7fffffff bytes (2^31 = the out-of-range sentinel): every
+    tensor must stay under 2^29 floats, and `supported` says 0 at the edge."""
+    # 3x3: x = n ci h w, y = n ko h w floats
+    assert L.smmd_wino3x3_supported(1, 8, 64, 2048, 4096 - 2) == 1           # y just under 2^29
+    assert L.smmd_wino3x3_supported(1, 8, 64, 2048, 4096) == 0               # y = 2^29
+    assert L.smmd_wino3x3_supported(1, 64, 64, 2048, 4096) == 0              # x = 2^29
+    # stride 2: x = n ci h w, y = n ko h w / 4
+    assert L.smmd_wino4x4s2_supported(1, 8, 64, 4096, 8192 - 4) == 1
+    assert L.smmd_wino4x4s2_supported(1, 8, 64, 4096, 8192) == 0            # y = 2^29
+    assert L.smmd_wino4x4s2_supported(1, 32, 64, 4096, 4096) == 0           # x = 2^29
+    # transposed: gy = n k hg wg, dx = 4 n c hg wg
+    assert L.smmd_wino4x4s2t_supported(1, 8, 64, 1024, 2048 - 2) == 1
+    assert L.smmd_wino4x4s2t_supported(1, 8, 64, 1024, 2048) == 0           # dx = 2^29
+    assert L.smmd_wino4x4s2t_supported(1, 256, 64, 1024, 2048) == 0         # gy = 2^29
+    # 3x3 weight gradient: one image's 64-channel range under 2 GiB
+    assert L.smmd_wino3x3_wgrad_supported(1, 64, 64, 2048, 4096 - 4) == 1
+    assert L.smmd_wino3x3_wgrad_supported(1, 64, 64, 2048, 4096) == 0
+    # the Python routing helper holds the same bound
+    from gan.core import convops
+
+    class _T:
+        def __init__(self, shape):
+            self.shape = shape
+
+        def numel(self):
+            n = 1
+            for s in self.shape:
+                n *= s
+            return n
+    assert convops._under_2g(_T((1, 8, 2048, 4094)), 64)
+    assert not convops._under_2g(_T((1, 8, 2048, 4096)), 64)
+    assert not convops._under_2g(_T((1, 64, 2048, 4096)), 1)
+
+
 def test_product_never_imports_oracle():
     pkg = os.path.join(ROOT, 'scaled-mmd-gan_amd')
     for dp, _, fs in os.walk(pkg):

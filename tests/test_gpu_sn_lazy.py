@@ -118,3 +118,52 @@ def test_critic_step_lazy_equals_written(monkeypatch):
     assert l1 == l0
     assert ((m1 - m0).abs().max() / m0.abs().max()).item() < 1e-5
     assert (p1 - p0).abs().max().item() <= 2.0001 * lr
+
+
+def test_critic_step_lazy_channels_last(monkeypatch):
+    """With channels_last weights no layer is registered lazy --
+    the _filter_sn transforms read W as OIHW -- and a critic update with
+    SMMD_SN_LAZY=1 equals one with 0 (same tolerance as above)."""
+    import bench
+    from gan.core import convops, miopen_db
+    from gan.core.smmd import SMMD
+    miopen_db.install()
+    res = []
+    for lazy in ('1', '0'):
+        monkeypatch.setenv('SMMD_SN_LAZY', lazy)
+        convops.clear_wino_cache()
+        cfg = bench.imagenet_config(8)
+        torch.manual_seed(2)
+        model = SMMD(cfg, device=torch.device(DEV), channels_last=True)
+        g = torch.Generator(device=DEV).manual_seed(0)
+        imgs = torch.rand(8, 3, 64, 64, device=DEV, generator=g).contiguous(
+            memory_format=torch.channels_last)
+        with torch.no_grad():
+            outs = model.sn_D.refresh(update_u=False)
+        assert not any(convops.is_lazy(w) for w in outs)
+        torch.manual_seed(5)
+        g_loss, d_loss, _ = model.d_step(imgs)
+        res.append((float(d_loss), model.d_optim.m.clone()))
+    (l1, m1), (l0, m0) = res
+    assert abs(l1 - l0) <= 1e-6 * max(1.0, abs(l0))
+    assert ((m1 - m0).abs().max() / m0.abs().max()).item() < 1e-5
+
+
+def test_stale_lazy_weight_raises():
+    """A lazy W_eff read after its layer's next refresh (or an update of W)
+    raises instead of being formed from the new W, sigma and s."""
+    from gan.core import convops
+    bank = _bank([(128, 64, 3)], [False], seed=4)
+    bank.set_lazy([0])
+    old = bank.refresh(update_u=True)[0]
+    assert convops.is_lazy(old) and convops._lazy(old) is not None
+    new = bank.refresh(update_u=True)[0]
+    assert convops._lazy(new) is not None
+    with pytest.raises(convops.StaleLazyWeight):
+        convops._lazy(old)
+    with pytest.raises(convops.StaleLazyWeight):
+        convops.materialize(old)
+    with torch.no_grad():
+        bank.entries[0].weight.mul_(1.5)          # an in-place update of W
+    with pytest.raises(convops.StaleLazyWeight):
+        convops._wino_filter(new, 128, 64, 0)

@@ -1,6 +1,13 @@
-"""Bit-for-bit comparison of two library builds on the stride-2 forward
-convolution (plain and pair form), for block-order changes that must not move
-a single bit: python tools/lib_bitexact.py LIB_A LIB_B"""
+"""Bit-for-bit comparison of two library builds on the Winograd convolutions,
+for changes that must not move a single bit (block orders, the LDS-DMA wait
+placement): python tools/lib_bitexact.py LIB_A LIB_B
+
+Covered: the 3x3 conv over every tests/test_gpu_wino.py shape in both forms
+(8-wave default, SMMD_WINO8=0 the 4-wave one), modes 0 and 1 of the filter,
+the relu epilogue and the pair form; the stride-2 conv (plain and pair) over
+its fold-layer shapes.  `make -C scaled-mmd-gan_amd/csrc conservative` builds
+the conservative variant (every filter-stage LDS-DMA piece waited for right
+after its issue, -DWN_DMA_SYNC) that this compares with the shipped build."""
 import ctypes
 import os
 import sys
@@ -9,11 +16,17 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, 'scaled-mmd-gan_amd'))
+sys.path.insert(0, os.path.join(ROOT, 'tests'))
 from gan.core import _lib  # noqa: E402
 
 # (N, C, K, H, W): split reductions, the edge kernel, odd tile counts, the fold layers
-SHAPES = [(2, 8, 64, 8, 12), (1, 64, 64, 4, 264), (4, 512, 64, 8, 8), (2, 6, 128, 12, 8),
-          (64, 64, 128, 64, 64), (64, 256, 512, 16, 16), (64, 512, 512, 8, 8)]
+S2_SHAPES = [(2, 8, 64, 8, 12), (1, 64, 64, 4, 264), (4, 512, 64, 8, 8), (2, 6, 128, 12, 8),
+             (64, 64, 128, 64, 64), (64, 256, 512, 16, 16), (64, 512, 512, 8, 8)]
+
+
+def _w3_shapes():
+    from test_gpu_wino import PAIR_SHAPES, SHAPES
+    return SHAPES, PAIR_SHAPES
 
 
 def load(path):
@@ -25,7 +38,11 @@ def load(path):
     return L
 
 
-def run(L, x, w, b, x2, w2, st):
+def _ws(nbytes, dev):
+    return torch.empty(max(nbytes // 4, 4), device=dev)
+
+
+def run_s2(L, x, w, b, x2, w2, st):
     N, C, H, W = x.shape
     K = w.shape[0]
     u = torch.empty(L.smmd_wino4x4s2_filter_bytes(K, C) // 4, device=x.device)
@@ -34,16 +51,52 @@ def run(L, x, w, b, x2, w2, st):
     assert L.smmd_wino4x4s2_filter(_lib.ptr(w2), K, C, _lib.ptr(u2), u2.numel() * 4, st) == 0
     y = torch.empty(N, K, H // 2, W // 2, device=x.device)
     nb = L.smmd_wino4x4s2_workspace_bytes(N, C, K, H, W)
-    ws = torch.empty(max(nb // 4, 4), device=x.device)
+    ws = _ws(nb, x.device)
     assert L.smmd_wino4x4s2_conv(_lib.ptr(x), _lib.ptr(u), _lib.ptr(b), _lib.ptr(y), N, C, K, H, W,
                                  _lib.ptr(ws), nb, st) == 0
     y2 = torch.empty_like(y)
     nb2 = L.smmd_wino4x4s2_conv2_workspace_bytes(N, C, K, H, W)
-    ws2 = torch.empty(max(nb2 // 4, 4), device=x.device)
+    ws2 = _ws(nb2, x.device)
     assert L.smmd_wino4x4s2_conv2(_lib.ptr(x), _lib.ptr(u), _lib.ptr(x2), _lib.ptr(u2), _lib.ptr(b),
                                   _lib.ptr(y2), N, C, K, H, W, _lib.ptr(ws2), nb2, st) == 0
     torch.cuda.synchronize()
     return y.cpu(), y2.cpu()
+
+
+def run_w3(L, x, w, b, x2, w2, st, pair):
+    """mode-0 conv, mode-1 conv (w read as [ci', co'] = the input gradient's
+    filter), relu; the pair form when `pair`."""
+    N, C, H, W = x.shape
+    K = w.shape[0]
+    outs = []
+    nb = L.smmd_wino3x3_workspace_bytes(N, C, K, H, W)
+    ws = _ws(nb, x.device)
+    for mode in ((0,) if pair else (0, 1)):
+        u = torch.empty(L.smmd_wino3x3_filter_bytes(K, C) // 4, device=x.device)
+        wm = w if mode == 0 else w.reshape(C, K, 3, 3)    # same bytes, other reading
+        assert L.smmd_wino3x3_filter(_lib.ptr(wm), K, C, mode, _lib.ptr(u), u.numel() * 4, st) == 0
+        y = torch.empty(N, K, H, W, device=x.device)
+        if pair:
+            u2 = torch.empty_like(u)
+            assert L.smmd_wino3x3_filter(_lib.ptr(w2), K, C, 0, _lib.ptr(u2), u2.numel() * 4,
+                                         st) == 0
+            nb2 = L.smmd_wino3x3_conv2_workspace_bytes(N, C, K, H, W)
+            ws2 = _ws(nb2, x.device)
+            assert L.smmd_wino3x3_conv2(_lib.ptr(x), _lib.ptr(u), _lib.ptr(x2), _lib.ptr(u2),
+                                        _lib.ptr(b), _lib.ptr(y), N, C, K, H, W, _lib.ptr(ws2),
+                                        nb2, st) == 0
+            outs.append(y)
+            continue
+        assert L.smmd_wino3x3_conv(_lib.ptr(x), _lib.ptr(u), _lib.ptr(b), _lib.ptr(y), N, C, K,
+                                   H, W, _lib.ptr(ws), nb, st) == 0
+        outs.append(y)
+        if mode == 0:
+            yr = torch.empty_like(y)
+            assert L.smmd_wino3x3_conv_relu(_lib.ptr(x), _lib.ptr(u), _lib.ptr(b), _lib.ptr(yr), N,
+                                            C, K, H, W, _lib.ptr(ws), nb, st) == 0
+            outs.append(yr)
+    torch.cuda.synchronize()
+    return [o.cpu() for o in outs]
 
 
 def main():
@@ -51,15 +104,31 @@ def main():
     dev = torch.device('cuda:0')
     st = _lib.stream_handle(dev)
     ok = True
-    for (N, C, K, H, W) in SHAPES:
+    w3, w3pair = _w3_shapes()
+    for form in ('1', '0'):
+        os.environ['SMMD_WINO8'] = form          # read by the library at every call
+        for pair, shapes in ((False, w3), (True, w3pair)):
+            for (N, C, K, H, W) in shapes:
+                g = torch.Generator(device=dev).manual_seed(N + C + K + H + W)
+                x, x2 = (torch.randn(N, C, H, W, device=dev, generator=g) for _ in range(2))
+                w, w2 = (torch.randn(K, C, 3, 3, device=dev, generator=g) for _ in range(2))
+                b = torch.randn(K, device=dev, generator=g)
+                ra = run_w3(A, x, w, b, x2, w2, st, pair)
+                rb = run_w3(B, x, w, b, x2, w2, st, pair)
+                same = all(torch.equal(p, q) for p, q in zip(ra, rb))
+                ok &= same
+                print('3x3', 'wino8' if form == '1' else 'wino4', 'pair' if pair else 'conv',
+                      (N, C, K, H, W), 'bit-identical' if same else 'DIFFERENT', flush=True)
+    os.environ.pop('SMMD_WINO8', None)
+    for (N, C, K, H, W) in S2_SHAPES:
         g = torch.Generator(device=dev).manual_seed(N + C + K + H + W)
         x, x2 = (torch.randn(N, C, H, W, device=dev, generator=g) for _ in range(2))
         w, w2 = (torch.randn(K, C, 4, 4, device=dev, generator=g) for _ in range(2))
         b = torch.randn(K, device=dev, generator=g)
-        ra, rb = run(A, x, w, b, x2, w2, st), run(B, x, w, b, x2, w2, st)
+        ra, rb = run_s2(A, x, w, b, x2, w2, st), run_s2(B, x, w, b, x2, w2, st)
         same = all(torch.equal(p, q) for p, q in zip(ra, rb))
         ok &= same
-        print((N, C, K, H, W), 'bit-identical' if same else 'DIFFERENT', flush=True)
+        print('s2', (N, C, K, H, W), 'bit-identical' if same else 'DIFFERENT', flush=True)
     print('ALL BIT-IDENTICAL' if ok else 'MISMATCH')
     sys.exit(0 if ok else 1)
 
