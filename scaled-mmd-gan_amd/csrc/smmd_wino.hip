@@ -28,6 +28,7 @@
 // 128 accumulator registers and two workgroups per CU (129 / 110 / 101 / 118
 // us vs 132 / 112 / 97 / 102 us on the four SNResNet-64 layers).
 #include "smmd_common.hpp"
+#include "smmd_ldsdma.hpp"
 
 namespace smmd {
 
@@ -214,38 +215,6 @@ __device__ __forceinline__ void wn_vrow(const float (&tl)[4], const float (&tx)[
     v[3] = tx[i] - tr[i];
 }
 
-// LDS byte offset of a shared-memory pointer
-__device__ __forceinline__ uint32_t wn_lds_addr(const void *p) {
-    return (uint32_t)reinterpret_cast<uintptr_t>(
-        (const __attribute__((address_space(3))) void *)p);
-}
-
-// one 1-KiB LDS-DMA piece: 64 lanes x 16 bytes from sbase + voff
-// into LDS at the wave-uniform byte offset lds_dst (lane l at + 16 l).
-// Written as asm because the compiler's own form would make every later LDS
-// read wait for it; its completion is the explicit waits below, then a
-// barrier.  The address is a uniform SGPR base plus a fixed per-lane offset,
-// so a chunk's pieces cost no vector arithmetic
-// Every piece's completion is a vmcnt(0) wait by its issuing wave before the
-// stage barrier (wn_wait_vm0 below; no partial counts).  The compiler does
-// not count these loads, which can only make its own vmcnt(N) waits for the
-// row loads wait longer, never shorter.  WN_DMA_SYNC (the `conservative` make
-// target, checked bit for bit against the shipped build by
-// tools/lib_bitexact.py) waits for each piece right after its issue.
-#ifdef WN_DMA_SYNC
-#define WN_DMA_WAIT "\n\ts_waitcnt vmcnt(0)"
-#else
-#define WN_DMA_WAIT ""
-#endif
-__device__ __forceinline__ void wn_glds16(uint32_t voff, const void *sbase, uint32_t lds_dst) {
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
-                 "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0" WN_DMA_WAIT
-                 : "=&s"(keep)
-                 : "v"(voff), "s"(sbase), "s"(lds_dst)
-                 : "memory");
-}
-
 // one patch row (two floats per lane) at sbase + voff: an ordinary load, so
 // the compiler tracks it (an asm load's destination would count as written
 // at once, and the compiler may copy or reuse the register before the data
@@ -259,7 +228,6 @@ __device__ __forceinline__ f2v wn_ld2(uint32_t voff, __amdgpu_buffer_rsrc_t rs) 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t wn_rsrc(const float *base) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(base), 0, 0x7fffffff, 0x00020000);
 }
-__device__ __forceinline__ void wn_wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 #ifdef WN_CLOCK        // diagnostic build only (-DWN_CLOCK): per-block clock stamps
                        // (tools/wino_pmc.py reads them through smmd_diag_wino_clock)
@@ -343,7 +311,7 @@ __global__ __launch_bounds__(WN_T, 1) void wino_conv_kernel(
 #pragma unroll
             for (int i = 0; i < 4; ++i) raw[e][i] = wn_ld2(xoff[e][i], rs);
     };
-    const uint32_t us_lds = wn_lds_addr(Us) + (uint32_t)__builtin_amdgcn_readfirstlane(w) * 8192u;
+    const uint32_t us_lds = lds_addr(Us) + (uint32_t)__builtin_amdgcn_readfirstlane(w) * 8192u;
     // (per-piece lane offsets, no instruction offset: an LDS-DMA's immediate
     // offset would move its LDS destination too)
     uint32_t uoff[8];
@@ -353,7 +321,7 @@ __global__ __launch_bounds__(WN_T, 1) void wino_conv_kernel(
         const float4 *sb = ubase(cc);
         const uint32_t dst = us_lds + (uint32_t)(cc & 1) * (WN_STAGE * 4);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) wn_glds16(uoff[i], sb, dst + i * 1024);
+        for (int i = 0; i < 8; ++i) glds16(uoff[i], sb, dst + i * 1024);
     };
     f32x16 acc[16];
 #pragma unroll
@@ -414,7 +382,7 @@ __global__ __launch_bounds__(WN_T, 1) void wino_conv_kernel(
                     make_float2(v[0][i][j], v[1][i][j]);
     }
     if (tid < WN_KB) Bs[tid] = bias_k;
-    wn_wait_vm0();                          // chunk 0's stage landed (the rows' waits did it)
+    dma_wait_all();                          // chunk 0's stage landed (the rows' waits did it)
     __syncthreads();
 
     for (int cc = 0; cc + 1 < nchunk; ++cc) {
@@ -504,7 +472,7 @@ __global__ __launch_bounds__(WN_T, 1) void wino_conv_kernel(
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
-        wn_wait_vm0();                      // chunk cc + 1's filter stage landed
+        dma_wait_all();                      // chunk cc + 1's filter stage landed
         __syncthreads();
     }
     WN_MFMA_CHUNK((nchunk - 1) & 1);
@@ -704,7 +672,7 @@ __device__ __forceinline__ void wino8_body(const float *__restrict__ x, const fl
         for (int i = 0; i < 4; ++i) raw[i] = wn_ld2(xoff[i], rs);
     };
     // filter stage: 4 LDS-DMA pieces per wave
-    const uint32_t us_lds = wn_lds_addr(Us) + (uint32_t)__builtin_amdgcn_readfirstlane(w) * 4096u;
+    const uint32_t us_lds = lds_addr(Us) + (uint32_t)__builtin_amdgcn_readfirstlane(w) * 4096u;
     uint32_t uoff[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) uoff[i] = (uint32_t)((w * 256 + i * 64 + lane) * 16);
@@ -712,7 +680,7 @@ __device__ __forceinline__ void wino8_body(const float *__restrict__ x, const fl
         const float4 *sb = ubase(cc);
         const uint32_t dst = us_lds + (uint32_t)(cc & 1) * (WN_STAGE * 4);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) wn_glds16(uoff[i], sb, dst + i * 1024);
+        for (int i = 0; i < 4; ++i) glds16(uoff[i], sb, dst + i * 1024);
     };
     // V of this wave's channel: float index ((p h t) c4) with h = w >> 2, c4 = w & 3
     auto store_vrow = [&](float *Vf, int i, const float (&v)[4]) {
@@ -751,7 +719,7 @@ __device__ __forceinline__ void wino8_body(const float *__restrict__ x, const fl
         }
     }
     if (tid < WN_KB) Bs[tid] = bias_k;
-    wn_wait_vm0();
+    dma_wait_all();
     __syncthreads();
 #ifdef WN_CLOCK
     ck[1] = __builtin_amdgcn_s_memtime();
@@ -827,7 +795,7 @@ __device__ __forceinline__ void wino8_body(const float *__restrict__ x, const fl
             }
         }
         if (!more) break;
-        wn_wait_vm0();
+        dma_wait_all();
         __syncthreads();
     }
 #ifdef WN_CLOCK

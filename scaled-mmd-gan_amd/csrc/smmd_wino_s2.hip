@@ -19,6 +19,7 @@
 // channels (2 input channels x 4 phases) through a double-buffered 36 KB LDS
 // stage, so two workgroups fit a CU.
 #include "smmd_common.hpp"
+#include "smmd_ldsdma.hpp"
 
 namespace smmd {
 
@@ -145,6 +146,43 @@ struct S2Geom {
     const float *x2, *u2;
 };
 
+// The MFMA stream of one chunk, shared by the forward and the transposed
+// kernel: 9 points x 4 MFMAs on the wave's 32 x 32 quadrant, point p's
+// accumulator chained in c4 order (the accumulation order of every point is
+// that of the unsliced loop, so the results are bit-identical to it).  Point
+// p + 1's fragments are read right after point p's first MFMA, so three
+// MFMAs (192 cycles) cover the LDS latency instead of none.  After every
+// MFMA `slice(K)` (K = 4 p + m) issues that slot's piece of the next chunk's
+// work (the transform and the V stores: the f32 MFMA holds the SIMD's VALU,
+// so the pieces cost their issue time wherever they go, but inside the
+// stream their load and store latencies are covered); sched_barrier pins
+// the order.  The first fragments are read by the caller before it issues
+// the next chunk's loads.
+template <typename Slice>
+__device__ __forceinline__ void s2_mfma_chunk(f32x16 (&acc)[9], const float4 *U, const float4 *V,
+                                              int ua, int vb, float4 a, float4 b, Slice &&slice) {
+#pragma unroll
+    for (int p = 0; p < 9; ++p) {
+        const float4 ca = a, cb = b;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca[m], cb[m], acc[p], 0, 0, 0);
+            if (m == 0 && p < 8) {
+                a = U[((p + 1) * 2) * 64 + ua];
+                b = V[((p + 1) * 2) * 64 + vb];
+            }
+            slice(p * 4 + m);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+}
+
+// first MFMA slot of the transform slices: the rows were issued at the top
+// of the chunk, 20 MFMAs (~1300 cycles) earlier
+#ifndef S2_SLOT
+#define S2_SLOT 20
+#endif
+
 template <bool EDGE>
 __global__ __launch_bounds__(S2_T, 2) void s2_conv_kernel(
     const float *__restrict__ x, const float *__restrict__ u, const float *__restrict__ bias,
@@ -205,94 +243,90 @@ __global__ __launch_bounds__(S2_T, 2) void s2_conv_kernel(
     };
 
     f4v raw[3];
-    f4v ur[5];
-    auto load = [&](int cc) {
+    auto load_rows = [&](int cc) {
         const __amdgpu_buffer_rsrc_t rs =
             s2_rsrc(reinterpret_cast<const char *>(x) + xshift(cc));
-#ifndef S2_NO_ROWS      // (S2_NO_*: timing-only diagnostic builds, wrong results)
 #pragma unroll
         for (int a = 0; a < 3; ++a)
             raw[a] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, xo[a], 0, 0));
-#else
-        (void)rs;
-#endif
-        const __amdgpu_buffer_rsrc_t us = s2_rsrc(uchunk(cc));
-#pragma unroll
-        for (int i = 0; i < 5; ++i)
-            if (i * S2_T + tid < S2_STAGE / 4)
-                ur[i] = __builtin_bit_cast(
-                    f4v, __builtin_amdgcn_raw_buffer_load_b128(us, (uint32_t)(i * S2_T + tid) * 16, 0, 0));
     };
-    auto store = [&](int cc, int buf) {
-        f4v *U = reinterpret_cast<f4v *>(Us + buf * (S2_STAGE / 4)) + tid;
+    // the filter stage (18 KiB, contiguous in u) by LDS-DMA: wave w moves
+    // pieces w, w + 4, ... of 1 KiB (waves 0 and 1 five, 2 and 3 four)
+    const int wu = __builtin_amdgcn_readfirstlane(w);
+    const uint32_t us_lds = lds_addr(Us);
+    auto load_u = [&](int cc) {
+        const float4 *sb = uchunk(cc);
+        const uint32_t dst = us_lds + (uint32_t)(cc & 1) * (S2_STAGE * 4);
 #pragma unroll
-        for (int i = 0; i < 5; ++i)
-            if (i * S2_T + tid < S2_STAGE / 4) U[i * S2_T] = ur[i];
-#ifdef S2_NO_XFORM
-        return;
-#endif
-        float v0[9], v1[9];
+        for (int i = 0; i < 5; ++i) {
+            const int piece = wu + 4 * i;
+            if (piece < S2_STAGE / 256)
+                glds16((uint32_t)(piece * 64 + lane) * 16, sb, dst + (uint32_t)piece * 1024);
+        }
+    };
+    // the transform: V = B^T d B of the lane's tile for its (channel, row
+    // phase) and both column phases, as row i's three points (v0: column
+    // phase 0, v1: phase 1); t = B^T over the rows (the column-factored form:
+    // the own columns packed, the outer columns from the neighbour lanes by
+    // DPP with the image-edge zero applied at the source lane)
+    f4v t[3];
+    float d0[3][3], d1[3][3];        // EDGE: the whole tile's d, B^T applied
+    auto xf_cols = [&](int cc) {
         if constexpr (!EDGE) {
-            // column-factored: Bᵀ over the rows on the lane's own four columns
-            // (packed), the outer columns' from the neighbour lanes by DPP
-            // folded into the subtraction, the image-edge zero applied at the
-            // source lane; term for term the form below
-            const bool eL = ttx == 0, eR = ttx == g.TW - 1;
-            f4v t[3];
+            (void)cc;
             t[0] = raw[0] - raw[1];
             t[1] = raw[1];
             t[2] = raw[2] - raw[1];
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                const float ws = eR ? 0.f : t[i].w, xs = eL ? 0.f : t[i].x;
-                v0[i * 3 + 0] = s2_from_left(ws) - t[i].y;      // columns (L, 1, 3)
-                v0[i * 3 + 1] = t[i].y;
-                v0[i * 3 + 2] = t[i].w - t[i].y;
-                v1[i * 3 + 0] = t[i].x - t[i].z;                // columns (0, 2, R)
-                v1[i * 3 + 1] = t[i].z;
-                v1[i * 3 + 2] = s2_from_right(xs) - t[i].z;
-            }
         } else {
-        const float *xc = xchunk(cc);
-        // rows: columns 4tx-1 .. 4tx+4; pj = 0 takes (-1, 1, 3), pj = 1 (0, 2, 4)
-        float d0[3][3], d1[3][3];
+            const float *xc = xchunk(cc);
+            // rows: columns 4tx-1 .. 4tx+4; pj = 0 takes (-1, 1, 3), pj = 1 (0, 2, 4)
 #pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            const int yy = 4 * tty - 1 + pi + 2 * a;
-            const bool row = yy >= 0 && yy < g.H;     // (outside: loaded as zeros)
-            const float c0v = raw[a].x, c1v = raw[a].y, c2v = raw[a].z, c3v = raw[a].w;
-            float L = s2_from_left(c3v), R = s2_from_right(c0v);
-            if (EDGE) {
+            for (int a = 0; a < 3; ++a) {
+                const int yy = 4 * tty - 1 + pi + 2 * a;
+                const bool row = yy >= 0 && yy < g.H;     // (outside: loaded as zeros)
+                const float c0v = raw[a].x, c1v = raw[a].y, c2v = raw[a].z, c3v = raw[a].w;
+                float L = s2_from_left(c3v), R = s2_from_right(c0v);
                 if (ttx > 0 && lane == 0) L = row ? xc[(int64_t)yy * g.W + 4 * ttx - 1] : 0.f;
                 if (ttx < g.TW - 1 && lane == 63) R = row ? xc[(int64_t)yy * g.W + 4 * ttx + 4] : 0.f;
+                L = ttx == 0 ? 0.f : L;
+                R = ttx == g.TW - 1 ? 0.f : R;
+                d0[a][0] = L;   d0[a][1] = c1v; d0[a][2] = c3v;
+                d1[a][0] = c0v; d1[a][1] = c2v; d1[a][2] = R;
             }
-            L = ttx == 0 ? 0.f : L;
-            R = ttx == g.TW - 1 ? 0.f : R;
-            d0[a][0] = L;   d0[a][1] = c1v; d0[a][2] = c3v;
-            d1[a][0] = c0v; d1[a][1] = c2v; d1[a][2] = R;
-        }
 #pragma unroll
-        for (int b = 0; b < 3; ++b) {      // B^T d per column
-            const float t00 = d0[0][b] - d0[1][b], t01 = d0[1][b], t02 = d0[2][b] - d0[1][b];
-            const float t10 = d1[0][b] - d1[1][b], t11 = d1[1][b], t12 = d1[2][b] - d1[1][b];
-            d0[0][b] = t00; d0[1][b] = t01; d0[2][b] = t02;
-            d1[0][b] = t10; d1[1][b] = t11; d1[2][b] = t12;
+            for (int b = 0; b < 3; ++b) {      // B^T d per column
+                const float t00 = d0[0][b] - d0[1][b], t01 = d0[1][b], t02 = d0[2][b] - d0[1][b];
+                const float t10 = d1[0][b] - d1[1][b], t11 = d1[1][b], t12 = d1[2][b] - d1[1][b];
+                d0[0][b] = t00; d0[1][b] = t01; d0[2][b] = t02;
+                d1[0][b] = t10; d1[1][b] = t11; d1[2][b] = t12;
+            }
         }
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {      // (B^T d) B per row
-            v0[i * 3 + 0] = d0[i][0] - d0[i][1];
-            v0[i * 3 + 1] = d0[i][1];
-            v0[i * 3 + 2] = d0[i][2] - d0[i][1];
-            v1[i * 3 + 0] = d1[i][0] - d1[i][1];
-            v1[i * 3 + 1] = d1[i][1];
-            v1[i * 3 + 2] = d1[i][2] - d1[i][1];
-        }
+    };
+    const bool eL = ttx == 0, eR = ttx == g.TW - 1;
+    // row i of V (points 3i .. 3i + 2) into stage buffer buf
+    auto xf_row = [&](int i, int buf) {
+        float v0[3], v1[3];
+        if constexpr (!EDGE) {
+            const float ws = eR ? 0.f : t[i].w, xs = eL ? 0.f : t[i].x;
+            v0[0] = s2_from_left(ws) - t[i].y;      // columns (L, 1, 3)
+            v0[1] = t[i].y;
+            v0[2] = t[i].w - t[i].y;
+            v1[0] = t[i].x - t[i].z;                // columns (0, 2, R)
+            v1[1] = t[i].z;
+            v1[2] = s2_from_right(xs) - t[i].z;
+        } else {
+            v0[0] = d0[i][0] - d0[i][1];
+            v0[1] = d0[i][1];
+            v0[2] = d0[i][2] - d0[i][1];
+            v1[0] = d1[i][0] - d1[i][1];
+            v1[1] = d1[i][1];
+            v1[2] = d1[i][2] - d1[i][1];
         }
         float2 *const Vl = reinterpret_cast<float2 *>(Vs + buf * (S2_STAGE / 4)) +
                            (e * 64 + lane) * 2 + pi;
 #pragma unroll
-        for (int p = 0; p < 9; ++p)
-            Vl[p * 256] = make_float2(v0[p], v1[p]);      // point p: + p * 2 KB
+        for (int j = 0; j < 3; ++j)
+            Vl[(3 * i + j) * 256] = make_float2(v0[j], v1[j]);      // point p: + p * 2 KB
     };
 
     f32x16 acc[9];
@@ -300,34 +334,54 @@ __global__ __launch_bounds__(S2_T, 2) void s2_conv_kernel(
     for (int p = 0; p < 9; ++p) acc[p] = f32x16{};
 
     const int th = w & 1, kh = w >> 1, hl = lane >> 5, l32 = lane & 31;
-    auto mfma_chunk = [&](int buf) {
-        const float4 *V = Vs + buf * (S2_STAGE / 4);
-        const float4 *U = Us + buf * (S2_STAGE / 4);
-#pragma unroll
-        for (int p = 0; p < 9; ++p) {
-            const float4 a = U[(p * 2 + hl) * 64 + kh * 32 + l32];
-            const float4 b = V[(p * 2 + hl) * 64 + th * 32 + l32];
-            acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, acc[p], 0, 0, 0);
-            acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, acc[p], 0, 0, 0);
-            acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, acc[p], 0, 0, 0);
-            acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, acc[p], 0, 0, 0);
-        }
-    };
+    const int ua = hl * 64 + kh * 32 + l32, vb = hl * 64 + th * 32 + l32;
 
-    load(0);
+    // chunk 0 staged before the loop
     const float bias_k = (bias && tid < S2_KB) ? bias[kb * S2_KB + tid] : 0.f;
-    store(0, 0);
+    load_u(0);
+    load_rows(0);
+    xf_cols(0);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) xf_row(i, 0);
     if (tid < S2_KB) Bs[tid] = bias_k;
+    dma_wait_all();
     __syncthreads();
-    for (int cc = 0; cc + 1 < nchunk; ++cc) {
-        load(cc + 1);
+    for (int cc = 0;; ++cc) {
+        const bool more = cc + 1 < nchunk;
+        const int buf = cc & 1, nbuf = buf ^ 1;
+        const float4 *U = Us + buf * (S2_STAGE / 4);
+        const float4 *V = Vs + buf * (S2_STAGE / 4);
+        // the first fragments' reads go out before the next chunk's loads
+        const float4 a0 = U[ua], b0 = V[vb];
         __builtin_amdgcn_sched_barrier(0);
-        mfma_chunk(cc & 1);
-        __builtin_amdgcn_sched_barrier(0);
-        store(cc + 1, (cc + 1) & 1);
+        if (more) {
+#ifndef S2_NO_DMA        // (S2_NO_*: timing-only diagnostic builds, wrong results)
+            load_u(cc + 1);
+#endif
+            __builtin_amdgcn_sched_barrier(0);
+#ifndef S2_NO_ROWS
+            load_rows(cc + 1);
+#endif
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        s2_mfma_chunk(acc, U, V, ua, vb, a0, b0, [&](int K) {
+#ifdef S2_NO_XFORM
+            return;
+#endif
+            if (!more) return;
+            if (K == S2_SLOT) {
+                // (an empty asm on the rows: their arithmetic cannot be
+                // hoisted above this slot, so their wait lands here)
+                asm volatile("" : "+v"(raw[0]), "+v"(raw[1]), "+v"(raw[2]));
+                xf_cols(cc + 1);
+            } else if (K == S2_SLOT + 2 || K == S2_SLOT + 4 || K == S2_SLOT + 6) {
+                xf_row((K - S2_SLOT - 2) >> 1, nbuf);
+            }
+        });
+        if (!more) break;
+        dma_wait_all();                     // chunk cc + 1's filter stage landed
         __syncthreads();
     }
-    mfma_chunk((nchunk - 1) & 1);
 
     // epilogue: C_p[k][tile]; output tile (2ty, 2tx) of y [N, K, H/2, W/2];
     // rows in pairs (r, r + 1: channels k, k + 1, adjacent registers) for
@@ -490,7 +544,6 @@ __device__ __forceinline__ void s2t_body(const float *__restrict__ gy, const flo
     // lane's offsets fixed; a row outside the image reads zeros
     typedef float f2v __attribute__((ext_vector_type(2)));
     f2v raw[2][3];
-    f4v ur[5];
     uint32_t roff[2][3];
 #pragma unroll
     for (int e = 0; e < 2; ++e)
@@ -502,107 +555,107 @@ __device__ __forceinline__ void s2t_body(const float *__restrict__ gy, const flo
                              : (uint32_t)((((int64_t)tn * g.K + 2 * w + e) * HW +
                                            (int64_t)yy * g.Wg + 2 * ttx) * 4);
         }
-    auto load = [&](int cc) {
+    auto load_rows = [&](int cc) {
         const __amdgpu_buffer_rsrc_t rs = s2_rsrc(gy + ((int64_t)c0 + cc) * 8 * HW);
 #pragma unroll
         for (int e = 0; e < 2; ++e)
 #pragma unroll
-            for (int a = 0; a < 3; ++a) {
-#ifndef S2_NO_ROWS
+            for (int a = 0; a < 3; ++a)
                 raw[e][a] = __builtin_bit_cast(
                     f2v, __builtin_amdgcn_raw_buffer_load_b64(rs, roff[e][a], 0, 0));
-#endif
-            }
-        const __amdgpu_buffer_rsrc_t us = s2_rsrc(ub + (int64_t)cc * (S2_STAGE / 4));
-#pragma unroll
-        for (int i = 0; i < 5; ++i)
-            if (i * S2_T + tid < S2_STAGE / 4)
-                ur[i] = __builtin_bit_cast(
-                    f4v, __builtin_amdgcn_raw_buffer_load_b128(us, (uint32_t)(i * S2_T + tid) * 16, 0, 0));
     };
-    auto store = [&](int cc, int buf) {
-        f4v *U = reinterpret_cast<f4v *>(Us + buf * (S2_STAGE / 4)) + tid;
+    // the filter stage (18 KiB, contiguous in u) by LDS-DMA, as the forward's
+    const int wu = __builtin_amdgcn_readfirstlane(w);
+    const uint32_t us_lds = lds_addr(Us);
+    auto load_u = [&](int cc) {
+        const float4 *sb = ub + (int64_t)cc * (S2_STAGE / 4);
+        const uint32_t dst = us_lds + (uint32_t)(cc & 1) * (S2_STAGE * 4);
 #pragma unroll
-        for (int i = 0; i < 5; ++i)
-            if (i * S2_T + tid < S2_STAGE / 4) U[i * S2_T] = ur[i];
-#ifdef S2_NO_XFORM
-        return;
-#endif
-        float v[2][9];
+        for (int i = 0; i < 5; ++i) {
+            const int piece = wu + 4 * i;
+            if (piece < S2_STAGE / 256)
+                glds16((uint32_t)(piece * 64 + lane) * 16, sb, dst + (uint32_t)piece * 1024);
+        }
+    };
+    // the transform of the lane's phase tile for both k channels: t = B^T
+    // over the rows (column-factored: the own two columns packed, the outer
+    // column from the neighbour lane by DPP, its image-edge zero applied at
+    // the source lane: a lane at its row's right edge passes 0 to the right,
+    // one at the left edge 0 to the left); EDGE: d with B^T applied
+    f2v t[2][3];
+    float dd[2][3][3];
+    const bool eL = ttx == 0, eR = ttx == g.TW - 1;
+    auto xf_cols = [&](int cc) {
         if constexpr (!EDGE) {
-            // column-factored: Bᵀ over the rows on the lane's own two columns
-            // (packed), the outer column's from the neighbour lane by DPP
-            // folded into the subtraction, its image-edge zero applied at the
-            // source lane (a lane at its row's right edge passes 0 to the
-            // right, one at the left edge 0 to the left); term for term the
-            // form below
-            const bool eL = ttx == 0, eR = ttx == g.TW - 1;
+            (void)cc;
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
-                f2v t[3];
-                t[0] = raw[e][0] - raw[e][1];
-                t[1] = raw[e][1];
-                t[2] = raw[e][2] - raw[e][1];
-#pragma unroll
-                for (int i = 0; i < 3; ++i) {
-                    if (qj == 0) {          // columns (L, x, y)
-                        const float ys = eR ? 0.f : t[i].y;
-                        v[e][i * 3 + 0] = s2_from_left(ys) - t[i].x;
-                        v[e][i * 3 + 1] = t[i].x;
-                        v[e][i * 3 + 2] = t[i].y - t[i].x;
-                    } else {                // columns (x, y, R)
-                        const float xs = eL ? 0.f : t[i].x;
-                        v[e][i * 3 + 0] = t[i].x - t[i].y;
-                        v[e][i * 3 + 1] = t[i].y;
-                        v[e][i * 3 + 2] = s2_from_right(xs) - t[i].y;
-                    }
-                }
+                t[e][0] = raw[e][0] - raw[e][1];
+                t[e][1] = raw[e][1];
+                t[e][2] = raw[e][2] - raw[e][1];
             }
-        } else
+        } else {
 #pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            const float *gc = gn + ((int64_t)cc * 8 + e) * HW;
-            float d[3][3];
+            for (int e = 0; e < 2; ++e) {
+                const float *gc = gn + ((int64_t)cc * 8 + e) * HW;
+                float (&d)[3][3] = dd[e];
 #pragma unroll
-            for (int a = 0; a < 3; ++a) {
-                const int yy = 2 * tty - 1 + qi + a;
-                // rows 2ty - 1 (phase row 0) and 2ty + 2 (phase row 1) can be
-                // outside the image (loaded as zeros); a tile past the end is
-                // never stored
-                const bool row = (a == 0 && qi == 0) ? tty > 0
-                                 : (a == 2 && qi == 1) ? tty < THg - 1 : true;
-                const float cx = raw[e][a].x, cy = raw[e][a].y;
-                float L = s2_from_left(cy), R = s2_from_right(cx);
-                if (EDGE) {
+                for (int a = 0; a < 3; ++a) {
+                    const int yy = 2 * tty - 1 + qi + a;
+                    // rows 2ty - 1 (phase row 0) and 2ty + 2 (phase row 1) can be
+                    // outside the image (loaded as zeros); a tile past the end is
+                    // never stored
+                    const bool row = (a == 0 && qi == 0) ? tty > 0
+                                     : (a == 2 && qi == 1) ? tty < THg - 1 : true;
+                    const float cx = raw[e][a].x, cy = raw[e][a].y;
+                    float L = s2_from_left(cy), R = s2_from_right(cx);
                     if (ttx > 0 && lane == 0) L = row ? gc[(int64_t)yy * g.Wg + 2 * ttx - 1] : 0.f;
                     if (ttx < g.TW - 1 && lane == 63)
                         R = row ? gc[(int64_t)yy * g.Wg + 2 * ttx + 2] : 0.f;
+                    L = ttx == 0 ? 0.f : L;
+                    R = ttx == g.TW - 1 ? 0.f : R;
+                    // columns 2tx - 1 + qj + b
+                    d[a][0] = qj ? cx : L;
+                    d[a][1] = qj ? cy : cx;
+                    d[a][2] = qj ? R : cy;
                 }
-                L = ttx == 0 ? 0.f : L;
-                R = ttx == g.TW - 1 ? 0.f : R;
-                // columns 2tx - 1 + qj + b
-                d[a][0] = qj ? cx : L;
-                d[a][1] = qj ? cy : cx;
-                d[a][2] = qj ? R : cy;
-            }
 #pragma unroll
-            for (int b = 0; b < 3; ++b) {
-                const float t0 = d[0][b] - d[1][b], t2 = d[2][b] - d[1][b];
-                d[0][b] = t0;
-                d[2][b] = t2;
+                for (int b = 0; b < 3; ++b) {
+                    const float t0 = d[0][b] - d[1][b], t2 = d[2][b] - d[1][b];
+                    d[0][b] = t0;
+                    d[2][b] = t2;
+                }
             }
+        }
+    };
+    // row i of V (points 3i .. 3i + 2), both k channels, into stage buffer buf
+    auto xf_row = [&](int i, int buf) {
+        float v[2][3];
 #pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                v[e][i * 3 + 0] = d[i][0] - d[i][1];
-                v[e][i * 3 + 1] = d[i][1];
-                v[e][i * 3 + 2] = d[i][2] - d[i][1];
+        for (int e = 0; e < 2; ++e) {
+            if constexpr (!EDGE) {
+                if (qj == 0) {          // columns (L, x, y)
+                    const float ys = eR ? 0.f : t[e][i].y;
+                    v[e][0] = s2_from_left(ys) - t[e][i].x;
+                    v[e][1] = t[e][i].x;
+                    v[e][2] = t[e][i].y - t[e][i].x;
+                } else {                // columns (x, y, R)
+                    const float xs = eL ? 0.f : t[e][i].x;
+                    v[e][0] = t[e][i].x - t[e][i].y;
+                    v[e][1] = t[e][i].y;
+                    v[e][2] = s2_from_right(xs) - t[e][i].y;
+                }
+            } else {
+                v[e][0] = dd[e][i][0] - dd[e][i][1];
+                v[e][1] = dd[e][i][1];
+                v[e][2] = dd[e][i][2] - dd[e][i][1];
             }
         }
         float2 *const Vl = reinterpret_cast<float2 *>(Vs + buf * (S2_STAGE / 4)) +
                            ((w >> 1) * 64 + lane) * 2 + (w & 1);
 #pragma unroll
-        for (int p = 0; p < 9; ++p)
-            Vl[p * 256] = make_float2(v[0][p], v[1][p]);  // point p: + p * 2 KB
+        for (int j = 0; j < 3; ++j)
+            Vl[(3 * i + j) * 256] = make_float2(v[0][j], v[1][j]);  // point p: + p * 2 KB
     };
 
     f32x16 acc[9];
@@ -610,34 +663,51 @@ __device__ __forceinline__ void s2t_body(const float *__restrict__ gy, const flo
     for (int p = 0; p < 9; ++p) acc[p] = f32x16{};
 
     const int th = w & 1, kh = w >> 1, hl = lane >> 5, l32 = lane & 31;
-    auto mfma_chunk = [&](int buf) {
-        const float4 *V = Vs + buf * (S2_STAGE / 4);
-        const float4 *U = Us + buf * (S2_STAGE / 4);
-#pragma unroll
-        for (int p = 0; p < 9; ++p) {
-            const float4 a = U[(p * 2 + hl) * 64 + kh * 32 + l32];
-            const float4 b = V[(p * 2 + hl) * 64 + th * 32 + l32];
-            acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, acc[p], 0, 0, 0);
-            acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, acc[p], 0, 0, 0);
-            acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, acc[p], 0, 0, 0);
-            acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, acc[p], 0, 0, 0);
-        }
-    };
+    const int ua = hl * 64 + kh * 32 + l32, vb = hl * 64 + th * 32 + l32;
 
-    load(0);
     const float bias_c = (bias && tid < 64) ? bias[cb * 64 + tid] : 0.f;
-    store(0, 0);
+    load_u(0);
+    load_rows(0);
+    xf_cols(0);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) xf_row(i, 0);
     if (tid < 64) Bs[tid] = bias_c;
+    dma_wait_all();
     __syncthreads();
-    for (int cc = 0; cc + 1 < nchunk; ++cc) {
-        load(cc + 1);
+    for (int cc = 0;; ++cc) {
+        const bool more = cc + 1 < nchunk;
+        const int buf = cc & 1, nbuf = buf ^ 1;
+        const float4 *U = Us + buf * (S2_STAGE / 4);
+        const float4 *V = Vs + buf * (S2_STAGE / 4);
+        const float4 a0 = U[ua], b0 = V[vb];
         __builtin_amdgcn_sched_barrier(0);
-        mfma_chunk(cc & 1);
-        __builtin_amdgcn_sched_barrier(0);
-        store(cc + 1, (cc + 1) & 1);
+        if (more) {
+#ifndef S2_NO_DMA
+            load_u(cc + 1);
+#endif
+            __builtin_amdgcn_sched_barrier(0);
+#ifndef S2_NO_ROWS
+            load_rows(cc + 1);
+#endif
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        s2_mfma_chunk(acc, U, V, ua, vb, a0, b0, [&](int K) {
+#ifdef S2_NO_XFORM
+            return;
+#endif
+            if (!more) return;
+            if (K == S2_SLOT) {
+                asm volatile("" : "+v"(raw[0][0]), "+v"(raw[0][1]), "+v"(raw[0][2]),
+                             "+v"(raw[1][0]), "+v"(raw[1][1]), "+v"(raw[1][2]));
+                xf_cols(cc + 1);
+            } else if (K == S2_SLOT + 2 || K == S2_SLOT + 4 || K == S2_SLOT + 6) {
+                xf_row((K - S2_SLOT - 2) >> 1, nbuf);
+            }
+        });
+        if (!more) break;
+        dma_wait_all();
         __syncthreads();
     }
-    mfma_chunk((nchunk - 1) & 1);
 
     // epilogue: phase tile (ty, tx) -> dx rows 2 (2ty + a) + qi, cols 2 (2tx + b) + qj;
     // buffer stores at the lane's fixed offsets plus a uniform per-channel

@@ -230,8 +230,10 @@ def test_rccl_world1_critic_update_equals_groupless(dev, mode):
         assert seen['all_gather_into_tensor'] == 1  # the step's one packed all-gather
     else:
         assert seen['all_gather_into_tensor'] == 0
-    np.testing.assert_allclose(d_loss, ref[0], rtol=1e-5)
-    np.testing.assert_allclose(aux[3], ref[1][3], rtol=1e-5)
+    # the global mode takes the unfused loss launches (the Jacobian's
+    # partials ride in the all-gather), so d_loss sums in another order
+    np.testing.assert_allclose(d_loss, ref[0], rtol=1e-4)
+    np.testing.assert_allclose(aux[3], ref[1][3], rtol=1e-4)
     scale = np.abs(ref[2]).max()
     np.testing.assert_allclose(grad, ref[2], rtol=1e-3, atol=2e-3 * scale)
     assert np.abs(params - ref[3]).max() <= 2.0001 * _cfg().learning_rate
