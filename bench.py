@@ -50,6 +50,7 @@ MFMA_F32_PEAK_TFS = 157.3      # v_mfma_f32_32x32x2_f32 dense
 VALU_LANE_OPS = FP32_PEAK_TFS / 2 * 1e12
 TRANS_SLOTS = 4                # v_exp_f32 / v_log_f32: quarter rate (MI355X_MICROARCH.md)
 BATCH = 64
+_JSON_OUT = sys.stdout           # the result line's stream (main: the real fd 1)
 
 # committed counter evidence of this workload, each file stamped with the
 # smmd_source_hash of the library build it was measured on (tools/stamp.py);
@@ -645,6 +646,12 @@ def main():
                           'rank': int(os.environ.get('RANK', '0')), 'gpus': args.gpus}),
               flush=True)
         return
+    # ONE JSON line on stdout: whatever native code prints there (RCCL's init
+    # banner goes to fd 1) is sent to stderr, and the line goes to the saved fd
+    sys.stdout.flush()
+    global _JSON_OUT
+    _JSON_OUT = os.fdopen(os.dup(1), 'w')
+    os.dup2(2, 1)
 
     if not args.miopen_winograd:      # read by MIOpen at its first solver query
         for k in ('MIOPEN_DEBUG_AMD_WINOGRAD_RXS_F2X3', 'MIOPEN_DEBUG_AMD_WINOGRAD_RXS_F3X2',
@@ -979,7 +986,7 @@ def main():
         except Exception as e:   # report, never hide the GPU number
             result['cpu_baseline'] = {'error': repr(e)}
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        print(json.dumps(result), file=_JSON_OUT, flush=True)
     if world > 1 or dp_forced:
         dist.barrier()
         dist.destroy_process_group()

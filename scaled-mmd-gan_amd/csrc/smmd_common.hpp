@@ -151,6 +151,15 @@ __device__ __forceinline__ float clip_factor_slab(const double *part, int b0, in
     return sh[0];
 }
 
+// Work item of block b in a 1-D grid of n blocks, XCD-aware: the dispatcher
+// deals blocks round-robin to the 8 XCDs (b and b + 8 share one and its L2;
+// MI355X_MICROARCH.md, dispatch), so XCD x takes the x-th contiguous range of
+// the work order.  A bijection on [0, n) for any n; placement is only speed.
+__device__ __forceinline__ int xcd_order(int b, int n) {
+    const int q = n >> 3, r = n & 7, x = b & 7, i = b >> 3;
+    return x * q + (x < r ? x : r) + i;
+}
+
 inline smmd_status hip_status(hipError_t e) {
     return e == hipSuccess ? SMMD_OK : SMMD_EHIP;
 }

@@ -62,12 +62,16 @@ struct SnLayerDev {
     int fold;        // W_eff / G are the pool-folded 4 x 4 filters (K = 9 nfc)
     int nfc;         // filters per row (fold)
     int unit_begin;  // first P3 / backward work unit: tiles, or fold blocks
+    int p3_begin;    // first unit in the P3 launch (layers it writes; others own 0 units)
+    int m3_begin;    // first tile in R2's launch (small plain layers whose W_eff R2 writes)
 };
 
 struct SnTable {
     int n_layers;
     int total_tiles;
     int total_units;
+    int total_p3;    // units of the P3 launch
+    int total_m3;    // W_eff tiles of the R2 launch
     int iter;        // current power iteration (0 -> read layer.u)
     int last_iter;
     int update_u;
@@ -92,6 +96,25 @@ __device__ __forceinline__ int find_unit_layer(const SnTable &t, int unit) {
 #pragma unroll
     for (int i = 1; i < SN_CHUNK; ++i)
         l += (i < t.n_layers && unit >= t.L[i].unit_begin) ? 1 : 0;
+    return __builtin_amdgcn_readfirstlane(l);
+}
+
+// layer of a unit of the P3 launch / of a W_eff tile of the R2 launch.  The
+// begins are monotone and a layer with no units shares its begin with the
+// next layer, so the scan (the largest i with begin <= unit) never stops at it
+__device__ __forceinline__ int find_p3_layer(const SnTable &t, int unit) {
+    int l = 0;
+#pragma unroll
+    for (int i = 1; i < SN_CHUNK; ++i)
+        l += (i < t.n_layers && unit >= t.L[i].p3_begin) ? 1 : 0;
+    return __builtin_amdgcn_readfirstlane(l);
+}
+
+__device__ __forceinline__ int find_m3_layer(const SnTable &t, int unit) {
+    int l = 0;
+#pragma unroll
+    for (int i = 1; i < SN_CHUNK; ++i)
+        l += (i < t.n_layers && unit >= t.L[i].m3_begin) ? 1 : 0;
     return __builtin_amdgcn_readfirstlane(l);
 }
 
@@ -280,11 +303,16 @@ __global__ __launch_bounds__(256) void sn_p1_kernel(SnTable t) {
     p1_tile(uin, L.p1, L.N, L.K, rt, r0, c0, wt);
 }
 
+// P2 walks each layer's tiles column-major and XCD-aware: the nrt row tiles of
+// a column tile run on one XCD, so the P1 slab column they all sum is fetched
+// into that L2 once instead of once per row tile on whichever XCD it landed
+// (the slab re-read was ~28 MB per refresh on the SNResNet-64 critic, 0.7x
+// its 40 MB of W).
 __global__ __launch_bounds__(256) void sn_p2_kernel(SnTable t) {
-    const int tile = blockIdx.x;
+    const int tile = xcd_order(blockIdx.x, t.total_tiles);
     const SnLayerDev L = t.L[find_layer(t, tile)];
     const int lt = tile - L.tile_begin;
-    const int rt = lt / L.nct, ct = lt % L.nct;
+    const int ct = lt / L.nrt, rt = lt - ct * L.nrt;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int r0 = rt * SN_TR + w * SN_RPW;
     const int c0 = ct * SN_TC + lane * 4;
@@ -321,13 +349,30 @@ __global__ __launch_bounds__(256) void sn_p2_kernel(SnTable t) {
 #pragma unroll
     for (int i = 0; i < SN_RPW; ++i)
         part[i] = fmaf(v3, wt[i].w, fmaf(v2, wt[i].z, fmaf(v1, wt[i].y, v0 * wt[i].x)));
+    // the wave's 8 row sums by a transposed butterfly: each exchange halves
+    // the values a lane carries (10 cross-lane moves instead of 8 x 6); lane
+    // 8 i ends with row i's sum
+    static_assert(SN_RPW == 8, "P2's row-sum butterfly is written for 8 rows per wave");
+    float a4[4], b2[2];
+    {
+        const bool h = lane & 32;
 #pragma unroll
-    for (int i = 0; i < SN_RPW; ++i) part[i] = wave_sum(part[i]);
-    if (lane == 0) {
-#pragma unroll
-        for (int i = 0; i < SN_RPW; ++i)
-            if (r0 + i < L.N) L.q2[(size_t)(r0 + i) * L.nctp + ct] = part[i];
+        for (int j = 0; j < 4; ++j)
+            a4[j] = (h ? part[4 + j] : part[j]) + __shfl_xor(h ? part[j] : part[4 + j], 32);
     }
+    {
+        const bool h = lane & 16;
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            b2[j] = (h ? a4[2 + j] : a4[j]) + __shfl_xor(h ? a4[j] : a4[2 + j], 16);
+    }
+    const bool h3 = lane & 8;
+    float rsum = (h3 ? b2[1] : b2[0]) + __shfl_xor(h3 ? b2[0] : b2[1], 8);
+    rsum += __shfl_xor(rsum, 4);
+    rsum += __shfl_xor(rsum, 2);
+    rsum += __shfl_xor(rsum, 1);
+    const int row = r0 + (lane >> 3);
+    if ((lane & 7) == 0 && row < L.N) L.q2[(size_t)row * L.nctp + ct] = rsum;
 }
 
 // u_raw[n] * ||v_raw|| = sum over column tiles c < nct of q2[n][c], in order.
@@ -364,10 +409,20 @@ __device__ __forceinline__ float q2_row_sum(const SnLayerDev &L, int n) {
 constexpr int EP_KREG = 8;    // v_raw values per thread kept in registers (K <= 8192)
 constexpr int EP_NREG = 2;    // rows per thread kept in registers (N <= 2048)
 
-__device__ void sn_layer_epilogue(const SnTable &t, const SnLayerDev &L, int last_iter,
-                                  double *red) {
+struct SnNorms {
+    double sa, uu;   // ||v_raw||^2, ||u_raw||^2
+    float nv, nu;
+};
+
+// The norms of one layer by a 1024-thread block (every thread gets them); vr
+// and rs keep this thread's v_raw values and row sums.  The same code, so the
+// same bits, in R2's layer block and in R2's W_eff tiles (sn_m3_tile).  Only a
+// layer with N > EP_NREG * 1024 writes (raw u into ucur), and such a layer
+// has no W_eff tiles in R2.
+__device__ __forceinline__ SnNorms sn_layer_norms(const SnTable &t, const SnLayerDev &L,
+                                                  float (&vr)[EP_KREG], float (&rs)[EP_NREG],
+                                                  double *red) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    float vr[EP_KREG], rs[EP_NREG];
 #pragma unroll
     for (int j = 0; j < EP_KREG; ++j) {
         const int k = tid + j * 1024;
@@ -406,9 +461,21 @@ __device__ void sn_layer_epilogue(const SnTable &t, const SnLayerDev &L, int las
         sa += red[i];
         sb += red[16 + i];
     }
-    const float nv = (float)sqrt(sa) + t.eps;                   // sn.py:13
-    const double uu = sb / ((double)nv * (double)nv);           // ||u_raw||^2
-    const float nu = (float)sqrt(uu) + t.eps;
+    SnNorms q;
+    q.sa = sa;
+    q.nv = (float)sqrt(sa) + t.eps;                             // sn.py:13
+    q.uu = sb / ((double)q.nv * (double)q.nv);                  // ||u_raw||^2
+    q.nu = (float)sqrt(q.uu) + t.eps;
+    return q;
+}
+
+__device__ void sn_layer_epilogue(const SnTable &t, const SnLayerDev &L, int last_iter,
+                                  double *red) {
+    const int tid = threadIdx.x;
+    float vr[EP_KREG], rs[EP_NREG];
+    const SnNorms q = sn_layer_norms(t, L, vr, rs, red);
+    const double sa = q.sa, uu = q.uu;
+    const float nv = q.nv, nu = q.nu;
 #pragma unroll
     for (int j = 0; j < EP_KREG; ++j) {
         const int k = tid + j * 1024;
@@ -438,17 +505,55 @@ __device__ void sn_layer_epilogue(const SnTable &t, const SnLayerDev &L, int las
     }
 }
 
-// R2: one 1024-thread block per layer runs the epilogue
-__global__ __launch_bounds__(1024) void sn_r2_kernel(SnTable t) {
-    __shared__ double red[32];
-    sn_layer_epilogue(t, t.L[blockIdx.x], t.last_iter, red);
+// W_eff of one 32 x 256 tile of a small plain layer inside R2's launch: the
+// block forms sigma itself from v_raw and the row partials, with the layer
+// block's code (so its bits), instead of a P3 launch waiting for R2.  The
+// redundant reads, (nctp N + K) floats per tile, are bounded by the tile's own
+// 8 K (m3_fits); 16 waves x 2 rows.
+constexpr int M3_RPW = SN_TR / 16;
+static_assert(SN_TR % 16 == 0, "R2's W_eff tiles: 16 waves over the tile rows");
+
+__device__ __forceinline__ void sn_m3_tile(const SnTable &t, const SnLayerDev &L, int lt,
+                                           double *red) {
+    const int rt = lt / L.nct, ct = lt - (lt / L.nct) * L.nct;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int r0 = rt * SN_TR + w * M3_RPW;
+    const int c0 = ct * SN_TC + lane * 4;
+    float4 wt[M3_RPW];
+    load_tile(L.W, L.N, L.K, L.vec, r0, c0, wt);    // in flight with the norms' loads
+    float vr[EP_KREG], rs[EP_NREG];
+    const SnNorms q = sn_layer_norms(t, L, vr, rs, red);
+    const float sigma = (float)(q.uu / (double)q.nu);           // R2's sigma, bit for bit
+    const float s = L.s ? L.s[0] : 1.f;
+#pragma unroll
+    for (int i = 0; i < M3_RPW; ++i) {
+        // W_bar = W / sigma (sn.py:43), then s * W_bar (snops.py:84)
+        wt[i].x = (wt[i].x / sigma) * s;
+        wt[i].y = (wt[i].y / sigma) * s;
+        wt[i].z = (wt[i].z / sigma) * s;
+        wt[i].w = (wt[i].w / sigma) * s;
+    }
+    store_tile(L.W_eff, L.N, L.K, L.vec, r0, c0, wt);
 }
 
+// R2: one 1024-thread block per layer runs the epilogue; on the last
+// iteration the blocks after them write the small layers' W_eff tiles
+__global__ __launch_bounds__(1024) void sn_r2_kernel(SnTable t) {
+    __shared__ double red[32];
+    if ((int)blockIdx.x < t.n_layers) {
+        sn_layer_epilogue(t, t.L[blockIdx.x], t.last_iter, red);
+        return;
+    }
+    const int unit = blockIdx.x - t.n_layers;
+    const SnLayerDev &L = t.L[find_m3_layer(t, unit)];
+    sn_m3_tile(t, L, unit - L.m3_begin, red);
+}
+
+// P3 over the units of the layers it writes (W_eff not NULL, not R2's)
 __global__ __launch_bounds__(256) void sn_p3_kernel(SnTable t) {
     const int unit = blockIdx.x;
-    const SnLayerDev L = t.L[find_unit_layer(t, unit)];
-    if (!L.W_eff) return;
-    const int lt = unit - L.unit_begin;
+    const SnLayerDev L = t.L[find_p3_layer(t, unit)];
+    const int lt = unit - L.p3_begin;
     if (L.fold) {
         snf_p3(L, lt);
         return;
@@ -583,6 +688,62 @@ __global__ __launch_bounds__(256) void sn_bwd_b_kernel(SnTable t) {
     }
 }
 
+// The layer sums of the gstat partials (4 waves, each lane strided by 256, 8
+// loads per slab in flight; waves added in order), then the record {coef,
+// ||dL/dW||^2, sigma, s} and gs.
+
+__device__ __forceinline__ void gstat_finish(const SnLayerDev &L) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int units = layer_units(L);
+    // the record's inputs (earlier launches' writes) in flight with the partials
+    const double vv = L.stats[4], uu = L.stats[5];   // ||v||^2, ||u'||^2 (refresh R2)
+    const float sigma = L.sigma[0];
+    const float s = L.s ? L.s[0] : 1.f;
+    double dd = 0.0, gg = 0.0, ug = 0.0;
+    for (int base = threadIdx.x; base < units; base += 8 * 256) {
+        float a[8], b[8], c[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int i = base + j * 256;
+            a[j] = (i < units) ? L.dotp[i] : 0.f;
+            b[j] = (i < units) ? L.ggp[i] : 0.f;
+            c[j] = (i < units) ? L.ugvp[i] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            dd += (double)a[j];
+            gg += (double)b[j];
+            ug += (double)c[j];
+        }
+    }
+    __shared__ double red[3][4];
+    dd = wave_sum(dd);
+    gg = wave_sum(gg);
+    ug = wave_sum(ug);
+    if (lane == 0) {
+        red[0][w] = dd;
+        red[1][w] = gg;
+        red[2][w] = ug;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        dd = ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
+        gg = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
+        ug = ((red[2][0] + red[2][1]) + red[2][2]) + red[2][3];
+        const float d = (float)dd;
+        if (L.gs) L.gs[0] = d / sigma;                   // dL/ds, as sn_bwd_b
+        const float coef = (s * d) / (sigma * sigma);    // as sn_bwd_b
+        const double a = (double)s / (double)sigma;
+        double nsq = a * a * gg - 2.0 * a * (double)coef * ug +
+                     (double)coef * (double)coef * uu * vv;
+        if (!(nsq > 0.0)) nsq = 0.0;
+        L.stats[0] = coef;
+        L.stats[1] = (float)nsq;
+        L.stats[2] = sigma;
+        L.stats[3] = s;
+    }
+}
+
 // ---- gradient statistics for the G-direct update (smmd_sn_grad_stats) ------
 // Instead of writing dL/dW, the backward reduces what the optimizer needs to
 // form it on the fly from G (smmd_adam_flat_sn2, SMMD_ADAM_SN_GDIRECT):
@@ -596,7 +757,6 @@ __global__ __launch_bounds__(256) void sn_gstat_a_kernel(SnTable t) {
     const SnLayerDev L = t.L[find_unit_layer(t, unit)];
     if (!L.G) return;                            // this call skips the layer
     const int lt = unit - L.unit_begin;
-    __shared__ float red[4];
     float ad = 0.f, ag = 0.f, au = 0.f;
     if (L.fold) {
         __shared__ float s9[SNF_T * 9];
@@ -656,9 +816,31 @@ __global__ __launch_bounds__(256) void sn_gstat_a_kernel(SnTable t) {
             au = fmaf(uc[i], gv, au);
         }
     }
-    ad = block_sum<4>(ad, red);
-    ag = block_sum<4>(ag, red);
-    au = block_sum<4>(au, red);
+    // the three block sums through one barrier (block_sum's order, so its bits)
+    ad = wave_sum(ad);
+    ag = wave_sum(ag);
+    au = wave_sum(au);
+    __shared__ float red3[3][4];
+    {
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+        if (lane == 0) {
+            red3[0][w] = ad;
+            red3[1][w] = ag;
+            red3[2][w] = au;
+        }
+    }
+    __syncthreads();
+    ad = ag = au = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        ad += red3[0][i];
+        ag += red3[1][i];
+        au += red3[2][i];
+    }
+    // Measured and not kept: the layer's last unit reducing the partials in
+    // this launch (write-through partials, one arrival ticket per unit on a
+    // per-layer counter): 30 -> 45 us per call, the 2048 units of the largest
+    // layer serialising on one counter's atomics
     if (threadIdx.x == 0) {
         L.dotp[lt] = ad;
         L.ggp[lt] = ag;
@@ -666,60 +848,11 @@ __global__ __launch_bounds__(256) void sn_gstat_a_kernel(SnTable t) {
     }
 }
 
-// one 256-thread block per layer: the layer sums (4 waves, each lane
-// strided by 256, 8 loads per slab in flight; waves added in order), then the
-// record {coef, ||dL/dW||^2, sigma, s} and gs
+// one 256-thread block per layer: the layer sums and the record
 __global__ __launch_bounds__(256) void sn_gstat_r_kernel(SnTable t) {
-    const SnLayerDev L = t.L[blockIdx.x];
+    const SnLayerDev &L = t.L[blockIdx.x];
     if (!L.G) return;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int units = layer_units(L);
-    double dd = 0.0, gg = 0.0, ug = 0.0;
-    for (int base = threadIdx.x; base < units; base += 8 * 256) {
-        float a[8], b[8], c[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int i = base + j * 256;
-            a[j] = (i < units) ? L.dotp[i] : 0.f;
-            b[j] = (i < units) ? L.ggp[i] : 0.f;
-            c[j] = (i < units) ? L.ugvp[i] : 0.f;
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            dd += (double)a[j];
-            gg += (double)b[j];
-            ug += (double)c[j];
-        }
-    }
-    __shared__ double red[3][4];
-    dd = wave_sum(dd);
-    gg = wave_sum(gg);
-    ug = wave_sum(ug);
-    if (lane == 0) {
-        red[0][w] = dd;
-        red[1][w] = gg;
-        red[2][w] = ug;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        dd = ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
-        gg = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
-        ug = ((red[2][0] + red[2][1]) + red[2][2]) + red[2][3];
-        const double vv = L.stats[4], uu = L.stats[5];   // ||v||^2, ||u'||^2 (refresh R2)
-        const float d = (float)dd;
-        const float sigma = L.sigma[0];
-        const float s = L.s ? L.s[0] : 1.f;
-        if (L.gs) L.gs[0] = d / sigma;                   // dL/ds, as sn_bwd_b
-        const float coef = (s * d) / (sigma * sigma);    // as sn_bwd_b
-        const double a = (double)s / (double)sigma;
-        double nsq = a * a * gg - 2.0 * a * (double)coef * ug +
-                     (double)coef * (double)coef * uu * vv;
-        if (!(nsq > 0.0)) nsq = 0.0;
-        L.stats[0] = coef;
-        L.stats[1] = (float)nsq;
-        L.stats[2] = sigma;
-        L.stats[3] = s;
-    }
+    gstat_finish(L);
 }
 
 // ---------------------------------------------------------------------------
@@ -786,13 +919,22 @@ static bool build_table(const smmd_sn_layer *layers, int first, int count, char 
             L.nfc = src.K / 9;
         }
         L.unit_begin = (int)units;
-        units += L.fold ? ((int64_t)src.N * L.nfc + SNF_T - 1) / SNF_T
-                        : (int64_t)L.nrt * L.nct;
+        const int64_t lu = L.fold ? ((int64_t)src.N * L.nfc + SNF_T - 1) / SNF_T
+                                  : (int64_t)L.nrt * L.nct;
+        units += lu;
         if (units > 0x7fffffff) return false;
+        L.nctp = (L.nct + 3) & ~3;
+        // W_eff written by R2's launch (small plain layers: the tile's redundant
+        // norm reads <= its own 8 K floats) or by P3 (the rest)
+        const bool m3 = src.W_eff && !L.fold && L.N <= EP_NREG * 1024 && L.K <= EP_KREG * 1024 &&
+                        (int64_t)L.nctp * L.N + L.K <= (int64_t)SN_TR * SN_TC;
+        L.m3_begin = t.total_m3;
+        L.p3_begin = t.total_p3;
+        if (m3) t.total_m3 += (int)lu;
+        else if (src.W_eff) t.total_p3 += (int)lu;
         char *p = ws + off;
         L.p1 = (float *)p;   p += align_up((size_t)L.nrt * L.K * 4, 256);
         L.vraw = (float *)p; p += align_up((size_t)L.K * 4, 256);
-        L.nctp = (L.nct + 3) & ~3;
         L.q2 = (float *)p;   p += align_up((size_t)L.nctp * L.N * 4, 256);
         L.ucur = (float *)p; p += align_up((size_t)L.N * 4, 256);
         L.dotp = (float *)p; p += align_up((size_t)dotp_slots(L.N, L.K) * 4, 256);
@@ -896,11 +1038,11 @@ smmd_status smmd_sn_power_iter_ex(const smmd_sn_layer *layers, int n_layers, int
             if (it > 0 || !(flags & SMMD_SN_P1_READY))   // else written by smmd_adam_flat_sn
                 hipLaunchKernelGGL(sn_p1_kernel, dim3(t.total_tiles), dim3(256), 0, s, t);
             hipLaunchKernelGGL(sn_p2_kernel, dim3(t.total_tiles), dim3(256), 0, s, t);
-            hipLaunchKernelGGL(sn_r2_kernel, dim3(t.n_layers), dim3(1024), 0, s, t);
+            const int m3 = t.last_iter ? t.total_m3 : 0;
+            hipLaunchKernelGGL(sn_r2_kernel, dim3(t.n_layers + m3), dim3(1024), 0, s, t);
         }
-        bool any_eff = false;
-        for (int i = 0; i < count; ++i) any_eff |= (t.L[i].W_eff != nullptr);
-        if (any_eff) hipLaunchKernelGGL(sn_p3_kernel, dim3(t.total_units), dim3(256), 0, s, t);
+        if (t.total_p3 > 0)
+            hipLaunchKernelGGL(sn_p3_kernel, dim3(t.total_p3), dim3(256), 0, s, t);
         smmd_status st = last_launch_status();
         if (st != SMMD_OK) return st;
     }

@@ -170,3 +170,40 @@ def test_stale_lazy_weight_raises():
         bank.entries[0].weight.mul_(1.5)          # an in-place update of W
     with pytest.raises(convops.StaleLazyWeight):
         convops._wino_filter(new, 128, 64, 0)
+
+
+def test_refresh_w_eff_writers_bit_exact():
+    """W_eff is written by R2's launch for small plain layers (the tile forms
+    sigma itself with the layer block's code) and by P3 for the rest (larger
+    ones, fold layers): both are bit for bit (W / sigma) * s with the sigma
+    the refresh stored, also with the Winograd-fed layers lazy.  Shapes: the
+    SNResNet-64 critic's non-lazy layers (thin input conv, 1x1 shortcuts, the
+    linear layer), a wide plain layer over R2's redundancy bound, a fold layer."""
+    from gan.core.sn import SpectralNormBank
+    g = torch.Generator(device=DEV).manual_seed(5)
+    specs = [((64, 3, 3, 3), False), ((128, 64, 1, 1), False), ((512, 256, 1, 1), False),
+             ((1024, 512, 1, 1), False), ((1, 1024), False), ((1024, 4608), False),
+             ((256, 128, 3, 3), True), ((128, 128, 3, 3), False)]
+    mods = []
+    for shape, fold in specs:
+        m = torch.nn.Module()
+        m.weight = torch.nn.Parameter(torch.randn(*shape, device=DEV, generator=g) * 0.05)
+        m.sn_scale = torch.nn.Parameter(torch.full((1,), 1.7, device=DEV))
+        m.sn_fold = fold
+        mods.append(m)
+    bank = SpectralNormBank(mods)
+    bank.set_lazy([7])                       # a Winograd-fed layer: not written
+    for _ in range(3):
+        with torch.no_grad():
+            outs = bank.refresh(update_u=True)
+        for i, (e, w) in enumerate(zip(bank.entries, outs)):
+            if i == 7:
+                continue
+            ref = (e.weight.detach() / e.sigma) * e.scale.detach()
+            if e.fold:
+                from gan.core.convops import fold_pool_weight
+                ref = fold_pool_weight(ref)
+            assert torch.equal(w, ref), i
+        with torch.no_grad():
+            for m in mods:
+                m.weight.add_(torch.randn(m.weight.shape, device=DEV, generator=g) * 0.01)
