@@ -91,9 +91,10 @@ __global__ __launch_bounds__(W2_T, 1) void s2_wgrad_kernel(
         if (P::NI > 1) {
             n0 = (int)(chunk * P::NI);
             ty0 = 0;
-        } else {
-            n0 = (int)(chunk / cpi);
-            ty0 = (int)(chunk - (int64_t)n0 * cpi) * RT;
+        } else {                  // 32-bit: a 64-bit division is ~130 scalar instructions
+            const uint32_t ch32 = (uint32_t)chunk;
+            n0 = (int)(ch32 / (uint32_t)cpi);
+            ty0 = (int)(ch32 - (uint32_t)n0 * (uint32_t)cpi) * RT;
         }
         const uint32_t xrange = (uint32_t)(((P::NI - 1) * g.C + 16) * HW) * 4u;
         const uint32_t grange = (uint32_t)(((P::NI - 1) * g.K + 64) * HWo) * 4u;
@@ -210,12 +211,14 @@ __global__ __launch_bounds__(W2_T, 1) void s2_wgrad_kernel(
         gload(ch0);
         lstore(0);
         __syncthreads();
-        float ca[9], cbv[9];
+        // the MFMA operands, double-buffered: k-step m reads set m & 1 and
+        // forms the next k-step's into the other (no copy into a fixed set)
+        float oa[2][9], ob[2][9];
         {
             float d[9], gv[4], t[9];
             lds_read(0, tp, d, gv);
 #pragma unroll
-            for (int q = 0; q < 9; ++q) tslice(q, d, gv, t, ca, cbv);
+            for (int q = 0; q < 9; ++q) tslice(q, d, gv, t, oa[0], ob[0]);
         }
         for (int c = 0; c < nchunk; ++c) {
             const int buf = c & 1;
@@ -225,7 +228,8 @@ __global__ __launch_bounds__(W2_T, 1) void s2_wgrad_kernel(
             gload(ch0 + min(c + 1, nchunk - 1));
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
-                float na[9], nb[9], d[9], gv[4], t[9];
+                const int cur = m & 1, nxt = cur ^ 1;   // 4 k-steps: set 0 at every chunk start
+                float d[9], gv[4], t[9];
                 if (m == 3) {
                     lstore(buf ^ 1);
                     __syncthreads();                 // every wave stored chunk c + 1
@@ -235,12 +239,11 @@ __global__ __launch_bounds__(W2_T, 1) void s2_wgrad_kernel(
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int q = 0; q < 9; ++q) {
-                    acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca[q], cbv[q], acc[q], 0, 0, 0);
-                    tslice(q, d, gv, t, na, nb);
+                    acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(oa[cur][q], ob[cur][q], acc[q],
+                                                                  0, 0, 0);
+                    tslice(q, d, gv, t, oa[nxt], ob[nxt]);
                     __builtin_amdgcn_sched_barrier(0);
                 }
-#pragma unroll
-                for (int p = 0; p < 9; ++p) { ca[p] = na[p]; cbv[p] = nb[p]; }
             }
         }
     }

@@ -29,6 +29,33 @@ constexpr int WG_STAGE = 16 * WG_TC * 64;      // floats per dM (and per V) stag
 constexpr size_t WG_LDS = 2 * 2 * WG_STAGE * sizeof(float);   // 128 KB
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// one v_pk_add_f32 each (VOP3P: op_sel / op_sel_hi pick each source's half for
+// the low / high result, neg_lo / neg_hi negate it; written as vector ops the
+// compiler folded none of this and regrouped the pairs with v_mov), the same
+// IEEE adds as the scalar forms.  Their results feed MFMAs a k-step later, and
+// overwrite operands whose MFMAs issued at least two MFMAs earlier.
+// (r.x + r.y, r.x - r.y)
+__device__ __forceinline__ f2v wg_pm(f2v r) {
+    f2v o;
+    asm("v_pk_add_f32 %0, %1, %1 op_sel:[0,1] op_sel_hi:[0,1] neg_hi:[0,1]" : "=v"(o) : "v"(r));
+    return o;
+}
+// (t0 - t2, t1 + t2) from t01, t23
+__device__ __forceinline__ f2v wg_b01(f2v t01, f2v t23) {
+    f2v o;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,0] op_sel_hi:[1,0] neg_lo:[0,1]"
+        : "=v"(o) : "v"(t01), "v"(t23));
+    return o;
+}
+// (t2 - t1, t1 - t3) = (-t1 + t2, t1 + -t3)
+__device__ __forceinline__ f2v wg_b23(f2v t01, f2v t23) {
+    f2v o;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1] neg_lo:[1,0] neg_hi:[0,1]"
+        : "=v"(o) : "v"(t01), "v"(t23));
+    return o;
+}
 
 struct WgGeom {
     int N, C, K, H, W, TW, Timg;
@@ -329,9 +356,12 @@ __device__ __forceinline__ void wgrad2_body(const float *__restrict__ x,
     float hr[P::NH > 0 ? P::NH : 1];
     constexpr uint32_t OOB = 0x80000000u;
     const uint32_t plane = (uint32_t)HW * 4u;
-    auto gload = [&](int64_t chunk) {
-        const int n = (int)(chunk / cpi);
-        const int q = (int)(chunk - (int64_t)n * cpi);
+    auto gload = [&](int64_t chunk64) {
+        // 32-bit (the chunk count is far below 2^31): the 64-bit division
+        // was ~130 scalar instructions per chunk
+        const uint32_t chunk = (uint32_t)chunk64;
+        const int n = (int)(chunk / (uint32_t)cpi);
+        const int q = (int)(chunk - (uint32_t)n * (uint32_t)cpi);
         const int ty0 = (q / segs) * P::RT, tx0 = (q % segs) * CT;
         const __amdgpu_buffer_rsrc_t xs = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<float *>(x + ((int64_t)n * g.C + cb * 64) * HW), 0, 64 * plane, 0x00020000);
@@ -420,31 +450,40 @@ __device__ __forceinline__ void wgrad2_body(const float *__restrict__ x,
         gv[0] = gk[0]; gv[1] = gk[1]; gv[2] = gk[P::GRS]; gv[3] = gk[P::GRS + 1];
     };
     // slice q of this wave's half of the transforms (after MFMA q of the
-    // current k-step): a = rows 2 ph, 2 ph + 1 of dM = A dY A^T (A = [[1,0],
-    // [1,1],[1,-1],[0,-1]]), b = the same rows of V = B^T d B (d = the patch
-    // rows ph .. ph + 2 read above)
-    auto tslice = [&](int q, const float (&d)[12], const float (&gv)[4], float (&t)[8],
+    // current k-step): a = rows 2 ph, 2 ph + 1 of dM' = A' dY A'^T, b = the
+    // same rows of V = B^T d B (d = the patch rows ph .. ph + 2 read above).
+    // A' = [[1,0],[1,1],[1,-1],[0,1]] is A = [[1,0],[1,1],[1,-1],[0,-1]] with
+    // its last row negated, so dM'_ij = s_i s_j dM_ij (s_3 = -1, else 1) needs
+    // no negations; the epilogue undoes the signs, bit for bit (negation is
+    // exact and rounding symmetric)
+    // Packed: the patch and gy rows arrive as column pairs (ds_read2_b32), so
+    // each slice is v_pk_add_f32 on them (8 + 3 per k-step; scalar adds on
+    // pairs the compiler regrouped cost ~9 v_mov per k-step besides)
+    auto tslice = [&](int q, const float (&d)[12], const float (&gv)[4], f2v (&t)[4],
                       float (&a)[8], float (&b)[8]) {
         if (q == 1) {
-            // rows 0, 1 of A dY: (g0, g0 + g1); rows 2, 3: (g0 - g1, -g1)
-            const float r00 = ph ? gv[0] - gv[2] : gv[0], r01 = ph ? gv[1] - gv[3] : gv[1];
-            const float r10 = ph ? -gv[2] : gv[0] + gv[2], r11 = ph ? -gv[3] : gv[1] + gv[3];
-            a[0] = r00; a[1] = r00 + r01; a[2] = r00 - r01; a[3] = -r01;
-            a[4] = r10; a[5] = r10 + r11; a[6] = r10 - r11; a[7] = -r11;
-        } else if (q == 2 || q == 3) {   // columns of t = rows (2 ph, 2 ph + 1) of B^T d
+            // rows of A' dY: ph 0 (g01, g01 + g23), ph 1 (g01 - g23, g23); each
+            // row R gives (R.x, R.x + R.y, R.x - R.y, R.y)
+            const f2v g01 = {gv[0], gv[1]}, g23 = {gv[2], gv[3]};
+            const f2v r0 = ph ? g01 - g23 : g01, r1 = ph ? g23 : g01 + g23;
+            const f2v p0 = wg_pm(r0), p1 = wg_pm(r1);
+            a[0] = r0.x; a[1] = p0.x; a[2] = p0.y; a[3] = r0.y;
+            a[4] = r1.x; a[5] = p1.x; a[6] = p1.y; a[7] = r1.y;
+        } else if (q == 2 || q == 3) {   // t row q - 2: rows (2 ph, 2 ph + 1) of B^T d
+            // ph 0: rows 0, 1 = (d0 - d2, d1 + d2); ph 1: rows 2, 3 = (d2 - d1, d1 - d3)
+            const int r = q - 2;
 #pragma unroll
-            for (int jj = 0; jj < 2; ++jj) {
-                const int j = 2 * (q - 2) + jj;
-                // ph 0: rows 0, 1 = (d0 - d2, d1 + d2); ph 1: rows 2, 3 = (d2 - d1, d1 - d3)
-                t[j] = ph ? d[1 * 4 + j] - d[0 * 4 + j] : d[0 * 4 + j] - d[2 * 4 + j];
-                t[4 + j] = ph ? d[0 * 4 + j] - d[2 * 4 + j] : d[1 * 4 + j] + d[2 * 4 + j];
+            for (int h = 0; h < 2; ++h) {
+                const f2v e0 = {d[0 * 4 + 2 * h], d[0 * 4 + 2 * h + 1]};
+                const f2v e1 = {d[1 * 4 + 2 * h], d[1 * 4 + 2 * h + 1]};
+                const f2v e2 = {d[2 * 4 + 2 * h], d[2 * 4 + 2 * h + 1]};
+                t[2 * r + h] = r == 0 ? (ph ? e1 - e0 : e0 - e2) : (ph ? e0 - e2 : e1 + e2);
             }
-        } else if (q == 4 || q == 5) {   // row of V = t B
+        } else if (q == 4 || q == 5) {   // row of V = t B: (t0 - t2, t1 + t2, t2 - t1, t1 - t3)
             const int i = q - 4;
-            b[i * 4 + 0] = t[i * 4 + 0] - t[i * 4 + 2];
-            b[i * 4 + 1] = t[i * 4 + 1] + t[i * 4 + 2];
-            b[i * 4 + 2] = t[i * 4 + 2] - t[i * 4 + 1];
-            b[i * 4 + 3] = t[i * 4 + 1] - t[i * 4 + 3];
+            const f2v b01 = wg_b01(t[2 * i], t[2 * i + 1]), b23 = wg_b23(t[2 * i], t[2 * i + 1]);
+            b[i * 4 + 0] = b01.x; b[i * 4 + 1] = b01.y;
+            b[i * 4 + 2] = b23.x; b[i * 4 + 3] = b23.y;
         }
     };
 
@@ -464,12 +503,16 @@ __device__ __forceinline__ void wgrad2_body(const float *__restrict__ x,
         gload(ch0);
         lstore(0);
         __syncthreads();
-        float ca[8], cbv[8];
+        // the MFMA operands, double-buffered: k-step s reads set s & 1 and
+        // forms the next k-step's into the other (a copy of the next set into
+        // one fixed set cost ~80 v_mov per 64 MFMAs)
+        float oa[2][8], ob[2][8];
         {
-            float d[12], gv[4], t[8];
+            float d[12], gv[4];
+            f2v t[4];
             lds_read(0, 0, d, gv);
 #pragma unroll
-            for (int q = 0; q < 8; ++q) tslice(q, d, gv, t, ca, cbv);
+            for (int q = 0; q < 8; ++q) tslice(q, d, gv, t, oa[0], ob[0]);
         }
         for (int c = 0; c < nchunk; ++c) {
             const int buf = c & 1;
@@ -483,20 +526,21 @@ __device__ __forceinline__ void wgrad2_body(const float *__restrict__ x,
             gload(ch0 + min(c + 1, nchunk - 1));
 #pragma unroll
             for (int s = 0; s < 8; ++s) {
-                float na[8], nb[8], d[12], gv[4], t[8];
+                const int cur = s & 1, nxt = cur ^ 1;   // 8 k-steps: set 0 at every chunk start
+                float d[12], gv[4];
+                f2v t[4];
                 if (s == 7) __syncthreads();             // every wave stored chunk c + 1
                 __builtin_amdgcn_sched_barrier(0);
                 lds_read(s < 7 ? buf : buf ^ 1, (s + 1) & 7, d, gv);
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int q = 0; q < 8; ++q) {
-                    acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca[q], cbv[q], acc[q], 0, 0, 0);
-                    tslice(q, d, gv, t, na, nb);
+                    acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(oa[cur][q], ob[cur][q], acc[q],
+                                                                  0, 0, 0);
+                    tslice(q, d, gv, t, oa[nxt], ob[nxt]);
                     if (s == 5 && q == 0) lstore(buf ^ 1);
                     __builtin_amdgcn_sched_barrier(0);
                 }
-#pragma unroll
-                for (int p = 0; p < 8; ++p) { ca[p] = na[p]; cbv[p] = nb[p]; }
             }
         }
     }
@@ -529,19 +573,23 @@ __device__ __forceinline__ void wgrad2_body(const float *__restrict__ x,
                     u[p] = acc[p][r];
                     u[8 + p] = E[(p * 8 + rr) * 64 + lane];
                 }
+                // u holds dU' (u'_ij = s_i s_j u_ij, s_3 = -1): with T = the
+                // row pass on u', t[a][j] = T[a][j] for j < 3 and -T[a][j]
+                // for j = 3, so each sign lands on a subtraction that equals
+                // the original addition bit for bit
                 float t[3][4];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     t[0][j] = u[j] + 0.5f * (u[4 + j] + u[8 + j]);
                     t[1][j] = 0.5f * (u[4 + j] - u[8 + j]);
-                    t[2][j] = 0.5f * (u[4 + j] + u[8 + j]) + u[12 + j];
+                    t[2][j] = 0.5f * (u[4 + j] + u[8 + j]) - u[12 + j];
                 }
                 float *o = out + ((int64_t)k * g.C + c) * 9;
 #pragma unroll
                 for (int a = 0; a < 3; ++a) {
                     o[a * 3 + 0] = t[a][0] + 0.5f * (t[a][1] + t[a][2]);
                     o[a * 3 + 1] = 0.5f * (t[a][1] - t[a][2]);
-                    o[a * 3 + 2] = 0.5f * (t[a][1] + t[a][2]) + t[a][3];
+                    o[a * 3 + 2] = 0.5f * (t[a][1] + t[a][2]) - t[a][3];
                 }
             }
         }

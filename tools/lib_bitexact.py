@@ -4,8 +4,9 @@ placement): python tools/lib_bitexact.py LIB_A LIB_B
 
 Covered: the 3x3 conv over every tests/test_gpu_wino.py shape in both forms
 (8-wave default, SMMD_WINO8=0 the 4-wave one), modes 0 and 1 of the filter,
-the relu epilogue and the pair form; the stride-2 conv (plain and pair) over
-its fold-layer shapes.  `make -C scaled-mmd-gan_amd/csrc conservative` builds
+the relu epilogue and the pair form; the stride-2 conv (plain and pair) and
+the transposed stride-2 conv over the fold-layer shapes; both weight
+gradients (3x3, stride 2) over their test shapes and the bench layers.  `make -C scaled-mmd-gan_amd/csrc conservative` builds
 the conservative variant (every filter-stage LDS-DMA piece waited for right
 after its issue, -DWN_DMA_SYNC) that this compares with the shipped build."""
 import ctypes
@@ -61,6 +62,34 @@ def run_s2(L, x, w, b, x2, w2, st):
                                   _lib.ptr(y2), N, C, K, H, W, _lib.ptr(ws2), nb2, st) == 0
     torch.cuda.synchronize()
     return y.cpu(), y2.cpu()
+
+
+def run_s2t(L, gy, w, b, st):
+    N, K, Hg, Wg = gy.shape
+    C = w.shape[1]
+    u = torch.empty(L.smmd_wino4x4s2_filter_bytes(K, C) // 4, device=gy.device)
+    assert L.smmd_wino4x4s2t_filter(_lib.ptr(w), K, C, _lib.ptr(u), u.numel() * 4, st) == 0
+    dx = torch.empty(N, C, 2 * Hg, 2 * Wg, device=gy.device)
+    nb = L.smmd_wino4x4s2t_workspace_bytes(N, K, C, Hg, Wg)
+    ws = _ws(nb, gy.device)
+    assert L.smmd_wino4x4s2t_conv(_lib.ptr(gy), _lib.ptr(u), _lib.ptr(b), _lib.ptr(dx), N, K, C,
+                                  Hg, Wg, _lib.ptr(ws), nb, st) == 0
+    torch.cuda.synchronize()
+    return [dx.cpu()]
+
+
+def run_wgrad(L, x, gy, s2, st):
+    N, C, H, W = x.shape
+    K = gy.shape[1]
+    kk = 4 if s2 else 3
+    gw = torch.empty(K, C, kk, kk, device=x.device)
+    fb = L.smmd_wino4x4s2_wgrad_workspace_bytes if s2 else L.smmd_wino3x3_wgrad_workspace_bytes
+    fn = L.smmd_wino4x4s2_wgrad if s2 else L.smmd_wino3x3_wgrad
+    nb = fb(N, C, K, H, W)
+    ws = _ws(nb, x.device)
+    assert fn(_lib.ptr(x), _lib.ptr(gy), _lib.ptr(gw), N, C, K, H, W, _lib.ptr(ws), nb, st) == 0
+    torch.cuda.synchronize()
+    return [gw.cpu()]
 
 
 def run_w3(L, x, w, b, x2, w2, st, pair):
@@ -129,6 +158,34 @@ def main():
         same = all(torch.equal(p, q) for p, q in zip(ra, rb))
         ok &= same
         print('s2', (N, C, K, H, W), 'bit-identical' if same else 'DIFFERENT', flush=True)
+    for (N, C, K, H, W) in S2_SHAPES:             # the transposed conv: gy [N, K, H/2, W/2]
+        if C % 8 or K % 64:
+            continue
+        g = torch.Generator(device=dev).manual_seed(N + C + K + H + W + 1)
+        gy = torch.randn(N, C, H // 2, W // 2, device=dev, generator=g)
+        w = torch.randn(C, K, 4, 4, device=dev, generator=g)
+        b = torch.randn(K, device=dev, generator=g)
+        same = all(torch.equal(p, q) for p, q in zip(run_s2t(A, gy, w, b, st),
+                                                      run_s2t(B, gy, w, b, st)))
+        ok &= same
+        print('s2t', (N, C, K, H, W), 'bit-identical' if same else 'DIFFERENT', flush=True)
+    from test_gpu_wino import WGRAD_SHAPES
+    from test_gpu_wino_s2 import S2_WGRAD_SHAPES
+    for s2, shapes in ((False, WGRAD_SHAPES + [(64, 64, 64, 64, 64), (64, 512, 512, 8, 8)]),
+                       (True, S2_WGRAD_SHAPES + [(64, 64, 128, 64, 64), (64, 512, 1024, 8, 8)])):
+        sup = A.smmd_wino4x4s2_wgrad_supported if s2 else A.smmd_wino3x3_wgrad_supported
+        for (N, C, K, H, W) in shapes:
+            if not sup(N, C, K, H, W):
+                continue
+            g = torch.Generator(device=dev).manual_seed(N + C + K + H + W + 2)
+            x = torch.randn(N, C, H, W, device=dev, generator=g)
+            d = 2 if s2 else 1
+            gy = torch.randn(N, K, H // d, W // d, device=dev, generator=g)
+            same = all(torch.equal(p, q) for p, q in zip(run_wgrad(A, x, gy, s2, st),
+                                                          run_wgrad(B, x, gy, s2, st)))
+            ok &= same
+            print('s2 wgrad' if s2 else '3x3 wgrad', (N, C, K, H, W),
+                  'bit-identical' if same else 'DIFFERENT', flush=True)
     print('ALL BIT-IDENTICAL' if ok else 'MISMATCH')
     sys.exit(0 if ok else 1)
 

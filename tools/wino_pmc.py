@@ -4,7 +4,7 @@ stride-2 layers (smmd_wino4x4s2_conv) at batch 64, random data, --iters
 launches each, through the stamped library.  Prints per-shape HIP-event
 times (no profiler: run it bare for times, under rocprofv3 --pmc for counters).
 
-python tools/wino_pmc.py [--iters N] [--only 3x3|s2|s2t|wgrad] [--lib PATH]
+python tools/wino_pmc.py [--iters N] [--only 3x3|s2|s2t|wgrad|s2w] [--lib PATH]
 (--lib: another build of the library, unstamped, for interleaved A/B runs)
 """
 import argparse
@@ -161,6 +161,26 @@ def main():
                                                  'executed_tflops': round(fl / us / 1e6, 1),
                                                  'mfma_frac': round(fl / us / 1e6 / 157.3, 3)}
             print(json.dumps(out['wgrad_%d_%d_%d' % (C, K, H)]), flush=True)
+    if a.only in ('', 's2w'):
+        # the critic's folded ConvMeanPool layers: x [64, C, H, H], gy [64, K, H/2, H/2]
+        for (N, C, K, H) in ((64, 64, 128, 64), (64, 128, 256, 32), (64, 256, 512, 16),
+                             (64, 512, 1024, 8)):
+            x = torch.randn(N, C, H, H, device=dev)
+            gy = torch.randn(N, K, H // 2, H // 2, device=dev)
+            gw = torch.empty(K, C, 4, 4, device=dev)
+            nb = L.smmd_wino4x4s2_wgrad_workspace_bytes(N, C, K, H, H)
+            ws = torch.empty(max(nb // 4, 4), device=dev)
+
+            def f():
+                s = L.smmd_wino4x4s2_wgrad(_lib.ptr(x), _lib.ptr(gy), _lib.ptr(gw), N, C, K, H,
+                                           H, _lib.ptr(ws), nb, st)
+                assert s == 0
+            us = timed(f, a.iters)
+            fl = 2.0 * 9 * 4 * N * (H // 4) ** 2 * C * K
+            out['s2w_%d_%d_%d' % (C, K, H)] = {'us': round(us, 2),
+                                               'executed_tflops': round(fl / us / 1e6, 1),
+                                               'mfma_frac': round(fl / us / 1e6 / 157.3, 3)}
+            print(json.dumps(out['s2w_%d_%d_%d' % (C, K, H)]), flush=True)
     print(json.dumps(out))
 
 
