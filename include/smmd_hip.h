@@ -68,7 +68,8 @@ int smmd_abi_version(void);         /* bumped on any ABI change (2: Gram/poly,
                                        smmd_wino3x3_wgrad*, 9: smmd_wino4x4s2_wgrad*,
                                        smmd_wino3x3_filter_sn, smmd_wino4x4s2(t)_filter_sn,
                                        smmd_sn_clip_g, 10: smmd_wino3x3_conv2*,
-                                       smmd_wino4x4s2_conv2*) */
+                                       smmd_wino4x4s2_conv2*, 11: smmd_fold_up_weight,
+                                       smmd_conv1x1*) */
 const char *smmd_source_hash(void); /* first 16 hex digits of the SHA-256 of the
                                        sources this binary was built from
                                        (csrc .hip and .hpp files in byte order,
@@ -446,6 +447,19 @@ smmd_status smmd_fold_pool_weights(const float *const *src, float *const *dst,
                                    const int64_t *n_filters, int n_layers, int adjoint,
                                    smmd_stream_t stream);
 
+/* UpsampleConv filter fold (gan/core/resnet/block.py:53-60: concat x4 +
+ * depth_to_space, i.e. a nearest x2 upsample, then conv3x3 SAME), run by the
+ * product as ONE 4x4 stride-2 transposed conv (ABI 11; replaces
+ * convops.fold_up_weight's pad / avg_pool / scale / flip / transpose ops).
+ *  adjoint = 0: src W [cout, cin, 3, 3] -> dst K [cin, cout, 4, 4],
+ *               K[ci][co][s][t] = sum_{a,b in {0,1}} W[co][ci][3-s-a][3-t-b]
+ *               (4 x the ConvMeanPool fold, flipped in both axes, transposed)
+ *  adjoint = 1: src gK [cin, cout, 4, 4] -> dst gW [cout, cin, 3, 3],
+ *               gW[co][ci][u][v] = sum_{a,b in {0,1}} gK[ci][co][3-u-a][3-v-b]
+ * src and dst 16-byte aligned. */
+smmd_status smmd_fold_up_weight(const float *src, float *dst, int cout, int cin, int adjoint,
+                                smmd_stream_t stream);
+
 /* ---------------------------------------------------------------------------
  * Convolution bias gradient: out[c] = sum_{n, hw} gy[n, c, hw] over an NCHW
  * tensor [N, C, HW] (TF's BiasAddGrad of the bias_add in snops.conv2d,
@@ -746,6 +760,39 @@ size_t smmd_wino4x4s2_wgrad_workspace_bytes(int n, int ci, int co, int h, int w_
 smmd_status smmd_wino4x4s2_wgrad(const float *x, const float *gy, float *gw, int n, int ci,
                                  int co, int h, int w_img, void *ws, size_t ws_bytes,
                                  smmd_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * The 1x1 stride-1 convolutions of the residual shortcuts (ABI 11;
+ * gan/core/resnet/block.py:28-40: MeanPoolConv in the critic's down blocks,
+ * the 1x1 conv of the generator's up-block shortcut, snops.conv2d's
+ * tf.nn.conv2d / Conv2DBackpropInput / Conv2DBackpropFilter, snops.py:69-90)
+ * on the f32 MFMA, NCHW without layout transposes.  p = pixels per image.
+ *
+ * smmd_conv1x1: y [n, m, p] = a [m, r] . x [n, r, p] (+ bias [m], may be NULL).
+ *   The forward is a = W [k, c] (m = k, r = c); the input gradient is
+ *   a = W^T as a [c, k] row-major copy (m = c, r = k) with x = gy.  Needs
+ *   m % 64 == 0, r % 32 == 0, p % 4 == 0, n p % 64 == 0
+ *   (smmd_conv1x1_supported(n, r, m, p)); a, x, y 16-byte aligned.  Shapes
+ *   with few output tiles split the reduction over workgroups whose partial
+ *   outputs (smmd_conv1x1_workspace_bytes; 0 = none) are added in slice order.
+ * smmd_conv1x1_wgrad: gw [k, c] = sum over n, p of gy [n, k, p] x [n, c, p];
+ *   needs c, k % 64 == 0, p % 4 == 0, n p % 32 == 0; the columns are split
+ *   over workgroups whose partials (smmd_conv1x1_wgrad_workspace_bytes; 0 =
+ *   none) are added in slice order.  Deterministic.
+ * ------------------------------------------------------------------------- */
+int smmd_conv1x1_supported(int n, int r, int m, int p);
+
+size_t smmd_conv1x1_workspace_bytes(int n, int r, int m, int p);
+
+smmd_status smmd_conv1x1(const float *a, const float *x, const float *bias, float *y, int n,
+                         int r, int m, int p, void *ws, size_t ws_bytes, smmd_stream_t stream);
+
+int smmd_conv1x1_wgrad_supported(int n, int c, int k, int p);
+
+size_t smmd_conv1x1_wgrad_workspace_bytes(int n, int c, int k, int p);
+
+smmd_status smmd_conv1x1_wgrad(const float *gy, const float *x, float *gw, int n, int c, int k,
+                               int p, void *ws, size_t ws_bytes, smmd_stream_t stream);
 
 #ifdef __cplusplus
 }

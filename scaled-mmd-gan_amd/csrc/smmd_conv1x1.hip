@@ -1,0 +1,456 @@
+// smmd_conv1x1.hip -- the 1x1 convolutions of the residual blocks' shortcuts
+// (gan/core/resnet/block.py:28-40: MeanPoolConv in the critic's down blocks,
+// the 1x1 conv before the nearest upsample in the generator's up blocks) on
+// the f32 MFMA, NCHW in place: no layout transposes.
+//
+// All three directions are GEMMs over a "column" index j = (n, p) of the
+// batch and the pixels (p fastest, images stride M P):
+//   forward          y[n][k][p]  = sum_c W[k][c] x[n][c][p] (+ b[k])
+//   input gradient   dx[n][c][p] = sum_k W[k][c] gy[n][k][p]  (the forward with
+//                    A = W^T, a [C][K] copy the caller keeps per weight)
+//   weight gradient  dW[k][c]    = sum_{n,p} gy[n][k][p] x[n][c][p]
+// MIOpen ran them through NHWC transposes (batched_transpose) and igemm /
+// GEMM solvers at 15-45 us per 1.07 GFLOP call; the step spent ~8 % of its GPU
+// time there (profiles/r14/step_kernel_top_r14g.txt).
+//
+// c1_gemm (forward / input gradient): block = 64 rows m x 64 columns j, 4 waves,
+// wave (mh, jh) the 32 x 32 quadrant on v_mfma_f32_32x32x2_f32.  The reduction
+// runs in chunks of 32 through a double-buffered LDS stage kept in the global
+// layouts: A [m][r] (row stride 36), B [r][j] (row stride 68), both with
+// 16-byte rows for the float4 stores.  MFMA t of a chunk reduces over r = t
+// and 16 + t (lane half h = lane / 32 takes 16 h + t): a lane's A values are
+// one contiguous run (a 16-byte read feeds 4 MFMAs), its B values one read
+// per MFMA (pairs merged into ds_read2_b32).  The next chunk's
+// global loads (float4 along the contiguous dimension) are issued before the
+// current chunk's MFMAs and stored to the other buffer after them; occupancy
+// (4 blocks per CU) covers the rest.
+//
+// c1_wgrad: block = 64 k x 64 c over one slice of the columns; A = gy [k][j],
+// B = x [c][j], both [row][j] with row stride 36 and the same t / 16 + t
+// pairing (one 16-byte read of each feeds 4 MFMAs), chunks of 32 columns; each
+// slice writes a partial dW, the slices are added in order by c1_sum.
+//
+// Accumulation order: fixed (per chunk, MFMA t in order; slices in order), so
+// the results are deterministic; fp32 products and sums, as the reference.
+#include "smmd_common.hpp"
+
+namespace smmd {
+
+namespace {
+
+constexpr int C1_T = 256;
+constexpr int C1_RC = 32;                   // reduction values per chunk
+constexpr int C1_AS = C1_RC + 4;            // [row][32] stage row stride: 16-byte rows
+constexpr int C1_BS = 64 + 4;               // B row stride (floats)
+constexpr int C1_ASTAGE = 64 * C1_AS;
+constexpr int C1_BSTAGE = C1_RC * C1_BS;
+constexpr int C1_STAGE = C1_ASTAGE + C1_BSTAGE;
+constexpr int C1_WS = 64 * C1_AS;           // wgrad stage per operand: 64 rows x 36
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// column j of an [N][rows][P] tensor: byte-free float offset of (row, j)
+__device__ __forceinline__ int64_t c1_off(int64_t j, int row, int rows, int P) {
+    const int64_t n = j / P;
+    const int64_t p = j - n * P;
+    return (n * rows + row) * (int64_t)P + p;
+}
+
+// forward / input gradient: Y [N][M][P] = A [M][R] . X [N][R][P] (+ bias[m])
+// Split-K: blockIdx.y = slice s of the reduction, chunks [s cps, (s + 1) cps)
+// of 32; with several slices Y is slab s of the workspace (bias NULL) and
+// c1_sum adds the slabs in order.
+__global__ __launch_bounds__(C1_T) void c1_gemm_kernel(const float *__restrict__ A,
+                                                       const float *__restrict__ X,
+                                                       const float *__restrict__ bias,
+                                                       float *__restrict__ Y, int M, int R, int P,
+                                                       int64_t J, int cps) {
+    __shared__ float lds[2 * C1_STAGE];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    // blocks: the row blocks of one column tile run on one XCD (its X
+    // columns, the large operand, read once into that L2)
+    const int mb_n = M / 64;
+    const int64_t jb_n = J / 64;
+    const int64_t blk = xcd_order(blockIdx.x, (int)(jb_n * mb_n));
+    const int mb = (int)(blk % mb_n);
+    const int64_t jb = blk / mb_n;
+    const int m0 = mb * 64;
+    const int64_t j0 = jb * 64;
+
+    // global -> register loads of one chunk: A 64 x 32 (2 float4 / thread,
+    // thread -> (row f / 8, quad f % 8)), X 32 x 64 (2 float4 / thread,
+    // thread -> (row f / 16, quad f % 16)); the thread's element offsets at
+    // chunk 0 (chunk c adds 32 c to A's and 32 c P to X's): the (n, p) split
+    // of its columns is done once.
+    const int f0 = tid, f1 = tid + C1_T;
+    const int rbeg = blockIdx.y * cps * C1_RC;
+    const int nchunk = min(cps, R / C1_RC - (int)blockIdx.y * cps);
+    const float *pa0 = A + (int64_t)(m0 + (f0 >> 3)) * R + 4 * (f0 & 7) + rbeg;
+    const float *pa1 = A + (int64_t)(m0 + (f1 >> 3)) * R + 4 * (f1 & 7) + rbeg;
+    const float *px0 = X + c1_off(j0 + 4 * (f0 & 15), f0 >> 4, R, P) + (int64_t)rbeg * P;
+    const float *px1 = X + c1_off(j0 + 4 * (f1 & 15), f1 >> 4, R, P) + (int64_t)rbeg * P;
+    float *const sa0 = lds + (f0 >> 3) * C1_AS + 4 * (f0 & 7);
+    float *const sa1 = lds + (f1 >> 3) * C1_AS + 4 * (f1 & 7);
+    float *const sb0 = lds + C1_ASTAGE + (f0 >> 4) * C1_BS + 4 * (f0 & 15);
+    float *const sb1 = lds + C1_ASTAGE + (f1 >> 4) * C1_BS + 4 * (f1 & 15);
+    const int64_t xstep = (int64_t)C1_RC * P;
+    // One chunk in flight in registers: chunk c + 1's loads are issued before
+    // chunk c's MFMAs and stored to the other LDS stage after them; the load
+    // past the last chunk re-reads it (no branch: a conditional load made the
+    // compiler wait for every load in flight).  Macros over named registers:
+    // float4 arrays captured by lambdas went to scratch, whose stores waited
+    // for the loads at issue.  (Three chunks in flight measured 2-8 % slower,
+    // profiles/r14/conv1x1_variants.txt.)
+    float4 g0a0, g0a1, g0b0, g0b1;
+#define C1_GLOAD(g, c)                                                         \
+    {                                                                          \
+        const int cc_ = min((c), nchunk - 1);                                  \
+        g##a0 = *reinterpret_cast<const float4 *>(pa0 + C1_RC * cc_);          \
+        g##a1 = *reinterpret_cast<const float4 *>(pa1 + C1_RC * cc_);          \
+        g##b0 = *reinterpret_cast<const float4 *>(px0 + xstep * cc_);          \
+        g##b1 = *reinterpret_cast<const float4 *>(px1 + xstep * cc_);          \
+    }
+#define C1_LSTORE(g, buf)                                                      \
+    {                                                                          \
+        const int o_ = (buf) * C1_STAGE;                                       \
+        *reinterpret_cast<float4 *>(sa0 + o_) = g##a0;                         \
+        *reinterpret_cast<float4 *>(sa1 + o_) = g##a1;                         \
+        *reinterpret_cast<float4 *>(sb0 + o_) = g##b0;                         \
+        *reinterpret_cast<float4 *>(sb1 + o_) = g##b1;                         \
+    }
+
+    const int mh = w >> 1, jh = w & 1, h = lane >> 5, l32 = lane & 31;
+    // MFMA t (0..15) of a chunk reduces over r = t (lane half 0) and 16 + t
+    // (half 1): a lane's A values are the contiguous run A[m][16 h .. 16 h +
+    // 15] (four 16-byte reads; rows 144 B apart hit distinct banks), its B
+    // values B[16 h + t][j] (ds_read2_b32 pairs).  All of a chunk's operand
+    // reads are issued before its MFMAs (one LDS latency per chunk, the MFMAs
+    // then wait on counted reads).
+    const int arow = (mh * 32 + l32) * C1_AS + 16 * h;
+    const int bcol = 16 * h * C1_BS + jh * 32 + l32;
+    f32x16 acc = f32x16{};
+#define C1_CHUNK(buf)                                                          \
+    {                                                                          \
+        const float *As_ = lds + (buf) * C1_STAGE;                             \
+        const float *Bs_ = As_ + C1_ASTAGE;                                    \
+        float4 a4_[4];                                                         \
+        float bv_[16];                                                         \
+        _Pragma("unroll") for (int q = 0; q < 4; ++q) a4_[q] =                 \
+            *reinterpret_cast<const float4 *>(As_ + arow + 4 * q);             \
+        _Pragma("unroll") for (int t = 0; t < 16; ++t) bv_[t] = Bs_[bcol + t * C1_BS]; \
+        __builtin_amdgcn_sched_barrier(0);                                     \
+        _Pragma("unroll") for (int q = 0; q < 4; ++q) {                        \
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4_[q].x, bv_[4 * q], acc, 0, 0, 0);     \
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4_[q].y, bv_[4 * q + 1], acc, 0, 0, 0); \
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4_[q].z, bv_[4 * q + 2], acc, 0, 0, 0); \
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4_[q].w, bv_[4 * q + 3], acc, 0, 0, 0); \
+        }                                                                      \
+        __builtin_amdgcn_sched_barrier(0);                                     \
+    }
+    Y += (int64_t)blockIdx.y * J * M;
+    C1_GLOAD(g0, 0);
+    C1_LSTORE(g0, 0);
+    __syncthreads();
+    int c = 0;
+    do {
+        C1_GLOAD(g0, c + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        C1_CHUNK(c & 1);
+        if (c + 1 < nchunk) {
+            C1_LSTORE(g0, (c + 1) & 1);
+            __syncthreads();
+        }
+        ++c;
+    } while (c < nchunk);
+#undef C1_CHUNK
+#undef C1_LSTORE
+#undef C1_GLOAD
+    // epilogue: lane (h, l32) holds rows (r & 3) + 8 (r >> 2) + 4 h of column
+    // jh 32 + l32: per register one coalesced 128-byte row segment per half
+    const int64_t j = j0 + jh * 32 + l32;
+    const int64_t n = j / P, p = j - n * (int64_t)P;
+    float *yc = Y + n * (int64_t)M * P + p;
+    const int mr = m0 + mh * 32 + 4 * h;
+    if (bias) {
+        float bv[16];                           // all 16 loads in flight at once
+#pragma unroll
+        for (int r = 0; r < 16; ++r) bv[r] = bias[mr + (r & 3) + 8 * (r >> 2)];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) yc[(int64_t)(mr + (r & 3) + 8 * (r >> 2)) * P] = acc[r] + bv[r];
+    } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) yc[(int64_t)(mr + (r & 3) + 8 * (r >> 2)) * P] = acc[r];
+    }
+}
+
+// weight gradient partial of slice blockIdx.y: part[s][K][C] over columns
+// [s * cps, (s + 1) * cps) of gy [N][K][P] and x [N][C][P]
+__global__ __launch_bounds__(C1_T) void c1_wgrad_kernel(const float *__restrict__ gy,
+                                                        const float *__restrict__ x,
+                                                        float *__restrict__ part, int K, int C,
+                                                        int P, int64_t J, int64_t cps) {
+    __shared__ float lds[2 * 2 * C1_WS];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int cb_n = C / 64;
+    const int kb = blockIdx.x / cb_n, cb = blockIdx.x - kb * cb_n;
+    const int s = blockIdx.y;
+    const int64_t jbeg = (int64_t)s * cps;
+    const int64_t jend = min(J, jbeg + cps);
+    const int k0 = kb * 64, c0 = cb * 64;
+    // chunk loads: 64 rows x 32 columns per operand = 512 float4, thread ->
+    // (row f / 8, quad f % 8); the thread's column (n, p) of the next chunk to
+    // load advances by one chunk per load ((dn, dp) = the chunk's 32 columns
+    // split over images once, no division per chunk) and stays on the last
+    // chunk.  One chunk in flight in registers, as c1_gemm.
+    const int q4 = 4 * (tid & 7);
+    int cn = (int)((jbeg + q4) / P), cp = (int)((jbeg + q4) - (int64_t)cn * P);
+    const int dn = C1_RC / P, dp = C1_RC - (C1_RC / P) * P;
+    const int64_t gplane = (int64_t)K * P, xplane = (int64_t)C * P;
+    const int row0 = tid >> 3, row1 = (tid + C1_T) >> 3;
+    const float *gy0 = gy + (int64_t)(k0 + row0) * P, *gy1 = gy + (int64_t)(k0 + row1) * P;
+    const float *x0 = x + (int64_t)(c0 + row0) * P, *x1 = x + (int64_t)(c0 + row1) * P;
+    float *const sa0 = lds + row0 * C1_AS + q4, *const sa1 = lds + row1 * C1_AS + q4;
+    const int nchunk = (int)((jend - jbeg) / C1_RC);
+    int nload = 0;                              // chunks whose loads are issued
+    float4 g0a0, g0a1, g0b0, g0b1;
+#define C1_GLOAD(g)                                                            \
+    {                                                                          \
+        const int64_t go_ = cn * gplane + cp, xo_ = cn * xplane + cp;          \
+        g##a0 = *reinterpret_cast<const float4 *>(gy0 + go_);                  \
+        g##a1 = *reinterpret_cast<const float4 *>(gy1 + go_);                  \
+        g##b0 = *reinterpret_cast<const float4 *>(x0 + xo_);                   \
+        g##b1 = *reinterpret_cast<const float4 *>(x1 + xo_);                   \
+        if (++nload < nchunk) {                                                \
+            cp += dp;                                                          \
+            cn += dn;                                                          \
+            if (cp >= P) {                                                     \
+                cp -= P;                                                       \
+                ++cn;                                                          \
+            }                                                                  \
+        }                                                                      \
+    }
+#define C1_LSTORE(g, buf)                                                      \
+    {                                                                          \
+        const int o_ = (buf) * 2 * C1_WS;                                      \
+        *reinterpret_cast<float4 *>(sa0 + o_) = g##a0;                         \
+        *reinterpret_cast<float4 *>(sa1 + o_) = g##a1;                         \
+        *reinterpret_cast<float4 *>(sa0 + o_ + C1_WS) = g##b0;                 \
+        *reinterpret_cast<float4 *>(sa1 + o_ + C1_WS) = g##b1;                 \
+    }
+    const int kh = w >> 1, ch = w & 1, h = lane >> 5, l32 = lane & 31;
+    // MFMA t of a chunk reduces over columns t and 16 + t (lane halves): each
+    // lane's operands are contiguous 16-float runs of its gy and x rows, all
+    // 8 reads issued before the chunk's MFMAs
+    const int arow = (kh * 32 + l32) * C1_AS + 16 * h;
+    const int brow = (ch * 32 + l32) * C1_AS + 16 * h;
+    f32x16 acc = f32x16{};
+#define C1_CHUNK(buf)                                                          \
+    {                                                                          \
+        const float *As_ = lds + (buf) * 2 * C1_WS;                            \
+        const float *Bs_ = As_ + C1_WS;                                        \
+        float4 a4_[4], b4_[4];                                                 \
+        _Pragma("unroll") for (int q = 0; q < 4; ++q) {                        \
+            a4_[q] = *reinterpret_cast<const float4 *>(As_ + arow + 4 * q);    \
+            b4_[q] = *reinterpret_cast<const float4 *>(Bs_ + brow + 4 * q);    \
+        }                                                                      \
+        __builtin_amdgcn_sched_barrier(0);                                     \
+        _Pragma("unroll") for (int q = 0; q < 4; ++q) {                        \
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4_[q].x, b4_[q].x, acc, 0, 0, 0); \
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4_[q].y, b4_[q].y, acc, 0, 0, 0); \
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4_[q].z, b4_[q].z, acc, 0, 0, 0); \
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4_[q].w, b4_[q].w, acc, 0, 0, 0); \
+        }                                                                      \
+        __builtin_amdgcn_sched_barrier(0);                                     \
+    }
+    if (nchunk > 0) {
+        C1_GLOAD(g0);
+        C1_LSTORE(g0, 0);
+        __syncthreads();
+        int c = 0;
+        do {
+            C1_GLOAD(g0);
+            __builtin_amdgcn_sched_barrier(0);
+            C1_CHUNK(c & 1);
+            if (c + 1 < nchunk) {
+                C1_LSTORE(g0, (c + 1) & 1);
+                __syncthreads();
+            }
+            ++c;
+        } while (c < nchunk);
+    }
+#undef C1_CHUNK
+#undef C1_LSTORE
+#undef C1_GLOAD
+    float *o = part + (int64_t)s * K * C;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int k = k0 + kh * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        o[(int64_t)k * C + c0 + ch * 32 + l32] = acc[r];
+    }
+}
+
+// out[i] = sum over slabs [g G, min(S, g G + G)) of n4 float4 each for group
+// g = blockIdx.y, in slab order (+ bias[(i / (rowlen / 4)) % nb] when bias):
+// the first level of a two-level fixed-order slab sum (G slabs per group;
+// one group: the whole sum), 8 loads in flight per thread
+__global__ void c1_sum_kernel(const float4 *__restrict__ part, int S, int G, int64_t n4,
+                              float4 *__restrict__ out, const float *__restrict__ bias,
+                              int rowlen, int nb) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n4) return;
+    const int s0 = blockIdx.y * G, s1 = min(S, s0 + G);
+    float4 a = part[(int64_t)s0 * n4 + i];
+    for (int b = s0 + 1; b < s1; b += 8) {
+        float4 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            v[j] = (b + j < s1) ? part[(int64_t)(b + j) * n4 + i] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if (b + j < s1) {
+                a.x += v[j].x; a.y += v[j].y; a.z += v[j].z; a.w += v[j].w;
+            }
+        }
+    }
+    if (bias) {
+        const float bb = bias[(int)((i * 4 / rowlen) % nb)];
+        a.x += bb; a.y += bb; a.z += bb; a.w += bb;
+    }
+    out[(int64_t)blockIdx.y * n4 + i] = a;
+}
+
+constexpr int C1_GROUP = 16;
+int c1_groups(int S) { return S > 2 * C1_GROUP ? (S + C1_GROUP - 1) / C1_GROUP : 0; }
+
+// Reduction slices so that tiles x slices fills ~C1_TARGET workgroups (4 per
+// CU: the kernel hides its latencies by occupancy), at least min_chunks
+// chunks each: 16 for c1_gemm (a launch without the slab sum beat two slices
+// + c1_sum at 16 chunks), 8 for c1_wgrad (profiles/r14/conv1x1_variants.txt)
+#ifndef C1_TARGET
+#define C1_TARGET 1024
+#endif
+#ifndef C1_MINCH_GEMM
+#define C1_MINCH_GEMM 16
+#endif
+#ifndef C1_MINCH_WGRAD
+#define C1_MINCH_WGRAD 8
+#endif
+int c1_slices(int tiles, int64_t nchunk, int min_chunks) {
+    int64_t S = (C1_TARGET + tiles - 1) / tiles;
+    S = min(S, max((int64_t)1, nchunk / min_chunks));
+    return (int)max((int64_t)1, S);
+}
+
+// the slab sum of S slabs of n floats (in order; two levels above 2 G slabs)
+// into out; gbuf holds the groups (c1_groups(S) slabs)
+smmd_status c1_reduce(const float *part, int S, int64_t n, float *gbuf, float *out,
+                      const float *bias, int rowlen, int nb, hipStream_t st) {
+    const int64_t n4 = n / 4;
+    const unsigned gx = (unsigned)((n4 + 255) / 256);
+    const int ng = c1_groups(S);
+    if (ng > 0) {
+        c1_sum_kernel<<<dim3(gx, (unsigned)ng), dim3(256), 0, st>>>(
+            reinterpret_cast<const float4 *>(part), S, C1_GROUP, n4,
+            reinterpret_cast<float4 *>(gbuf), nullptr, 1, 1);
+        const smmd_status e = last_launch_status();
+        if (e != SMMD_OK) return e;
+        part = gbuf;
+        S = ng;
+    }
+    c1_sum_kernel<<<dim3(gx, 1), dim3(256), 0, st>>>(reinterpret_cast<const float4 *>(part), S, S,
+                                                     n4, reinterpret_cast<float4 *>(out), bias,
+                                                     rowlen, nb);
+    return last_launch_status();
+}
+
+bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace
+
+}  // namespace smmd
+
+using namespace smmd;
+
+extern "C" int smmd_conv1x1_supported(int n, int r, int m, int p) {
+    // r: the reduction channels, m: the output channels, p: pixels per image
+    const int64_t J = (int64_t)n * p;
+    return n > 0 && r > 0 && m > 0 && p > 0 && m % 64 == 0 && r % C1_RC == 0 && p % 4 == 0 &&
+           J % 64 == 0 && (int64_t)n * (r > m ? r : m) * p < (1ll << 40);
+}
+
+namespace {
+int c1_gemm_slices(int n, int r, int m, int p) {
+    const int64_t J = (int64_t)n * p;
+    const int64_t tiles = (J / 64) * (m / 64);
+    return tiles >= C1_TARGET ? 1 : c1_slices((int)tiles, r / C1_RC, C1_MINCH_GEMM);
+}
+}  // namespace
+
+extern "C" size_t smmd_conv1x1_workspace_bytes(int n, int r, int m, int p) {
+    if (!smmd_conv1x1_supported(n, r, m, p)) return 0;
+    const int S = c1_gemm_slices(n, r, m, p);
+    if (S == 1) return 0;
+    return (size_t)(S + c1_groups(S)) * n * m * p * sizeof(float);
+}
+
+extern "C" smmd_status smmd_conv1x1(const float *a, const float *x, const float *bias, float *y,
+                                    int n, int r, int m, int p, void *ws, size_t ws_bytes,
+                                    smmd_stream_t stream) {
+    if (!a || !x || !y) return SMMD_EINVAL;
+    if (!smmd_conv1x1_supported(n, r, m, p)) return SMMD_EUNSUPPORTED;
+    if (!aligned16(a) || !aligned16(x) || !aligned16(y)) return SMMD_EINVAL;
+    const int64_t J = (int64_t)n * p;
+    const int64_t blocks = (J / 64) * (m / 64);
+    if (blocks > 0x7fffffff) return SMMD_EUNSUPPORTED;
+    const int S = c1_gemm_slices(n, r, m, p);
+    const size_t need = smmd_conv1x1_workspace_bytes(n, r, m, p);
+    if (need && (!ws || ws_bytes < need || !aligned16(ws))) return SMMD_EWORKSPACE;
+    const int nch = r / C1_RC;
+    const int cps = (nch + S - 1) / S;
+    const int Sused = (nch + cps - 1) / cps;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    float *part = Sused > 1 ? static_cast<float *>(ws) : y;
+    c1_gemm_kernel<<<dim3((unsigned)blocks, (unsigned)Sused), dim3(C1_T), 0, st>>>(
+        a, x, Sused > 1 ? nullptr : bias, part, m, r, p, J, cps);
+    smmd_status e = last_launch_status();
+    if (e != SMMD_OK || Sused == 1) return e;
+    const int64_t total = J * m;
+    return c1_reduce(part, Sused, total, part + (size_t)Sused * total, y, bias, p, m, st);
+}
+
+extern "C" int smmd_conv1x1_wgrad_supported(int n, int c, int k, int p) {
+    const int64_t J = (int64_t)n * p;
+    return n > 0 && c > 0 && k > 0 && p > 0 && c % 64 == 0 && k % 64 == 0 && p % 4 == 0 &&
+           J % C1_RC == 0 && (int64_t)n * (c > k ? c : k) * p < (1ll << 40);
+}
+
+extern "C" size_t smmd_conv1x1_wgrad_workspace_bytes(int n, int c, int k, int p) {
+    if (!smmd_conv1x1_wgrad_supported(n, c, k, p)) return 0;
+    const int S = c1_slices((k / 64) * (c / 64), (int64_t)n * p / C1_RC, C1_MINCH_WGRAD);
+    return S > 1 ? (size_t)(S + c1_groups(S)) * k * c * sizeof(float) : 0;
+}
+
+extern "C" smmd_status smmd_conv1x1_wgrad(const float *gy, const float *x, float *gw, int n,
+                                          int c, int k, int p, void *ws, size_t ws_bytes,
+                                          smmd_stream_t stream) {
+    if (!gy || !x || !gw) return SMMD_EINVAL;
+    if (!smmd_conv1x1_wgrad_supported(n, c, k, p)) return SMMD_EUNSUPPORTED;
+    if (!aligned16(gy) || !aligned16(x) || !aligned16(gw)) return SMMD_EINVAL;
+    const int64_t J = (int64_t)n * p;
+    const int tiles = (k / 64) * (c / 64);
+    const int64_t nch = J / C1_RC;
+    const int S = c1_slices(tiles, nch, C1_MINCH_WGRAD);
+    const size_t need = smmd_conv1x1_wgrad_workspace_bytes(n, c, k, p);
+    if (need && (!ws || ws_bytes < need || !aligned16(ws))) return SMMD_EWORKSPACE;
+    // columns per slice: whole chunks
+    const int64_t cps = ((nch + S - 1) / S) * C1_RC;
+    const int Sused = (int)((J + cps - 1) / cps);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    float *part = Sused > 1 ? static_cast<float *>(ws) : gw;
+    c1_wgrad_kernel<<<dim3((unsigned)tiles, (unsigned)Sused), dim3(C1_T), 0, st>>>(
+        gy, x, part, k, c, p, J, cps);
+    smmd_status e = last_launch_status();
+    if (e != SMMD_OK || Sused == 1) return e;
+    const int64_t total = (int64_t)k * c;
+    return c1_reduce(part, Sused, total, part + (size_t)Sused * total, gw, nullptr, 1, 1, st);
+}

@@ -153,9 +153,113 @@ __global__ __launch_bounds__(FOLD_T) void fold_adj_kernel(FoldTable t) {
     store9(t.dst[l] + f0 * 9, s9, nb * 9);
 }
 
+// ---- UpsampleConv fold (block.py:53-60) -------------------------------------
+// K [cin][cout][s][t] = 4 W'[cout][cin][3-s][3-t] with W' = fold(W): the
+// transposed 4x4 stride-2 conv equal to conv3x3(upsample_nearest2(x), W)
+// (convops.fold_up_weight).  4 * (1/4 * sum) is the plain sum (exact), so a
+// K value is the fold's sum in its (a, b) order.  Thread per source filter
+// (cout, cin) of the block's 256: its 9 floats staged through LDS (coalesced
+// float4), its 16 outputs one 64-byte line of K written by four float4
+// stores (the line's filter is (cin, cout): lanes stride cout * 64 B, each a
+// whole line).  The adjoint reads that line back and sums the 2 x 2 windows
+// of the un-flipped G'[s][t] = gK[3-s][3-t]: gW[u][v] = sum_{a,b} G'[u+a][v+b].
+__global__ __launch_bounds__(FOLD_T) void fold_up_kernel(const float *__restrict__ w,
+                                                         float *__restrict__ k, int cout, int cin) {
+    __shared__ float s9[FOLD_T * 9];
+    const int64_t nf = (int64_t)cout * cin;
+    const int64_t f0 = (int64_t)blockIdx.x * FOLD_T;
+    const int nb = (int)min<int64_t>(FOLD_T, nf - f0);
+    load9(w + f0 * 9, s9, nb * 9);
+    __syncthreads();
+    const int f = threadIdx.x;
+    if (f >= nb) return;
+    const int64_t q = f0 + f;
+    const int co = (int)(q / cin), ci = (int)(q - (int64_t)co * cin);
+    float kk[9], o[16];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) kk[j] = s9[f * 9 + j];
+#pragma unroll
+    for (int si = 0; si < 4; ++si) {
+#pragma unroll
+        for (int ti = 0; ti < 4; ++ti) {
+            float acc = 0.f;
+#pragma unroll
+            for (int a = 0; a < 2; ++a) {
+#pragma unroll
+                for (int b = 0; b < 2; ++b) {
+                    const int u = si - a, v = ti - b;
+                    if (u >= 0 && u < 3 && v >= 0 && v < 3) acc += kk[u * 3 + v];
+                }
+            }
+            o[15 - (si * 4 + ti)] = acc;               // flipped in both axes
+        }
+    }
+    float4 *d4 = reinterpret_cast<float4 *>(k + ((int64_t)ci * cout + co) * 16);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) d4[i] = make_float4(o[4 * i], o[4 * i + 1], o[4 * i + 2], o[4 * i + 3]);
+}
+
+__global__ __launch_bounds__(FOLD_T) void fold_up_adj_kernel(const float *__restrict__ gk,
+                                                             float *__restrict__ gw, int cout,
+                                                             int cin) {
+    __shared__ float s9[FOLD_T * 9];
+    const int64_t nf = (int64_t)cout * cin;
+    const int64_t f0 = (int64_t)blockIdx.x * FOLD_T;
+    const int nb = (int)min<int64_t>(FOLD_T, nf - f0);
+    const int f = threadIdx.x;
+    if (f < nb) {
+        const int64_t q = f0 + f;
+        const int co = (int)(q / cin), ci = (int)(q - (int64_t)co * cin);
+        const float4 *s4 = reinterpret_cast<const float4 *>(gk + ((int64_t)ci * cout + co) * 16);
+        float g[16];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float4 x = s4[i];
+            // G'[j] = gK[15 - j]
+            g[15 - 4 * i] = x.x;
+            g[14 - 4 * i] = x.y;
+            g[13 - 4 * i] = x.z;
+            g[12 - 4 * i] = x.w;
+        }
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+#pragma unroll
+            for (int v = 0; v < 3; ++v) {
+                float acc = 0.f;
+#pragma unroll
+                for (int a = 0; a < 2; ++a) {
+#pragma unroll
+                    for (int b = 0; b < 2; ++b) acc += g[(u + a) * 4 + (v + b)];
+                }
+                s9[f * 9 + u * 3 + v] = acc;
+            }
+        }
+    }
+    __syncthreads();
+    store9(gw + f0 * 9, s9, nb * 9);
+}
+
 }  // namespace smmd
 
 using namespace smmd;
+
+extern "C" smmd_status smmd_fold_up_weight(const float *src, float *dst, int cout, int cin,
+                                           int adjoint, smmd_stream_t stream) {
+    if (cout < 0 || cin < 0) return SMMD_EINVAL;
+    const int64_t nf = (int64_t)cout * cin;
+    if (nf == 0) return SMMD_OK;
+    if (!src || !dst) return SMMD_EINVAL;
+    if (((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) != 0)
+        return SMMD_EINVAL;
+    const int64_t blocks = (nf + FOLD_T - 1) / FOLD_T;
+    if (blocks > 0x7fffffff) return SMMD_EINVAL;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (adjoint)
+        fold_up_adj_kernel<<<dim3((unsigned)blocks), dim3(FOLD_T), 0, s>>>(src, dst, cout, cin);
+    else
+        fold_up_kernel<<<dim3((unsigned)blocks), dim3(FOLD_T), 0, s>>>(src, dst, cout, cin);
+    return last_launch_status();
+}
 
 extern "C" smmd_status smmd_fold_pool_weights(const float *const *src, float *const *dst,
                                               const int64_t *n_filters, int n_layers,

@@ -632,6 +632,87 @@ def conv_transpose_s2(x, w, b=None):
     return F.conv_transpose2d(x, w, b, stride=2, padding=1)
 
 
+# SMMD_CONV1X1=0: the 1x1 shortcut convolutions on MIOpen
+CONV1X1 = os.environ.get('SMMD_CONV1X1', '1') != '0'
+
+
+def _is_c1(x, w, stride, padding):
+    """A 1x1 stride-1 unpadded conv on an NCHW fp32 contiguous device tensor
+    (the residual shortcuts, block.py:28-40): `smmd_conv1x1*`."""
+    return (CONV1X1 and w.dim() == 4 and tuple(w.shape[2:]) == (1, 1)
+            and list(stride) == [1, 1] and list(padding) == [0, 0] and x.is_cuda
+            and x.dtype == torch.float32 and w.dtype == torch.float32 and x.dim() == 4
+            and x.is_contiguous() and x.shape[1] == w.shape[1] and x.data_ptr() % 16 == 0)
+
+
+def _c1_gemm(a, x, b, m):
+    """y [N, m, H, W] = a [m, r] . x [N, r, H, W] (+ b) on smmd_conv1x1, or
+    None when the library does not tile the shape."""
+    from . import _lib
+    N, r, H, W = x.shape
+    P = H * W
+    L = _lib.lib()
+    if not L.smmd_conv1x1_supported(N, r, m, P) or a.data_ptr() % 16:
+        return None
+    y = torch.empty((N, m, H, W), dtype=x.dtype, device=x.device)
+    if b is not None:
+        b = b.contiguous()
+    nb = L.smmd_conv1x1_workspace_bytes(N, r, m, P)
+    ws = _lib.workspace('conv1x1', nb, x.device) if nb else None
+    _lib.add_bytes('smmd_conv1x1', (x.numel() + y.numel() + a.numel()) * 4)
+    _lib.add_flops('smmd_conv1x1', 2 * N * P * r * m)
+    with _lib.timed('smmd_conv1x1'):
+        st = L.smmd_conv1x1(_lib.ptr(a), _lib.ptr(x), _lib.ptr(b), _lib.ptr(y), N, r, m, P,
+                            _lib.ptr(ws), nb, _lib.stream_handle(x.device))
+    _lib.check(st, 'smmd_conv1x1')
+    return y
+
+
+def _c1_fwd(x, w, b):
+    w = materialize(w)
+    return _c1_gemm(w.reshape(w.shape[0], w.shape[1]).contiguous(), x, b, w.shape[0])
+
+
+def _c1_wt(w):
+    """W^T [cin, cout] of a 1x1 weight, cached like the filter transforms (a
+    critic step takes several input gradients of each shortcut)."""
+    capturing = torch.cuda.is_current_stream_capturing()
+    key = (id(w), 'c1t')
+    if not capturing:
+        u = _cache_get(key, w)
+        if u is not None:
+            return u
+    u = materialize(w).reshape(w.shape[0], w.shape[1]).t().contiguous()
+    if not capturing:
+        _cache_put(key, w, u)
+    return u
+
+
+def _c1_dx(gy, w):
+    return _c1_gemm(_c1_wt(w), gy, None, w.shape[1])
+
+
+def _c1_wgrad(gy, x):
+    from . import _lib
+    N, C, H, W = x.shape
+    K = gy.shape[1]
+    P = H * W
+    L = _lib.lib()
+    if (not L.smmd_conv1x1_wgrad_supported(N, C, K, P) or gy.data_ptr() % 16
+            or not gy.is_contiguous()):
+        return None
+    gw = torch.empty((K, C, 1, 1), dtype=x.dtype, device=x.device)
+    nb = L.smmd_conv1x1_wgrad_workspace_bytes(N, C, K, P)
+    ws = _lib.workspace('conv1x1_wgrad', nb, x.device) if nb else None
+    _lib.add_bytes('smmd_conv1x1_wgrad', (x.numel() + gy.numel() + gw.numel()) * 4)
+    _lib.add_flops('smmd_conv1x1_wgrad', 2 * N * P * C * K)
+    with _lib.timed('smmd_conv1x1_wgrad'):
+        st = L.smmd_conv1x1_wgrad(_lib.ptr(gy), _lib.ptr(x), _lib.ptr(gw), N, C, K, P,
+                                  _lib.ptr(ws), nb, _lib.stream_handle(x.device))
+    _lib.check(st, 'smmd_conv1x1_wgrad')
+    return gw
+
+
 def _is_thin(x, w, stride, padding):
     return thin_applicable(x, w.shape[1], w.shape[0], w.shape[2], stride, padding) \
         and w.shape[2] == w.shape[3]
@@ -645,6 +726,10 @@ def _fwd(x, w, b, stride, padding):
         return _wino_conv(x, w, b, 0)
     if _is_s2(x, w, stride, padding):
         return _s2_conv(x, w, b)
+    if _is_c1(x, w, stride, padding):
+        y = _c1_fwd(x, w, b)
+        if y is not None:
+            return y
     return F.conv2d(x, materialize(w), b, stride, padding)
 
 
@@ -673,6 +758,11 @@ def _bwd(gy, x, w, stride, padding, mask):
         gx = _thin_conv(gy, w, None, 1) if mask[0] else None
         gw = _thin_wgrad(gy, x) if mask[1] else None
         return gx, gw
+    if _is_c1(x, w, stride, padding) and _is_c1(gy, w.transpose(0, 1), stride, padding):
+        gx = _c1_dx(gy, w) if mask[0] else None
+        gw = _c1_wgrad(gy, x) if mask[1] else None
+        if (gx is not None or not mask[0]) and (gw is not None or not mask[1]):
+            return gx, gw
     if mask[1] and _wgrad_ok(x, gy, w, stride, padding):
         gw = _wino_wgrad(x, gy)
         gx = None
@@ -1001,8 +1091,54 @@ def fold_up_weight(w):
     per axis the two output phases see taps (W0, W1 + W2) and (W0 + W1, W2) of
     x, i.e. K = flip([W0, W0 + W1, W1 + W2, W2]) = flip(4 fold_pool_weight(W))
     (UpsampleConv, gan/core/resnet/block.py:53-60, without the 4x larger
-    upsampled input; linear, so differentiable to any order)."""
+    upsampled input; linear, so differentiable to any order).  Device tensors
+    run `smmd_fold_up_weight` (one launch each way, K contiguous; the torch
+    form was pad, avg_pool2d, scale, flip and a transposing copy, and its
+    backward's avg_pool2d_backward alone took 127 us on the 1024 -> 512
+    layer); host tensors the torch ops."""
+    if w.is_cuda and w.dim() == 4 and tuple(w.shape[2:]) == (3, 3) and w.dtype == torch.float32:
+        return _FoldUp.apply(w)
     return torch.flip(_fold_torch(w) * 4.0, (2, 3)).transpose(0, 1)
+
+
+def _fold_up_launch(src, adjoint):
+    from . import _lib
+    src = src.contiguous()
+    if adjoint:                       # gK [cin, cout, 4, 4] -> gW [cout, cin, 3, 3]
+        cin, cout = src.shape[0], src.shape[1]
+        dst = torch.empty(cout, cin, 3, 3, device=src.device, dtype=src.dtype)
+    else:                             # W [cout, cin, 3, 3] -> K [cin, cout, 4, 4]
+        cout, cin = src.shape[0], src.shape[1]
+        dst = torch.empty(cin, cout, 4, 4, device=src.device, dtype=src.dtype)
+    _lib.add_bytes('smmd_fold_up_weight', 25 * cout * cin * 4)
+    with _lib.timed('smmd_fold_up_weight'):
+        st = _lib.lib().smmd_fold_up_weight(_lib.ptr(src), _lib.ptr(dst), cout, cin,
+                                            int(adjoint), _lib.stream_handle(src.device))
+    _lib.check(st, 'smmd_fold_up_weight')
+    return dst
+
+
+class _FoldUp(torch.autograd.Function):
+    """fold_up_weight on the library; its backward is the adjoint launch,
+    whose backward is this forward again (the map is linear)."""
+
+    @staticmethod
+    def forward(ctx, w):
+        return _fold_up_launch(materialize(w), False)
+
+    @staticmethod
+    def backward(ctx, gk):
+        return _FoldUpAdj.apply(gk)
+
+
+class _FoldUpAdj(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gk):
+        return _fold_up_launch(gk, True)
+
+    @staticmethod
+    def backward(ctx, ggw):
+        return _FoldUp.apply(ggw)
 
 
 def mean_pool2(x):

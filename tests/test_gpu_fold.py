@@ -240,3 +240,34 @@ def test_upsample_fold_two_backwards_without_step():
     for _ in range(2):
         up(z).square().sum().backward()
     assert up.conv.weight.grad is not None and torch.isfinite(up.conv.weight.grad).all()
+
+
+@pytest.mark.parametrize('shape', SHAPES + [(512, 1024)])
+def test_fold_up_weight_and_adjoint_match_oracle(shape):
+    """UpsampleConv fold on the library (`smmd_fold_up_weight`, ABI 11): K =
+    flip(4 fold(W)) transposed against the float64 oracle's fold, its adjoint
+    against the transpose of that linear map, and the double backward (the
+    adjoint's backward is the fold again)."""
+    from gan.core.convops import fold_up_weight
+    co, ci = shape
+    rng = np.random.default_rng(co * 7 + ci)
+    W = rng.standard_normal((co, ci, 3, 3)).astype(np.float32)
+    G = rng.standard_normal((ci, co, 4, 4)).astype(np.float32)
+    dev = torch.device('cuda:0')
+    w = torch.tensor(W, device=dev, requires_grad=True)
+    k = fold_up_weight(w)
+    assert k.shape == (ci, co, 4, 4) and k.is_contiguous()
+    ref = np.flip(4.0 * O.fold_pool_weight(W.astype(np.float64)), (2, 3)).transpose(1, 0, 2, 3)
+    np.testing.assert_allclose(k.detach().cpu().numpy(), ref, rtol=1e-6, atol=1e-6)
+    g = torch.tensor(G, device=dev)
+    gw, = torch.autograd.grad(k, w, g, create_graph=True)
+    gref = 4.0 * O.fold_pool_weight_adjoint(np.flip(G.astype(np.float64), (2, 3))
+                                            .transpose(1, 0, 2, 3))
+    np.testing.assert_allclose(gw.detach().cpu().numpy(), gref, rtol=1e-6, atol=1e-6)
+    # second order: d/dG <gw, V> = fold_up(V) (the adjoint's backward)
+    v = torch.randn(co, ci, 3, 3, device=dev)
+    gt = g.clone().requires_grad_(True)
+    gw2, = torch.autograd.grad(fold_up_weight(w), w, gt, create_graph=True)
+    h, = torch.autograd.grad((gw2 * v).sum(), gt)
+    np.testing.assert_allclose(h.cpu().numpy(), fold_up_weight(v).cpu().numpy(), rtol=1e-6,
+                               atol=1e-6)

@@ -1,7 +1,8 @@
 """The critic's 1x1 shortcut convolutions (MeanPoolConv: the 1x1 conv on the
 pooled block input, gan/core/resnet/block.py:28-40) at bench.py's shapes:
 MIOpen (F.conv2d / convolution_backward, what the step runs) against GEMM
-forms on NCHW without transposes (torch.matmul -> hipBLASLt batched GEMMs).
+forms on NCHW without transposes (torch.matmul -> hipBLASLt batched GEMMs)
+and the library's smmd_conv1x1* (lib_*).
 
     python tools/conv1x1_bench.py [--iters 50]
 """
@@ -61,12 +62,20 @@ def main():
         row['mm_dx'] = timeit(lambda: torch.matmul(w2.t(), gy3), args.iters)
         row['bmm_dw_sum'] = timeit(lambda: torch.bmm(gy3, x3.transpose(1, 2)).sum(0), args.iters)
         row['einsum_dw'] = timeit(lambda: torch.einsum('nkp,ncp->kc', gy3, x3), args.iters)
+        from gan.core import convops
+        row['lib_fwd'] = timeit(lambda: convops._c1_fwd(x, w, None), args.iters)
+        row['lib_dx'] = timeit(lambda: convops._c1_dx(gy, w), args.iters)
+        row['lib_dw'] = timeit(lambda: convops._c1_wgrad(gy, x), args.iters)
         y0 = F.conv2d(x, w)
         y1 = torch.matmul(w2, x3).view_as(y0)
         d0 = aten.convolution_backward(gy, x, w, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
                                        [False, True, False])[1].view(k, c)
         d1 = torch.einsum('nkp,ncp->kc', gy3, x3)
         row['fwd_maxdiff'] = float((y0 - y1).abs().max() / y0.abs().max())
+        row['lib_fwd_maxdiff'] = float((y0 - convops._c1_fwd(x, w, None)).abs().max()
+                                       / y0.abs().max())
+        row['lib_dw_maxdiff'] = float((d0 - convops._c1_wgrad(gy, x).view(k, c)).abs().max()
+                                      / d0.abs().max())
         row['dw_maxdiff'] = float((d0 - d1).abs().max() / d0.abs().max())
         row = {q: (round(v, 2) if 'diff' not in q else v) for q, v in row.items()}
         row['gflop'] = round(fl / 1e9, 3)
