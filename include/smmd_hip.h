@@ -69,7 +69,8 @@ int smmd_abi_version(void);         /* bumped on any ABI change (2: Gram/poly,
                                        smmd_wino3x3_filter_sn, smmd_wino4x4s2(t)_filter_sn,
                                        smmd_sn_clip_g, 10: smmd_wino3x3_conv2*,
                                        smmd_wino4x4s2_conv2*, 11: smmd_fold_up_weight,
-                                       smmd_conv1x1*) */
+                                       smmd_conv1x1*, 12: smmd_wino4x4s2t_conv_mask,
+                                       smmd_row_lrelu_sum, smmd_row_lrelu_bcast) */
 const char *smmd_source_hash(void); /* first 16 hex digits of the SHA-256 of the
                                        sources this binary was built from
                                        (csrc .hip and .hpp files in byte order,
@@ -514,6 +515,21 @@ smmd_status smmd_mask_pool2_adj(const float *a, const float *b, const float *m, 
 smmd_status smmd_up_add(const float *s, const float *bs, const float *h, const float *bh, int C,
                         int64_t planes, int H, int W, float *out, smmd_stream_t stream);
 
+/* The critic's tail, lrelu(h).sum(dim=(2, 3)) with h = a + b the last block's
+ * two paths (architecture.py:430-433; the reference's final lrelu and
+ * tf.reduce_sum): rows = N * C of hw pixels (hw % 4 == 0, 16-byte aligned).
+ * smmd_row_lrelu_sum: y[r] = sum_i lrelu(a + b) (b NULL: a alone); with mu
+ *   set, y[r] = sum_i (a + b) * s(mu + mv), s(h) = 1 for h > 0 else slope --
+ *   the adjoint of smmd_row_lrelu_bcast (the tail's double backward).
+ * smmd_row_lrelu_bcast: out[r][i] = h > 0 ? g[r] : g[r] * slope, h = mu + mv
+ *   (mv NULL: mu) -- the tail's backward, bit-identical to torch's expand +
+ *   leaky_relu_backward.  The row sums run in pixel order (not torch's). */
+smmd_status smmd_row_lrelu_sum(const float *a, const float *b, const float *mu, const float *mv,
+                               float *y, int64_t rows, int hw, float slope, smmd_stream_t stream);
+
+smmd_status smmd_row_lrelu_bcast(const float *g, const float *mu, const float *mv, float *out,
+                                 int64_t rows, int hw, float slope, smmd_stream_t stream);
+
 /* ---------------------------------------------------------------------------
  * Training-mode batch norm + ReLU when no gradient is taken (the generator's
  * forward in a critic step): tf.layers.batch_normalization(training=True,
@@ -684,6 +700,16 @@ smmd_status smmd_wino4x4s2_conv(const float *x, const float *u, const float *bia
 smmd_status smmd_wino4x4s2t_conv(const float *gy, const float *u, const float *bias, float *dx,
                                  int n, int k, int c, int hg, int wg, void *ws, size_t ws_bytes,
                                  smmd_stream_t stream);
+
+/* smmd_wino4x4s2t_conv followed by TF's ReLU gradient in the same launch:
+ * dx = (mask <= 0 ? 0 : conv_transpose2d(gy, W') + bias), mask [n, c, 2 hg,
+ * 2 wg] (16-byte aligned) the conv's input, a ReLU output whose producer then
+ * skips its own mask (convops._Conv2dReLU with consumer_masks; replaces
+ * threshold_backward(dx, mask, 0) after the input gradient of the critic's
+ * ConvMeanPool conv, gan/core/resnet/block.py:44-50, :63-66). */
+smmd_status smmd_wino4x4s2t_conv_mask(const float *gy, const float *u, const float *bias,
+                                      const float *mask, float *dx, int n, int k, int c, int hg,
+                                      int wg, void *ws, size_t ws_bytes, smmd_stream_t stream);
 
 /* the pair form of smmd_wino4x4s2_conv: y = conv(x, u) + conv(x2, u2) + bias
  * in one launch (as smmd_wino3x3_conv2). */

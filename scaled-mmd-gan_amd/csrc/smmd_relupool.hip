@@ -176,6 +176,54 @@ __global__ __launch_bounds__(RP_T) void up_add_kernel(const float *__restrict__ 
     *reinterpret_cast<float4 *>(out + o0 + W) = add4(u, h1);
 }
 
+// The critic's tail (architecture.py:430-433, _forward_chained): y[r] =
+// sum_i lrelu(a[r][i] + b[r][i]) over the hw pixels of each (n, c) row, and in
+// mask mode (mu set) the adjoint of the backward below: y[r] = sum_i (a + b)
+// * s(mu + mv) with s(h) = 1 for h > 0 else slope (leaky_relu_backward's
+// select).  One thread per row, float4 loads, the row summed in pixel order.
+__global__ __launch_bounds__(RP_T) void row_lrelu_sum_kernel(
+    const float *__restrict__ a, const float *__restrict__ b, const float *__restrict__ mu,
+    const float *__restrict__ mv, float *__restrict__ y, int64_t rows, int hw, float slope) {
+    const int64_t r = (int64_t)blockIdx.x * RP_T + threadIdx.x;
+    if (r >= rows) return;
+    const size_t o = (size_t)r * hw;
+    float acc = 0.f;
+    for (int i = 0; i < hw; i += 4) {
+        float4 t = *reinterpret_cast<const float4 *>(a + o + i);
+        if (b) t = add4(t, *reinterpret_cast<const float4 *>(b + o + i));
+        float tv[4] = {t.x, t.y, t.z, t.w};
+        if (mu) {
+            float4 h = *reinterpret_cast<const float4 *>(mu + o + i);
+            if (mv) h = add4(h, *reinterpret_cast<const float4 *>(mv + o + i));
+            const float hv[4] = {h.x, h.y, h.z, h.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc += hv[j] > 0.f ? tv[j] : tv[j] * slope;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc += tv[j] > 0.f ? tv[j] : tv[j] * slope;
+        }
+    }
+    y[r] = acc;
+}
+
+// the tail's backward: out[r][i] = g[r] * s(mu + mv) (the row sum's broadcast,
+// then leaky_relu_backward: h > 0 ? g : g * slope, bit-identical to them)
+__global__ __launch_bounds__(RP_T) void row_lrelu_bcast_kernel(
+    const float *__restrict__ g, const float *__restrict__ mu, const float *__restrict__ mv,
+    float *__restrict__ out, int64_t rows, int hw, float slope) {
+    const int64_t r = (int64_t)blockIdx.x * RP_T + threadIdx.x;
+    if (r >= rows) return;
+    const size_t o = (size_t)r * hw;
+    const float gv = g[r], gs = gv * slope;
+    for (int i = 0; i < hw; i += 4) {
+        float4 h = *reinterpret_cast<const float4 *>(mu + o + i);
+        if (mv) h = add4(h, *reinterpret_cast<const float4 *>(mv + o + i));
+        *reinterpret_cast<float4 *>(out + o + i) =
+            make_float4(h.x > 0.f ? gv : gs, h.y > 0.f ? gv : gs, h.z > 0.f ? gv : gs,
+                        h.w > 0.f ? gv : gs);
+    }
+}
+
 static bool rp_shape_ok(int64_t planes, int H, int W) {
     return planes >= 0 && H > 0 && W > 0 && (H % 2) == 0 && (W % 4) == 0;
 }
@@ -231,5 +279,31 @@ extern "C" smmd_status smmd_up_add(const float *s, const float *bs, const float 
     if (blocks > 0x7fffffff) return SMMD_EINVAL;
     hipLaunchKernelGGL(up_add_kernel, dim3((unsigned)blocks), dim3(RP_T), 0, (hipStream_t)stream,
                        s, bs, h, bh, C, patches, H, W, out);
+    return last_launch_status();
+}
+
+extern "C" smmd_status smmd_row_lrelu_sum(const float *a, const float *b, const float *mu,
+                                          const float *mv, float *y, int64_t rows, int hw,
+                                          float slope, smmd_stream_t stream) {
+    if (!a || !y || rows < 0 || hw <= 0 || hw % 4 != 0 || (mv && !mu)) return SMMD_EINVAL;
+    if (!al16(a) || !al16(b) || !al16(mu) || !al16(mv)) return SMMD_EINVAL;
+    if (rows == 0) return SMMD_OK;
+    const int64_t blocks = (rows + RP_T - 1) / RP_T;
+    if (blocks > 0x7fffffff) return SMMD_EINVAL;
+    hipLaunchKernelGGL(row_lrelu_sum_kernel, dim3((unsigned)blocks), dim3(RP_T), 0,
+                       (hipStream_t)stream, a, b, mu, mv, y, rows, hw, slope);
+    return last_launch_status();
+}
+
+extern "C" smmd_status smmd_row_lrelu_bcast(const float *g, const float *mu, const float *mv,
+                                            float *out, int64_t rows, int hw, float slope,
+                                            smmd_stream_t stream) {
+    if (!g || !mu || !out || rows < 0 || hw <= 0 || hw % 4 != 0) return SMMD_EINVAL;
+    if (!al16(mu) || !al16(mv) || !al16(out)) return SMMD_EINVAL;
+    if (rows == 0) return SMMD_OK;
+    const int64_t blocks = (rows + RP_T - 1) / RP_T;
+    if (blocks > 0x7fffffff) return SMMD_EINVAL;
+    hipLaunchKernelGGL(row_lrelu_bcast_kernel, dim3((unsigned)blocks), dim3(RP_T), 0,
+                       (hipStream_t)stream, g, mu, mv, out, rows, hw, slope);
     return last_launch_status();
 }

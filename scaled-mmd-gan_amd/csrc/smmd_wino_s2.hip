@@ -484,6 +484,9 @@ struct S2TGeom {
     int N, K, C, Hg, Wg, TW, Timg;  // gy [N, K, Hg, Wg]; dx [N, C, 2Hg, 2Wg]; tiles of a phase
     int64_t T, slab;
     int CB, S;                      // channel blocks (C / 64), K slices
+    // smmd_wino4x4s2t_conv_mask: dx = (mask <= 0 ? 0 : dx), mask of dx's shape
+    // (the conv's input, a ReLU output: its producer's mask applied here)
+    const float *mask;
 };
 
 // The block's work from its 1-D id, XCD-aware: blocks b and b + 8 share an
@@ -724,6 +727,25 @@ __device__ __forceinline__ void s2t_body(const float *__restrict__ gy, const flo
     const uint32_t o1 = o0 + (uint32_t)Wx * 8;            // output row + 2
     const uint32_t hw4 = (uint32_t)Hx * (uint32_t)Wx * 4;
     const __amdgpu_buffer_rsrc_t ds = s2_rsrc(dx);
+    // the mask's 64 values of the lane, all loaded before the first store (the
+    // stage's registers are free here): one latency per block instead of one
+    // per output row pair
+    float mk[16][4];
+    const bool masked = g.mask != nullptr;
+    if (masked) {
+        const __amdgpu_buffer_rsrc_t ms = s2_rsrc(g.mask);
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const uint32_t so = (uint32_t)((r & 3) + 8 * (r >> 2) + h) * hw4;
+                mk[r + h][0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ms, o0, so, 0));
+                mk[r + h][1] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ms, o0 + 8, so, 0));
+                mk[r + h][2] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ms, o1, so, 0));
+                mk[r + h][3] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ms, o1 + 8, so, 0));
+            }
+        }
+    }
 #ifdef S2_NO_EPI
     for (int r = 0; r < 2; r += 2) {
 #else
@@ -743,11 +765,17 @@ __device__ __forceinline__ void s2t_body(const float *__restrict__ gy, const flo
                 s1[j] = m[3 + j] + m[6 + j];
             }
             const float b = Bs[cl0 + cr + h];
+            float v[4] = {s0[0] + s0[1] + b, s0[1] + s0[2] + b, s1[0] + s1[1] + b,
+                          s1[1] + s1[2] + b};
+            if (masked) {               // threshold_backward(v, mask, 0)'s select
+#pragma unroll
+                for (int i = 0; i < 4; ++i) v[i] = mk[r + h][i] <= 0.f ? 0.f : v[i];
+            }
             const uint32_t so = (uint32_t)(cr + h) * hw4;
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, s0[0] + s0[1] + b), ds, o0, so, 0);
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, s0[1] + s0[2] + b), ds, o0 + 8, so, 0);
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, s1[0] + s1[1] + b), ds, o1, so, 0);
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, s1[1] + s1[2] + b), ds, o1 + 8, so, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[0]), ds, o0, so, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[1]), ds, o0 + 8, so, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[2]), ds, o1, so, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[3]), ds, o1 + 8, so, 0);
         }
     }
 }
@@ -771,11 +799,14 @@ __global__ __launch_bounds__(S2_T, 2) void s2t_conv_kernel(
     }
 }
 
+// (mask: the transposed conv's ReLU mask, applied after the bias)
 __global__ void s2_reduce_kernel(const float *__restrict__ part, const float *__restrict__ bias,
-                                 float *__restrict__ y, int64_t n4, int S, int K, int HW) {
+                                 float *__restrict__ y, int64_t n4, int S, int K, int HW,
+                                 const float *__restrict__ mask) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n4) return;
     const float4 *p4 = reinterpret_cast<const float4 *>(part);
+    const float4 mv = mask ? reinterpret_cast<const float4 *>(mask)[i] : float4{};
     float4 s = p4[i];
     for (int z = 1; z < S; ++z) {
         const float4 t = p4[i + z * n4];
@@ -784,6 +815,12 @@ __global__ void s2_reduce_kernel(const float *__restrict__ part, const float *__
     if (bias) {
         const float b = bias[(int)((i * 4 / HW) % K)];
         s.x += b; s.y += b; s.z += b; s.w += b;
+    }
+    if (mask) {
+        s.x = mv.x <= 0.f ? 0.f : s.x;
+        s.y = mv.y <= 0.f ? 0.f : s.y;
+        s.z = mv.z <= 0.f ? 0.f : s.z;
+        s.w = mv.w <= 0.f ? 0.f : s.w;
     }
     reinterpret_cast<float4 *>(y)[i] = s;
 }
@@ -911,7 +948,7 @@ static smmd_status s2_conv(const float *x, const float *u, const float *x2, cons
     if (e != SMMD_OK || S == 1) return e;
     const int64_t n4 = total / 4;
     s2_reduce_kernel<<<dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st>>>(out, bias, y, n4,
-                                                                              S, ko, HWo);
+                                                                              S, ko, HWo, nullptr);
     return last_launch_status();
 }
 
@@ -978,15 +1015,15 @@ extern "C" size_t smmd_wino4x4s2t_workspace_bytes(int n, int k, int c, int hg, i
 }
 
 // dx [n, c, 2 hg, 2 wg] = conv_transpose2d(gy [n, k, hg, wg], W' [k, c, 4, 4], stride 2, pad 1) + bias
-extern "C" smmd_status smmd_wino4x4s2t_conv(const float *gy, const float *u, const float *bias,
-                                            float *dx, int n, int k, int c, int hg, int wg,
-                                            void *ws, size_t ws_bytes, smmd_stream_t stream) {
+static smmd_status s2t_launch(const float *gy, const float *u, const float *bias,
+                              const float *mask, float *dx, int n, int k, int c, int hg, int wg,
+                              void *ws, size_t ws_bytes, smmd_stream_t stream) {
     if (n < 0 || k <= 0 || c <= 0 || hg < 0 || wg < 0) return SMMD_EINVAL;
     if (n == 0 || hg == 0 || wg == 0) return SMMD_OK;
     if (!gy || !u || !dx) return SMMD_EINVAL;
     if (!smmd_wino4x4s2t_supported(n, k, c, hg, wg)) return SMMD_EUNSUPPORTED;
     if ((reinterpret_cast<uintptr_t>(gy) | reinterpret_cast<uintptr_t>(dx) |
-         reinterpret_cast<uintptr_t>(u)) & 15)
+         reinterpret_cast<uintptr_t>(u) | reinterpret_cast<uintptr_t>(mask)) & 15)
         return SMMD_EINVAL;
     S2TGeom g;
     g.N = n; g.K = k; g.C = c; g.Hg = hg; g.Wg = wg;
@@ -1017,6 +1054,7 @@ extern "C" smmd_status smmd_wino4x4s2t_conv(const float *gy, const float *u, con
     g.slab = S > 1 ? total : 0;
     g.CB = c / 64;
     g.S = S;
+    g.mask = S > 1 ? nullptr : mask;           // several slices: the final sum masks
 
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const int64_t nblk = tb * (c / 64) * 4 * S;
@@ -1031,6 +1069,20 @@ extern "C" smmd_status smmd_wino4x4s2t_conv(const float *gy, const float *u, con
     if (e != SMMD_OK || S == 1) return e;
     const int64_t n4 = total / 4;
     s2_reduce_kernel<<<dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st>>>(
-        out, bias, dx, n4, S, c, 4 * hg * wg);
+        out, bias, dx, n4, S, c, 4 * hg * wg, mask);
     return last_launch_status();
+}
+
+extern "C" smmd_status smmd_wino4x4s2t_conv(const float *gy, const float *u, const float *bias,
+                                            float *dx, int n, int k, int c, int hg, int wg,
+                                            void *ws, size_t ws_bytes, smmd_stream_t stream) {
+    return s2t_launch(gy, u, bias, nullptr, dx, n, k, c, hg, wg, ws, ws_bytes, stream);
+}
+
+extern "C" smmd_status smmd_wino4x4s2t_conv_mask(const float *gy, const float *u,
+                                                 const float *bias, const float *mask, float *dx,
+                                                 int n, int k, int c, int hg, int wg, void *ws,
+                                                 size_t ws_bytes, smmd_stream_t stream) {
+    if (!mask) return SMMD_EINVAL;
+    return s2t_launch(gy, u, bias, mask, dx, n, k, c, hg, wg, ws, ws_bytes, stream);
 }

@@ -112,22 +112,24 @@ class _ConvMeanPool(nn.Module):
         literal conv -> pool order would pool it)."""
         return self.foldable() and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0
 
-    def forward(self, x, with_bias=True):
+    def forward(self, x, with_bias=True, mask_in=False):
         """with_bias False (the folded path only, see bias_deferrable): the
-        convolution alone, a consumer adds self.conv.bias."""
+        convolution alone, a consumer adds self.conv.bias.  mask_in: x is a
+        ReLU output whose producer leaves the mask to this conv's input
+        gradient (convops.conv2d)."""
         c = self.conv
         if not with_bias:
             assert self.bias_deferrable(x)
             w4 = self._w4 if self._w4 is not None else fold_pool_weight(c.effective_weight())
-            return conv2d(x, w4, None, 2, 1)
+            return conv2d(x, w4, None, 2, 1, mask_in=mask_in)
         if self.foldable() and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0:
             # meanpool2(conv3x3(x)) as ONE 4x4 stride-2 conv on the folded
             # weight: same value, a quarter of the output rows, no pool and no
             # upsample in the backward; MIOpen runs fwd / Dx / Dw of it in about
             # half the time of the 3x3 + pool (tools/fold_bench.py, r03 profiles)
             w4 = self._w4 if self._w4 is not None else fold_pool_weight(c.effective_weight())
-            return conv2d(x, w4, c.bias, 2, 1)
-        return mean_pool2(c(x))
+            return conv2d(x, w4, c.bias, 2, 1, mask_in=mask_in)
+        return mean_pool2(c(x, mask_in=mask_in))
 
 
 class prefolded:
@@ -234,17 +236,20 @@ class ResidualBlock(nn.Module):
         defer_bias the two convolutions leave their biases to the consumer
         (the next block's relu_pool) and return them; otherwise (None, None)."""
         r, p = convops.relu_pool(x, y, slope_p, bx, by)
-        if isinstance(self.bn2, _Identity):      # norm off: the ReLU in the conv's epilogue
-            h1 = self.conv_1(r, relu=True)
+        # norm off: the ReLU in conv_1's epilogue, and its mask in conv_2's
+        # input gradient (h1's only consumer; convops.conv2d_relu)
+        fuse = isinstance(self.bn2, _Identity)
+        if fuse:
+            h1 = self.conv_1(r, relu=True, consumer_masks=True)
         else:
             h1 = F.relu(self.bn2(self.conv_1(r)))
         sc = self.shortcut.conv
         if defer_bias and self.conv_2.bias_deferrable(h1) and sc.bias is not None \
                 and self.conv_2.conv.bias is not None:
             s = sc(p, with_bias=False)                   # _MeanPoolConv on the pooled input
-            h = self.conv_2(h1, with_bias=False)
+            h = self.conv_2(h1, with_bias=False, mask_in=fuse)
             return s, h, sc.bias, self.conv_2.conv.bias
-        return sc(p), self.conv_2(h1), None, None
+        return sc(p), self.conv_2(h1, mask_in=fuse), None, None
 
     def forward(self, x):
         if self._relu_pool and convops.relu_pool_applicable(x):
@@ -469,6 +474,10 @@ class SNResNetDiscriminator(nn.Module):
                 slope = 1.0
                 continue
             u, v, bu, bv, slope = b(self._join(u, v, bu, bv, slope)), None, None, None, 1.0
+        if bu is None and bv is None and slope == 1.0:
+            # the last block's two paths, their add, lrelu and the pixel sum
+            # in one launch (convops.lrelu_rowsum)
+            return self.h5_lin(convops.lrelu_rowsum(u, v, 0.2))
         h = self._join(u, v, bu, bv, slope)
         return self.h5_lin(lrelu(h).sum(dim=(2, 3)))
 

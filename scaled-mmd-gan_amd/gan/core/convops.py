@@ -515,9 +515,11 @@ def _s2_conv2(x, w, x2, w2):
     return y
 
 
-def _s2t_conv(g, w, b):
+def _s2t_conv(g, w, b, mask=None):
     """conv_transpose2d(g, w [k, c, 4, 4], b, stride 2, padding 1) on
-    smmd_wino4x4s2t_conv (the input gradient of conv(., w, stride 2))."""
+    smmd_wino4x4s2t_conv (the input gradient of conv(., w, stride 2)); with
+    mask (the conv's input, a ReLU output) TF's ReLU gradient of it in the same
+    launch (smmd_wino4x4s2t_conv_mask): threshold_backward(dx, mask, 0)."""
     from . import _lib
     g = g.contiguous()
     w = w.contiguous()
@@ -533,9 +535,18 @@ def _s2t_conv(g, w, b):
     ws = _lib.workspace('wino_s2t', nb, g.device) if nb else None
     _lib.add_bytes('smmd_wino4x4s2t_conv', (g.numel() + y.numel()) * 4)
     _lib.add_flops('smmd_wino4x4s2t_conv', 2 * 9 * N * (Hg // 2) * (Wg // 2) * 4 * k * c)
+    if mask is not None:
+        mask = mask.contiguous()
+        assert mask.shape == y.shape and mask.dtype == y.dtype
+        _lib.add_bytes('smmd_wino4x4s2t_conv', mask.numel() * 4)
     with _lib.timed('smmd_wino4x4s2t_conv'):
-        st = L.smmd_wino4x4s2t_conv(_lib.ptr(g), _lib.ptr(u), _lib.ptr(b), _lib.ptr(y), N, k, c,
-                                    Hg, Wg, _lib.ptr(ws), nb, _lib.stream_handle(g.device))
+        if mask is None:
+            st = L.smmd_wino4x4s2t_conv(_lib.ptr(g), _lib.ptr(u), _lib.ptr(b), _lib.ptr(y), N, k,
+                                        c, Hg, Wg, _lib.ptr(ws), nb, _lib.stream_handle(g.device))
+        else:
+            st = L.smmd_wino4x4s2t_conv_mask(_lib.ptr(g), _lib.ptr(u), _lib.ptr(b),
+                                             _lib.ptr(mask), _lib.ptr(y), N, k, c, Hg, Wg,
+                                             _lib.ptr(ws), nb, _lib.stream_handle(g.device))
     _lib.check(st, 'smmd_wino4x4s2t_conv')
     return y
 
@@ -750,19 +761,30 @@ def _fwd2(x, w, x2, w2, stride, padding):
     return None
 
 
-def _bwd(gy, x, w, stride, padding, mask):
-    """(Dx, Dw) of conv(x, w) at upstream gy via the native backward kernels."""
+def _bwd(gy, x, w, stride, padding, mask, xmask=None):
+    """(Dx, Dw) of conv(x, w) at upstream gy via the native backward kernels.
+    xmask (the input x, a ReLU output whose producer skips its mask): Dx
+    returned as threshold_backward(Dx, x, 0), inside the stride-2 transposed
+    conv's launch where it runs there."""
+    gx, gw, fused = _bwd_core(gy, x, w, stride, padding, mask, xmask)
+    if xmask is not None and gx is not None and not fused:
+        gx = _aten.threshold_backward(gx, xmask, 0.0)
+    return gx, gw
+
+
+def _bwd_core(gy, x, w, stride, padding, mask, xmask):
+    """_bwd's kernels: (Dx, Dw, Dx already masked by xmask)."""
     if mask[0] and not (_is_wino(gy, w, stride, padding, 1) or _is_s2t(gy, w, stride, padding)):
         materialize(w)          # a direct reader of w's values below
     if _is_thin(x, w, stride, padding):
         gx = _thin_conv(gy, w, None, 1) if mask[0] else None
         gw = _thin_wgrad(gy, x) if mask[1] else None
-        return gx, gw
+        return gx, gw, False
     if _is_c1(x, w, stride, padding) and _is_c1(gy, w.transpose(0, 1), stride, padding):
         gx = _c1_dx(gy, w) if mask[0] else None
         gw = _c1_wgrad(gy, x) if mask[1] else None
         if (gx is not None or not mask[0]) and (gw is not None or not mask[1]):
-            return gx, gw
+            return gx, gw, False
     if mask[1] and _wgrad_ok(x, gy, w, stride, padding):
         gw = _wino_wgrad(x, gy)
         gx = None
@@ -770,43 +792,50 @@ def _bwd(gy, x, w, stride, padding, mask):
             gx = (_wino_conv(gy, w, None, 1) if _is_wino(gy, w, stride, padding, 1) else
                   _aten.convolution_backward(gy, x, w, None, stride, padding, [1, 1], False,
                                              [0, 0], 1, [True, False, False])[0])
-        return gx, gw
+        return gx, gw, False
     if mask[0] and _is_wino(gy, w, stride, padding, 1):
         gx = _wino_conv(gy, w, None, 1)
         gw = None
         if mask[1]:
             _, gw, _ = _aten.convolution_backward(gy, x, w, None, stride, padding, [1, 1], False,
                                                   [0, 0], 1, [False, True, False])
-        return gx, gw
+        return gx, gw, False
     s2 = (w.dim() == 4 and tuple(w.shape[2:]) == (4, 4) and _s2_shape_ok(x, stride, padding)
           and tuple(x.shape[2:]) == (2 * gy.shape[2], 2 * gy.shape[3]))
     if s2 and (mask[1] or _is_s2t(gy, w, stride, padding)):
         gx = gw = None
+        fused = False
         if mask[0]:
-            gx = (_s2t_conv(gy, w, None) if _is_s2t(gy, w, stride, padding) else
-                  _aten.convolution_backward(gy, x, w, None, stride, padding, [1, 1], False,
-                                             [0, 0], 1, [True, False, False])[0])
+            if _is_s2t(gy, w, stride, padding):
+                fused = xmask is not None and xmask.shape == x.shape
+                gx = _s2t_conv(gy, w, None, mask=xmask if fused else None)
+            else:
+                gx = _aten.convolution_backward(gy, x, w, None, stride, padding, [1, 1], False,
+                                                [0, 0], 1, [True, False, False])[0]
         if mask[1]:
             gw = _s2_weight_grad(gy, x, w, stride, padding)
-        return gx, gw
+        return gx, gw, fused
     gx, gw, _ = _aten.convolution_backward(gy, x, w, None, stride, padding, [1, 1], False,
                                            [0, 0], 1, [mask[0], mask[1], False])
-    return gx, gw
+    return gx, gw, False
 
 
 class _ConvBackward(torch.autograd.Function):
-    """(gx, gw) = backward of conv(x, w); differentiable once more."""
+    """(gx, gw) = backward of conv(x, w); differentiable once more.  mask_in:
+    gx = threshold_backward(Dx, x, 0) (x a ReLU output whose producer skips
+    its mask, _Conv2d's mask_in), and so is the gradient this node returns
+    for x."""
 
     @staticmethod
-    def forward(ctx, x, w, gy, stride, padding, want_w):
+    def forward(ctx, x, w, gy, stride, padding, want_w, mask_in=False):
         ctx.save_for_backward(x, w, gy)
-        ctx.cfg = (stride, padding)
+        ctx.cfg = (stride, padding, mask_in)
         # an output nobody differentiates (the placeholder gw of the input-only
         # Jacobian pass, or gx/gw unused by the loss) arrives as None instead
         # of a materialised zero tensor: otherwise every critic conv of the
         # double backward ran conv(x, 0) and Dx(gy, 0) on it
         ctx.set_materialize_grads(False)
-        gx, gw = _bwd(gy, x, w, stride, padding, (True, want_w))
+        gx, gw = _bwd(gy, x, w, stride, padding, (True, want_w), x if mask_in else None)
         # gw None (the input-only pass): a non-tensor output, discarded by the
         # caller -- no placeholder tensor, so no fill kernel per call
         return gx, gw
@@ -814,11 +843,14 @@ class _ConvBackward(torch.autograd.Function):
     @staticmethod
     def backward(ctx, ggx, ggw):
         x, w, gy = ctx.saved_tensors
-        stride, padding = ctx.cfg
+        stride, padding, mask_in = ctx.cfg
         need_x, need_w, need_gy = ctx.needs_input_grad[:3]
         g_x = g_w = g_gy = None
         if ggx is not None:
             ggx = ggx.contiguous(memory_format=_fmt(x))
+            if mask_in:             # gx = m * Dx(gy): its adjoint masks ggx first
+                ggx = (_ReluMask.apply(ggx, x) if torch.is_grad_enabled()
+                       else _aten.threshold_backward(ggx, x, 0.0))
         # the upstream's gradient conv(ggx, w) + conv(x, ggw): one pair launch
         # when both take the same Winograd path, else two convs and their sum
         pair = None
@@ -834,10 +866,68 @@ class _ConvBackward(torch.autograd.Function):
                 t = _fwd(x, ggw, None, stride, padding)
                 g_gy = t if g_gy is None else g_gy + t
             if need_x:
-                g_x, _ = _bwd(gy, x, ggw, stride, padding, (True, False))
+                g_x, _ = _bwd(gy, x, ggw, stride, padding, (True, False),
+                              x if mask_in else None)
         if pair is not None:
             g_gy = pair
-        return g_x, g_w, g_gy, None, None, None
+        return g_x, _late_gw(w, g_w), g_gy, None, None, None, None
+
+
+# Late sums of weight gradients (SMMD_WGRAD_LATE_SUM=0: off).  A critic
+# weight (an SN bank output, marked by SpectralNormBank.refresh) is convolved
+# by the real and the fake forward and by the double backward, and autograd
+# adds those contributions as they arrive -- one latency-bound add kernel per
+# weight and extra contribution, ~26 per critic step.  While armed (around the
+# critic step's backward, MMD_GAN.d_step) the first contribution of such a
+# weight goes to autograd as usual and the later ones are queued; the SN
+# node's backward (their only consumer, which autograd runs after every
+# contribution exists) first adds the queue in arrival order with one
+# multi-tensor add per round: the same sums in the same order, bit-identical.
+WGRAD_LATE_SUM = os.environ.get('SMMD_WGRAD_LATE_SUM', '1') != '0'
+_late = {'armed': False, 'first': {}, 'queue': [], 'queued': 0}   # queued: a running count
+
+
+def arm_late_wgrad_sums(on):
+    """Start (True) or end (False) a backward whose SN-weight gradients are
+    summed late (flush_late_wgrad_sums); ending drops any state."""
+    _late['armed'] = bool(on) and WGRAD_LATE_SUM
+    _late['first'].clear()
+    _late['queue'].clear()
+
+
+def _late_gw(w, gw):
+    """gw for autograd, or None with gw queued onto w's first contribution."""
+    if gw is None or not _late['armed'] or not getattr(w, '_smmd_late_sum', False):
+        return gw
+    f = _late['first'].get(id(w))
+    if f is None or f[0] is not w:
+        _late['first'][id(w)] = (w, gw)
+        return gw
+    _late['queue'].append((f[1], gw))
+    _late['queued'] += 1
+    return None
+
+
+def flush_late_wgrad_sums():
+    """Add the queued contributions into their first ones, in arrival order:
+    round r adds each weight's r-th queued term (one _foreach_add_ per round,
+    no tensor twice in one launch)."""
+    q = _late['queue']
+    if not q:
+        return
+    rounds = []
+    seen = {}
+    for acc, g in q:
+        r = seen.get(id(acc), 0)
+        seen[id(acc)] = r + 1
+        if r == len(rounds):
+            rounds.append(([], []))
+        rounds[r][0].append(acc)
+        rounds[r][1].append(g)
+    with torch.no_grad():
+        for accs, gs in rounds:
+            torch._foreach_add_(accs, gs)
+    q.clear()
 
 
 def _fmt(t):
@@ -848,30 +938,35 @@ def _fmt(t):
 
 
 class _Conv2d(torch.autograd.Function):
+    """conv(x, w) + b.  mask_in (x a ReLU output whose producer,
+    _Conv2dReLU with consumer_masks, skips its mask): the input gradient is
+    returned already masked by x > 0 -- inside the stride-2 transposed conv's
+    launch (smmd_wino4x4s2t_conv_mask) instead of a threshold_backward pass."""
+
     @staticmethod
-    def forward(ctx, x, w, b, stride, padding):
+    def forward(ctx, x, w, b, stride, padding, mask_in=False):
         ctx.save_for_backward(x, w)
-        ctx.cfg = (stride, padding, b is not None)
+        ctx.cfg = (stride, padding, b is not None, mask_in)
         return _fwd(x, w, b, stride, padding)
 
     @staticmethod
     def backward(ctx, gy):
         x, w = ctx.saved_tensors
-        stride, padding, has_b = ctx.cfg
+        stride, padding, has_b, mask_in = ctx.cfg
         gy = gy.contiguous(memory_format=_fmt(x))
         want_w = ctx.needs_input_grad[1] and _input_only[0] == 0
         want_x = ctx.needs_input_grad[0] and not (_no_dx and x.data_ptr() in _no_dx)
         if torch.is_grad_enabled():          # create_graph: keep it differentiable
-            gx, gw = _ConvBackward.apply(x, w, gy, stride, padding, want_w)
+            gx, gw = _ConvBackward.apply(x, w, gy, stride, padding, want_w, mask_in)
             if not want_w:
                 gw = None
         elif want_x or want_w:
-            gx, gw = _bwd(gy, x, w, stride, padding, (want_x, want_w))
+            gx, gw = _bwd(gy, x, w, stride, padding, (want_x, want_w), x if mask_in else None)
         else:
             gx = gw = None
         gb = (bias_grad(gy) if (has_b and ctx.needs_input_grad[2] and _input_only[0] == 0)
               else None)
-        return gx, gw, gb, None, None
+        return gx, _late_gw(w, gw), gb, None, None, None
 
 
 def bias_grad(gy):
@@ -898,6 +993,29 @@ def bias_grad(gy):
     return out
 
 
+class _ReluMask(torch.autograd.Function):
+    """g -> g * (r > 0) (threshold_backward(g, r, 0), TF's relu gradient) as
+    the differentiable node of a create_graph backward.  Its own gradient is
+    the same mask for g and None for r: the mask's derivative is zero, and
+    autograd's ThresholdBackwardBackward0 materialised it as a zero tensor
+    (a fill of the activation's size) that the engine then added to r's other
+    gradient (a full-size add) -- per critic layer of every critic step."""
+
+    @staticmethod
+    def forward(ctx, g, r):
+        ctx.save_for_backward(r)
+        return _aten.threshold_backward(g, r, 0.0)
+
+    @staticmethod
+    def backward(ctx, gg):
+        r, = ctx.saved_tensors
+        if gg is None or not ctx.needs_input_grad[0]:
+            return None, None
+        gg = gg.contiguous()
+        return ((_ReluMask.apply(gg, r) if torch.is_grad_enabled()
+                 else _aten.threshold_backward(gg, r, 0.0)), None)
+
+
 class _Conv2dReLU(torch.autograd.Function):
     """relu(conv(x, w) + b) with the ReLU in the Winograd kernel's epilogue (the
     critic's first conv of each down block, block.py:44-46, norm off): no
@@ -906,17 +1024,25 @@ class _Conv2dReLU(torch.autograd.Function):
     backward of the scaling regulariser)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, stride, padding):
+    def forward(ctx, x, w, b, stride, padding, consumer_masks=False):
         r = _wino_conv(x, w, b, 0, relu=True)
         ctx.save_for_backward(x, w, r)
-        ctx.cfg = (stride, padding, b is not None)
+        ctx.cfg = (stride, padding, b is not None, consumer_masks)
         return r
 
     @staticmethod
     def backward(ctx, gr):
         x, w, r = ctx.saved_tensors
-        stride, padding, has_b = ctx.cfg
-        gy = _aten.threshold_backward(gr.contiguous(), r, 0.0)
+        stride, padding, has_b, consumer_masks = ctx.cfg
+        if consumer_masks:
+            # r's only consumer is a conv with mask_in (ResidualBlock.down_parts):
+            # every gradient that reaches r -- its input gradient, and in the
+            # double backward _ConvBackward's for its saved x -- is masked already
+            gy = gr.contiguous()
+        elif torch.is_grad_enabled():
+            gy = _ReluMask.apply(gr.contiguous(), r)
+        else:
+            gy = _aten.threshold_backward(gr.contiguous(), r, 0.0)
         want_w = ctx.needs_input_grad[1] and _input_only[0] == 0
         want_x = ctx.needs_input_grad[0] and not (_no_dx and x.data_ptr() in _no_dx)
         if torch.is_grad_enabled():
@@ -929,27 +1055,37 @@ class _Conv2dReLU(torch.autograd.Function):
             gx = gw = None
         gb = (bias_grad(gy) if (has_b and ctx.needs_input_grad[2] and _input_only[0] == 0)
               else None)
-        return gx, gw, gb, None, None
+        return gx, _late_gw(w, gw), gb, None, None, None
 
 
-def conv2d_relu(x, w, b=None, stride=1, padding=0):
+def conv2d_relu(x, w, b=None, stride=1, padding=0, consumer_masks=False):
     """relu(conv2d(x, w, b)): one Winograd launch on the 3x3 layers it tiles
-    (SMMD_CONV_RELU=0: a separate ReLU), the two ops otherwise."""
+    (SMMD_CONV_RELU=0: a separate ReLU), the two ops otherwise.
+    consumer_masks: the output's only consumer is a conv2d(..., mask_in=True),
+    which returns its input gradient masked, so this ReLU's backward skips
+    the mask (the separate-ReLU form keeps it: masking twice is exact)."""
     s = (stride, stride) if isinstance(stride, int) else tuple(stride)
     p = (padding, padding) if isinstance(padding, int) else tuple(padding)
     if CONV_RELU and _is_wino(x, w, list(s), list(p), 0):
-        return _Conv2dReLU.apply(x, w, b, list(s), list(p))
+        return _Conv2dReLU.apply(x, w, b, list(s), list(p), bool(consumer_masks and RELU_MASK_FUSE))
     return F.relu(conv2d(x, w, b, stride, padding))
 
 
 CONV_RELU = os.environ.get('SMMD_CONV_RELU', '1') != '0'
 
 
-def conv2d(x, w, b=None, stride=1, padding=0):
-    """F.conv2d with the MIOpen-friendly second-order rule above."""
+# SMMD_RELU_MASK_FUSE=0: the critic's conv-ReLU keeps its own mask pass
+# (threshold_backward) instead of its consumer's masked input gradient
+RELU_MASK_FUSE = os.environ.get('SMMD_RELU_MASK_FUSE', '1') != '0'
+
+
+def conv2d(x, w, b=None, stride=1, padding=0, mask_in=False):
+    """F.conv2d with the MIOpen-friendly second-order rule above.  mask_in: x
+    is a ReLU output; the input gradient comes back masked by x > 0 (see
+    conv2d_relu's consumer_masks)."""
     s = (stride, stride) if isinstance(stride, int) else tuple(stride)
     p = (padding, padding) if isinstance(padding, int) else tuple(padding)
-    return _Conv2d.apply(x, w, b, list(s), list(p))
+    return _Conv2d.apply(x, w, b, list(s), list(p), bool(mask_in and RELU_MASK_FUSE))
 
 
 class _Up2Quarter(torch.autograd.Function):
@@ -1353,3 +1489,95 @@ def up_add(s, bs, h, bh):
     if bh is not None:
         h = h + bh.view(1, -1, 1, 1)
     return F.interpolate(s, scale_factor=2, mode='nearest') + h
+
+
+# ---------------------------------------------------------------------------
+# the critic's tail: lrelu(u + v).sum(dim=(2, 3)) (architecture.py:430-433, the
+# last block's two paths, the final lrelu and tf.reduce_sum) in one launch,
+# its backward in one, its double backward in one (csrc/smmd_relupool.hip;
+# SMMD_TAIL=0: the torch ops -- an add, the lrelu and the sum forward, the
+# expand + leaky_relu_backward and, in the double backward, a zero fill and
+# an add of it for the mask input)
+TAIL = os.environ.get('SMMD_TAIL', '1') != '0'
+
+
+def _tail_ok(u, v):
+    return (TAIL and u.is_cuda and u.dtype == torch.float32 and u.dim() == 4
+            and u.is_contiguous() and (u.shape[2] * u.shape[3]) % 4 == 0
+            and u.data_ptr() % 16 == 0
+            and (v is None or (v.shape == u.shape and v.dtype == u.dtype and v.is_contiguous()
+                               and v.data_ptr() % 16 == 0)))
+
+
+def _row_sum(a, b, mu, mv, slope):
+    from . import _lib
+    N, C, H, W = a.shape
+    y = torch.empty((N, C), dtype=a.dtype, device=a.device)
+    _lib.add_bytes('smmd_row_lrelu_sum', a.numel() * 4 * (1 + (b is not None) + (mu is not None)
+                                                          + (mv is not None)))
+    with _lib.timed('smmd_row_lrelu_sum'):
+        st = _lib.lib().smmd_row_lrelu_sum(_lib.ptr(a), _lib.ptr(b), _lib.ptr(mu), _lib.ptr(mv),
+                                           _lib.ptr(y), N * C, H * W, float(slope),
+                                           _lib.stream_handle(a.device))
+    _lib.check(st, 'smmd_row_lrelu_sum')
+    return y
+
+
+class _TailBcast(torch.autograd.Function):
+    """g [N, C] -> g * s(u + v) [N, C, H, W]: the tail's backward; its own
+    adjoint is the masked row sum (the mask inputs get no gradient)."""
+
+    @staticmethod
+    def forward(ctx, g, u, v, slope):
+        from . import _lib
+        g = g.contiguous()
+        N, C, H, W = u.shape
+        out = torch.empty_like(u)
+        _lib.add_bytes('smmd_row_lrelu_bcast', u.numel() * 4 * (2 + (v is not None)))
+        with _lib.timed('smmd_row_lrelu_bcast'):
+            st = _lib.lib().smmd_row_lrelu_bcast(_lib.ptr(g), _lib.ptr(u), _lib.ptr(v),
+                                                 _lib.ptr(out), N * C, H * W, float(slope),
+                                                 _lib.stream_handle(u.device))
+        _lib.check(st, 'smmd_row_lrelu_bcast')
+        ctx.save_for_backward(u, v)
+        ctx.slope = slope
+        return out
+
+    @staticmethod
+    def backward(ctx, gg):
+        u, v = ctx.saved_tensors
+        if gg is None or not ctx.needs_input_grad[0]:
+            return None, None, None, None
+        return _row_sum(gg.contiguous(), None, u, v, ctx.slope), None, None, None
+
+
+class _TailSum(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, u, v, slope):
+        ctx.save_for_backward(u, v)
+        ctx.slope = slope
+        return _row_sum(u, v, None, None, slope)
+
+    @staticmethod
+    def backward(ctx, g):
+        u, v = ctx.saved_tensors
+        if g is None:
+            return None, None, None
+        gh = (_TailBcast.apply(g, u, v, ctx.slope) if torch.is_grad_enabled()
+              else _TailBcast.forward(_NoCtx(), g, u, v, ctx.slope))
+        return gh, (gh if v is not None else None), None
+
+
+class _NoCtx:
+    """a stand-in ctx for calling a Function's forward directly (no graph)."""
+
+    def save_for_backward(self, *a):
+        pass
+
+
+def lrelu_rowsum(u, v=None, slope=0.2):
+    """leaky_relu(u + v, slope).sum(dim=(2, 3)) (v None: u alone)."""
+    if _tail_ok(u, v):
+        return _TailSum.apply(u, v, slope)
+    h = u if v is None else u + v
+    return F.leaky_relu(h, slope).sum(dim=(2, 3))

@@ -480,6 +480,7 @@ class MMD_GAN:
             bk = self._bucket_for(self.d_optim)
             bk.clip_exclude = self._sn_tensor_ids() if tower_clip > 0 else frozenset()
         self._dpgd = dpgd
+        convops.arm_late_wgrad_sums(True)
         try:
             if ref:
                 d_loss.backward(inputs=self.d_vars)
@@ -489,6 +490,7 @@ class MMD_GAN:
                 with convops.no_input_grad(self._last_images):
                     d_loss.backward()
         finally:
+            convops.arm_late_wgrad_sums(False)
             self.sn_D.arm_gdirect(False)
             self.sn_D.arm_direct(False)
             self.sn_D.arm_dp_gdirect(False)

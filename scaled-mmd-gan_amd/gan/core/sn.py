@@ -112,6 +112,8 @@ class _SNBatch(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, *grads):
+        from . import convops
+        convops.flush_late_wgrad_sums()     # the conv nodes' queued G contributions
         bank = ctx.bank
         n = len(bank.entries)
         saved = ctx.saved_tensors
@@ -210,6 +212,8 @@ class _SNGroup(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, *grads):
+        from . import convops
+        convops.flush_late_wgrad_sums()     # the conv nodes' queued G contributions
         bank, members = ctx.bank, ctx.members
         k = len(members)
         saved = ctx.saved_tensors
@@ -351,6 +355,7 @@ class SpectralNormBank:
         else:
             outs = _SNBatch.apply(self, bool(update_u), flags, *Ws, *ss)
         for e, w in zip(self.entries, outs):
+            w._smmd_late_sum = True              # convops._late_gw: summed at the SN node
             if w.shape != e.weight.shape:        # the pool-folded 4 x 4 filter
                 e.module.w_eff, e.module.w_fold = None, w
             else:

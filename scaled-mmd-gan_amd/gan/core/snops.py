@@ -82,21 +82,23 @@ class Conv2d(nn.Module, _SNMixin):
         self.bias = nn.Parameter(torch.zeros(cout)) if bias else None
         self._init_sn(with_sn, with_learnable_sn_scale, scale)
 
-    def forward(self, x, with_bias=True, relu=False):
+    def forward(self, x, with_bias=True, relu=False, consumer_masks=False, mask_in=False):
         """with_bias False: the convolution alone (a consumer adds self.bias);
-        relu: relu(conv + bias) (convops.conv2d_relu)."""
+        relu: relu(conv + bias) (convops.conv2d_relu), consumer_masks: its
+        only consumer is a conv with mask_in (x a ReLU output: the input
+        gradient comes back masked, convops.conv2d)."""
         w = self.effective_weight()
         b = self.bias if with_bias else None
         ph = same_pad(x.shape[2], self.k, self.stride)
         pw = same_pad(x.shape[3], self.k, self.stride)
         if relu:
             if ph[0] == ph[1] and pw[0] == pw[1]:
-                return conv2d_relu(x, w, b, self.stride, (ph[0], pw[0]))
-            return F.relu(self.forward(x, with_bias))
+                return conv2d_relu(x, w, b, self.stride, (ph[0], pw[0]), consumer_masks)
+            return F.relu(self.forward(x, with_bias, mask_in=mask_in))
         if ph[0] == ph[1] and pw[0] == pw[1]:
-            return conv2d(x, w, b, self.stride, (ph[0], pw[0]))
+            return conv2d(x, w, b, self.stride, (ph[0], pw[0]), mask_in=mask_in)
         x = F.pad(x, (pw[0], pw[1], ph[0], ph[1]))
-        return conv2d(x, w, b, self.stride, 0)
+        return conv2d(x, w, b, self.stride, 0, mask_in=mask_in)
 
 
 class Deconv2d(nn.Module, _SNMixin):
