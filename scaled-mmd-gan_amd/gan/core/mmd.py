@@ -279,6 +279,8 @@ class _SMMDLoss(torch.autograd.Function):
         ctx.save_for_backward(gx, gy, jac, feat_c, out)
         ctx.cfg = (n_cols, b, per, dof, float(sc), variant, m, n, d)
         ctx.mark_non_differentiable(sums, out)
+        # the unused outputs' gradients arrive as None, not as zero fills
+        ctx.set_materialize_grads(False)
         return mm.view(()), out[0].view(()), sums, out
 
     @staticmethod

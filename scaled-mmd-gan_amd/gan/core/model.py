@@ -26,6 +26,7 @@ Data-parallel modes:
 """
 from __future__ import annotations
 
+import os
 import time
 
 import numpy as np
@@ -38,6 +39,8 @@ from .collectives import GradBuckets, StepExchange
 from .optim import FlatAdam
 from .sn import SpectralNormBank
 from .snops import sn_modules
+
+GRAD_GATHER = os.environ.get('SMMD_GRAD_GATHER', '1') != '0'
 
 
 class Timer:
@@ -571,6 +574,10 @@ class MMD_GAN:
             self.sn_D.refresh(update_u=True)
             if self.sn_G.entries:
                 self.sn_G.refresh(update_u=True)
+            # one process: the generator's gradients gathered into the flat
+            # buffer by one copy at the update (optim.FlatAdam.gather,
+            # SMMD_GRAD_GATHER=0: accumulated into it parameter by parameter)
+            self.g_optim.gather = GRAD_GATHER and not self.dp
             self.g_optim.zero_grad()
             fake = self.generator(self.sample_z(self.batch_size))
             g_loss, d_loss, aux = self.set_tower_loss(images, fake, need_critic_grad=ref)

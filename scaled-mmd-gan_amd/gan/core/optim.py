@@ -67,6 +67,12 @@ class FlatAdam:
                 p.grad = self._view(self.flat_grad, p, o)
         self.step_count = 0
         self._sn = None
+        # gather mode (set per step by MMD_GAN for one-process generator
+        # updates): zero_grad drops the .grad views, autograd's accumulation
+        # nodes then keep each parameter's gradient tensor as it is produced
+        # (no add kernel into a zeroed view per parameter), and step() copies
+        # them into flat_grad with one multi-tensor copy
+        self.gather = False
         # graph mode (model.StepGraphs): the update reads its bias-corrected
         # step size from this device scalar, written before every replay
         self.graph_mode = False
@@ -81,6 +87,10 @@ class FlatAdam:
         return torch.as_strided(flat, p.shape, p.stride(), o)
 
     def zero_grad(self, set_to_none=False):
+        if self.gather and self._sn is None and not self.graph_mode:
+            for p in self.params:
+                p.grad = None
+            return
         self.flat_grad.zero_()
         if self._sn is not None:
             self._sn[0]._gd_pending = None
@@ -90,7 +100,31 @@ class FlatAdam:
             if n and (p.grad is None or p.grad.data_ptr() != self.flat_grad[o:o + n].data_ptr()):
                 p.grad = self._view(self.flat_grad, p, o)
 
+    def _gather_grads(self):
+        """Gather mode: every parameter's gradient into flat_grad (one
+        _foreach_copy_; parameters without one get zeros) and the .grad views
+        re-attached."""
+        dst, src, empty = [], [], []
+        for i, p in enumerate(self.params):
+            if not p.numel():
+                continue
+            view = self._view(self.flat_grad, p, self.offsets[i])
+            g = p.grad
+            if g is None:
+                empty.append(view)
+            elif g.data_ptr() != view.data_ptr():
+                dst.append(view)
+                src.append(g)
+            p.grad = view
+        with torch.no_grad():
+            if dst:
+                torch._foreach_copy_(dst, src)
+            if empty:
+                torch._foreach_zero_(empty)
+
     def _check_grads(self):
+        if self.gather and self._sn is None and not self.graph_mode:
+            self._gather_grads()
         for i, p in enumerate(self.params):
             o, n = self.offsets[i], p.numel()
             if n and (p.grad is None or p.grad.data_ptr() != self.flat_grad[o:o + n].data_ptr()):

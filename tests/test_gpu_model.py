@@ -142,6 +142,37 @@ def test_late_wgrad_sums_bit_identical(dev, monkeypatch):
     assert late <= max(4 * same, 1e-6 * scale), (late, same, scale)
 
 
+def test_generator_gradient_gather_matches_accumulation(dev, monkeypatch):
+    """The generator step's gradients gathered into the flat buffer by one
+    multi-tensor copy (optim.FlatAdam.gather) update the generator as the
+    per-parameter accumulation does, within the step's run-to-run spread."""
+    from gan.core import model as M
+    from gan.core.smmd import SMMD
+    out = []
+    for on in (True, True, False):
+        monkeypatch.setattr(M, 'GRAD_GATHER', on)
+        torch.manual_seed(0)
+        model = SMMD(_cfg(architecture='snresnet', output_size=64, df_dim=16, gf_dim=16,
+                          batch_size=8), device=dev)
+        images = torch.rand(8, 3, 64, 64, generator=torch.Generator().manual_seed(1)).to(dev)
+        z = torch.empty(8, 128).uniform_(-1, 1, generator=torch.Generator().manual_seed(2)).to(dev)
+        model.sample_z = lambda n, z=z: z
+        before = model.g_optim.flat_param.clone()
+        model.g_step(images)
+        assert all(p.grad is not None and p.grad.data_ptr() ==
+                   model.g_optim.flat_grad[model.g_optim.offsets[i]:].data_ptr()
+                   for i, p in enumerate(model.g_optim.params) if p.numel())
+        out.append((model.g_optim.flat_param - before, model.g_optim.flat_grad.clone()))
+    scale = float(out[0][1].abs().max())
+    same = float((out[0][1] - out[1][1]).abs().max())
+    diff = float((out[0][1] - out[2][1]).abs().max())
+    assert diff <= max(4 * same, 1e-6 * scale), (diff, same, scale)
+    dscale = float(out[0][0].abs().max())
+    dsame = float((out[0][0] - out[1][0]).abs().max())
+    ddiff = float((out[0][0] - out[2][0]).abs().max())
+    assert ddiff <= max(4 * dsame, 1e-6 * dscale), (ddiff, dsame, dscale)
+
+
 def test_generator_step_updates_only_G(dev):
     from gan.core.smmd import SMMD
     torch.manual_seed(0)

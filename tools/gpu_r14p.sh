@@ -1,31 +1,27 @@
-# Late weight-gradient sums; ReLU mask in the stride-2 transposed conv's epilogue + the zero-free
-# create_graph ReLU mask: new tests, the critic-step mirror / wino tests,
-# elementwise sources, an interleaved bench A/B of SMMD_RELU_MASK_FUSE.
+# This round's elementwise fusions (ReLU mask in the stride-2 transposed conv,
+# zero-free create_graph ReLU mask, late weight-gradient sums, the critic tail,
+# the generator's gradient gather): their tests, the critic-step mirror and
+# the wino tests, the elementwise sources, and bench A/Bs -- everything off vs
+# on (interleaved, twice), then each switch off alone.
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_gpu_relu_mask.py tests/test_gpu_model.py tests/test_gpu_sn_lazy.py tests/test_gpu_fold.py tests/test_gpu_wino_s2.py tests/test_gpu_relupool.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/r14p_tests.txt 2>&1 || { echo "tests rc=$?"; tail -30 gpurun_out/r14p_tests.txt; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_gpu_relu_mask.py tests/test_gpu_model.py tests/test_gpu_sn_lazy.py tests/test_gpu_fold.py tests/test_gpu_wino_s2.py tests/test_gpu_relupool.py tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/r14p_tests.txt 2>&1 || { echo "tests rc=$?"; tail -30 gpurun_out/r14p_tests.txt; exit 1; }
 tail -1 gpurun_out/r14p_tests.txt
 timeout -k 10 300 python -u tools/op_sources.py --top 60 > gpurun_out/r14p_opsrc.txt 2>&1 || { echo "opsrc rc=$?"; tail -20 gpurun_out/r14p_opsrc.txt; exit 1; }
 grep "==" gpurun_out/r14p_opsrc.txt
+OFF="SMMD_RELU_MASK_FUSE=0 SMMD_WGRAD_LATE_SUM=0 SMMD_TAIL=0 SMMD_GRAD_GATHER=0"
+run() {  # tag env...
+  local tag=$1; shift
+  env "$@" timeout -k 10 400 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --mmd-sweep 0 --ref-schedule-steps 0 > gpurun_out/r14p_${tag}.json 2> gpurun_out/r14p_${tag}.err || { echo "bench $tag rc=$?"; tail -20 gpurun_out/r14p_${tag}.err; return 1; }
+  python -c "import json;d=json.load(open('gpurun_out/r14p_${tag}.json'));print('$tag',d['value'],d['ms_per_step'])"
+}
 for r in 1 2; do
-  for v in 0 1; do
-    SMMD_RELU_MASK_FUSE=$v timeout -k 10 400 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --mmd-sweep 0 --ref-schedule-steps 0 > gpurun_out/r14p_ab_${v}_${r}.json 2> gpurun_out/r14p_ab_${v}_${r}.err || { echo "bench rc=$?"; tail -20 gpurun_out/r14p_ab_${v}_${r}.err; exit 1; }
-    python -c "import json;d=json.load(open('gpurun_out/r14p_ab_${v}_${r}.json'));print('SMMD_RELU_MASK_FUSE=$v run $r',d['value'],d['ms_per_step'])"
-  done
+  run alloff_$r $OFF || exit 1
+  run allon_$r X=1 || exit 1
 done
+run nomask SMMD_RELU_MASK_FUSE=0 || exit 1
+run nolate SMMD_WGRAD_LATE_SUM=0 || exit 1
+run notail SMMD_TAIL=0 || exit 1
+run nogather SMMD_GRAD_GATHER=0 || exit 1
 echo done
-for r in 1 2; do
-  for v in 0 1; do
-    SMMD_WGRAD_LATE_SUM=$v timeout -k 10 400 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --mmd-sweep 0 --ref-schedule-steps 0 > gpurun_out/r14p_ls_${v}_${r}.json 2> gpurun_out/r14p_ls_${v}_${r}.err || { echo "bench rc=$?"; tail -20 gpurun_out/r14p_ls_${v}_${r}.err; exit 1; }
-    python -c "import json;d=json.load(open('gpurun_out/r14p_ls_${v}_${r}.json'));print('SMMD_WGRAD_LATE_SUM=$v run $r',d['value'],d['ms_per_step'])"
-  done
-done
-echo done2
-for r in 1 2; do
-  for v in 0 1; do
-    SMMD_TAIL=$v timeout -k 10 400 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --mmd-sweep 0 --ref-schedule-steps 0 > gpurun_out/r14p_tl_${v}_${r}.json 2> gpurun_out/r14p_tl_${v}_${r}.err || { echo "bench rc=$?"; tail -20 gpurun_out/r14p_tl_${v}_${r}.err; exit 1; }
-    python -c "import json;d=json.load(open('gpurun_out/r14p_tl_${v}_${r}.json'));print('SMMD_TAIL=$v run $r',d['value'],d['ms_per_step'])"
-  done
-done
-echo done3
