@@ -468,6 +468,7 @@ class MMD_GAN:
             fake = self.generator(self.sample_z(self.batch_size))
         for p in self.d_vars:
             p.requires_grad_(True)
+        self.d_optim.gather = GRAD_GATHER and not self.dp
         self.d_optim.zero_grad()
         g_loss, d_loss, aux = self.set_tower_loss(images, fake, need_critic_grad=True)
         self._arm(self.d_optim)

@@ -67,11 +67,12 @@ class FlatAdam:
                 p.grad = self._view(self.flat_grad, p, o)
         self.step_count = 0
         self._sn = None
-        # gather mode (set per step by MMD_GAN for one-process generator
-        # updates): zero_grad drops the .grad views, autograd's accumulation
-        # nodes then keep each parameter's gradient tensor as it is produced
-        # (no add kernel into a zeroed view per parameter), and step() copies
-        # them into flat_grad with one multi-tensor copy
+        # gather mode (set per step by MMD_GAN in one process): zero_grad
+        # drops the .grad views (an SN bank's weights and scales excepted),
+        # autograd's accumulation nodes then keep each parameter's gradient
+        # tensor as it is produced (no add kernel into a zeroed view per
+        # parameter), and step() copies them into flat_grad with one
+        # multi-tensor copy
         self.gather = False
         # graph mode (model.StepGraphs): the update reads its bias-corrected
         # step size from this device scalar, written before every replay
@@ -86,8 +87,11 @@ class FlatAdam:
             return flat[o:o + p.numel()].view_as(p)
         return torch.as_strided(flat, p.shape, p.stride(), o)
 
+    def _gathering(self):
+        return self.gather and not self.graph_mode
+
     def zero_grad(self, set_to_none=False):
-        if self.gather and self._sn is None and not self.graph_mode:
+        if self._gathering() and self._sn is None:
             for p in self.params:
                 p.grad = None
             return
@@ -99,6 +103,15 @@ class FlatAdam:
             o, n = self.offsets[i], p.numel()
             if n and (p.grad is None or p.grad.data_ptr() != self.flat_grad[o:o + n].data_ptr()):
                 p.grad = self._view(self.flat_grad, p, o)
+        if self._gathering():
+            # an SN bank's weights and scales keep their views (the G-direct
+            # backward writes dL/ds into them, and no AccumulateGrad touches
+            # the weights); the others gather (flat_grad already zero)
+            keep = {id(t) for e in self._sn[0].entries for t in (e.weight, e.scale)
+                    if t is not None}
+            for p in self.params:
+                if id(p) not in keep:
+                    p.grad = None
 
     def _gather_grads(self):
         """Gather mode: every parameter's gradient into flat_grad (one
@@ -119,11 +132,11 @@ class FlatAdam:
         with torch.no_grad():
             if dst:
                 torch._foreach_copy_(dst, src)
-            if empty:
+            if empty and self._sn is None:   # (with a bank zero_grad zeroed them)
                 torch._foreach_zero_(empty)
 
     def _check_grads(self):
-        if self.gather and self._sn is None and not self.graph_mode:
+        if self._gathering():
             self._gather_grads()
         for i, p in enumerate(self.params):
             o, n = self.offsets[i], p.numel()
@@ -187,6 +200,8 @@ class FlatAdam:
         """The flat gradient with every SN weight's dL/dW formed (a copy): under
         the G-direct update those ranges of ``flat_grad`` are never written
         (smmd_sn_weight_bwd from the kept G, for inspection and tests)."""
+        if self._gathering():
+            self._gather_grads()
         g = self.flat_grad.clone()
         if self._sn is None or self._sn[0]._gd_pending is None:
             return g
