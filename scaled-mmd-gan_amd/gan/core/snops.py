@@ -145,13 +145,25 @@ class Linear(nn.Module, _SNMixin):
         self._init_sn(with_sn, with_learnable_sn_scale, scale)
 
     def forward(self, x):
-        return F.linear(x, self.effective_weight(), self.bias)
+        w = self.effective_weight()
+        if LINEAR_MV and w.shape[0] == 1 and x.dim() == 2 and x.is_cuda:
+            # one output feature (the critic's output layer at dof_dim 1): a
+            # matrix-vector product; hipBLASLt ran this [B, F] x [F, 1] GEMM on
+            # one workgroup, 32 us per call
+            y = (torch.mv(x, w.view(-1)) if self.bias is None
+                 else torch.addmv(self.bias, x, w.view(-1)))
+            return y.unsqueeze(1)
+        return F.linear(x, w, self.bias)
 
 
 def batch_norm(c):
     """tf.layers.batch_normalization(momentum=.9, eps=1e-5, training=True)
     (snops.py:31-40, resnet/ops/batchnorm.py:10-18)."""
     return nn.BatchNorm2d(c, eps=1e-5, momentum=0.1)
+
+
+# SMMD_LINEAR_MV=0: a single-output linear layer through F.linear (hipBLASLt)
+LINEAR_MV = os.environ.get('SMMD_LINEAR_MV', '1') != '0'
 
 
 # SMMD_BN_RELU=0: torch's BatchNorm2d + relu for the generator outside autograd

@@ -1,0 +1,14 @@
+# single-output linear as a matrix-vector product: model tests + interleaved bench A/B
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests/test_gpu_model.py tests/test_gpu_dist.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/r14u_tests.txt 2>&1 || { echo "tests rc=$?"; tail -30 gpurun_out/r14u_tests.txt; exit 1; }
+tail -1 gpurun_out/r14u_tests.txt
+for r in 1 2; do
+  for v in 0 1; do
+    SMMD_LINEAR_MV=$v timeout -k 10 400 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --mmd-sweep 0 --ref-schedule-steps 0 > gpurun_out/r14u_${v}_${r}.json 2> gpurun_out/r14u_${v}_${r}.err || { echo "bench rc=$?"; tail -20 gpurun_out/r14u_${v}_${r}.err; exit 1; }
+    python -c "import json;d=json.load(open('gpurun_out/r14u_${v}_${r}.json'));print('SMMD_LINEAR_MV=$v run $r',d['value'],d['ms_per_step'])"
+  done
+done
+timeout -s KILL 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r14u_trace -o run -- python tools/step_cycle.py --cycles 2 > gpurun_out/r14u_trace.log 2>&1 || { echo "trace rc=$?"; exit 1; }
+echo done
