@@ -70,7 +70,8 @@ int smmd_abi_version(void);         /* bumped on any ABI change (2: Gram/poly,
                                        smmd_sn_clip_g, 10: smmd_wino3x3_conv2*,
                                        smmd_wino4x4s2_conv2*, 11: smmd_fold_up_weight,
                                        smmd_conv1x1*, 12: smmd_wino4x4s2t_conv_mask,
-                                       smmd_row_lrelu_sum, smmd_row_lrelu_bcast) */
+                                       smmd_row_lrelu_sum, smmd_row_lrelu_bcast,
+                                       13: the weight gradients' *_acc forms) */
 const char *smmd_source_hash(void); /* first 16 hex digits of the SHA-256 of the
                                        sources this binary was built from
                                        (csrc .hip and .hpp files in byte order,
@@ -601,6 +602,13 @@ smmd_status smmd_conv3x3_thin_wgrad(const float *gy, const float *x, float *gw, 
                                     int co, int h, int w_img, void *ws, size_t ws_bytes,
                                     smmd_stream_t stream);
 
+/* *_acc: the same weight gradient ADDED into gw (gw += dW, one rounding: the
+ * add autograd would run for a weight used by several convolutions; the
+ * caller's gw holds the earlier contributions), gan.core.convops._late_gw. */
+smmd_status smmd_conv3x3_thin_wgrad_acc(const float *gy, const float *x, float *gw, int n,
+                                        int ci, int co, int h, int w_img, void *ws,
+                                        size_t ws_bytes, smmd_stream_t stream);
+
 /* ---------------------------------------------------------------------------
  * 3x3 stride-1 SAME convolutions as fused Winograd F(2x2, 3x3) on the f32
  * MFMA: the critics' and generators' wide 3x3 layers (snops.conv2d /
@@ -763,6 +771,11 @@ smmd_status smmd_wino3x3_wgrad(const float *x, const float *gy, float *gw, int n
                                int h, int w_img, void *ws, size_t ws_bytes,
                                smmd_stream_t stream);
 
+/* (gw += dW, as smmd_conv3x3_thin_wgrad_acc) */
+smmd_status smmd_wino3x3_wgrad_acc(const float *x, const float *gy, float *gw, int n, int ci,
+                                   int co, int h, int w_img, void *ws, size_t ws_bytes,
+                                   smmd_stream_t stream);
+
 /* ---------------------------------------------------------------------------
  * The weight gradient of the 4x4 stride-2 pad-1 conv (TF's
  * Conv2DBackpropFilter of the folded ConvMeanPool layers, gan/core/resnet/
@@ -786,6 +799,11 @@ size_t smmd_wino4x4s2_wgrad_workspace_bytes(int n, int ci, int co, int h, int w_
 smmd_status smmd_wino4x4s2_wgrad(const float *x, const float *gy, float *gw, int n, int ci,
                                  int co, int h, int w_img, void *ws, size_t ws_bytes,
                                  smmd_stream_t stream);
+
+/* (gw += dW, as smmd_conv3x3_thin_wgrad_acc) */
+smmd_status smmd_wino4x4s2_wgrad_acc(const float *x, const float *gy, float *gw, int n, int ci,
+                                     int co, int h, int w_img, void *ws, size_t ws_bytes,
+                                     smmd_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * The 1x1 stride-1 convolutions of the residual shortcuts (ABI 11;
@@ -819,6 +837,11 @@ size_t smmd_conv1x1_wgrad_workspace_bytes(int n, int c, int k, int p);
 
 smmd_status smmd_conv1x1_wgrad(const float *gy, const float *x, float *gw, int n, int c, int k,
                                int p, void *ws, size_t ws_bytes, smmd_stream_t stream);
+
+/* (gw += dW, as smmd_conv3x3_thin_wgrad_acc) */
+smmd_status smmd_conv1x1_wgrad_acc(const float *gy, const float *x, float *gw, int n, int c,
+                                   int k, int p, void *ws, size_t ws_bytes,
+                                   smmd_stream_t stream);
 
 #ifdef __cplusplus
 }

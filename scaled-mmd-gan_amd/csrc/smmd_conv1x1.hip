@@ -188,7 +188,8 @@ __global__ __launch_bounds__(C1_T) void c1_gemm_kernel(const float *__restrict__
 __global__ __launch_bounds__(C1_T) void c1_wgrad_kernel(const float *__restrict__ gy,
                                                         const float *__restrict__ x,
                                                         float *__restrict__ part, int K, int C,
-                                                        int P, int64_t J, int64_t cps) {
+                                                        int P, int64_t J, int64_t cps,
+                                                        int accum) {
     __shared__ float lds[2 * 2 * C1_WS];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int cb_n = C / 64;
@@ -285,7 +286,8 @@ __global__ __launch_bounds__(C1_T) void c1_wgrad_kernel(const float *__restrict_
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const int k = k0 + kh * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        o[(int64_t)k * C + c0 + ch * 32 + l32] = acc[r];
+        float *d = o + (int64_t)k * C + c0 + ch * 32 + l32;
+        *d = accum ? *d + acc[r] : acc[r];      // accum: one slice straight into dW
     }
 }
 
@@ -295,7 +297,7 @@ __global__ __launch_bounds__(C1_T) void c1_wgrad_kernel(const float *__restrict_
 // one group: the whole sum), 8 loads in flight per thread
 __global__ void c1_sum_kernel(const float4 *__restrict__ part, int S, int G, int64_t n4,
                               float4 *__restrict__ out, const float *__restrict__ bias,
-                              int rowlen, int nb) {
+                              int rowlen, int nb, int accum) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n4) return;
     const int s0 = blockIdx.y * G, s1 = min(S, s0 + G);
@@ -316,7 +318,12 @@ __global__ void c1_sum_kernel(const float4 *__restrict__ part, int S, int G, int
         const float bb = bias[(int)((i * 4 / rowlen) % nb)];
         a.x += bb; a.y += bb; a.z += bb; a.w += bb;
     }
-    out[(int64_t)blockIdx.y * n4 + i] = a;
+    float4 *o = out + (int64_t)blockIdx.y * n4 + i;
+    if (accum) {                                // a weight's later gradient contribution
+        const float4 v = *o;
+        a = make_float4(v.x + a.x, v.y + a.y, v.z + a.z, v.w + a.w);
+    }
+    *o = a;
 }
 
 constexpr int C1_GROUP = 16;
@@ -344,14 +351,14 @@ int c1_slices(int tiles, int64_t nchunk, int min_chunks) {
 // the slab sum of S slabs of n floats (in order; two levels above 2 G slabs)
 // into out; gbuf holds the groups (c1_groups(S) slabs)
 smmd_status c1_reduce(const float *part, int S, int64_t n, float *gbuf, float *out,
-                      const float *bias, int rowlen, int nb, hipStream_t st) {
+                      const float *bias, int rowlen, int nb, hipStream_t st, int accum = 0) {
     const int64_t n4 = n / 4;
     const unsigned gx = (unsigned)((n4 + 255) / 256);
     const int ng = c1_groups(S);
     if (ng > 0) {
         c1_sum_kernel<<<dim3(gx, (unsigned)ng), dim3(256), 0, st>>>(
             reinterpret_cast<const float4 *>(part), S, C1_GROUP, n4,
-            reinterpret_cast<float4 *>(gbuf), nullptr, 1, 1);
+            reinterpret_cast<float4 *>(gbuf), nullptr, 1, 1, 0);
         const smmd_status e = last_launch_status();
         if (e != SMMD_OK) return e;
         part = gbuf;
@@ -359,7 +366,7 @@ smmd_status c1_reduce(const float *part, int S, int64_t n, float *gbuf, float *o
     }
     c1_sum_kernel<<<dim3(gx, 1), dim3(256), 0, st>>>(reinterpret_cast<const float4 *>(part), S, S,
                                                      n4, reinterpret_cast<float4 *>(out), bias,
-                                                     rowlen, nb);
+                                                     rowlen, nb, accum);
     return last_launch_status();
 }
 
@@ -430,9 +437,9 @@ extern "C" size_t smmd_conv1x1_wgrad_workspace_bytes(int n, int c, int k, int p)
     return S > 1 ? (size_t)(S + c1_groups(S)) * k * c * sizeof(float) : 0;
 }
 
-extern "C" smmd_status smmd_conv1x1_wgrad(const float *gy, const float *x, float *gw, int n,
-                                          int c, int k, int p, void *ws, size_t ws_bytes,
-                                          smmd_stream_t stream) {
+static smmd_status c1_wgrad_launch(const float *gy, const float *x, float *gw, int n, int c,
+                                   int k, int p, void *ws, size_t ws_bytes, int accum,
+                                   smmd_stream_t stream) {
     if (!gy || !x || !gw) return SMMD_EINVAL;
     if (!smmd_conv1x1_wgrad_supported(n, c, k, p)) return SMMD_EUNSUPPORTED;
     if (!aligned16(gy) || !aligned16(x) || !aligned16(gw)) return SMMD_EINVAL;
@@ -448,9 +455,22 @@ extern "C" smmd_status smmd_conv1x1_wgrad(const float *gy, const float *x, float
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     float *part = Sused > 1 ? static_cast<float *>(ws) : gw;
     c1_wgrad_kernel<<<dim3((unsigned)tiles, (unsigned)Sused), dim3(C1_T), 0, st>>>(
-        gy, x, part, k, c, p, J, cps);
+        gy, x, part, k, c, p, J, cps, Sused == 1 ? accum : 0);
     smmd_status e = last_launch_status();
     if (e != SMMD_OK || Sused == 1) return e;
     const int64_t total = (int64_t)k * c;
-    return c1_reduce(part, Sused, total, part + (size_t)Sused * total, gw, nullptr, 1, 1, st);
+    return c1_reduce(part, Sused, total, part + (size_t)Sused * total, gw, nullptr, 1, 1, st,
+                     accum);
+}
+
+extern "C" smmd_status smmd_conv1x1_wgrad(const float *gy, const float *x, float *gw, int n,
+                                          int c, int k, int p, void *ws, size_t ws_bytes,
+                                          smmd_stream_t stream) {
+    return c1_wgrad_launch(gy, x, gw, n, c, k, p, ws, ws_bytes, 0, stream);
+}
+
+extern "C" smmd_status smmd_conv1x1_wgrad_acc(const float *gy, const float *x, float *gw, int n,
+                                              int c, int k, int p, void *ws, size_t ws_bytes,
+                                              smmd_stream_t stream) {
+    return c1_wgrad_launch(gy, x, gw, n, c, k, p, ws, ws_bytes, 1, stream);
 }

@@ -490,7 +490,8 @@ constexpr int WF_T = 1024;
 __global__ __launch_bounds__(WF_T) void thin_wgrad_final_kernel(const float *__restrict__ part,
                                                                  int S, int CW, int CT,
                                                                  int thin_in,
-                                                                 float *__restrict__ gw) {
+                                                                 float *__restrict__ gw,
+                                                                 int accum) {
     __shared__ double red[WF_T / 64][64];
     const int E = CW * CT * 9;
     const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
@@ -518,7 +519,7 @@ __global__ __launch_bounds__(WF_T) void thin_wgrad_final_kernel(const float *__r
         const int k = kt / 9, tt = kt - k * 9;
         const size_t dst = thin_in ? ((size_t)c * CT + k) * 9 + tt
                                    : ((size_t)k * CW + c) * 9 + (8 - tt);
-        gw[dst] = (float)t;
+        gw[dst] = accum ? gw[dst] + (float)t : (float)t;   // accum: a later contribution
     }
 }
 
@@ -579,9 +580,9 @@ extern "C" size_t smmd_conv3x3_thin_wgrad_workspace_bytes(int n, int ci, int co,
     return (size_t)n * s * cw * ct * 9 * sizeof(float);
 }
 
-extern "C" smmd_status smmd_conv3x3_thin_wgrad(const float *gy, const float *x, float *gw, int n,
-                                               int ci, int co, int h, int w_img, void *ws,
-                                               size_t ws_bytes, smmd_stream_t stream) {
+static smmd_status thin_wgrad_launch(const float *gy, const float *x, float *gw, int n, int ci,
+                                     int co, int h, int w_img, void *ws, size_t ws_bytes,
+                                     int accum, smmd_stream_t stream) {
     if (n < 0 || ci <= 0 || co <= 0 || h < 0 || w_img < 0) return SMMD_EINVAL;
     if (ci > 4 && co > 4) return SMMD_EUNSUPPORTED;
     if (w_img > SMMD_WAVE) return SMMD_EUNSUPPORTED;
@@ -589,7 +590,7 @@ extern "C" smmd_status smmd_conv3x3_thin_wgrad(const float *gy, const float *x, 
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (n == 0 || h == 0 || w_img == 0) {
         const size_t bytes = (size_t)ci * co * 9 * sizeof(float);
-        return hip_status(hipMemsetAsync(gw, 0, bytes, st));
+        return accum ? SMMD_OK : hip_status(hipMemsetAsync(gw, 0, bytes, st));
     }
     if (!gy || !x) return SMMD_EINVAL;
     const int thin_in = ci <= 4;
@@ -643,6 +644,19 @@ extern "C" smmd_status smmd_conv3x3_thin_wgrad(const float *gy, const float *x, 
     // gy's spatial shift for a thin output side: the kernel shifted the thin
     // tensor by +d(t); gw[o][i][t] = sum_q x[i][q] gy[o][q - d(t)] = R[i][o][8 - t]
     thin_wgrad_final_kernel<<<dim3((E + 63) / 64), dim3(WF_T), 0, st>>>(
-        static_cast<const float *>(ws), S, cw, ct, thin_in, gw);
+        static_cast<const float *>(ws), S, cw, ct, thin_in, gw, accum);
     return last_launch_status();
+}
+
+extern "C" smmd_status smmd_conv3x3_thin_wgrad(const float *gy, const float *x, float *gw, int n,
+                                               int ci, int co, int h, int w_img, void *ws,
+                                               size_t ws_bytes, smmd_stream_t stream) {
+    return thin_wgrad_launch(gy, x, gw, n, ci, co, h, w_img, ws, ws_bytes, 0, stream);
+}
+
+extern "C" smmd_status smmd_conv3x3_thin_wgrad_acc(const float *gy, const float *x, float *gw,
+                                                   int n, int ci, int co, int h, int w_img,
+                                                   void *ws, size_t ws_bytes,
+                                                   smmd_stream_t stream) {
+    return thin_wgrad_launch(gy, x, gw, n, ci, co, h, w_img, ws, ws_bytes, 1, stream);
 }

@@ -291,14 +291,19 @@ __global__ __launch_bounds__(W2_T, 1) void s2_wgrad_kernel(
 }
 
 // out[i] = sum of the S slabs of n4 float4 each, in slab order
+// (acc: out += the sum, a weight's later gradient contribution)
 __global__ void s2w_sum_kernel(const float4 *__restrict__ part, int S, int64_t n4,
-                               float4 *__restrict__ out) {
+                               float4 *__restrict__ out, int acc) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n4) return;
     float4 a = part[i];
     for (int s = 1; s < S; ++s) {
         const float4 v = part[(int64_t)s * n4 + i];
         a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+    if (acc) {
+        const float4 o = out[i];
+        a = make_float4(o.x + a.x, o.y + a.y, o.z + a.z, o.w + a.w);
     }
     out[i] = a;
 }
@@ -377,13 +382,14 @@ extern "C" size_t smmd_wino4x4s2_wgrad_workspace_bytes(int n, int ci, int co, in
 
 // gw [co, ci, 4, 4] = the weight gradient of conv(x [n, ci, h, w], W', stride 2,
 // pad 1) at upstream gy [n, co, h/2, w/2]
-extern "C" smmd_status smmd_wino4x4s2_wgrad(const float *x, const float *gy, float *gw, int n,
-                                            int ci, int co, int h, int w_img, void *ws,
-                                            size_t ws_bytes, smmd_stream_t stream) {
+static smmd_status s2w_launch_all(const float *x, const float *gy, float *gw, int n, int ci,
+                                  int co, int h, int w_img, void *ws, size_t ws_bytes, int acc,
+                                  smmd_stream_t stream) {
     if (n < 0 || ci <= 0 || co <= 0 || h < 0 || w_img < 0 || !gw) return SMMD_EINVAL;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (n == 0 || h == 0 || w_img == 0)
-        return hip_status(hipMemsetAsync(gw, 0, (size_t)co * ci * 16 * sizeof(float), st));
+        return acc ? SMMD_OK
+                   : hip_status(hipMemsetAsync(gw, 0, (size_t)co * ci * 16 * sizeof(float), st));
     if (!x || !gy) return SMMD_EINVAL;
     if (!smmd_wino4x4s2_wgrad_supported(n, ci, co, h, w_img)) return SMMD_EUNSUPPORTED;
     if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(gy) |
@@ -425,6 +431,19 @@ extern "C" smmd_status smmd_wino4x4s2_wgrad(const float *x, const float *gy, flo
         Sfin = ng;
     }
     s2w_sum_kernel<<<dim3((unsigned)((nf4 + 255) / 256)), dim3(256), 0, st>>>(
-        reinterpret_cast<const float4 *>(part), Sfin, nf4, reinterpret_cast<float4 *>(gw));
+        reinterpret_cast<const float4 *>(part), Sfin, nf4, reinterpret_cast<float4 *>(gw), acc);
     return last_launch_status();
+}
+
+extern "C" smmd_status smmd_wino4x4s2_wgrad(const float *x, const float *gy, float *gw, int n,
+                                            int ci, int co, int h, int w_img, void *ws,
+                                            size_t ws_bytes, smmd_stream_t stream) {
+    return s2w_launch_all(x, gy, gw, n, ci, co, h, w_img, ws, ws_bytes, 0, stream);
+}
+
+extern "C" smmd_status smmd_wino4x4s2_wgrad_acc(const float *x, const float *gy, float *gw,
+                                                int n, int ci, int co, int h, int w_img,
+                                                void *ws, size_t ws_bytes,
+                                                smmd_stream_t stream) {
+    return s2w_launch_all(x, gy, gw, n, ci, co, h, w_img, ws, ws_bytes, 1, stream);
 }

@@ -234,7 +234,7 @@ __global__ void wino_wgrad_group_kernel(const float4 *__restrict__ part, int S, 
 
 // dW[k][c] = G^T (sum over slices, in order, of dU) G, G = [[1,0,0],[.5,.5,.5],[.5,-.5,.5],[0,0,1]]
 __global__ void wino_wgrad_final_kernel(const float *__restrict__ part, int S, int K, int C,
-                                        float *__restrict__ dw) {
+                                        float *__restrict__ dw, int acc) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= (int64_t)K * C) return;
     float u[16];
@@ -263,9 +263,12 @@ __global__ void wino_wgrad_final_kernel(const float *__restrict__ part, int S, i
     float *o = dw + idx * 9;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-        o[a * 3 + 0] = t[a][0] + 0.5f * (t[a][1] + t[a][2]);
-        o[a * 3 + 1] = 0.5f * (t[a][1] - t[a][2]);
-        o[a * 3 + 2] = 0.5f * (t[a][1] + t[a][2]) + t[a][3];
+        const float v0 = t[a][0] + 0.5f * (t[a][1] + t[a][2]);
+        const float v1 = 0.5f * (t[a][1] - t[a][2]);
+        const float v2 = 0.5f * (t[a][1] + t[a][2]) + t[a][3];
+        o[a * 3 + 0] = acc ? o[a * 3 + 0] + v0 : v0;
+        o[a * 3 + 1] = acc ? o[a * 3 + 1] + v1 : v1;
+        o[a * 3 + 2] = acc ? o[a * 3 + 2] + v2 : v2;
     }
 }
 
@@ -609,14 +612,20 @@ __global__ __launch_bounds__(WG2_T, 1) void wino_wgrad2_kernel(
 
 // out[i] = sum of the S slabs of n4 float4 each, in slab order (the last
 // level of the r11 slice reduction, straight into dW)
+// (acc: out += the sum, the later contribution of a weight used twice: the
+// same add autograd would run, convops._late_gw)
 __global__ void wino_wgrad_sum_kernel(const float4 *__restrict__ part, int S, int64_t n4,
-                                      float4 *__restrict__ out) {
+                                      float4 *__restrict__ out, int acc) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n4) return;
     float4 a = part[i];
     for (int s = 1; s < S; ++s) {
         const float4 v = part[(int64_t)s * n4 + i];
         a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+    if (acc) {
+        const float4 o = out[i];
+        a = make_float4(o.x + a.x, o.y + a.y, o.z + a.z, o.w + a.w);
     }
     out[i] = a;
 }
@@ -703,13 +712,14 @@ static smmd_status wgrad2_launch(const float *x, const float *gy, float *part, c
 
 // gw [co, ci, 3, 3] = the weight gradient of conv(x [n, ci, h, w], W, stride 1,
 // pad 1) at upstream gy [n, co, h, w]
-extern "C" smmd_status smmd_wino3x3_wgrad(const float *x, const float *gy, float *gw, int n,
-                                          int ci, int co, int h, int w_img, void *ws,
-                                          size_t ws_bytes, smmd_stream_t stream) {
+static smmd_status wgrad3_launch(const float *x, const float *gy, float *gw, int n, int ci,
+                                 int co, int h, int w_img, void *ws, size_t ws_bytes, int acc,
+                                 smmd_stream_t stream) {
     if (n < 0 || ci <= 0 || co <= 0 || h < 0 || w_img < 0 || !gw) return SMMD_EINVAL;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (n == 0 || h == 0 || w_img == 0)
-        return hip_status(hipMemsetAsync(gw, 0, (size_t)co * ci * 9 * sizeof(float), st));
+        return acc ? SMMD_OK
+                   : hip_status(hipMemsetAsync(gw, 0, (size_t)co * ci * 9 * sizeof(float), st));
     if (!x || !gy) return SMMD_EINVAL;
     if (!smmd_wino3x3_wgrad_supported(n, ci, co, h, w_img)) return SMMD_EUNSUPPORTED;
     if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(gy)) & 15) return SMMD_EINVAL;
@@ -750,7 +760,8 @@ extern "C" smmd_status smmd_wino3x3_wgrad(const float *x, const float *gy, float
             Sfin = ng;
         }
         wino_wgrad_sum_kernel<<<dim3((unsigned)((nf4 + 255) / 256)), dim3(256), 0, st>>>(
-            reinterpret_cast<const float4 *>(part), Sfin, nf4, reinterpret_cast<float4 *>(gw));
+            reinterpret_cast<const float4 *>(part), Sfin, nf4, reinterpret_cast<float4 *>(gw),
+            acc);
         return last_launch_status();
     }
     const int64_t nchunks = (g.T + WG_TC - 1) / WG_TC;
@@ -781,6 +792,18 @@ extern "C" smmd_status smmd_wino3x3_wgrad(const float *x, const float *gy, float
         part = grp;
     }
     wino_wgrad_final_kernel<<<dim3((unsigned)((nkc + 255) / 256)), dim3(256), 0, st>>>(
-        part, ng > 0 ? ng : Sused, co, ci, gw);
+        part, ng > 0 ? ng : Sused, co, ci, gw, acc);
     return last_launch_status();
+}
+
+extern "C" smmd_status smmd_wino3x3_wgrad(const float *x, const float *gy, float *gw, int n,
+                                          int ci, int co, int h, int w_img, void *ws,
+                                          size_t ws_bytes, smmd_stream_t stream) {
+    return wgrad3_launch(x, gy, gw, n, ci, co, h, w_img, ws, ws_bytes, 0, stream);
+}
+
+extern "C" smmd_status smmd_wino3x3_wgrad_acc(const float *x, const float *gy, float *gw, int n,
+                                              int ci, int co, int h, int w_img, void *ws,
+                                              size_t ws_bytes, smmd_stream_t stream) {
+    return wgrad3_launch(x, gy, gw, n, ci, co, h, w_img, ws, ws_bytes, 1, stream);
 }

@@ -29,7 +29,7 @@ SN_P1_READY = 1            # smmd_sn_power_iter_ex flag
 ADAM_SN_GDIRECT = 1        # smmd_adam_flat_sn2 flag
 OPT_MAX_FUSED = 96         # tensors smmd_adam_flat_sn takes in one call
 SN_MAX_FUSED = 16          # SN layers smmd_adam_flat_sn takes in one call
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 KIND_RBF, KIND_RQ, KIND_DISTANCE, KIND_DOT = 0, 1, 2, 3
 SMMD_EUNSUPPORTED = 4       # smmd_status (include/smmd_hip.h)
@@ -142,6 +142,7 @@ _SIGS = {
     'smmd_conv1x1_wgrad_supported': (_I, [_I, _I, _I, _I]),
     'smmd_conv1x1_wgrad_workspace_bytes': (_SZ, [_I, _I, _I, _I]),
     'smmd_conv1x1_wgrad': (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _SZ, _P]),
+    'smmd_conv1x1_wgrad_acc': (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _SZ, _P]),
     'smmd_channel_sum_workspace_bytes': (_SZ, [_I, _I]),
     'smmd_channel_sum': (_I, [_P, _I, _I, _I, _P, _P, _SZ, _P]),
     'smmd_conv3x3_thin': (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
@@ -154,6 +155,7 @@ _SIGS = {
     'smmd_bn_relu_bwd': (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _SZ, _P]),
     'smmd_conv3x3_thin_wgrad_workspace_bytes': (_SZ, [_I, _I, _I, _I, _I]),
     'smmd_conv3x3_thin_wgrad': (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P, _SZ, _P]),
+    'smmd_conv3x3_thin_wgrad_acc': (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P, _SZ, _P]),
     'smmd_wino3x3_supported': (_I, [_I, _I, _I, _I, _I]),
     'smmd_wino3x3_filter_bytes': (_SZ, [_I, _I]),
     'smmd_wino3x3_filter': (_I, [_P, _I, _I, _I, _P, _SZ, _P]),
@@ -179,12 +181,14 @@ _SIGS = {
     'smmd_wino3x3_wgrad_supported': (_I, [_I, _I, _I, _I, _I]),
     'smmd_wino3x3_wgrad_workspace_bytes': (_SZ, [_I, _I, _I, _I, _I]),
     'smmd_wino3x3_wgrad': (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P, _SZ, _P]),
+    'smmd_wino3x3_wgrad_acc': (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P, _SZ, _P]),
     'smmd_wino3x3_filter_sn': (_I, [_P, _P, _P, _I, _I, _I, _P, _SZ, _P]),
     'smmd_wino4x4s2_filter_sn': (_I, [_P, _P, _P, _I, _I, _I, _P, _SZ, _P]),
     'smmd_wino4x4s2t_filter_sn': (_I, [_P, _P, _P, _I, _I, _I, _P, _SZ, _P]),
     'smmd_wino4x4s2_wgrad_supported': (_I, [_I, _I, _I, _I, _I]),
     'smmd_wino4x4s2_wgrad_workspace_bytes': (_SZ, [_I, _I, _I, _I, _I]),
     'smmd_wino4x4s2_wgrad': (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P, _SZ, _P]),
+    'smmd_wino4x4s2_wgrad_acc': (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P, _SZ, _P]),
     'smmd_poly_diff_ratio': (_I, [ctypes.POINTER(PolySums), ctypes.POINTER(PolySums),
                                   ctypes.POINTER(PolySums), ctypes.POINTER(PolySums), _I, _P,
                                   _P]),

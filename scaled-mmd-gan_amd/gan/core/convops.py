@@ -111,8 +111,18 @@ def _thin_conv(x, w, b, mode):
     return y
 
 
-def _thin_wgrad(gy, x):
-    """smmd_conv3x3_thin_wgrad: gw[o][i][t] = sum gy[n, o, p] x[n, i, p + d(t)]."""
+def _gw_out(into, shape, like):
+    """the weight gradient's output: a new tensor, or `into` (a contiguous
+    earlier contribution the *_acc entry point adds to; convops._late_gw)."""
+    if into is None:
+        return torch.empty(shape, dtype=like.dtype, device=like.device), ''
+    assert tuple(into.shape) == tuple(shape) and into.is_contiguous()
+    return into, '_acc'
+
+
+def _thin_wgrad(gy, x, into=None):
+    """smmd_conv3x3_thin_wgrad: gw[o][i][t] = sum gy[n, o, p] x[n, i, p + d(t)]
+    (into: added to it)."""
     from . import _lib
     gy = gy.contiguous()
     x = x.contiguous()
@@ -122,11 +132,12 @@ def _thin_wgrad(gy, x):
     L = _lib.lib()
     nbytes = L.smmd_conv3x3_thin_wgrad_workspace_bytes(N, ci, co, H, W)
     ws = _lib.workspace('thin_wgrad', nbytes, gy.device)
-    gw = torch.empty((co, ci, 3, 3), dtype=gy.dtype, device=gy.device)
+    gw, acc = _gw_out(into, (co, ci, 3, 3), gy)
     _lib.add_bytes('smmd_conv3x3_thin_wgrad', (gy.numel() + x.numel()) * 4)
     with _lib.timed('smmd_conv3x3_thin_wgrad'):
-        st = L.smmd_conv3x3_thin_wgrad(_lib.ptr(gy), _lib.ptr(x), _lib.ptr(gw), N, ci, co, H, W,
-                                       _lib.ptr(ws), ws.numel(), _lib.stream_handle(gy.device))
+        st = getattr(L, 'smmd_conv3x3_thin_wgrad' + acc)(
+            _lib.ptr(gy), _lib.ptr(x), _lib.ptr(gw), N, ci, co, H, W, _lib.ptr(ws), ws.numel(),
+            _lib.stream_handle(gy.device))
     _lib.check(st, 'smmd_conv3x3_thin_wgrad')
     return gw
 
@@ -369,8 +380,9 @@ def _wino_conv2(x, w, x2, w2):
 WINO_WGRAD = os.environ.get('SMMD_WINO_WGRAD', '1') != '0'
 
 
-def _wino_wgrad(x, gy):
-    """smmd_wino3x3_wgrad: gw [co, ci, 3, 3] of conv(x, W, stride 1, pad 1) at gy."""
+def _wino_wgrad(x, gy, into=None):
+    """smmd_wino3x3_wgrad: gw [co, ci, 3, 3] of conv(x, W, stride 1, pad 1) at gy
+    (into: added to it)."""
     from . import _lib
     x = x.contiguous()
     gy = gy.contiguous()
@@ -380,12 +392,13 @@ def _wino_wgrad(x, gy):
     L = _lib.lib()
     nb = L.smmd_wino3x3_wgrad_workspace_bytes(N, ci, co, H, W)
     ws = _lib.workspace('wino_wgrad', nb, x.device)
-    gw = torch.empty((co, ci, 3, 3), dtype=x.dtype, device=x.device)
+    gw, acc = _gw_out(into, (co, ci, 3, 3), x)
     _lib.add_bytes('smmd_wino3x3_wgrad', (x.numel() + gy.numel()) * 4)
     _lib.add_flops('smmd_wino3x3_wgrad', 2 * 16 * N * (H // 2) * (W // 2) * ci * co)
     with _lib.timed('smmd_wino3x3_wgrad'):
-        st = L.smmd_wino3x3_wgrad(_lib.ptr(x), _lib.ptr(gy), _lib.ptr(gw), N, ci, co, H, W,
-                                  _lib.ptr(ws), nb, _lib.stream_handle(x.device))
+        st = getattr(L, 'smmd_wino3x3_wgrad' + acc)(
+            _lib.ptr(x), _lib.ptr(gy), _lib.ptr(gw), N, ci, co, H, W, _lib.ptr(ws), nb,
+            _lib.stream_handle(x.device))
     _lib.check(st, 'smmd_wino3x3_wgrad')
     return gw
 
@@ -571,9 +584,9 @@ def _s2_wgrad_ok(x, gy, co):
     return bool(_lib.lib().smmd_wino4x4s2_wgrad_supported(n, ci, co, h, w))
 
 
-def _s2_wgrad(x, gy):
+def _s2_wgrad(x, gy, into=None):
     """smmd_wino4x4s2_wgrad: gw [co, ci, 4, 4] of conv(x, W', stride 2, pad 1)
-    at gy [n, co, h/2, w/2]."""
+    at gy [n, co, h/2, w/2] (into: added to it)."""
     from . import _lib
     _lib.require_cuda(x, gy)
     N, ci, H, W = x.shape
@@ -581,22 +594,24 @@ def _s2_wgrad(x, gy):
     L = _lib.lib()
     nb = L.smmd_wino4x4s2_wgrad_workspace_bytes(N, ci, co, H, W)
     ws = _lib.workspace('wino_s2_wgrad', nb, x.device)
-    gw = torch.empty((co, ci, 4, 4), dtype=x.dtype, device=x.device)
+    gw, acc = _gw_out(into, (co, ci, 4, 4), x)
     _lib.add_bytes('smmd_wino4x4s2_wgrad', (x.numel() + gy.numel()) * 4)
     # 9 point products per 2 x 2 output tile and (phase column, co) pair
     _lib.add_flops('smmd_wino4x4s2_wgrad', 2 * 9 * N * (H // 4) * (W // 4) * 4 * ci * co)
     with _lib.timed('smmd_wino4x4s2_wgrad'):
-        st = L.smmd_wino4x4s2_wgrad(_lib.ptr(x), _lib.ptr(gy), _lib.ptr(gw), N, ci, co, H, W,
-                                    _lib.ptr(ws), nb, _lib.stream_handle(x.device))
+        st = getattr(L, 'smmd_wino4x4s2_wgrad' + acc)(
+            _lib.ptr(x), _lib.ptr(gy), _lib.ptr(gw), N, ci, co, H, W, _lib.ptr(ws), nb,
+            _lib.stream_handle(x.device))
     _lib.check(st, 'smmd_wino4x4s2_wgrad')
     return gw
 
 
-def _s2_weight_grad(gy, x, w, stride, padding):
+def _s2_weight_grad(gy, x, w, stride, padding, into=None):
     """gw of conv(x, w [co, ci, 4, 4], stride 2, pad 1) at gy: the library's
-    polyphase kernel where it tiles the shapes, MIOpen otherwise."""
+    polyphase kernel where it tiles the shapes, MIOpen otherwise (into: added
+    to it; the returned tensor is then `into`)."""
     if _s2_wgrad_ok(x, gy, w.shape[0]):
-        return _s2_wgrad(x.contiguous(), gy.contiguous())
+        return _s2_wgrad(x.contiguous(), gy.contiguous(), into)
     return _aten.convolution_backward(gy, x, w, None, stride, padding, [1, 1], False,
                                       [0, 0], 1, [False, True, False])[1]
 
@@ -703,7 +718,7 @@ def _c1_dx(gy, w):
     return _c1_gemm(_c1_wt(w), gy, None, w.shape[1])
 
 
-def _c1_wgrad(gy, x):
+def _c1_wgrad(gy, x, into=None):
     from . import _lib
     N, C, H, W = x.shape
     K = gy.shape[1]
@@ -712,14 +727,15 @@ def _c1_wgrad(gy, x):
     if (not L.smmd_conv1x1_wgrad_supported(N, C, K, P) or gy.data_ptr() % 16
             or not gy.is_contiguous()):
         return None
-    gw = torch.empty((K, C, 1, 1), dtype=x.dtype, device=x.device)
+    gw, acc = _gw_out(into, (K, C, 1, 1), x)
     nb = L.smmd_conv1x1_wgrad_workspace_bytes(N, C, K, P)
     ws = _lib.workspace('conv1x1_wgrad', nb, x.device) if nb else None
     _lib.add_bytes('smmd_conv1x1_wgrad', (x.numel() + gy.numel() + gw.numel()) * 4)
     _lib.add_flops('smmd_conv1x1_wgrad', 2 * N * P * C * K)
     with _lib.timed('smmd_conv1x1_wgrad'):
-        st = L.smmd_conv1x1_wgrad(_lib.ptr(gy), _lib.ptr(x), _lib.ptr(gw), N, C, K, P,
-                                  _lib.ptr(ws), nb, _lib.stream_handle(x.device))
+        st = getattr(L, 'smmd_conv1x1_wgrad' + acc)(
+            _lib.ptr(gy), _lib.ptr(x), _lib.ptr(gw), N, C, K, P, _lib.ptr(ws), nb,
+            _lib.stream_handle(x.device))
     _lib.check(st, 'smmd_conv1x1_wgrad')
     return gw
 
@@ -761,32 +777,36 @@ def _fwd2(x, w, x2, w2, stride, padding):
     return None
 
 
-def _bwd(gy, x, w, stride, padding, mask, xmask=None):
+def _bwd(gy, x, w, stride, padding, mask, xmask=None, gw_into=None):
     """(Dx, Dw) of conv(x, w) at upstream gy via the native backward kernels.
     xmask (the input x, a ReLU output whose producer skips its mask): Dx
     returned as threshold_backward(Dx, x, 0), inside the stride-2 transposed
-    conv's launch where it runs there."""
-    gx, gw, fused = _bwd_core(gy, x, w, stride, padding, mask, xmask)
+    conv's launch where it runs there.  gw_into: Dw is added into it (the
+    library's *_wgrad_acc kernels, or an add after the others) and returned."""
+    gx, gw, fused = _bwd_core(gy, x, w, stride, padding, mask, xmask, gw_into)
     if xmask is not None and gx is not None and not fused:
         gx = _aten.threshold_backward(gx, xmask, 0.0)
+    if gw_into is not None and gw is not None and gw is not gw_into:
+        gw_into.add_(gw)
+        gw = gw_into
     return gx, gw
 
 
-def _bwd_core(gy, x, w, stride, padding, mask, xmask):
+def _bwd_core(gy, x, w, stride, padding, mask, xmask, into=None):
     """_bwd's kernels: (Dx, Dw, Dx already masked by xmask)."""
     if mask[0] and not (_is_wino(gy, w, stride, padding, 1) or _is_s2t(gy, w, stride, padding)):
         materialize(w)          # a direct reader of w's values below
     if _is_thin(x, w, stride, padding):
         gx = _thin_conv(gy, w, None, 1) if mask[0] else None
-        gw = _thin_wgrad(gy, x) if mask[1] else None
+        gw = _thin_wgrad(gy, x, into) if mask[1] else None
         return gx, gw, False
     if _is_c1(x, w, stride, padding) and _is_c1(gy, w.transpose(0, 1), stride, padding):
         gx = _c1_dx(gy, w) if mask[0] else None
-        gw = _c1_wgrad(gy, x) if mask[1] else None
+        gw = _c1_wgrad(gy, x, into) if mask[1] else None
         if (gx is not None or not mask[0]) and (gw is not None or not mask[1]):
             return gx, gw, False
     if mask[1] and _wgrad_ok(x, gy, w, stride, padding):
-        gw = _wino_wgrad(x, gy)
+        gw = _wino_wgrad(x, gy, into)
         gx = None
         if mask[0]:
             gx = (_wino_conv(gy, w, None, 1) if _is_wino(gy, w, stride, padding, 1) else
@@ -813,7 +833,7 @@ def _bwd_core(gy, x, w, stride, padding, mask, xmask):
                 gx = _aten.convolution_backward(gy, x, w, None, stride, padding, [1, 1], False,
                                                 [0, 0], 1, [True, False, False])[0]
         if mask[1]:
-            gw = _s2_weight_grad(gy, x, w, stride, padding)
+            gw = _s2_weight_grad(gy, x, w, stride, padding, into)
         return gx, gw, fused
     gx, gw, _ = _aten.convolution_backward(gy, x, w, None, stride, padding, [1, 1], False,
                                            [0, 0], 1, [mask[0], mask[1], False])
@@ -845,7 +865,7 @@ class _ConvBackward(torch.autograd.Function):
         x, w, gy = ctx.saved_tensors
         stride, padding, mask_in = ctx.cfg
         need_x, need_w, need_gy = ctx.needs_input_grad[:3]
-        g_x = g_w = g_gy = None
+        g_x = g_w = g_gy = into = None
         if ggx is not None:
             ggx = ggx.contiguous(memory_format=_fmt(x))
             if mask_in:             # gx = m * Dx(gy): its adjoint masks ggx first
@@ -860,7 +880,8 @@ class _ConvBackward(torch.autograd.Function):
             if need_gy and pair is None:
                 g_gy = _fwd(ggx, w, None, stride, padding)
             if need_w:
-                _, g_w = _bwd(gy, ggx, w, stride, padding, (False, True))
+                into = _late_target(w)
+                _, g_w = _bwd(gy, ggx, w, stride, padding, (False, True), None, into)
         if ggw is not None:
             if need_gy and pair is None:
                 t = _fwd(x, ggw, None, stride, padding)
@@ -870,7 +891,7 @@ class _ConvBackward(torch.autograd.Function):
                               x if mask_in else None)
         if pair is not None:
             g_gy = pair
-        return g_x, _late_gw(w, g_w), g_gy, None, None, None, None
+        return g_x, _late_gw(w, g_w, into), g_gy, None, None, None, None
 
 
 # Late sums of weight gradients (SMMD_WGRAD_LATE_SUM=0: off).  A critic
@@ -884,6 +905,7 @@ class _ConvBackward(torch.autograd.Function):
 # contribution exists) first adds the queue in arrival order with one
 # multi-tensor add per round: the same sums in the same order, bit-identical.
 WGRAD_LATE_SUM = os.environ.get('SMMD_WGRAD_LATE_SUM', '1') != '0'
+WGRAD_ACC = os.environ.get('SMMD_WGRAD_ACC', '1') != '0'    # later ones into the first
 _late = {'armed': False, 'first': {}, 'queue': [], 'queued': 0}   # queued: a running count
 
 
@@ -895,8 +917,21 @@ def arm_late_wgrad_sums(on):
     _late['queue'].clear()
 
 
-def _late_gw(w, gw):
-    """gw for autograd, or None with gw queued onto w's first contribution."""
+def _late_target(w):
+    """w's first gradient contribution of the armed backward (a later one is
+    computed straight into it by the library's *_wgrad_acc kernels), or None."""
+    if not (WGRAD_ACC and _late['armed'] and getattr(w, '_smmd_late_sum', False)):
+        return None
+    f = _late['first'].get(id(w))
+    return f[1] if f is not None and f[0] is w else None
+
+
+def _late_gw(w, gw, into=None):
+    """gw for autograd, or None: added into w's first contribution already
+    (into, _late_target), or queued onto it."""
+    if gw is not None and into is not None and gw is into:
+        _late['queued'] += 1
+        return None
     if gw is None or not _late['armed'] or not getattr(w, '_smmd_late_sum', False):
         return gw
     f = _late['first'].get(id(w))
@@ -956,17 +991,20 @@ class _Conv2d(torch.autograd.Function):
         gy = gy.contiguous(memory_format=_fmt(x))
         want_w = ctx.needs_input_grad[1] and _input_only[0] == 0
         want_x = ctx.needs_input_grad[0] and not (_no_dx and x.data_ptr() in _no_dx)
+        into = None
         if torch.is_grad_enabled():          # create_graph: keep it differentiable
             gx, gw = _ConvBackward.apply(x, w, gy, stride, padding, want_w, mask_in)
             if not want_w:
                 gw = None
         elif want_x or want_w:
-            gx, gw = _bwd(gy, x, w, stride, padding, (want_x, want_w), x if mask_in else None)
+            into = _late_target(w) if want_w else None
+            gx, gw = _bwd(gy, x, w, stride, padding, (want_x, want_w), x if mask_in else None,
+                          into)
         else:
             gx = gw = None
         gb = (bias_grad(gy) if (has_b and ctx.needs_input_grad[2] and _input_only[0] == 0)
               else None)
-        return gx, _late_gw(w, gw), gb, None, None, None
+        return gx, _late_gw(w, gw, into), gb, None, None, None
 
 
 def bias_grad(gy):
@@ -1045,17 +1083,19 @@ class _Conv2dReLU(torch.autograd.Function):
             gy = _aten.threshold_backward(gr.contiguous(), r, 0.0)
         want_w = ctx.needs_input_grad[1] and _input_only[0] == 0
         want_x = ctx.needs_input_grad[0] and not (_no_dx and x.data_ptr() in _no_dx)
+        into = None
         if torch.is_grad_enabled():
             gx, gw = _ConvBackward.apply(x, w, gy, stride, padding, want_w)
             if not want_w:
                 gw = None
         elif want_x or want_w:
-            gx, gw = _bwd(gy, x, w, stride, padding, (want_x, want_w))
+            into = _late_target(w) if want_w else None
+            gx, gw = _bwd(gy, x, w, stride, padding, (want_x, want_w), None, into)
         else:
             gx = gw = None
         gb = (bias_grad(gy) if (has_b and ctx.needs_input_grad[2] and _input_only[0] == 0)
               else None)
-        return gx, _late_gw(w, gw), gb, None, None, None
+        return gx, _late_gw(w, gw, into), gb, None, None, None
 
 
 def conv2d_relu(x, w, b=None, stride=1, padding=0, consumer_masks=False):
