@@ -71,7 +71,8 @@ int smmd_abi_version(void);         /* bumped on any ABI change (2: Gram/poly,
                                        smmd_wino4x4s2_conv2*, 11: smmd_fold_up_weight,
                                        smmd_conv1x1*, 12: smmd_wino4x4s2t_conv_mask,
                                        smmd_row_lrelu_sum, smmd_row_lrelu_bcast,
-                                       13: the weight gradients' *_acc forms) */
+                                       13: the weight gradients' *_acc forms,
+                                       14: smmd_wino3x3_conv_mask) */
 const char *smmd_source_hash(void); /* first 16 hex digits of the SHA-256 of the
                                        sources this binary was built from
                                        (csrc .hip and .hpp files in byte order,
@@ -651,6 +652,14 @@ smmd_status smmd_wino3x3_conv(const float *x, const float *u, const float *bias,
 smmd_status smmd_wino3x3_conv_relu(const float *x, const float *u, const float *bias, float *y,
                                    int n, int ci, int ko, int h, int w_img, void *ws,
                                    size_t ws_bytes, smmd_stream_t stream);
+
+/* the same with the next layer's ReLU mask applied to the output: y = (mask <= 0 ?
+ * 0 : conv + bias), mask [n, ko, h, w_img] (TF's relu gradient, threshold_backward's
+ * select).  The double backward's upstream gradient of a conv-ReLU whose consumer
+ * masks (gan/core/resnet/block.py:44-46 -> :63-66; convops _ConvBackward gy_mask). */
+smmd_status smmd_wino3x3_conv_mask(const float *x, const float *u, const float *bias,
+                                   const float *mask, float *y, int n, int ci, int ko, int h,
+                                   int w_img, void *ws, size_t ws_bytes, smmd_stream_t stream);
 
 /* the pair form: y = conv(x, u) + conv(x2, u2) + bias, both inputs [n, ci, h,
  * w_img] and both filters from smmd_wino3x3_filter at the same (ko, ci), in

@@ -129,7 +129,9 @@ __global__ void wino_filter_kernel(const float *__restrict__ w, int KO, int CI, 
 struct WnGeom {
     int N, C, K, H, W, TW, Timg;
     int64_t T, slab;        // slab: floats between split-C partial outputs
-    int relu;               // 1: the output is relu(conv + bias) (not on partial slabs)
+    int relu;               // 1: the output is relu(conv + bias) (not on partial slabs);
+                            // 2: mask <= 0 ? 0 : conv + bias (threshold_backward's select)
+    const float *mask;      // relu 2: of y's shape (smmd_wino3x3_conv_mask)
     // the pair form (smmd_wino3x3_conv2): a second input and filter, the
     // input-channel loop running over both (chunks nch1 .. 2 nch1 - 1 from
     // them), so y = conv(x, U) + conv(x2, U2) in one set of accumulators
@@ -608,7 +610,7 @@ __device__ __forceinline__ W8Block w8_block(const WnGeom &g) {
     return b;
 }
 
-template <bool EDGE, int PH, bool RELU>
+template <bool EDGE, int PH, int EPI>
 __device__ __forceinline__ void wino8_body(const float *__restrict__ x, const float *__restrict__ u,
                                            const float *__restrict__ bias, float *__restrict__ y,
                                            const WnGeom &g) {
@@ -806,6 +808,38 @@ __device__ __forceinline__ void wino8_body(const float *__restrict__ x, const fl
     // through LDS, the stages being free once every wave is past its last
     // MFMA), then each finishes rows 8 PH .. 8 PH + 7 of the quadrant with all
     // 16 points.  X[w][p local][r4][lane] float4 (16 KB per wave).
+    const int partner = w ^ 4;
+    const int64_t et = tile0 + th * 32 + l32;
+    const bool eok = et < g.T;
+    const int en = eok ? (int)(et / g.Timg) : 0;
+    const int er = (int)(et - (int64_t)en * g.Timg);
+    const int ety = er / g.TW, etx = er - ety * g.TW;
+    const int k0 = kb * WN_KB + kh * 32 + 4 * hl;
+    const uint32_t yo =
+        (uint32_t)(((((int64_t)en * g.K + k0) * g.H + 2 * ety) * g.W + 2 * etx) * 4);
+    const uint32_t hw4 = (uint32_t)(HW * 4), yo1 = yo + (uint32_t)g.W * 4;
+    // EPI 2: the mask's 32 values of the lane, loaded before the exchange (a
+    // tile past the end reads zeros at the out-of-range offset and is not stored)
+    f2v mk[2][2][2][2];
+    if constexpr (EPI == 2) {
+        const __amdgpu_buffer_rsrc_t ms = wn_rsrc(g.mask);
+        const uint32_t m0 = eok ? yo : 0x80000000u, m1 = eok ? yo1 : 0x80000000u;
+#pragma unroll
+        for (int r4 = 0; r4 < 2; ++r4)
+#pragma unroll
+            for (int rp = 0; rp < 2; ++rp) {
+                const int r = 8 * PH + 4 * r4 + 2 * rp;
+                const int kr = (r & 3) + 8 * (r >> 2);
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const uint32_t so = (uint32_t)(kr + h) * hw4;
+                    mk[r4][rp][h][0] = __builtin_bit_cast(
+                        f2v, __builtin_amdgcn_raw_buffer_load_b64(ms, m0, so, 0));
+                    mk[r4][rp][h][1] = __builtin_bit_cast(
+                        f2v, __builtin_amdgcn_raw_buffer_load_b64(ms, m1, so, 0));
+                }
+            }
+    }
     __syncthreads();
 #ifdef WN_CLOCK
     ck[3] = __builtin_amdgcn_s_memtime();
@@ -823,21 +857,11 @@ __device__ __forceinline__ void wino8_body(const float *__restrict__ x, const fl
 #ifdef WN_CLOCK
     ck[4] = __builtin_amdgcn_s_memtime();
 #endif
-    const int partner = w ^ 4;
-    const int64_t et = tile0 + th * 32 + l32;
-    const bool eok = et < g.T;
-    const int en = eok ? (int)(et / g.Timg) : 0;
-    const int er = (int)(et - (int64_t)en * g.Timg);
-    const int ety = er / g.TW, etx = er - ety * g.TW;
     // stores: a uniform descriptor on this slab, the lane's byte offset of
     // its row-0 channel (k0) fixed, each row adding a uniform multiple of H W
     // (y under 2 GiB: smmd_wino3x3_supported); each lane stores its own
     // tile's two output rows (8 bytes each, 32 tiles of a row contiguous)
-    const int k0 = kb * WN_KB + kh * 32 + 4 * hl;
-    const uint32_t yo =
-        (uint32_t)(((((int64_t)en * g.K + k0) * g.H + 2 * ety) * g.W + 2 * etx) * 4);
     const __amdgpu_buffer_rsrc_t ys = wn_rsrc(y);
-    const uint32_t hw4 = (uint32_t)(HW * 4), yo1 = yo + (uint32_t)g.W * 4;
     typedef unsigned u2v __attribute__((ext_vector_type(2)));
     // the output transform on row pairs (r, r + 1): both rows' values of a
     // point sit in adjacent registers (acc[p][r], acc[p][r + 1]; the
@@ -866,7 +890,7 @@ __device__ __forceinline__ void wino8_body(const float *__restrict__ x, const fl
             const f2v b = *reinterpret_cast<const f2v *>(Bs + (k0 - kb * WN_KB) + kr);
             f2v y00 = s0[0] + s0[1] + s0[2] + b, y01 = s0[1] - s0[2] - s0[3] + b;
             f2v y10 = s1[0] + s1[1] + s1[2] + b, y11 = s1[1] - s1[2] - s1[3] + b;
-            if constexpr (RELU) {
+            if constexpr (EPI == 1) {
                 y00 = __builtin_elementwise_max(y00, f2v{0.f, 0.f});
                 y01 = __builtin_elementwise_max(y01, f2v{0.f, 0.f});
                 y10 = __builtin_elementwise_max(y10, f2v{0.f, 0.f});
@@ -876,6 +900,13 @@ __device__ __forceinline__ void wino8_body(const float *__restrict__ x, const fl
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     const uint32_t so = (uint32_t)(kr + h) * hw4;
+                    if constexpr (EPI == 2) {     // row 2 ety: (y00, y01), row + 1: (y10, y11)
+                        const f2v a = mk[r4][rp][h][0], c = mk[r4][rp][h][1];
+                        y00[h] = a.x <= 0.f ? 0.f : y00[h];
+                        y01[h] = a.y <= 0.f ? 0.f : y01[h];
+                        y10[h] = c.x <= 0.f ? 0.f : y10[h];
+                        y11[h] = c.y <= 0.f ? 0.f : y11[h];
+                    }
                     __builtin_amdgcn_raw_buffer_store_b64(
                         __builtin_bit_cast(u2v, f2v{y00[h], y01[h]}), ys, yo, so, 0);
                     __builtin_amdgcn_raw_buffer_store_b64(
@@ -894,21 +925,21 @@ __device__ __forceinline__ void wino8_body(const float *__restrict__ x, const fl
 #endif
 }
 
-template <bool EDGE, bool RELU>
+template <bool EDGE, int EPI>
 __global__ __launch_bounds__(W8_T, 1) void wino_conv8_kernel(
     const float *__restrict__ x, const float *__restrict__ u, const float *__restrict__ bias,
     float *__restrict__ y, WnGeom g) {
     if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 8))
-        wino8_body<EDGE, 1, RELU>(x, u, bias, y, g);
+        wino8_body<EDGE, 1, EPI>(x, u, bias, y, g);
     else
-        wino8_body<EDGE, 0, RELU>(x, u, bias, y, g);
+        wino8_body<EDGE, 0, EPI>(x, u, bias, y, g);
 }
 
 // y = bias + sum over the S partial slabs in slice order (float4 when the
 // plane size allows)
 __global__ void wino_reduce_kernel(const float *__restrict__ part, const float *__restrict__ bias,
                                    float *__restrict__ y, int64_t n4, int S, int K, int HW,
-                                   int relu) {
+                                   int relu, const float *__restrict__ mask) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n4) return;
     const float4 *p4 = reinterpret_cast<const float4 *>(part);
@@ -921,8 +952,14 @@ __global__ void wino_reduce_kernel(const float *__restrict__ part, const float *
         const float b = bias[(int)((i * 4 / HW) % K)];
         s.x += b; s.y += b; s.z += b; s.w += b;
     }
-    if (relu) {
+    if (relu == 1) {
         s.x = fmaxf(s.x, 0.f); s.y = fmaxf(s.y, 0.f); s.z = fmaxf(s.z, 0.f); s.w = fmaxf(s.w, 0.f);
+    } else if (relu == 2) {
+        const float4 m = reinterpret_cast<const float4 *>(mask)[i];
+        s.x = m.x <= 0.f ? 0.f : s.x;
+        s.y = m.y <= 0.f ? 0.f : s.y;
+        s.z = m.z <= 0.f ? 0.f : s.z;
+        s.w = m.w <= 0.f ? 0.f : s.w;
     }
     reinterpret_cast<float4 *>(y)[i] = s;
 }
@@ -1011,17 +1048,20 @@ extern "C" size_t smmd_wino3x3_workspace_bytes(int n, int ci, int ko, int h, int
 static smmd_status wino3x3_conv(const float *x, const float *u, const float *x2,
                                 const float *u2, const float *bias, float *y, int n, int ci,
                                 int ko, int h, int w_img, void *ws, size_t ws_bytes, int relu,
-                                smmd_stream_t stream) {
+                                smmd_stream_t stream, const float *mask = nullptr) {
     if (n < 0 || ci <= 0 || ko <= 0 || h < 0 || w_img < 0) return SMMD_EINVAL;
     if (n == 0 || h == 0 || w_img == 0) return SMMD_OK;
-    if (!x || !u || !y || (!x2 != !u2)) return SMMD_EINVAL;
+    if (!x || !u || !y || (!x2 != !u2) || ((relu == 2) != (mask != nullptr))) return SMMD_EINVAL;
     if (!smmd_wino3x3_supported(n, ci, ko, h, w_img)) return SMMD_EUNSUPPORTED;
     if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y) |
          reinterpret_cast<uintptr_t>(u) | reinterpret_cast<uintptr_t>(x2) |
-         reinterpret_cast<uintptr_t>(u2)) & 15)
+         reinterpret_cast<uintptr_t>(u2) | reinterpret_cast<uintptr_t>(mask)) & 15)
         return SMMD_EINVAL;
+    // the mask epilogue is the 8-wave kernel's (the 4-wave form: unsupported)
+    if (relu == 2 && !wino8_enabled()) return SMMD_EUNSUPPORTED;
     const int pair = x2 ? 2 : 1;
     WnGeom g;
+    g.mask = mask;
     g.x2 = x2;
     g.u2 = u2;
     g.N = n; g.C = ci; g.K = ko; g.H = h; g.W = w_img;
@@ -1040,12 +1080,14 @@ static smmd_status wino3x3_conv(const float *x, const float *u, const float *x2,
     }
     static bool attr = false;
     if (!attr) {
-        const void *ks[6] = {reinterpret_cast<const void *>(wino_conv_kernel<false>),
+        const void *ks[8] = {reinterpret_cast<const void *>(wino_conv_kernel<false>),
                              reinterpret_cast<const void *>(wino_conv_kernel<true>),
-                             reinterpret_cast<const void *>(wino_conv8_kernel<false, false>),
-                             reinterpret_cast<const void *>(wino_conv8_kernel<true, false>),
-                             reinterpret_cast<const void *>(wino_conv8_kernel<false, true>),
-                             reinterpret_cast<const void *>(wino_conv8_kernel<true, true>)};
+                             reinterpret_cast<const void *>(wino_conv8_kernel<false, 0>),
+                             reinterpret_cast<const void *>(wino_conv8_kernel<true, 0>),
+                             reinterpret_cast<const void *>(wino_conv8_kernel<false, 1>),
+                             reinterpret_cast<const void *>(wino_conv8_kernel<true, 1>),
+                             reinterpret_cast<const void *>(wino_conv8_kernel<false, 2>),
+                             reinterpret_cast<const void *>(wino_conv8_kernel<true, 2>)};
         for (const void *k : ks)
             if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)WN_LDS) !=
                 hipSuccess)
@@ -1065,8 +1107,12 @@ static smmd_status wino3x3_conv(const float *x, const float *u, const float *x2,
         g.S = S;
         const int64_t nblk = tb * g.KB * S;
         if (nblk > 0x7fffffff) return SMMD_EINVAL;
-        auto k8 = edge ? (g.relu ? wino_conv8_kernel<true, true> : wino_conv8_kernel<true, false>)
-                       : (g.relu ? wino_conv8_kernel<false, true> : wino_conv8_kernel<false, false>);
+        auto k8 = edge ? (g.relu == 2   ? wino_conv8_kernel<true, 2>
+                          : g.relu ? wino_conv8_kernel<true, 1>
+                                   : wino_conv8_kernel<true, 0>)
+                       : (g.relu == 2   ? wino_conv8_kernel<false, 2>
+                          : g.relu ? wino_conv8_kernel<false, 1>
+                                   : wino_conv8_kernel<false, 0>);
         k8<<<dim3((unsigned)nblk), dim3(W8_T), WN_LDS, st>>>(x, u, b1, out, g);
     } else if (!edge) {
         wino_conv_kernel<false><<<grid, dim3(WN_T), WN_LDS, st>>>(x, u, b1, out, g);
@@ -1077,7 +1123,7 @@ static smmd_status wino3x3_conv(const float *x, const float *u, const float *x2,
     if (e != SMMD_OK || S == 1) return e;
     const int64_t n4 = total / 4;
     wino_reduce_kernel<<<dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st>>>(
-        out, bias, y, n4, S, ko, h * w_img, relu);
+        out, bias, y, n4, S, ko, h * w_img, relu, mask);
     return last_launch_status();
 }
 
@@ -1108,4 +1154,17 @@ extern "C" smmd_status smmd_wino3x3_conv_relu(const float *x, const float *u, co
                                               void *ws, size_t ws_bytes, smmd_stream_t stream) {
     return wino3x3_conv(x, u, nullptr, nullptr, bias, y, n, ci, ko, h, w_img, ws, ws_bytes, 1,
                         stream);
+}
+
+// y = (mask <= 0 ? 0 : conv(x, U) + bias), mask of y's shape: the input
+// gradient's ReLU mask of the next layer applied in the epilogue (convops
+// _ConvBackward's gy_mask: the double backward's upstream gradient of a
+// conv-ReLU whose consumer masks)
+extern "C" smmd_status smmd_wino3x3_conv_mask(const float *x, const float *u, const float *bias,
+                                              const float *mask, float *y, int n, int ci, int ko,
+                                              int h, int w_img, void *ws, size_t ws_bytes,
+                                              smmd_stream_t stream) {
+    if (!mask) return SMMD_EINVAL;
+    return wino3x3_conv(x, u, nullptr, nullptr, bias, y, n, ci, ko, h, w_img, ws, ws_bytes, 2,
+                        stream, mask);
 }

@@ -323,10 +323,11 @@ def clear_wino_cache():
     _wino_cache_bytes[0] = 0
 
 
-def _wino_conv(x, w, b, mode, relu=False):
+def _wino_conv(x, w, b, mode, relu=False, mask=None):
     """smmd_wino3x3_filter + smmd_wino3x3_conv: mode 0 conv(x, w) + b
     (w [co, ci, 3, 3]); mode 1 the input gradient of a conv with weight
-    w [ci', co', 3, 3] at upstream x."""
+    w [ci', co', 3, 3] at upstream x.  mask (y's shape): y = (mask <= 0 ? 0 :
+    y), smmd_wino3x3_conv_mask."""
     from . import _lib
     x = x.contiguous()
     w = w.contiguous()
@@ -343,10 +344,16 @@ def _wino_conv(x, w, b, mode, relu=False):
     _lib.add_bytes('smmd_wino3x3_conv', (x.numel() + y.numel()) * 4)
     # 16 transform-point products per 2 x 2 output tile and (ci, co) pair
     _lib.add_flops('smmd_wino3x3_conv', 2 * 16 * N * (H // 2) * (W // 2) * ci * co)
-    fn = L.smmd_wino3x3_conv_relu if relu else L.smmd_wino3x3_conv
     with _lib.timed('smmd_wino3x3_conv'):
-        st = fn(_lib.ptr(x), _lib.ptr(u), _lib.ptr(b), _lib.ptr(y), N, ci, co, H, W, _lib.ptr(ws),
-                nb, _lib.stream_handle(x.device))
+        if mask is not None:
+            assert mask.shape == y.shape and mask.is_contiguous() and mask.dtype == y.dtype
+            st = L.smmd_wino3x3_conv_mask(_lib.ptr(x), _lib.ptr(u), _lib.ptr(b), _lib.ptr(mask),
+                                          _lib.ptr(y), N, ci, co, H, W, _lib.ptr(ws), nb,
+                                          _lib.stream_handle(x.device))
+        else:
+            fn = L.smmd_wino3x3_conv_relu if relu else L.smmd_wino3x3_conv
+            st = fn(_lib.ptr(x), _lib.ptr(u), _lib.ptr(b), _lib.ptr(y), N, ci, co, H, W,
+                    _lib.ptr(ws), nb, _lib.stream_handle(x.device))
     _lib.check(st, 'smmd_wino3x3_conv')
     return y
 
@@ -745,8 +752,15 @@ def _is_thin(x, w, stride, padding):
         and w.shape[2] == w.shape[3]
 
 
-def _fwd(x, w, b, stride, padding):
-    """conv(x, w) + b: the library's thin kernel or MIOpen."""
+def _fwd(x, w, b, stride, padding, ymask=None):
+    """conv(x, w) + b: the library's kernels or MIOpen.  ymask (the output's
+    shape): the result masked as threshold_backward(y, ymask, 0), in the 3x3
+    Winograd kernel's epilogue where it runs there."""
+    if ymask is not None:
+        if (_is_wino(x, w, stride, padding, 0) and ymask.is_contiguous()
+                and os.environ.get('SMMD_WINO8', '1') != '0'):
+            return _wino_conv(x, w, b, 0, mask=ymask)
+        return _aten.threshold_backward(_fwd(x, w, b, stride, padding), ymask, 0.0)
     if _is_thin(x, w, stride, padding):
         return _thin_conv(x, materialize(w), b, 0)
     if _is_wino(x, w, stride, padding, 0):
@@ -844,12 +858,17 @@ class _ConvBackward(torch.autograd.Function):
     """(gx, gw) = backward of conv(x, w); differentiable once more.  mask_in:
     gx = threshold_backward(Dx, x, 0) (x a ReLU output whose producer skips
     its mask, _Conv2d's mask_in), and so is the gradient this node returns
-    for x."""
+    for x.  gy_mask (gy is that masked gx of a mask_in node, _Conv2dReLU with
+    consumer_masks): the gradient this node returns for gy is masked by it --
+    in the 3x3 Winograd epilogue (smmd_wino3x3_conv_mask) -- and the mask_in
+    node, whose only upstream that is, skips its own mask of it
+    (_ggx_masked; the select is idempotent, so the result is bit-identical)."""
 
     @staticmethod
-    def forward(ctx, x, w, gy, stride, padding, want_w, mask_in=False):
-        ctx.save_for_backward(x, w, gy)
+    def forward(ctx, x, w, gy, stride, padding, want_w, mask_in=False, gy_mask=None):
+        ctx.save_for_backward(x, w, gy, gy_mask)
         ctx.cfg = (stride, padding, mask_in)
+        ctx._smmd_mask_in = bool(mask_in)
         # an output nobody differentiates (the placeholder gw of the input-only
         # Jacobian pass, or gx/gw unused by the loss) arrives as None instead
         # of a materialised zero tensor: otherwise every critic conv of the
@@ -862,15 +881,18 @@ class _ConvBackward(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, ggx, ggw):
-        x, w, gy = ctx.saved_tensors
+        x, w, gy, gy_mask = ctx.saved_tensors
         stride, padding, mask_in = ctx.cfg
         need_x, need_w, need_gy = ctx.needs_input_grad[:3]
         g_x = g_w = g_gy = into = None
         if ggx is not None:
             ggx = ggx.contiguous(memory_format=_fmt(x))
-            if mask_in:             # gx = m * Dx(gy): its adjoint masks ggx first
+            # gx = m * Dx(gy): its adjoint masks ggx first (unless the node
+            # that produced ggx masked it already, _Conv2dReLU's gy_mask)
+            if mask_in and not getattr(ctx, '_smmd_ggx_masked', False):
                 ggx = (_ReluMask.apply(ggx, x) if torch.is_grad_enabled()
                        else _aten.threshold_backward(ggx, x, 0.0))
+        fused_mask = gy_mask is not None and not torch.is_grad_enabled()
         # the upstream's gradient conv(ggx, w) + conv(x, ggw): one pair launch
         # when both take the same Winograd path, else two convs and their sum
         pair = None
@@ -878,7 +900,8 @@ class _ConvBackward(torch.autograd.Function):
             pair = _fwd2(ggx, w, x, ggw, stride, padding)
         if ggx is not None:
             if need_gy and pair is None:
-                g_gy = _fwd(ggx, w, None, stride, padding)
+                g_gy = _fwd(ggx, w, None, stride, padding,
+                            gy_mask if fused_mask and ggw is None else None)
             if need_w:
                 into = _late_target(w)
                 _, g_w = _bwd(gy, ggx, w, stride, padding, (False, True), None, into)
@@ -891,7 +914,11 @@ class _ConvBackward(torch.autograd.Function):
                               x if mask_in else None)
         if pair is not None:
             g_gy = pair
-        return g_x, _late_gw(w, g_w, into), g_gy, None, None, None, None
+        if gy_mask is not None and g_gy is not None and not (fused_mask and ggx is not None
+                                                             and ggw is None):
+            g_gy = (_ReluMask.apply(g_gy.contiguous(), gy_mask) if torch.is_grad_enabled()
+                    else _aten.threshold_backward(g_gy, gy_mask, 0.0))
+        return g_x, _late_gw(w, g_w, into), g_gy, None, None, None, None, None
 
 
 # Late sums of weight gradients (SMMD_WGRAD_LATE_SUM=0: off).  A critic
@@ -1083,9 +1110,14 @@ class _Conv2dReLU(torch.autograd.Function):
             gy = _aten.threshold_backward(gr.contiguous(), r, 0.0)
         want_w = ctx.needs_input_grad[1] and _input_only[0] == 0
         want_x = ctx.needs_input_grad[0] and not (_no_dx and x.data_ptr() in _no_dx)
+        want_b = has_b and ctx.needs_input_grad[2] and _input_only[0] == 0
         into = None
         if torch.is_grad_enabled():
-            gx, gw = _ConvBackward.apply(x, w, gy, stride, padding, want_w)
+            # (a differentiable bias gradient is a second consumer of gr: then
+            # the mask_in node keeps its own mask)
+            gx, gw = _ConvBackward.apply(
+                x, w, gy, stride, padding, want_w, False,
+                r if consumer_masks and not want_b and _ggx_masked(gr) else None)
             if not want_w:
                 gw = None
         elif want_x or want_w:
@@ -1093,9 +1125,26 @@ class _Conv2dReLU(torch.autograd.Function):
             gx, gw = _bwd(gy, x, w, stride, padding, (want_x, want_w), None, into)
         else:
             gx = gw = None
-        gb = (bias_grad(gy) if (has_b and ctx.needs_input_grad[2] and _input_only[0] == 0)
-              else None)
+        gb = bias_grad(gy) if want_b else None
         return gx, _late_gw(w, gw, into), gb, None, None, None
+
+
+# the double backward's gradient of a consumer-masked conv-ReLU's upstream
+# masked where it is produced (SMMD_GGX_MASK_FUSE=0: by the consumer)
+GGX_MASK_FUSE = os.environ.get('SMMD_GGX_MASK_FUSE', '1') != '0'
+
+
+def _ggx_masked(gr):
+    """gr (a consumer-masked ReLU output's gradient) is exactly the input
+    gradient of one mask_in _ConvBackward node: mark that node so that it
+    skips its mask of the gradient it receives for gr -- which then comes
+    only from the node built on gr here, masking it (_ConvBackward gy_mask)."""
+    fn = gr.grad_fn
+    if not (GGX_MASK_FUSE and fn is not None and gr.output_nr == 0
+            and getattr(fn, '_smmd_mask_in', False)):
+        return False
+    fn._smmd_ggx_masked = True
+    return True
 
 
 def conv2d_relu(x, w, b=None, stride=1, padding=0, consumer_masks=False):

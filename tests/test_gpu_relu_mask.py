@@ -4,7 +4,10 @@ conv2d(mask_in), ResidualBlock.down_parts): the masked transposed conv is
 bit-identical to the transposed conv followed by threshold_backward, with and
 without the split-K slab sum, and the block's gradients -- first order and
 through the scaling regulariser's double backward -- are bit-identical to the
-unfused path (the ReLU's own threshold_backward) and match float64."""
+unfused path (the ReLU's own threshold_backward) and match float64.  In the
+double backward the consumer's mask of its upstream gradient moves into the
+producing 3x3 Winograd conv's epilogue (smmd_wino3x3_conv_mask, ABI 14;
+convops _ConvBackward gy_mask), again bit-identical."""
 import pytest
 
 torch = pytest.importorskip('torch')
@@ -131,3 +134,59 @@ def test_critic_tail_vs_torch(order):
     if order == 1:
         plain = _tail_run(lambda u, v: F.leaky_relu(u + v, 0.2).sum(dim=(2, 3)), u0, v0, t, 1)
         assert torch.equal(got[1], plain[1]) and torch.equal(got[2], plain[2])
+
+
+# (N, C, K, H): conv(x [N, C, H, H], w [K, C, 3, 3]) masked by m [N, K, H, H]:
+# the critic's 64- and 128-channel first convs at batch 64 (one launch), the
+# deep ones (split-C slabs: the mask in the slab reduction), a tile row that
+# does not divide the wave (the EDGE kernel)
+WINO_MASK = [(64, 64, 64, 64), (64, 128, 128, 32), (64, 512, 512, 8), (4, 64, 64, 16),
+             (2, 64, 64, 12)]
+
+
+@pytest.mark.parametrize('shape', WINO_MASK)
+def test_wino_conv_mask_equals_threshold_after(shape):
+    from gan.core import convops
+    N, C, K, H = shape
+    g = torch.Generator(device=DEV).manual_seed(N + C + K + H)
+    x = torch.randn(N, C, H, H, device=DEV, generator=g)
+    w = torch.randn(K, C, 3, 3, device=DEV, generator=g) / (9 * C) ** 0.5
+    b = torch.randn(K, device=DEV, generator=g)
+    m = torch.randn(N, K, H, H, device=DEV, generator=g)
+    m[0, 0, :2] = 0.0                       # threshold_backward's (mask <= 0) boundary
+    assert convops._is_wino(x, w, [1, 1], [1, 1], 0)
+    for bias in (None, b):
+        fused = convops._wino_conv(x, w, bias, 0, mask=m)
+        plain = torch.ops.aten.threshold_backward(convops._wino_conv(x, w, bias, 0), m, 0.0)
+        assert torch.equal(fused, plain)
+    # the dispatcher's route (convops._fwd ymask) is the fused launch
+    assert torch.equal(convops._fwd(x, w, b, [1, 1], [1, 1], ymask=m), fused)
+
+
+def _count_thresholds(fn):
+    from torch.profiler import ProfilerActivity, profile
+    with profile(activities=[ProfilerActivity.CPU]) as prof:
+        out = fn()
+    return out, sum(1 for e in prof.events() if e.name == 'aten::threshold_backward')
+
+
+@pytest.mark.parametrize('shape', [(4, 64, 128, 16), (64, 64, 128, 64)])
+def test_double_backward_mask_moves_to_producer(shape, monkeypatch):
+    """The scaling regulariser's double backward through conv-ReLU -> stride-2
+    conv: with the upstream mask in the producer's epilogue the gradients are
+    bit-identical to the consumer masking it, with one threshold_backward
+    fewer."""
+    from gan.core import convops
+    N, C, K, H = shape
+    g = torch.Generator(device=DEV).manual_seed(N + C + K + H + 9)
+    x0 = torch.randn(N, C, H, H, device=DEV, generator=g)
+    w1 = torch.randn(C, C, 3, 3, device=DEV, generator=g) / (9 * C) ** 0.5
+    w2 = torch.randn(K, C, 4, 4, device=DEV, generator=g) / (16 * C) ** 0.5
+    t1 = torch.randn(N, K, H // 2, H // 2, device=DEV, generator=g)
+    t2 = torch.randn(N, K, H // 2, H // 2, device=DEV, generator=g)
+    on, n_on = _count_thresholds(lambda: _block(True, x0, w1, w2, t1, t2, 2))
+    monkeypatch.setattr(convops, 'GGX_MASK_FUSE', False)
+    off, n_off = _count_thresholds(lambda: _block(True, x0, w1, w2, t1, t2, 2))
+    for a, b, what in zip(on, off, ('dx', 'dw1', 'dw2')):
+        assert torch.equal(a, b), what
+    assert n_on == n_off - 1, (n_on, n_off)
