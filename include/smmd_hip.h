@@ -72,7 +72,8 @@ int smmd_abi_version(void);         /* bumped on any ABI change (2: Gram/poly,
                                        smmd_conv1x1*, 12: smmd_wino4x4s2t_conv_mask,
                                        smmd_row_lrelu_sum, smmd_row_lrelu_bcast,
                                        13: the weight gradients' *_acc forms,
-                                       14: smmd_wino3x3_conv_mask) */
+                                       14: smmd_wino3x3_conv_mask,
+                                       15: smmd_wino4x4s2_conv_acc) */
 const char *smmd_source_hash(void); /* first 16 hex digits of the SHA-256 of the
                                        sources this binary was built from
                                        (csrc .hip and .hpp files in byte order,
@@ -713,6 +714,14 @@ size_t smmd_wino4x4s2t_workspace_bytes(int n, int k, int c, int hg, int wg);
 smmd_status smmd_wino4x4s2_conv(const float *x, const float *u, const float *bias, float *y,
                                 int n, int ci, int ko, int h, int w_img, void *ws,
                                 size_t ws_bytes, smmd_stream_t stream);
+
+/* the same added into y: y += conv(x, W') + bias (the earlier value first, so
+ * y_old + result, autograd's sum of two gradient contributions; convops
+ * _ConvBackward: a critic block's main-path and shortcut gradients of the
+ * gradient both read, in the scaling regulariser's double backward) */
+smmd_status smmd_wino4x4s2_conv_acc(const float *x, const float *u, const float *bias, float *y,
+                                    int n, int ci, int ko, int h, int w_img, void *ws,
+                                    size_t ws_bytes, smmd_stream_t stream);
 
 smmd_status smmd_wino4x4s2t_conv(const float *gy, const float *u, const float *bias, float *dx,
                                  int n, int k, int c, int hg, int wg, void *ws, size_t ws_bytes,

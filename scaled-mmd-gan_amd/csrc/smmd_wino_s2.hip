@@ -183,7 +183,8 @@ __device__ __forceinline__ void s2_mfma_chunk(f32x16 (&acc)[9], const float4 *U,
 #define S2_SLOT 20
 #endif
 
-template <bool EDGE>
+// ACC: y += the result (smmd_wino4x4s2_conv_acc, one slab only)
+template <bool EDGE, bool ACC>
 __global__ __launch_bounds__(S2_T, 2) void s2_conv_kernel(
     const float *__restrict__ x, const float *__restrict__ u, const float *__restrict__ bias,
     float *__restrict__ y, S2Geom g) {
@@ -401,6 +402,20 @@ __global__ __launch_bounds__(S2_T, 2) void s2_conv_kernel(
     const uint32_t o1 = o0 + (uint32_t)Wo * 4;
     const uint32_t hw4 = (uint32_t)Ho * (uint32_t)Wo * 4;
     const __amdgpu_buffer_rsrc_t ys = s2_rsrc(y);
+    // ACC: the earlier values, all loaded before the first store (a load
+    // after a store to the same buffer would wait for it: one latency per row
+    // pair instead of one per block)
+    f2v yo[16][2];
+    if constexpr (ACC) {
+#pragma unroll
+        for (int r = 0; r < 16; r += 2)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const uint32_t so = (uint32_t)((r & 3) + 8 * (r >> 2) + h) * hw4;
+                yo[r + h][0] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(ys, o0, so, 0));
+                yo[r + h][1] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(ys, o1, so, 0));
+            }
+    }
 #ifdef S2_NO_EPI
     for (int r = 0; r < 2; r += 2) {
 #else
@@ -419,11 +434,18 @@ __global__ __launch_bounds__(S2_T, 2) void s2_conv_kernel(
             s1[j] = m[3 + j] + m[6 + j];
         }
         const f2v b = *reinterpret_cast<const f2v *>(Bs + kl0 + kr);
-        const f2v y00 = s0[0] + s0[1] + b, y01 = s0[1] + s0[2] + b;
-        const f2v y10 = s1[0] + s1[1] + b, y11 = s1[1] + s1[2] + b;
+        f2v y00 = s0[0] + s0[1] + b, y01 = s0[1] + s0[2] + b;
+        f2v y10 = s1[0] + s1[1] + b, y11 = s1[1] + s1[2] + b;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const uint32_t so = (uint32_t)(kr + h) * hw4;
+            if constexpr (ACC) {    // the earlier contribution + this one (autograd's sum)
+                const f2v a = yo[r + h][0], c = yo[r + h][1];
+                y00[h] = a.x + y00[h];
+                y01[h] = a.y + y01[h];
+                y10[h] = c.x + y10[h];
+                y11[h] = c.y + y11[h];
+            }
             __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, f2v{y00[h], y01[h]}), ys, o0, so, 0);
             __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, f2v{y10[h], y11[h]}), ys, o1, so, 0);
         }
@@ -802,7 +824,7 @@ __global__ __launch_bounds__(S2_T, 2) void s2t_conv_kernel(
 // (mask: the transposed conv's ReLU mask, applied after the bias)
 __global__ void s2_reduce_kernel(const float *__restrict__ part, const float *__restrict__ bias,
                                  float *__restrict__ y, int64_t n4, int S, int K, int HW,
-                                 const float *__restrict__ mask) {
+                                 const float *__restrict__ mask, int acc) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n4) return;
     const float4 *p4 = reinterpret_cast<const float4 *>(part);
@@ -821,6 +843,10 @@ __global__ void s2_reduce_kernel(const float *__restrict__ part, const float *__
         s.y = mv.y <= 0.f ? 0.f : s.y;
         s.z = mv.z <= 0.f ? 0.f : s.z;
         s.w = mv.w <= 0.f ? 0.f : s.w;
+    }
+    if (acc) {                  // y += the result
+        const float4 o = reinterpret_cast<const float4 *>(y)[i];
+        s = make_float4(o.x + s.x, o.y + s.y, o.z + s.z, o.w + s.w);
     }
     reinterpret_cast<float4 *>(y)[i] = s;
 }
@@ -897,7 +923,7 @@ extern "C" size_t smmd_wino4x4s2_workspace_bytes(int n, int ci, int ko, int h, i
 
 static smmd_status s2_conv(const float *x, const float *u, const float *x2, const float *u2,
                            const float *bias, float *y, int n, int ci, int ko, int h, int w_img,
-                           void *ws, size_t ws_bytes, smmd_stream_t stream) {
+                           void *ws, size_t ws_bytes, smmd_stream_t stream, int acc = 0) {
     if (n < 0 || ci <= 0 || ko <= 0 || h < 0 || w_img < 0) return SMMD_EINVAL;
     if (n == 0 || h == 0 || w_img == 0) return SMMD_OK;
     if (!x || !u || !y || (!x2 != !u2)) return SMMD_EINVAL;
@@ -927,28 +953,30 @@ static smmd_status s2_conv(const float *x, const float *u, const float *x2, cons
     }
     static bool attr = false;
     if (!attr) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void *>(s2_conv_kernel<false>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)S2_LDS) != hipSuccess ||
-            hipFuncSetAttribute(reinterpret_cast<const void *>(s2_conv_kernel<true>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)S2_LDS) != hipSuccess)
-            return SMMD_EHIP;
+        const void *ks[4] = {reinterpret_cast<const void *>(s2_conv_kernel<false, false>),
+                             reinterpret_cast<const void *>(s2_conv_kernel<true, false>),
+                             reinterpret_cast<const void *>(s2_conv_kernel<false, true>),
+                             reinterpret_cast<const void *>(s2_conv_kernel<true, true>)};
+        for (const void *k : ks)
+            if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)S2_LDS) !=
+                hipSuccess)
+                return SMMD_EHIP;
         attr = true;
     }
     g.slab = S > 1 ? total : 0;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const dim3 grid((unsigned)tb, (unsigned)(ko / S2_KB), (unsigned)S);
     const float *b1 = S > 1 ? nullptr : bias;
-    if (64 % g.TW == 0)
-        s2_conv_kernel<false><<<grid, dim3(S2_T), S2_LDS, st>>>(x, u, b1, out, g);
-    else
-        s2_conv_kernel<true><<<grid, dim3(S2_T), S2_LDS, st>>>(x, u, b1, out, g);
+    const bool ka = acc && S == 1;      // sliced: the reduction adds
+    auto k = 64 % g.TW == 0 ? (ka ? s2_conv_kernel<false, true> : s2_conv_kernel<false, false>)
+                            : (ka ? s2_conv_kernel<true, true> : s2_conv_kernel<true, false>);
+    k<<<grid, dim3(S2_T), S2_LDS, st>>>(x, u, b1, out, g);
     smmd_status e = last_launch_status();
     if (e != SMMD_OK || S == 1) return e;
     const int64_t n4 = total / 4;
     s2_reduce_kernel<<<dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st>>>(out, bias, y, n4,
-                                                                              S, ko, HWo, nullptr);
+                                                                              S, ko, HWo, nullptr,
+                                                                              acc);
     return last_launch_status();
 }
 
@@ -956,6 +984,16 @@ extern "C" smmd_status smmd_wino4x4s2_conv(const float *x, const float *u, const
                                            float *y, int n, int ci, int ko, int h, int w_img,
                                            void *ws, size_t ws_bytes, smmd_stream_t stream) {
     return s2_conv(x, u, nullptr, nullptr, bias, y, n, ci, ko, h, w_img, ws, ws_bytes, stream);
+}
+
+// y += conv(x, W') + bias: a later gradient contribution summed into an
+// earlier one where autograd would add the two (convops._ConvBackward, the
+// double backward's gradient of a gradient both a block's main path and its
+// shortcut read)
+extern "C" smmd_status smmd_wino4x4s2_conv_acc(const float *x, const float *u, const float *bias,
+                                               float *y, int n, int ci, int ko, int h, int w_img,
+                                               void *ws, size_t ws_bytes, smmd_stream_t stream) {
+    return s2_conv(x, u, nullptr, nullptr, bias, y, n, ci, ko, h, w_img, ws, ws_bytes, stream, 1);
 }
 
 extern "C" size_t smmd_wino4x4s2_conv2_workspace_bytes(int n, int ci, int ko, int h, int w_img) {
@@ -1069,7 +1107,7 @@ static smmd_status s2t_launch(const float *gy, const float *u, const float *bias
     if (e != SMMD_OK || S == 1) return e;
     const int64_t n4 = total / 4;
     s2_reduce_kernel<<<dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st>>>(
-        out, bias, dx, n4, S, c, 4 * hg * wg, mask);
+        out, bias, dx, n4, S, c, 4 * hg * wg, mask, 0);
     return last_launch_status();
 }
 

@@ -29,7 +29,7 @@ SN_P1_READY = 1            # smmd_sn_power_iter_ex flag
 ADAM_SN_GDIRECT = 1        # smmd_adam_flat_sn2 flag
 OPT_MAX_FUSED = 96         # tensors smmd_adam_flat_sn takes in one call
 SN_MAX_FUSED = 16          # SN layers smmd_adam_flat_sn takes in one call
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 KIND_RBF, KIND_RQ, KIND_DISTANCE, KIND_DOT = 0, 1, 2, 3
 SMMD_EUNSUPPORTED = 4       # smmd_status (include/smmd_hip.h)
@@ -173,6 +173,7 @@ _SIGS = {
     'smmd_wino4x4s2_workspace_bytes': (_SZ, [_I, _I, _I, _I, _I]),
     'smmd_wino4x4s2t_workspace_bytes': (_SZ, [_I, _I, _I, _I, _I]),
     'smmd_wino4x4s2_conv': (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _SZ, _P]),
+    'smmd_wino4x4s2_conv_acc': (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _SZ, _P]),
     'smmd_wino4x4s2_conv2_workspace_bytes': (_SZ, [_I, _I, _I, _I, _I]),
     'smmd_wino4x4s2_conv2': (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _SZ, _P]),
     'smmd_wino4x4s2t_conv': (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _SZ, _P]),

@@ -485,8 +485,9 @@ def _s2_filter(w, transposed):
     return u
 
 
-def _s2_conv(x, w, b):
-    """conv2d(x, w, b, stride 2, padding 1) on smmd_wino4x4s2_conv."""
+def _s2_conv(x, w, b, into=None):
+    """conv2d(x, w, b, stride 2, padding 1) on smmd_wino4x4s2_conv (into: added
+    to it, smmd_wino4x4s2_conv_acc, and returned)."""
     from . import _lib
     x = x.contiguous()
     w = w.contiguous()
@@ -497,15 +498,19 @@ def _s2_conv(x, w, b):
     co = w.shape[0]
     L = _lib.lib()
     u = _s2_filter(w, False)
-    y = torch.empty((N, co, H // 2, W // 2), dtype=x.dtype, device=x.device)
+    shape = (N, co, H // 2, W // 2)
+    if into is not None:
+        assert tuple(into.shape) == shape and into.is_contiguous() and into.dtype == x.dtype
+    y = torch.empty(shape, dtype=x.dtype, device=x.device) if into is None else into
     nb = L.smmd_wino4x4s2_workspace_bytes(N, ci, co, H, W)
     ws = _lib.workspace('wino_s2', nb, x.device) if nb else None
     _lib.add_bytes('smmd_wino4x4s2_conv', (x.numel() + y.numel()) * 4)
     # 9 point products per 2 x 2 output tile and (phase channel, co) pair
     _lib.add_flops('smmd_wino4x4s2_conv', 2 * 9 * N * (H // 4) * (W // 4) * 4 * ci * co)
+    fn = L.smmd_wino4x4s2_conv if into is None else L.smmd_wino4x4s2_conv_acc
     with _lib.timed('smmd_wino4x4s2_conv'):
-        st = L.smmd_wino4x4s2_conv(_lib.ptr(x), _lib.ptr(u), _lib.ptr(b), _lib.ptr(y), N, ci, co,
-                                   H, W, _lib.ptr(ws), nb, _lib.stream_handle(x.device))
+        st = fn(_lib.ptr(x), _lib.ptr(u), _lib.ptr(b), _lib.ptr(y), N, ci, co, H, W, _lib.ptr(ws),
+                nb, _lib.stream_handle(x.device))
     _lib.check(st, 'smmd_wino4x4s2_conv')
     return y
 
@@ -752,10 +757,16 @@ def _is_thin(x, w, stride, padding):
         and w.shape[2] == w.shape[3]
 
 
-def _fwd(x, w, b, stride, padding, ymask=None):
+def _fwd(x, w, b, stride, padding, ymask=None, into=None):
     """conv(x, w) + b: the library's kernels or MIOpen.  ymask (the output's
     shape): the result masked as threshold_backward(y, ymask, 0), in the 3x3
-    Winograd kernel's epilogue where it runs there."""
+    Winograd kernel's epilogue where it runs there.  into (not with ymask):
+    the result added to it (into + y, in the stride-2 kernel's epilogue where
+    it runs there) and returned."""
+    if into is not None:
+        if _is_s2(x, w, stride, padding) and into.is_contiguous():
+            return _s2_conv(x, w, b, into)
+        return into.add_(_fwd(x, w, b, stride, padding))
     if ymask is not None:
         if (_is_wino(x, w, stride, padding, 0) and ymask.is_contiguous()
                 and os.environ.get('SMMD_WINO8', '1') != '0'):
@@ -893,6 +904,12 @@ class _ConvBackward(torch.autograd.Function):
                 ggx = (_ReluMask.apply(ggx, x) if torch.is_grad_enabled()
                        else _aten.threshold_backward(ggx, x, 0.0))
         fused_mask = gy_mask is not None and not torch.is_grad_enabled()
+        # another node's gradient for the same gy input (a critic block's
+        # main path and shortcut both read _ReluPool's gu): this one is
+        # computed into it and none returned -- the sum autograd would form
+        shared = _shared_gy_key(ctx) if (need_gy and ggx is not None and ggw is None
+                                         and gy_mask is None) else None
+        gy_into = _late['gy'].get(shared) if shared is not None else None
         # the upstream's gradient conv(ggx, w) + conv(x, ggw): one pair launch
         # when both take the same Winograd path, else two convs and their sum
         pair = None
@@ -901,7 +918,8 @@ class _ConvBackward(torch.autograd.Function):
         if ggx is not None:
             if need_gy and pair is None:
                 g_gy = _fwd(ggx, w, None, stride, padding,
-                            gy_mask if fused_mask and ggw is None else None)
+                            gy_mask if fused_mask and ggw is None else None,
+                            gy_into[1] if gy_into is not None else None)
             if need_w:
                 into = _late_target(w)
                 _, g_w = _bwd(gy, ggx, w, stride, padding, (False, True), None, into)
@@ -918,6 +936,12 @@ class _ConvBackward(torch.autograd.Function):
                                                              and ggw is None):
             g_gy = (_ReluMask.apply(g_gy.contiguous(), gy_mask) if torch.is_grad_enabled()
                     else _aten.threshold_backward(g_gy, gy_mask, 0.0))
+        if shared is not None and g_gy is not None:
+            if gy_into is not None:     # added into the earlier contribution
+                g_gy = None
+                _late['gy_acc'] += 1
+            elif g_gy.is_contiguous():
+                _late['gy'][shared] = (ctx.next_functions[2][0], g_gy)
         return g_x, _late_gw(w, g_w, into), g_gy, None, None, None, None, None
 
 
@@ -933,7 +957,11 @@ class _ConvBackward(torch.autograd.Function):
 # multi-tensor add per round: the same sums in the same order, bit-identical.
 WGRAD_LATE_SUM = os.environ.get('SMMD_WGRAD_LATE_SUM', '1') != '0'
 WGRAD_ACC = os.environ.get('SMMD_WGRAD_ACC', '1') != '0'    # later ones into the first
-_late = {'armed': False, 'first': {}, 'queue': [], 'queued': 0}   # queued: a running count
+# the same for two double-backward nodes' gradients of one gy input
+# (_ConvBackward, _shared_gy_key; SMMD_GY_ACC=0: autograd adds them)
+GY_ACC = os.environ.get('SMMD_GY_ACC', '1') != '0'
+_late = {'armed': False, 'first': {}, 'queue': [], 'queued': 0, 'gy': {}, 'gy_acc': 0}
+# (queued, gy_acc: running counts)
 
 
 def arm_late_wgrad_sums(on):
@@ -942,6 +970,20 @@ def arm_late_wgrad_sums(on):
     _late['armed'] = bool(on) and WGRAD_LATE_SUM
     _late['first'].clear()
     _late['queue'].clear()
+    _late['gy'].clear()
+
+
+def _shared_gy_key(ctx):
+    """The autograd edge of a _ConvBackward node's gy input -- (producer node,
+    output index): two nodes with the same edge have their gradients for gy
+    summed by autograd into one input of that producer, which runs after both
+    -- or None outside an armed backward.  The producer node is kept alive by
+    the entry (_late['gy'], cleared by arm_late_wgrad_sums), so its id is not
+    reused while the key stands."""
+    if not (GY_ACC and _late['armed']) or torch.is_grad_enabled():
+        return None
+    fn, nr = ctx.next_functions[2]
+    return None if fn is None else (id(fn), nr)
 
 
 def _late_target(w):

@@ -190,3 +190,48 @@ def test_double_backward_mask_moves_to_producer(shape, monkeypatch):
     for a, b, what in zip(on, off, ('dx', 'dw1', 'dw2')):
         assert torch.equal(a, b), what
     assert n_on == n_off - 1, (n_on, n_off)
+
+
+def _two_blocks(x0, t, on, monkeypatch):
+    """Two critic down blocks (the second reading the first's two paths
+    through relu_pool, so its gu feeds both of the first block's convs), the
+    scaling regulariser's pattern: the input gradient with create_graph, then
+    a loss of it and of the output, differentiated in an armed backward."""
+    from gan.core import convops
+    from gan.core.architecture import ResidualBlock
+    monkeypatch.setattr(convops, 'GY_ACC', on)
+    torch.manual_seed(3)
+    b1 = ResidualBlock(64, 128, 3, 'down').to(DEV)
+    b2 = ResidualBlock(128, 256, 3, 'down').to(DEV)
+    x = x0.clone().requires_grad_(True)
+    s, h = b1.down_parts(x)[:2]
+    s2, h2 = b2.down_parts(s, h)[:2]
+    out = s2 + h2
+    jx, = torch.autograd.grad((out * t).sum(), x, create_graph=True)
+    loss = jx.square().sum() + (out * t).sum()
+    params = list(b1.parameters()) + list(b2.parameters())
+    n0 = convops._late['gy_acc']
+    convops.arm_late_wgrad_sums(True)
+    try:
+        grads = torch.autograd.grad(loss, params + [x], allow_unused=True)
+    finally:
+        convops.arm_late_wgrad_sums(False)
+    return grads, convops._late['gy_acc'] - n0
+
+
+@pytest.mark.parametrize('N,H', [(4, 16), (64, 32)])
+def test_shared_gy_contributions_summed_in_kernel(N, H, monkeypatch):
+    """The double backward's two gradients of one block-output gradient (main
+    path's stride-2 conv and shortcut's 1x1 conv, both fed _ReluPool's gu):
+    the second computed into the first (smmd_wino4x4s2_conv_acc, ABI 15) gives
+    the gradients autograd's own sum gives, bit for bit."""
+    g = torch.Generator(device=DEV).manual_seed(N + H)
+    x0 = torch.randn(N, 64, H, H, device=DEV, generator=g)
+    t = torch.randn(N, 256, H // 4, H // 4, device=DEV, generator=g)
+    on, n_on = _two_blocks(x0, t, True, monkeypatch)
+    off, n_off = _two_blocks(x0, t, False, monkeypatch)
+    assert n_on > 0 and n_off == 0, (n_on, n_off)
+    for i, (a, b) in enumerate(zip(on, off)):
+        assert (a is None) == (b is None), i
+        if a is not None:
+            assert torch.equal(a, b), i
