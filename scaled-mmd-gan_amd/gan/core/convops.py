@@ -973,6 +973,59 @@ def arm_late_wgrad_sums(on):
     _late['gy'].clear()
 
 
+# Late sums of bias gradients (SMMD_BIAS_LATE_SUM=0: off): a critic conv bias
+# gets one gradient per pass (real, fake), and autograd adds them -- one
+# latency-bound add launch per bias.  While armed (MMD_GAN.d_step, one process,
+# gathered gradients) the first goes to the parameter's AccumulateGrad as usual
+# and the later ones are queued; flush_late_bias_sums adds them to .grad after
+# the backward, one multi-tensor add per round: first + second, the sum
+# autograd forms, bit for bit.
+BIAS_LATE_SUM = os.environ.get('SMMD_BIAS_LATE_SUM', '1') != '0'
+_lateb = {'armed': False, 'first': {}, 'queue': [], 'queued': 0}
+
+
+def arm_late_bias_sums(on):
+    _lateb['armed'] = bool(on) and BIAS_LATE_SUM
+    _lateb['first'].clear()
+    _lateb['queue'].clear()
+
+
+def _late_bias(p, g):
+    """g for autograd, or None: queued for p.grad (a later contribution)."""
+    if (g is None or p is None or not _lateb['armed'] or not p.is_leaf
+            or torch.is_grad_enabled()):
+        return g
+    f = _lateb['first'].get(id(p))
+    if f is None or f is not p:
+        _lateb['first'][id(p)] = p
+        return g
+    _lateb['queue'].append((p, g))
+    _lateb['queued'] += 1
+    return None
+
+
+def flush_late_bias_sums():
+    """Add the queued bias contributions to the parameters' .grad in arrival
+    order (round r: every parameter's r-th queued term, one _foreach_add_)."""
+    q = _lateb['queue']
+    if not q:
+        return
+    rounds, seen = [], {}
+    for p, g in q:
+        r = seen.get(id(p), 0)
+        seen[id(p)] = r + 1
+        if r == len(rounds):
+            rounds.append(([], []))
+        if p.grad is None:          # (the first went nowhere: a hook dropped it)
+            raise RuntimeError('late bias sum: %s has no gradient to add to' % (tuple(p.shape),))
+        rounds[r][0].append(p.grad)
+        rounds[r][1].append(g)
+    with torch.no_grad():
+        for accs, gs in rounds:
+            torch._foreach_add_(accs, gs)
+    q.clear()
+
+
 def _shared_gy_key(ctx):
     """The autograd edge of a _ConvBackward node's gy input -- (producer node,
     output index): two nodes with the same edge have their gradients for gy
@@ -1051,6 +1104,7 @@ class _Conv2d(torch.autograd.Function):
     def forward(ctx, x, w, b, stride, padding, mask_in=False):
         ctx.save_for_backward(x, w)
         ctx.cfg = (stride, padding, b is not None, mask_in)
+        ctx.bias_ref = b                    # the parameter (_late_bias)
         return _fwd(x, w, b, stride, padding)
 
     @staticmethod
@@ -1073,7 +1127,7 @@ class _Conv2d(torch.autograd.Function):
             gx = gw = None
         gb = (bias_grad(gy) if (has_b and ctx.needs_input_grad[2] and _input_only[0] == 0)
               else None)
-        return gx, _late_gw(w, gw, into), gb, None, None, None
+        return gx, _late_gw(w, gw, into), _late_bias(ctx.bias_ref, gb), None, None, None
 
 
 def bias_grad(gy):
@@ -1135,6 +1189,7 @@ class _Conv2dReLU(torch.autograd.Function):
         r = _wino_conv(x, w, b, 0, relu=True)
         ctx.save_for_backward(x, w, r)
         ctx.cfg = (stride, padding, b is not None, consumer_masks)
+        ctx.bias_ref = b
         return r
 
     @staticmethod
@@ -1168,7 +1223,7 @@ class _Conv2dReLU(torch.autograd.Function):
         else:
             gx = gw = None
         gb = bias_grad(gy) if want_b else None
-        return gx, _late_gw(w, gw, into), gb, None, None, None
+        return gx, _late_gw(w, gw, into), _late_bias(ctx.bias_ref, gb), None, None, None
 
 
 # the double backward's gradient of a consumer-masked conv-ReLU's upstream
@@ -1531,6 +1586,7 @@ class _ReluPool(torch.autograd.Function):
         ctx.save_for_backward(r)
         ctx.slope_p = slope_p
         ctx.has = (y is not None, bx is not None, by is not None)
+        ctx.bias_refs = (bx, by)
         ctx.set_materialize_grads(False)
         return r, p
 
@@ -1545,8 +1601,9 @@ class _ReluPool(torch.autograd.Function):
         if (has_bx and ctx.needs_input_grad[2]) or (has_by and ctx.needs_input_grad[3]):
             if _input_only[0] == 0:         # not the Jacobian's input-only pass
                 gb = bias_grad(gu)
-        return (gu, (gu if has_y else None), (gb if has_bx else None), (gb if has_by else None),
-                None)
+        bx, by = ctx.bias_refs
+        return (gu, (gu if has_y else None), _late_bias(bx, gb if has_bx else None),
+                _late_bias(by, gb if has_by else None), None)
 
 
 def relu_pool(x, y=None, slope_p=1.0, bx=None, by=None):

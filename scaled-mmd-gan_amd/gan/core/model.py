@@ -485,6 +485,9 @@ class MMD_GAN:
             bk.clip_exclude = self._sn_tensor_ids() if tower_clip > 0 else frozenset()
         self._dpgd = dpgd
         convops.arm_late_wgrad_sums(True)
+        # the bias gradients' later contributions added after the backward
+        # (one process, gathered gradients: no hook reads .grad during it)
+        convops.arm_late_bias_sums(self.d_optim.gather)
         try:
             if ref:
                 d_loss.backward(inputs=self.d_vars)
@@ -493,8 +496,10 @@ class MMD_GAN:
                 # first conv skips the input gradient nobody reads
                 with convops.no_input_grad(self._last_images):
                     d_loss.backward()
+            convops.flush_late_bias_sums()
         finally:
             convops.arm_late_wgrad_sums(False)
+            convops.arm_late_bias_sums(False)
             self.sn_D.arm_gdirect(False)
             self.sn_D.arm_direct(False)
             self.sn_D.arm_dp_gdirect(False)

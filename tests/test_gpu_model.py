@@ -142,6 +142,42 @@ def test_late_wgrad_sums_bit_identical(dev, monkeypatch):
     assert late <= max(4 * same, 1e-6 * scale), (late, same, scale)
 
 
+def test_late_bias_sums_match_accumulation(dev, monkeypatch):
+    """The critic biases' later gradient contributions (the fake pass after
+    the real one) added to .grad after the backward (convops late bias sums)
+    give dL/db -- and every other gradient -- within the run-to-run spread of
+    the critic step itself."""
+    from gan.core import convops
+    from gan.core.smmd import SMMD
+    grads, queued = [], []
+    for on in (True, True, False):
+        monkeypatch.setattr(convops, 'BIAS_LATE_SUM', on)
+        torch.manual_seed(0)
+        model = SMMD(_cfg(architecture='snresnet', output_size=64, df_dim=16, gf_dim=16,
+                          batch_size=8), device=dev)
+        images = torch.rand(8, 3, 64, 64, generator=torch.Generator().manual_seed(1)).to(dev)
+        z = torch.empty(8, 128).uniform_(-1, 1, generator=torch.Generator().manual_seed(2)).to(dev)
+        model.sample_z = lambda n, z=z: z
+        cap = {}
+        orig = model.d_optim.step
+
+        def c(*a, _cap=cap, _m=model, _o=orig, **k):
+            _cap['g'] = _m.d_optim.dense_grad().clone()
+            return _o(*a, **k)
+        model.d_optim.step = c
+        model.step = 25
+        model.d_counter, model.g_counter = 0, 0
+        n0 = convops._lateb['queued']
+        model.d_step(images)
+        queued.append(convops._lateb['queued'] - n0)
+        grads.append(cap['g'])
+    assert queued[0] > 0 and queued[2] == 0
+    scale = float(grads[0].abs().max())
+    same = float((grads[0] - grads[1]).abs().max())
+    late = float((grads[0] - grads[2]).abs().max())
+    assert late <= max(4 * same, 1e-6 * scale), (late, same, scale)
+
+
 def test_generator_gradient_gather_matches_accumulation(dev, monkeypatch):
     """The generator step's gradients gathered into the flat buffer by one
     multi-tensor copy (optim.FlatAdam.gather) update the generator as the
