@@ -495,7 +495,7 @@ class MMD_GAN:
                 # the real images are a leaf only for the Jacobian: the critic's
                 # first conv skips the input gradient nobody reads
                 with convops.no_input_grad(self._last_images):
-                    d_loss.backward()
+                    d_loss.backward(ops.grad_seed(d_loss))
             convops.flush_late_bias_sums()
         finally:
             convops.arm_late_wgrad_sums(False)

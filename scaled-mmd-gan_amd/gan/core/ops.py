@@ -41,17 +41,41 @@ def dot(x, y, name=None):
     return (x * y).sum()
 
 
+_SEEDS = {}
+
+
+def grad_seed(y, i=None):
+    """The gradient d(sum y[:, i]) / dy (i None: d(sum y) / dy) as a constant
+    tensor, kept per shape outside a graph capture: seeding autograd with it
+    gives the same gradient as differentiating the select and the sum -- the
+    same ones in the same places -- without their zero, copy and fill
+    kernels.  (Autograd never adds into a seed it does not own alone.)"""
+    key = (tuple(y.shape), y.dtype, y.device, i)
+    t = _SEEDS.get(key)
+    if t is None:
+        if i is None:
+            t = torch.ones(y.shape, dtype=y.dtype, device=y.device)
+        else:
+            t = torch.zeros(y.shape, dtype=y.dtype, device=y.device)
+            t[:, i] = 1
+        if y.is_cuda and torch.cuda.is_current_stream_capturing():
+            return t
+        _SEEDS[key] = t
+    return t
+
+
 def jacobian_columns(y, x, create_graph=True):
     """Stack of d(sum_b y[b, i]) / dx for every critic output column i
     (gan/core/ops.py:230-231): returns [d, *x.shape].  The critic has no
     cross-sample coupling in the configs (no BN in D), so
-    row b of column i is d y[b, i] / d x[b]."""
+    row b of column i is d y[b, i] / d x[b].  Each column's pass is seeded
+    with grad_seed(y, i), the gradient of y[:, i].sum() w.r.t. y."""
     d = y.shape[1]
     cols = []
     for i in range(d):
         with input_grad_only():       # no weight-gradient kernels in this pass
-            g, = torch.autograd.grad(y[:, i].sum(), x, create_graph=create_graph,
-                                     retain_graph=True)
+            g, = torch.autograd.grad(y, x, grad_outputs=grad_seed(y, i),
+                                     create_graph=create_graph, retain_graph=True)
         cols.append(g)
     return torch.stack(cols, 0) if d > 1 else cols[0].unsqueeze(0)
 
