@@ -73,7 +73,8 @@ int smmd_abi_version(void);         /* bumped on any ABI change (2: Gram/poly,
                                        smmd_row_lrelu_sum, smmd_row_lrelu_bcast,
                                        13: the weight gradients' *_acc forms,
                                        14: smmd_wino3x3_conv_mask,
-                                       15: smmd_wino4x4s2_conv_acc) */
+                                       15: smmd_wino4x4s2_conv_acc,
+                                       16: smmd_conv1x1_t) */
 const char *smmd_source_hash(void); /* first 16 hex digits of the SHA-256 of the
                                        sources this binary was built from
                                        (csrc .hip and .hpp files in byte order,
@@ -848,6 +849,12 @@ size_t smmd_conv1x1_workspace_bytes(int n, int r, int m, int p);
 
 smmd_status smmd_conv1x1(const float *a, const float *x, const float *bias, float *y, int n,
                          int r, int m, int p, void *ws, size_t ws_bytes, smmd_stream_t stream);
+
+/* the same with a given transposed, a [r][m]: y = a^T x (+ bias).  The input
+ * gradient of a 1x1 conv straight from its weight W [K][C] (dx = W^T gy,
+ * r = K, m = C) without a per-step W^T copy; same workspace as smmd_conv1x1. */
+smmd_status smmd_conv1x1_t(const float *a, const float *x, const float *bias, float *y, int n,
+                           int r, int m, int p, void *ws, size_t ws_bytes, smmd_stream_t stream);
 
 int smmd_conv1x1_wgrad_supported(int n, int c, int k, int p);
 

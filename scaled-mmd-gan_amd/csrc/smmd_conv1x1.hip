@@ -59,7 +59,10 @@ __device__ __forceinline__ int64_t c1_off(int64_t j, int row, int rows, int P) {
 // forward / input gradient: Y [N][M][P] = A [M][R] . X [N][R][P] (+ bias[m])
 // Split-K: blockIdx.y = slice s of the reduction, chunks [s cps, (s + 1) cps)
 // of 32; with several slices Y is slab s of the workspace (bias NULL) and
-// c1_sum adds the slabs in order.
+// c1_sum adds the slabs in order.  TA: A given as its transpose, [R][M] (the
+// input gradient straight from W [K][C]: no per-step W^T copy); the thread's
+// float4 runs along m and goes to the [m][r] stage as four scalar stores.
+template <bool TA>
 __global__ __launch_bounds__(C1_T) void c1_gemm_kernel(const float *__restrict__ A,
                                                        const float *__restrict__ X,
                                                        const float *__restrict__ bias,
@@ -85,12 +88,20 @@ __global__ __launch_bounds__(C1_T) void c1_gemm_kernel(const float *__restrict__
     const int f0 = tid, f1 = tid + C1_T;
     const int rbeg = blockIdx.y * cps * C1_RC;
     const int nchunk = min(cps, R / C1_RC - (int)blockIdx.y * cps);
-    const float *pa0 = A + (int64_t)(m0 + (f0 >> 3)) * R + 4 * (f0 & 7) + rbeg;
-    const float *pa1 = A + (int64_t)(m0 + (f1 >> 3)) * R + 4 * (f1 & 7) + rbeg;
+    // (TA: thread -> row r = (f & 7) + 8 (f >> 7) of A^T, quad (f >> 3) & 15
+    // along m: a wave reads 8 rows x 128 contiguous bytes, and its scalar
+    // stores to the [m][r] stage meet at most two lanes per bank)
+    const int tr0 = (f0 & 7) + 8 * (f0 >> 7), tq0 = (f0 >> 3) & 15;
+    const int tr1 = (f1 & 7) + 8 * (f1 >> 7), tq1 = (f1 >> 3) & 15;
+    const float *pa0 = TA ? A + (int64_t)(rbeg + tr0) * M + m0 + 4 * tq0
+                          : A + (int64_t)(m0 + (f0 >> 3)) * R + 4 * (f0 & 7) + rbeg;
+    const float *pa1 = TA ? A + (int64_t)(rbeg + tr1) * M + m0 + 4 * tq1
+                          : A + (int64_t)(m0 + (f1 >> 3)) * R + 4 * (f1 & 7) + rbeg;
+    const int64_t astep = TA ? (int64_t)C1_RC * M : C1_RC;
     const float *px0 = X + c1_off(j0 + 4 * (f0 & 15), f0 >> 4, R, P) + (int64_t)rbeg * P;
     const float *px1 = X + c1_off(j0 + 4 * (f1 & 15), f1 >> 4, R, P) + (int64_t)rbeg * P;
-    float *const sa0 = lds + (f0 >> 3) * C1_AS + 4 * (f0 & 7);
-    float *const sa1 = lds + (f1 >> 3) * C1_AS + 4 * (f1 & 7);
+    float *const sa0 = TA ? lds + 4 * tq0 * C1_AS + tr0 : lds + (f0 >> 3) * C1_AS + 4 * (f0 & 7);
+    float *const sa1 = TA ? lds + 4 * tq1 * C1_AS + tr1 : lds + (f1 >> 3) * C1_AS + 4 * (f1 & 7);
     float *const sb0 = lds + C1_ASTAGE + (f0 >> 4) * C1_BS + 4 * (f0 & 15);
     float *const sb1 = lds + C1_ASTAGE + (f1 >> 4) * C1_BS + 4 * (f1 & 15);
     const int64_t xstep = (int64_t)C1_RC * P;
@@ -105,16 +116,23 @@ __global__ __launch_bounds__(C1_T) void c1_gemm_kernel(const float *__restrict__
 #define C1_GLOAD(g, c)                                                         \
     {                                                                          \
         const int cc_ = min((c), nchunk - 1);                                  \
-        g##a0 = *reinterpret_cast<const float4 *>(pa0 + C1_RC * cc_);          \
-        g##a1 = *reinterpret_cast<const float4 *>(pa1 + C1_RC * cc_);          \
+        g##a0 = *reinterpret_cast<const float4 *>(pa0 + astep * cc_);          \
+        g##a1 = *reinterpret_cast<const float4 *>(pa1 + astep * cc_);          \
         g##b0 = *reinterpret_cast<const float4 *>(px0 + xstep * cc_);          \
         g##b1 = *reinterpret_cast<const float4 *>(px1 + xstep * cc_);          \
     }
 #define C1_LSTORE(g, buf)                                                      \
     {                                                                          \
         const int o_ = (buf) * C1_STAGE;                                       \
-        *reinterpret_cast<float4 *>(sa0 + o_) = g##a0;                         \
-        *reinterpret_cast<float4 *>(sa1 + o_) = g##a1;                         \
+        if constexpr (TA) {                                                    \
+            sa0[o_] = g##a0.x; sa0[o_ + C1_AS] = g##a0.y;                      \
+            sa0[o_ + 2 * C1_AS] = g##a0.z; sa0[o_ + 3 * C1_AS] = g##a0.w;      \
+            sa1[o_] = g##a1.x; sa1[o_ + C1_AS] = g##a1.y;                      \
+            sa1[o_ + 2 * C1_AS] = g##a1.z; sa1[o_ + 3 * C1_AS] = g##a1.w;      \
+        } else {                                                               \
+            *reinterpret_cast<float4 *>(sa0 + o_) = g##a0;                     \
+            *reinterpret_cast<float4 *>(sa1 + o_) = g##a1;                     \
+        }                                                                      \
         *reinterpret_cast<float4 *>(sb0 + o_) = g##b0;                         \
         *reinterpret_cast<float4 *>(sb1 + o_) = g##b1;                         \
     }
@@ -400,9 +418,9 @@ extern "C" size_t smmd_conv1x1_workspace_bytes(int n, int r, int m, int p) {
     return (size_t)(S + c1_groups(S)) * n * m * p * sizeof(float);
 }
 
-extern "C" smmd_status smmd_conv1x1(const float *a, const float *x, const float *bias, float *y,
-                                    int n, int r, int m, int p, void *ws, size_t ws_bytes,
-                                    smmd_stream_t stream) {
+static smmd_status c1_gemm_launch(const float *a, const float *x, const float *bias, float *y,
+                                  int n, int r, int m, int p, void *ws, size_t ws_bytes, bool ta,
+                                  smmd_stream_t stream) {
     if (!a || !x || !y) return SMMD_EINVAL;
     if (!smmd_conv1x1_supported(n, r, m, p)) return SMMD_EUNSUPPORTED;
     if (!aligned16(a) || !aligned16(x) || !aligned16(y)) return SMMD_EINVAL;
@@ -417,12 +435,27 @@ extern "C" smmd_status smmd_conv1x1(const float *a, const float *x, const float 
     const int Sused = (nch + cps - 1) / cps;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     float *part = Sused > 1 ? static_cast<float *>(ws) : y;
-    c1_gemm_kernel<<<dim3((unsigned)blocks, (unsigned)Sused), dim3(C1_T), 0, st>>>(
+    auto k = ta ? c1_gemm_kernel<true> : c1_gemm_kernel<false>;
+    k<<<dim3((unsigned)blocks, (unsigned)Sused), dim3(C1_T), 0, st>>>(
         a, x, Sused > 1 ? nullptr : bias, part, m, r, p, J, cps);
     smmd_status e = last_launch_status();
     if (e != SMMD_OK || Sused == 1) return e;
     const int64_t total = J * m;
     return c1_reduce(part, Sused, total, part + (size_t)Sused * total, y, bias, p, m, st);
+}
+
+extern "C" smmd_status smmd_conv1x1(const float *a, const float *x, const float *bias, float *y,
+                                    int n, int r, int m, int p, void *ws, size_t ws_bytes,
+                                    smmd_stream_t stream) {
+    return c1_gemm_launch(a, x, bias, y, n, r, m, p, ws, ws_bytes, false, stream);
+}
+
+// y [n][m][p] = a^T x (+ bias) with a [r][m]: the input gradient of a 1x1 conv
+// straight from its weight W [K = r][C = m] (dx = W^T gy)
+extern "C" smmd_status smmd_conv1x1_t(const float *a, const float *x, const float *bias, float *y,
+                                      int n, int r, int m, int p, void *ws, size_t ws_bytes,
+                                      smmd_stream_t stream) {
+    return c1_gemm_launch(a, x, bias, y, n, r, m, p, ws, ws_bytes, true, stream);
 }
 
 extern "C" int smmd_conv1x1_wgrad_supported(int n, int c, int k, int p) {

@@ -754,7 +754,7 @@ const char *smmd_status_string(smmd_status s) {
     return "SMMD_?: unknown status";
 }
 
-int smmd_abi_version(void) { return 15; }
+int smmd_abi_version(void) { return 16; }
 
 // Path choice.  d > 32: the MFMA Gram path (the row sweep holds a row in
 // registers up to 32 features).  d <= 32: the row sweep, except where the

@@ -29,7 +29,7 @@ SN_P1_READY = 1            # smmd_sn_power_iter_ex flag
 ADAM_SN_GDIRECT = 1        # smmd_adam_flat_sn2 flag
 OPT_MAX_FUSED = 96         # tensors smmd_adam_flat_sn takes in one call
 SN_MAX_FUSED = 16          # SN layers smmd_adam_flat_sn takes in one call
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 KIND_RBF, KIND_RQ, KIND_DISTANCE, KIND_DOT = 0, 1, 2, 3
 SMMD_EUNSUPPORTED = 4       # smmd_status (include/smmd_hip.h)
@@ -139,6 +139,7 @@ _SIGS = {
     'smmd_conv1x1_supported': (_I, [_I, _I, _I, _I]),
     'smmd_conv1x1_workspace_bytes': (_SZ, [_I, _I, _I, _I]),
     'smmd_conv1x1': (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _SZ, _P]),
+    'smmd_conv1x1_t': (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _SZ, _P]),
     'smmd_conv1x1_wgrad_supported': (_I, [_I, _I, _I, _I]),
     'smmd_conv1x1_wgrad_workspace_bytes': (_SZ, [_I, _I, _I, _I]),
     'smmd_conv1x1_wgrad': (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _SZ, _P]),

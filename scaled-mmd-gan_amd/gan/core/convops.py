@@ -683,9 +683,10 @@ def _is_c1(x, w, stride, padding):
             and x.is_contiguous() and x.shape[1] == w.shape[1] and x.data_ptr() % 16 == 0)
 
 
-def _c1_gemm(a, x, b, m):
-    """y [N, m, H, W] = a [m, r] . x [N, r, H, W] (+ b) on smmd_conv1x1, or
-    None when the library does not tile the shape."""
+def _c1_gemm(a, x, b, m, ta=False):
+    """y [N, m, H, W] = a [m, r] . x [N, r, H, W] (+ b) on smmd_conv1x1 (ta: a
+    given as its transpose [r, m], smmd_conv1x1_t), or None when the library
+    does not tile the shape."""
     from . import _lib
     N, r, H, W = x.shape
     P = H * W
@@ -699,9 +700,10 @@ def _c1_gemm(a, x, b, m):
     ws = _lib.workspace('conv1x1', nb, x.device) if nb else None
     _lib.add_bytes('smmd_conv1x1', (x.numel() + y.numel() + a.numel()) * 4)
     _lib.add_flops('smmd_conv1x1', 2 * N * P * r * m)
+    fn = L.smmd_conv1x1_t if ta else L.smmd_conv1x1
     with _lib.timed('smmd_conv1x1'):
-        st = L.smmd_conv1x1(_lib.ptr(a), _lib.ptr(x), _lib.ptr(b), _lib.ptr(y), N, r, m, P,
-                            _lib.ptr(ws), nb, _lib.stream_handle(x.device))
+        st = fn(_lib.ptr(a), _lib.ptr(x), _lib.ptr(b), _lib.ptr(y), N, r, m, P, _lib.ptr(ws), nb,
+                _lib.stream_handle(x.device))
     _lib.check(st, 'smmd_conv1x1')
     return y
 
@@ -726,7 +728,15 @@ def _c1_wt(w):
     return u
 
 
+# SMMD_C1_DX_T=0: the input gradient from a W^T copy (_c1_wt) instead of W
+C1_DX_T = os.environ.get('SMMD_C1_DX_T', '1') != '0'
+
+
 def _c1_dx(gy, w):
+    if C1_DX_T:
+        wm = materialize(w).reshape(w.shape[0], w.shape[1])
+        if wm.is_contiguous():
+            return _c1_gemm(wm, gy, None, w.shape[1], ta=True)
     return _c1_gemm(_c1_wt(w), gy, None, w.shape[1])
 
 

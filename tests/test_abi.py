@@ -39,7 +39,7 @@ def test_status_strings(L):
     from gan.core import _lib
     assert L.smmd_status_string(0) == b'SMMD_OK'
     assert b'EINVAL' in L.smmd_status_string(1)
-    assert L.smmd_abi_version() == _lib.ABI_VERSION == 15
+    assert L.smmd_abi_version() == _lib.ABI_VERSION == 16
 
 
 def test_workspace_sizing(L):

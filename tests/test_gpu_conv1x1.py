@@ -93,3 +93,22 @@ def test_conv1x1_double_backward_vs_float64():
     ref = run(lambda x, w: F.conv2d(x, w), x0.double(), w0.double())
     for a, r, what in zip(got, ref, ('dx', 'dw')):
         _close(a, r, 1e-5, what)
+
+
+@pytest.mark.parametrize('N,C,K,H', [(64, 64, 128, 32), (64, 512, 1024, 4), (64, 128, 256, 16),
+                                     (4, 256, 512, 8), (4, 64, 128, 4)])
+def test_transposed_weight_gemm_equals_copy(N, C, K, H):
+    """smmd_conv1x1_t (ABI 16: the input gradient straight from W [K, C]) is
+    bit-identical to smmd_conv1x1 on the W^T copy, split-K slabs included."""
+    from gan.core import convops
+    g = torch.Generator(device=DEV).manual_seed(N + C + K + H)
+    w = torch.randn(K, C, 1, 1, device=DEV, generator=g) * 0.05
+    gy = torch.randn(N, K, H, H, device=DEV, generator=g)
+    wm = w.reshape(K, C)
+    a = convops._c1_gemm(wm, gy, None, C, ta=True)
+    b = convops._c1_gemm(wm.t().contiguous(), gy, None, C)
+    assert a is not None and b is not None
+    assert torch.equal(a, b)
+    ref = torch.nn.functional.conv_transpose2d(gy.double(), w.double())
+    err = float((a.double() - ref).abs().max())
+    assert err <= 2e-6 * float(ref.abs().max()) + 1e-30

@@ -2,5 +2,5 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 400 python tools/op_sources.py --top 60 > gpurun_out/opsrc_after.txt 2> gpurun_out/opsrc_after.err || { echo "rc=$?"; tail -20 gpurun_out/opsrc_after.err; exit 1; }
+timeout -k 10 400 python tools/op_sources.py --top 60 > gpurun_out/opsrc_final.txt 2> gpurun_out/opsrc_final.err || { echo "rc=$?"; tail -20 gpurun_out/opsrc_final.err; exit 1; }
 echo done
