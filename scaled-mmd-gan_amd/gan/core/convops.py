@@ -1668,10 +1668,11 @@ class _UpAdd(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         # the nearest upsample's adjoint is the 2x2 window sum: avg_pool2d's
-        # ((g00 + g01) + g10) + g11, then / 4 * 4 (exact), the order of
-        # upsample_nearest2d's backward
+        # ((g00 + g01) + g10) + g11 with divisor 1 -- the sum / 4 * 4 of the
+        # unfused form (exact: a power-of-two scale), one kernel instead of two
         g = g.contiguous()
-        gs = F.avg_pool2d(g, 2) * 4.0 if ctx.needs_input_grad[0] or ctx.has[0] else None
+        gs = (F.avg_pool2d(g, 2, divisor_override=1) if ctx.needs_input_grad[0] or ctx.has[0]
+              else None)
         gbs = bias_grad(gs) if ctx.has[0] and ctx.needs_input_grad[1] else None
         gbh = bias_grad(g) if ctx.has[1] and ctx.needs_input_grad[3] else None
         return gs, gbs, g, gbh
