@@ -985,29 +985,25 @@ def arm_late_wgrad_sums(on):
 
 # Late sums of bias gradients (SMMD_BIAS_LATE_SUM=0: off): a critic conv bias
 # gets one gradient per pass (real, fake), and autograd adds them -- one
-# latency-bound add launch per bias.  While armed (MMD_GAN.d_step, one process,
-# gathered gradients) the first goes to the parameter's AccumulateGrad as usual
-# and the later ones are queued; flush_late_bias_sums adds them to .grad after
-# the backward, one multi-tensor add per round: first + second, the sum
-# autograd forms, bit for bit.
+# latency-bound add launch per bias, and a copy where one channel sum feeds
+# two biases (_ReluPool's bx and by).  While armed (MMD_GAN.d_step, one
+# process, gathered gradients, .grad None at the start) every contribution is
+# queued instead and flush_late_bias_sums forms .grad after the backward:
+# first + second by one out-of-place multi-tensor add (+ later ones in
+# place), the sums autograd forms in arrival order, bit for bit.
 BIAS_LATE_SUM = os.environ.get('SMMD_BIAS_LATE_SUM', '1') != '0'
-_lateb = {'armed': False, 'first': {}, 'queue': [], 'queued': 0}
+_lateb = {'armed': False, 'queue': [], 'queued': 0}
 
 
 def arm_late_bias_sums(on):
     _lateb['armed'] = bool(on) and BIAS_LATE_SUM
-    _lateb['first'].clear()
     _lateb['queue'].clear()
 
 
 def _late_bias(p, g):
-    """g for autograd, or None: queued for p.grad (a later contribution)."""
+    """g for autograd, or None: queued for p.grad."""
     if (g is None or p is None or not _lateb['armed'] or not p.is_leaf
             or torch.is_grad_enabled()):
-        return g
-    f = _lateb['first'].get(id(p))
-    if f is None or f is not p:
-        _lateb['first'][id(p)] = p
         return g
     _lateb['queue'].append((p, g))
     _lateb['queued'] += 1
@@ -1015,25 +1011,44 @@ def _late_bias(p, g):
 
 
 def flush_late_bias_sums():
-    """Add the queued bias contributions to the parameters' .grad in arrival
-    order (round r: every parameter's r-th queued term, one _foreach_add_)."""
+    """p.grad = the sum of p's queued contributions in arrival order (round 1:
+    one out-of-place _foreach_add of the first two of every parameter; round
+    r > 1: one in-place _foreach_add_ of the r-th); a single contribution is
+    taken as it is, cloned when another parameter holds the same tensor."""
     q = _lateb['queue']
     if not q:
         return
-    rounds, seen = [], {}
+    per = {}
     for p, g in q:
-        r = seen.get(id(p), 0)
-        seen[id(p)] = r + 1
-        if r == len(rounds):
-            rounds.append(([], []))
-        if p.grad is None:          # (the first went nowhere: a hook dropped it)
-            raise RuntimeError('late bias sum: %s has no gradient to add to' % (tuple(p.shape),))
-        rounds[r][0].append(p.grad)
-        rounds[r][1].append(g)
-    with torch.no_grad():
-        for accs, gs in rounds:
-            torch._foreach_add_(accs, gs)
+        per.setdefault(id(p), (p, []))[1].append(g)
     q.clear()
+    with torch.no_grad():
+        pairs = [(p, gs) for p, gs in per.values() if len(gs) >= 2]
+        if pairs:
+            sums = torch._foreach_add([gs[0] for _, gs in pairs], [gs[1] for _, gs in pairs])
+            for (p, _), t in zip(pairs, sums):
+                _set_bias_grad(p, t)
+            r = 2
+            while True:
+                more = [(p, gs[r]) for p, gs in pairs if len(gs) > r]
+                if not more:
+                    break
+                torch._foreach_add_([p.grad for p, _ in more], [g for _, g in more])
+                r += 1
+        held = {}
+        for p, gs in per.values():
+            if len(gs) == 1:
+                held[id(gs[0])] = held.get(id(gs[0]), 0) + 1
+        for p, gs in per.values():
+            if len(gs) == 1:
+                _set_bias_grad(p, gs[0].clone() if held[id(gs[0])] > 1 else gs[0])
+
+
+def _set_bias_grad(p, t):
+    if p.grad is None:
+        p.grad = t
+    else:                           # (a contribution autograd accumulated itself)
+        p.grad.add_(t)
 
 
 def _shared_gy_key(ctx):
