@@ -150,6 +150,8 @@ class Linear(nn.Module, _SNMixin):
             # one output feature (the critic's output layer at dof_dim 1): a
             # matrix-vector product; hipBLASLt ran this [B, F] x [F, 1] GEMM on
             # one workgroup, 32 us per call
+            if LINEAR_NODE:
+                return _LinOut.apply(x, w, self.bias).unsqueeze(1)
             y = (torch.mv(x, w.view(-1)) if self.bias is None
                  else torch.addmv(self.bias, x, w.view(-1)))
             return y.unsqueeze(1)
@@ -164,6 +166,61 @@ def batch_norm(c):
 
 # SMMD_LINEAR_MV=0: a single-output linear layer through F.linear (hipBLASLt)
 LINEAR_MV = os.environ.get('SMMD_LINEAR_MV', '1') != '0'
+# SMMD_LINEAR_NODE=0: that layer's backward by torch's AddmvBackward0
+LINEAR_NODE = os.environ.get('SMMD_LINEAR_NODE', '1') != '0'
+
+
+class _LinOut(torch.autograd.Function):
+    """y [B] = x [B, F] . w [1, F] + b (snops.py:46-66 linear at one output,
+    the critic's last layer): torch.mv / addmv forward.  Backward: dx = dy w
+    (an outer product, _Outer under create_graph), dw = x^T dy, db = sum dy,
+    the ops AddmvBackward0 runs; the weight gradient skipped in an input-only
+    pass (convops.input_grad_only), and dw / db handed to convops' late sums
+    (an SN weight's contributions summed at its SN node, a bias's after the
+    backward) instead of autograd's adds."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.bias_ref = b
+        v = w.view(-1)
+        return torch.mv(x, v) if b is None else torch.addmv(b, x, v)
+
+    @staticmethod
+    def backward(ctx, gy):
+        from . import convops
+        x, w = ctx.saved_tensors
+        full = convops._input_only[0] == 0
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = (_Outer.apply(gy, w) if torch.is_grad_enabled()
+                  else torch.outer(gy, w.view(-1)))
+        if ctx.needs_input_grad[1] and full:
+            gw = convops._late_gw(w, torch.mv(x.t(), gy).view(1, -1))
+        if ctx.bias_ref is not None and ctx.needs_input_grad[2] and full:
+            gb = convops._late_bias(ctx.bias_ref, gy.sum(0, keepdim=True))
+        return gx, gw, gb
+
+
+class _Outer(torch.autograd.Function):
+    """dx = g w of _LinOut under create_graph (the scaling regulariser's
+    Jacobian pass): its own backward as two matrix-vector products (gemv)
+    instead of MulBackward0's broadcast multiplies and sums."""
+
+    @staticmethod
+    def forward(ctx, g, w):
+        ctx.save_for_backward(g, w)
+        return torch.outer(g, w.view(-1))
+
+    @staticmethod
+    def backward(ctx, gg):
+        from . import convops
+        g, w = ctx.saved_tensors
+        g_g = torch.mv(gg, w.view(-1)) if ctx.needs_input_grad[0] else None
+        g_w = None
+        if ctx.needs_input_grad[1]:
+            g_w = convops._late_gw(w, torch.mv(gg.t(), g).view(1, -1))
+        return g_g, g_w
 
 
 # SMMD_BN_RELU=0: torch's BatchNorm2d + relu for the generator outside autograd

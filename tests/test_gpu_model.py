@@ -473,3 +473,34 @@ def test_step_graphs_match_eager(dev):
             assert dist(ta, tb) <= 3 * noise + lim, (name, t, dist(ta, tb), noise, lim)
     b.enable_graphs(False)
     b.train_step(imgs[0])                      # back to eager
+
+
+@pytest.mark.parametrize('order', [1, 2])
+def test_linear_out_node_vs_float64(dev, order):
+    """snops._LinOut (the critic's single-output linear layer with its own
+    first- and second-order backward) against torch's addmv in float64: the
+    output, and the gradients of x, w, b -- through the scaling regulariser's
+    pattern (the input gradient with create_graph, a loss of it) at order 2."""
+    from gan.core import snops
+    g = torch.Generator(device=dev).manual_seed(4 + order)
+    x0 = torch.randn(64, 1024, device=dev, generator=g)
+    w0 = torch.randn(1, 1024, device=dev, generator=g) / 32
+    b0 = torch.randn(1, device=dev, generator=g)
+    t = torch.randn(64, device=dev, generator=g)
+
+    def run(fn, dt):
+        x = x0.to(dt).requires_grad_(True)
+        w = w0.to(dt).requires_grad_(True)
+        b = b0.to(dt).requires_grad_(True)
+        y = fn(x, w, b)
+        if order == 1:
+            return (y,) + torch.autograd.grad((y * t.to(dt)).sum(), (x, w, b))
+        jx, = torch.autograd.grad(y.sum(), x, create_graph=True)
+        loss = jx.square().sum() + (y * t.to(dt)).sum()
+        return (y,) + torch.autograd.grad(loss, (x, w, b))
+
+    got = run(lambda x, w, b: snops._LinOut.apply(x, w, b), torch.float32)
+    ref = run(lambda x, w, b: torch.addmv(b, x, w.view(-1)), torch.float64)
+    for a, r, what in zip(got, ref, ('y', 'dx', 'dw', 'db')):
+        err = float((a.double() - r).abs().max())
+        assert err <= 2e-5 * (float(r.abs().max()) + 1e-30), (what, err)
