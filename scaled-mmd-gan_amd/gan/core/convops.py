@@ -838,8 +838,16 @@ def _bwd_core(gy, x, w, stride, padding, mask, xmask, into=None):
     if _is_c1(x, w, stride, padding) and _is_c1(gy, w.transpose(0, 1), stride, padding):
         gx = _c1_dx(gy, w) if mask[0] else None
         gw = _c1_wgrad(gy, x, into) if mask[1] else None
-        if (gx is not None or not mask[0]) and (gw is not None or not mask[1]):
-            return gx, gw, False
+        # an output the library did not tile comes from aten ALONE: a gw the
+        # *_wgrad_acc kernel already added into `into` must not be formed twice
+        need_x, need_w = mask[0] and gx is None, mask[1] and gw is None
+        if need_x or need_w:
+            ax, aw, _ = _aten.convolution_backward(gy, x, materialize(w), None, stride, padding,
+                                                   [1, 1], False, [0, 0], 1,
+                                                   [need_x, need_w, False])
+            gx = ax if need_x else gx
+            gw = aw if need_w else gw
+        return gx, gw, False
     if mask[1] and _wgrad_ok(x, gy, w, stride, padding):
         gw = _wino_wgrad(x, gy, into)
         gx = None
@@ -968,7 +976,13 @@ class _ConvBackward(torch.autograd.Function):
 WGRAD_LATE_SUM = os.environ.get('SMMD_WGRAD_LATE_SUM', '1') != '0'
 WGRAD_ACC = os.environ.get('SMMD_WGRAD_ACC', '1') != '0'    # later ones into the first
 # the same for two double-backward nodes' gradients of one gy input
-# (_ConvBackward, _shared_gy_key; SMMD_GY_ACC=0: autograd adds them)
+# (_ConvBackward, _shared_gy_key; SMMD_GY_ACC=0: autograd adds them).
+# Single-consumer rule (both sums): every gradient reaching such an edge must
+# come from a node that takes part in the sum.  A native autograd gradient to
+# the same edge makes autograd's input buffer a new tensor (first + other), and
+# later in-place adds into `first` would be lost; for the SN weights
+# check_late_delivery enforces it at the SN node.  The gy sums are armed only
+# for _ReluPool's gu, whose consumers are the block's two convolutions.
 GY_ACC = os.environ.get('SMMD_GY_ACC', '1') != '0'
 _late = {'armed': False, 'first': {}, 'queue': [], 'queued': 0, 'gy': {}, 'gy_acc': 0}
 # (queued, gy_acc: running counts)
@@ -1088,6 +1102,28 @@ def _late_gw(w, gw, into=None):
     _late['queue'].append((f[1], gw))
     _late['queued'] += 1
     return None
+
+
+def check_late_delivery(out_ids, grads):
+    """The late sums' invariant, checked at the SN node: the gradient autograd
+    delivers for a marked SN output must BE its first recorded contribution
+    (the tensor later terms were queued onto or computed into).  Another
+    consumer sending a native autograd gradient to the same edge would make
+    autograd's input buffer a new tensor (first + other), and every term
+    added into `first` after that would be lost silently -- so raise instead.
+    out_ids: id() of the node's outputs, in the order of grads."""
+    if not _late['armed']:
+        return
+    for oid, g in zip(out_ids, grads):
+        f = _late['first'].get(oid)
+        if f is None or id(f[0]) != oid:
+            continue
+        if g is None or g.data_ptr() != f[1].data_ptr():
+            raise RuntimeError(
+                'late weight-gradient sum: the SN output %s received a gradient other than '
+                'its recorded first contribution (a consumer outside convops._Conv2d / '
+                '_LinOut / _Outer sent it a native gradient); run with '
+                'SMMD_WGRAD_LATE_SUM=0' % (tuple(f[0].shape),))
 
 
 def flush_late_wgrad_sums():

@@ -114,6 +114,7 @@ class _SNBatch(torch.autograd.Function):
     def backward(ctx, *grads):
         from . import convops
         convops.flush_late_wgrad_sums()     # the conv nodes' queued G contributions
+        convops.check_late_delivery(getattr(ctx, '_smmd_out_ids', ()), grads)
         bank = ctx.bank
         n = len(bank.entries)
         saved = ctx.saved_tensors
@@ -214,6 +215,7 @@ class _SNGroup(torch.autograd.Function):
     def backward(ctx, *grads):
         from . import convops
         convops.flush_late_wgrad_sums()     # the conv nodes' queued G contributions
+        convops.check_late_delivery(getattr(ctx, '_smmd_out_ids', ()), grads)
         bank, members = ctx.bank, ctx.members
         k = len(members)
         saved = ctx.saved_tensors
@@ -349,11 +351,15 @@ class SpectralNormBank:
                 m = tuple(members)
                 r = _SNGroup.apply(self, m, *[Ws[i] for i in m], *[ss[i] for i in m])
                 r = r if isinstance(r, tuple) else (r,)
+                if r[0].grad_fn is not None:     # the node's ctx (check_late_delivery)
+                    r[0].grad_fn._smmd_out_ids = tuple(id(t) for t in r)
                 for i, t in zip(m, r):
                     outs[i] = t
             self._fresh = None
         else:
             outs = _SNBatch.apply(self, bool(update_u), flags, *Ws, *ss)
+            if outs and outs[0].grad_fn is not None:     # the node's ctx
+                outs[0].grad_fn._smmd_out_ids = tuple(id(t) for t in outs)
         for e, w in zip(self.entries, outs):
             w._smmd_late_sum = True              # convops._late_gw: summed at the SN node
             if w.shape != e.weight.shape:        # the pool-folded 4 x 4 filter

@@ -255,7 +255,13 @@ def _count_batch(bn):
     to the device buffer when a state_dict is taken: with momentum set it is
     bookkeeping only (TF's batch norm has none), and a device add per call was
     one kernel launch per layer per step (9 x ~4 us per generator forward).
-    A load_state_dict drops the pending count with the value it replaces."""
+    A load_state_dict drops the pending count with the value it replaces.
+    While a step graph is captured (StepGraphs) the host code runs once, at
+    capture: there the device add is captured instead, so every replay counts."""
+    if bn.num_batches_tracked.is_cuda and torch.cuda.is_current_stream_capturing():
+        with torch.no_grad():
+            bn.num_batches_tracked.add_(1)
+        return
     if getattr(bn, '_smmd_batches', None) is None:
         bn._smmd_batches = 0
         bn.register_state_dict_pre_hook(_flush_batches)

@@ -112,3 +112,31 @@ def test_transposed_weight_gemm_equals_copy(N, C, K, H):
     ref = torch.nn.functional.conv_transpose2d(gy.double(), w.double())
     err = float((a.double() - ref).abs().max())
     assert err <= 2e-6 * float(ref.abs().max()) + 1e-30
+
+
+@pytest.mark.parametrize('N,H', [(6, 4), (8, 2), (2, 4)])
+def test_bwd_into_partial_library_shape_counts_dw_once(N, H):
+    """N*H*W % 64 == 32: the weight gradient tiles on the library (32-column
+    chunks) but the input-gradient GEMM (64-column tiles) does not.  `_bwd`
+    with gw_into must return base + dW, not base + 2 dW (the *_wgrad_acc
+    kernel's sum must not be followed by aten's dW of the same term), and
+    aten's dx alone."""
+    from gan.core import _lib, convops
+    C, K = 64, 128
+    L = _lib.lib()
+    assert L.smmd_conv1x1_wgrad_supported(N, C, K, H * H)
+    assert not L.smmd_conv1x1_supported(N, K, C, H * H)
+    g = torch.Generator(device=DEV).manual_seed(N * 31 + H)
+    x = torch.randn(N, C, H, H, device=DEV, generator=g)
+    w = torch.randn(K, C, 1, 1, device=DEV, generator=g) * 0.05
+    gy = torch.randn(N, K, H, H, device=DEV, generator=g)
+    base = torch.randn(K, C, 1, 1, device=DEV, generator=g)
+    into = base.clone()
+    gx, gw = convops._bwd(gy, x, w, [1, 1], [0, 0], (True, True), gw_into=into)
+    _, gxr, gwr = _ref(x, w, None, gy)
+    _close(gx, gxr, 2e-6, 'input gradient')
+    _close(gw - base, gwr, 1e-5, 'accumulated weight gradient')
+    # without `into` the same shape gives the plain dW
+    gx2, gw2 = convops._bwd(gy, x, w, [1, 1], [0, 0], (True, True))
+    _close(gw2, gwr, 1e-5, 'weight gradient')
+    assert torch.equal(gx2, gx)

@@ -104,109 +104,145 @@ def test_critic_step_matches_tf_mirror(dev, arch, size, dim, batch, cl):
         np.testing.assert_allclose(e.u.cpu().numpy(), u.numpy()[0], rtol=1e-4, atol=1e-6)
 
 
+def _aten_convs(prof):
+    """aten convolution ops (MIOpen) recorded by a CPU-activity profile."""
+    return sorted({e.name for e in prof.events()
+                   if e.name.startswith('aten::') and 'conv' in e.name})
+
+
+def _headline_model(dev, batch=64):
+    """SNResNet-64 at imagenet_smmd.yml's widths (every conv tiles on the
+    library: no MIOpen convolution in either step), fixed images and z."""
+    from gan.core.smmd import SMMD
+    torch.manual_seed(0)
+    model = SMMD(_cfg(architecture='snresnet', output_size=64, df_dim=64, gf_dim=64,
+                      batch_size=batch), device=dev)
+    images = torch.rand(batch, 3, 64, 64, generator=torch.Generator().manual_seed(1)).to(dev)
+    z = torch.empty(batch, 128).uniform_(-1, 1, generator=torch.Generator().manual_seed(2)).to(dev)
+    model.sample_z = lambda n, z=z: z
+    model.step = 25
+    model.d_counter, model.g_counter = 0, 0
+    return model, images
+
+
+def _capture_grads(opt):
+    cap = {}
+    orig = opt.step
+
+    def c(*a, **k):
+        cap['g'] = opt.dense_grad().clone()
+        return orig(*a, **k)
+    opt.step = c
+    return cap
+
+
+def _step_record(model, images, profile=False):
+    """Two critic updates (the second with the SN first pass written by the
+    first's fused update) and one generator update: every loss, flat
+    gradient, u, sigma and the parameters after each update."""
+    from torch.profiler import ProfilerActivity, profile as prof_ctx
+    dcap, gcap = _capture_grads(model.d_optim), _capture_grads(model.g_optim)
+    rec = []
+    convs = []
+
+    def run():
+        for kind in ('d', 'd', 'g'):
+            g_loss, d_loss, _ = (model.d_step if kind == 'd' else model.g_step)(images)
+            cap = dcap if kind == 'd' else gcap
+            rec.append((kind, g_loss.detach().clone(), d_loss.detach().clone(), cap.pop('g'),
+                        [e.u.clone() for e in model.sn_D.entries], model.sn_D.sigmas().clone(),
+                        model.d_optim.flat_param.clone(), model.g_optim.flat_param.clone()))
+    if profile:
+        with prof_ctx(activities=[ProfilerActivity.CPU]) as p:
+            run()
+        convs = _aten_convs(p)
+    else:
+        run()
+    torch.cuda.synchronize()
+    return rec, convs
+
+
+def test_headline_step_bit_identical_run_to_run(dev):
+    """Run-to-run determinism of the all-library headline step (DESIGN §3:
+    every library reduction is fixed-order).  Two models built from the same
+    seed take the same critic, critic, generator updates, the second under
+    the profiler (other host timing, so a timing-dependent kernel race shows
+    as a difference): every loss, flat gradient, u, sigma and updated
+    parameter is equal bit for bit (torch.equal), and no MIOpen convolution
+    ran."""
+    a, _ = _headline_model(dev)
+    b, images = _headline_model(dev)
+    assert torch.equal(a.d_optim.flat_param, b.d_optim.flat_param)
+    assert torch.equal(a.g_optim.flat_param, b.g_optim.flat_param)
+    ra, _ = _step_record(a, images)
+    rb, convs = _step_record(b, images, profile=True)
+    assert convs == [], convs
+    names = ('g_loss', 'd_loss', 'grad', 'u', 'sigma', 'd params', 'g params')
+    for i, (xa, xb) in enumerate(zip(ra, rb)):
+        assert xa[0] == xb[0]
+        for name, ta, tb in zip(names, xa[1:], xb[1:]):
+            if isinstance(ta, list):
+                assert all(torch.equal(p, q) for p, q in zip(ta, tb)), (i, xa[0], name)
+            else:
+                assert torch.equal(ta, tb), (i, xa[0], name, float((ta - tb).abs().max()))
+
+
+def _critic_grad(dev, monkeypatch, mod, flag, on, counter):
+    from gan.core import convops
+    monkeypatch.setattr(mod, flag, on)
+    model, images = _headline_model(dev, batch=8)
+    cap = _capture_grads(model.d_optim)
+    n0 = counter()
+    model.d_step(images)
+    return cap['g'], counter() - n0
+
+
 def test_late_wgrad_sums_bit_identical(dev, monkeypatch):
     """convops' late sums of the critic weights' gradient contributions (real
-    pass, fake pass, double backward; added at the SN node instead of by
-    autograd as they arrive, the same sums in the same order) give dL/dW
-    within the run-to-run spread of the critic step itself."""
+    pass, fake pass, double backward; added at the SN node, or computed into
+    the first by the *_wgrad_acc kernels, instead of by autograd as they
+    arrive: the same sums in the same order) give dL/dW bit for bit, on the
+    all-library step at the ImageNet config's width."""
     from gan.core import convops
-    from gan.core.smmd import SMMD
-    grads, queued = [], []
-    for on in (True, True, False):
-        monkeypatch.setattr(convops, 'WGRAD_LATE_SUM', on)
-        torch.manual_seed(0)
-        model = SMMD(_cfg(architecture='snresnet', output_size=64, df_dim=16, gf_dim=16,
-                          batch_size=8), device=dev)
-        images = torch.rand(8, 3, 64, 64, generator=torch.Generator().manual_seed(1)).to(dev)
-        z = torch.empty(8, 128).uniform_(-1, 1, generator=torch.Generator().manual_seed(2)).to(dev)
-        model.sample_z = lambda n, z=z: z
-        cap = {}
-        orig = model.d_optim.step
-
-        def c(*a, _cap=cap, _m=model, _o=orig, **k):
-            _cap['g'] = _m.d_optim.dense_grad().clone()
-            return _o(*a, **k)
-        model.d_optim.step = c
-        model.step = 25
-        model.d_counter, model.g_counter = 0, 0
-        n0 = convops._late['queued']
-        model.d_step(images)
-        queued.append(convops._late['queued'] - n0)
-        grads.append(cap['g'])
-    assert queued[0] > 0 and queued[2] == 0
-    # two model instances do not give bit-identical critic steps (the same
-    # path twice differs already), so the late sums are held to that spread
-    scale = float(grads[0].abs().max())
-    same = float((grads[0] - grads[1]).abs().max())
-    late = float((grads[0] - grads[2]).abs().max())
-    assert late <= max(4 * same, 1e-6 * scale), (late, same, scale)
+    on, q_on = _critic_grad(dev, monkeypatch, convops, 'WGRAD_LATE_SUM', True,
+                            lambda: convops._late['queued'])
+    off, q_off = _critic_grad(dev, monkeypatch, convops, 'WGRAD_LATE_SUM', False,
+                              lambda: convops._late['queued'])
+    assert q_on > 0 and q_off == 0
+    assert torch.equal(on, off), float((on - off).abs().max())
 
 
-def test_late_bias_sums_match_accumulation(dev, monkeypatch):
+def test_late_bias_sums_bit_identical(dev, monkeypatch):
     """The critic biases' later gradient contributions (the fake pass after
-    the real one) added to .grad after the backward (convops late bias sums)
-    give dL/db -- and every other gradient -- within the run-to-run spread of
-    the critic step itself."""
+    the real one) added to .grad after the backward (convops late bias sums):
+    dL/db -- and every other gradient -- bit for bit the accumulation's."""
     from gan.core import convops
-    from gan.core.smmd import SMMD
-    grads, queued = [], []
-    for on in (True, True, False):
-        monkeypatch.setattr(convops, 'BIAS_LATE_SUM', on)
-        torch.manual_seed(0)
-        model = SMMD(_cfg(architecture='snresnet', output_size=64, df_dim=16, gf_dim=16,
-                          batch_size=8), device=dev)
-        images = torch.rand(8, 3, 64, 64, generator=torch.Generator().manual_seed(1)).to(dev)
-        z = torch.empty(8, 128).uniform_(-1, 1, generator=torch.Generator().manual_seed(2)).to(dev)
-        model.sample_z = lambda n, z=z: z
-        cap = {}
-        orig = model.d_optim.step
-
-        def c(*a, _cap=cap, _m=model, _o=orig, **k):
-            _cap['g'] = _m.d_optim.dense_grad().clone()
-            return _o(*a, **k)
-        model.d_optim.step = c
-        model.step = 25
-        model.d_counter, model.g_counter = 0, 0
-        n0 = convops._lateb['queued']
-        model.d_step(images)
-        queued.append(convops._lateb['queued'] - n0)
-        grads.append(cap['g'])
-    assert queued[0] > 0 and queued[2] == 0
-    scale = float(grads[0].abs().max())
-    same = float((grads[0] - grads[1]).abs().max())
-    late = float((grads[0] - grads[2]).abs().max())
-    assert late <= max(4 * same, 1e-6 * scale), (late, same, scale)
+    on, q_on = _critic_grad(dev, monkeypatch, convops, 'BIAS_LATE_SUM', True,
+                            lambda: convops._lateb['queued'])
+    off, q_off = _critic_grad(dev, monkeypatch, convops, 'BIAS_LATE_SUM', False,
+                              lambda: convops._lateb['queued'])
+    assert q_on > 0 and q_off == 0
+    assert torch.equal(on, off), float((on - off).abs().max())
 
 
-def test_generator_gradient_gather_matches_accumulation(dev, monkeypatch):
+def test_generator_gradient_gather_bit_identical(dev, monkeypatch):
     """The generator step's gradients gathered into the flat buffer by one
-    multi-tensor copy (optim.FlatAdam.gather) update the generator as the
-    per-parameter accumulation does, within the step's run-to-run spread."""
+    multi-tensor copy (optim.FlatAdam.gather) update the generator bit for
+    bit as the per-parameter accumulation does (the all-library step at the
+    ImageNet config's width)."""
     from gan.core import model as M
-    from gan.core.smmd import SMMD
     out = []
-    for on in (True, True, False):
+    for on in (True, False):
         monkeypatch.setattr(M, 'GRAD_GATHER', on)
-        torch.manual_seed(0)
-        model = SMMD(_cfg(architecture='snresnet', output_size=64, df_dim=16, gf_dim=16,
-                          batch_size=8), device=dev)
-        images = torch.rand(8, 3, 64, 64, generator=torch.Generator().manual_seed(1)).to(dev)
-        z = torch.empty(8, 128).uniform_(-1, 1, generator=torch.Generator().manual_seed(2)).to(dev)
-        model.sample_z = lambda n, z=z: z
+        model, images = _headline_model(dev, batch=8)
         before = model.g_optim.flat_param.clone()
         model.g_step(images)
         assert all(p.grad is not None and p.grad.data_ptr() ==
                    model.g_optim.flat_grad[model.g_optim.offsets[i]:].data_ptr()
                    for i, p in enumerate(model.g_optim.params) if p.numel())
         out.append((model.g_optim.flat_param - before, model.g_optim.flat_grad.clone()))
-    scale = float(out[0][1].abs().max())
-    same = float((out[0][1] - out[1][1]).abs().max())
-    diff = float((out[0][1] - out[2][1]).abs().max())
-    assert diff <= max(4 * same, 1e-6 * scale), (diff, same, scale)
-    dscale = float(out[0][0].abs().max())
-    dsame = float((out[0][0] - out[1][0]).abs().max())
-    ddiff = float((out[0][0] - out[2][0]).abs().max())
-    assert ddiff <= max(4 * dsame, 1e-6 * dscale), (ddiff, dsame, dscale)
+    assert torch.equal(out[0][1], out[1][1]), float((out[0][1] - out[1][1]).abs().max())
+    assert torch.equal(out[0][0], out[1][0])
 
 
 def test_generator_step_updates_only_G(dev):
