@@ -74,7 +74,9 @@ int smmd_abi_version(void);         /* bumped on any ABI change (2: Gram/poly,
                                        13: the weight gradients' *_acc forms,
                                        14: smmd_wino3x3_conv_mask,
                                        15: smmd_wino4x4s2_conv_acc,
-                                       16: smmd_conv1x1_t) */
+                                       16: smmd_conv1x1_t,
+                                       17: smmd_smmd_loss_fwd_gathered,
+                                       smmd_smmd_loss_bwd_ex) */
 const char *smmd_source_hash(void); /* first 16 hex digits of the SHA-256 of the
                                        sources this binary was built from
                                        (csrc .hip and .hpp files in byte order,
@@ -218,6 +220,41 @@ smmd_status smmd_smmd_loss_bwd(const float *jac, int n_cols, int b, int64_t per_
                                const float *g_mmd2_grad, const float *gx_unit, int m,
                                const float *gy_unit, int n, int d, float *gjac, float *gfeat,
                                float *dX, float *dY, smmd_stream_t stream);
+
+/* The all-gather ('global') data-parallel mode's fused loss (ABI 17).
+ * Replaces, for the data-parallel SMMD step, the same reference code as
+ * smmd_smmd_loss_fwd (smmd.py:10-23, model.py:366-403 over the global batch
+ * of model.py:187-216) when every rank sweeps the gathered rows whole:
+ * X [m, d], Y [n, d] are the GLOBAL gathered feature rows, and J / nD are
+ * not reduced from a Jacobian here but summed in rank order from the
+ * gathered per-rank partials stats[r * stats_stride + 0] (J share) and
+ * [r * stats_stride + 1] (nD share), r < world -- each rank's
+ * smmd_scaled_loss_fwd out[3..4] over its own rows with b_total = the global
+ * batch (gan.core.ops.scaling_partials), carried by the feature all-gather.
+ * Outputs as smmd_smmd_loss_fwd (grad_x / grad_y for ALL m + n rows; out[8]
+ * with J, nD the summed values; per-sample norms are not formed).  loss_ws:
+ * at least smmd_scaled_loss_workspace_bytes(1, 1) (its arrival ticket).
+ * Returns SMMD_EUNSUPPORTED where smmd_smmd_loss_fwd would.
+ *
+ * smmd_smmd_loss_bwd_ex: smmd_smmd_loss_bwd with the Jacobian's normaliser
+ *   b_total (the global batch; b = this rank's samples in jac): gjac =
+ *   dL/dQ * 2 jac / b_total.  smmd_smmd_loss_bwd is this with b_total = b.
+ *   gx_unit / gy_unit: this rank's rows of the forward's unit gradients. */
+smmd_status smmd_smmd_loss_fwd_gathered(const smmd_kernel_desc *desc, const float *X, int m,
+                                        const float *Y, int n, int d, int biased,
+                                        const float *stats, int world, int stats_stride,
+                                        float sc, int variant, int sqrt_scale, float *out_sums,
+                                        float *out_mmd2, float *grad_x, float *grad_y, float *out,
+                                        void *ws, size_t ws_bytes, void *loss_ws,
+                                        size_t loss_ws_bytes, smmd_stream_t stream);
+
+smmd_status smmd_smmd_loss_bwd_ex(const float *jac, int n_cols, int b, int b_total,
+                                  int64_t per_sample, const float *feat, int dof,
+                                  const float *fwd_out, float sc, int variant, int sqrt_scale,
+                                  const float *g_loss_grad, const float *g_mmd2_grad,
+                                  const float *gx_unit, int m, const float *gy_unit, int n, int d,
+                                  float *gjac, float *gfeat, float *dX, float *dY,
+                                  smmd_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * Spectral normalisation, all layers of a network in one set of launches.

@@ -754,7 +754,7 @@ const char *smmd_status_string(smmd_status s) {
     return "SMMD_?: unknown status";
 }
 
-int smmd_abi_version(void) { return 16; }
+int smmd_abi_version(void) { return 17; }
 
 // Path choice.  d > 32: the MFMA Gram path (the row sweep holds a row in
 // registers up to 32 features).  d <= 32: the row sweep, except where the
@@ -957,6 +957,63 @@ smmd_status smmd_smmd_loss_fwd(const smmd_kernel_desc *desc, const float *X, int
     q.out = out;
     q.per_sample_out = per_sample_out;
     q.nblocks = rows_j * nchunk;
+    return tile_mmd2_launch(t, desc->kind, ws, (hipStream_t)stream, &q);
+}
+
+// The all-gather mode's fused loss: X, Y are the gathered global rows (every
+// rank sweeps them whole), J / nD come from the gathered per-rank partials
+// (no Jacobian pass here: each rank reduced its own rows before the gather).
+smmd_status smmd_smmd_loss_fwd_gathered(const smmd_kernel_desc *desc, const float *X, int m,
+                                        const float *Y, int n, int d, int biased,
+                                        const float *stats, int world, int stats_stride,
+                                        float sc, int variant, int sqrt_scale, float *out_sums,
+                                        float *out_mmd2, float *grad_x, float *grad_y, float *out,
+                                        void *ws, size_t ws_bytes, void *loss_ws,
+                                        size_t loss_ws_bytes, smmd_stream_t stream) {
+    if (!desc || !X || !Y || m < 1 || n < 1 || d < 1) return SMMD_EINVAL;
+    if (!out_mmd2 || !grad_x || !grad_y || !stats || !out || world < 1 || stats_stride < 2)
+        return SMMD_EINVAL;
+    if (variant != 0 && variant != 1) return SMMD_EINVAL;
+    KParams kp;
+    if (!make_kparams(desc, kp)) return SMMD_EINVAL;
+    if (!use_tile(m, n, d)) return SMMD_EUNSUPPORTED;      // the caller runs the separate calls
+    if (!ws || ws_bytes < smmd_mmd2_workspace_bytes(m, n, d)) return SMMD_EWORKSPACE;
+    if (!loss_ws || loss_ws_bytes < SQ_WS_HEADER) return SMMD_EWORKSPACE;
+    const double md = m, nd = n;
+    const int is_biased = biased ? 1 : 0;
+    const double wxx = is_biased ? 1.0 / (md * md) : 1.0 / (md * (md - 1.0));
+    const double wyy = is_biased ? 1.0 / (nd * nd) : 1.0 / (nd * (nd - 1.0));
+    TileArgs t;
+    memset(&t, 0, sizeof(t));
+    t.X = X; t.Y = Y; t.m = m; t.n = n; t.d = d;
+    t.nrows = m + n; t.nxr = m; t.x_begin = 0; t.y_begin = 0;
+    t.tanh_in = desc->tanh_inputs ? 1 : 0;
+    t.biased = is_biased;
+    t.has_const = desc->has_const_diag ? 1 : 0;
+    t.const_diag = desc->const_diag;
+    t.trace_mode = (!is_biased && !t.has_const) ? 1 : 0;
+    t.need_grad = 1;
+    t.gw_same_x = (float)(2.0 * wxx);
+    t.gw_same_y = (float)(2.0 * wyy);
+    t.gw_cross = (float)(-2.0 / (md * nd));
+    t.grad_x = grad_x; t.grad_y = grad_y;
+    t.out_sums = out_sums; t.out_mmd2 = out_mmd2;
+    t.kp = kp;
+    ScaledLossArgs q;
+    memset(&q, 0, sizeof(q));
+    q.counter = (unsigned *)loss_ws;
+    q.part = (double *)((char *)loss_ws + SQ_WS_HEADER);
+    q.nchunk = 1;
+    q.b_total = 1;
+    q.variant = variant;
+    q.sqrt_scale = sqrt_scale;
+    q.base_loss = out_mmd2;
+    q.sc = sc;
+    q.out = out;
+    q.nblocks = 0;                             // no squared-norm blocks
+    q.stats = stats;
+    q.stats_world = world;
+    q.stats_stride = stats_stride;
     return tile_mmd2_launch(t, desc->kind, ws, (hipStream_t)stream, &q);
 }
 

@@ -467,8 +467,21 @@ smmd_status smmd_smmd_loss_bwd(const float *jac, int n_cols, int b, int64_t per_
                                const float *g_mmd2_grad, const float *gx_unit, int m,
                                const float *gy_unit, int n, int d, float *gjac, float *gfeat,
                                float *dX, float *dY, smmd_stream_t stream) {
+    return smmd_smmd_loss_bwd_ex(jac, n_cols, b, b, per_sample, feat, dof, fwd_out, sc, variant,
+                                 sqrt_scale, g_loss_grad, g_mmd2_grad, gx_unit, m, gy_unit, n, d,
+                                 gjac, gfeat, dX, dY, stream);
+}
+
+smmd_status smmd_smmd_loss_bwd_ex(const float *jac, int n_cols, int b, int b_total,
+                                  int64_t per_sample, const float *feat, int dof,
+                                  const float *fwd_out, float sc, int variant, int sqrt_scale,
+                                  const float *g_loss_grad, const float *g_mmd2_grad,
+                                  const float *gx_unit, int m, const float *gy_unit, int n, int d,
+                                  float *gjac, float *gfeat, float *dX, float *dY,
+                                  smmd_stream_t stream) {
     if (!jac || !fwd_out || !g_loss_grad || n_cols < 1 || b < 1 || per_sample < 1)
         return SMMD_EINVAL;
+    if (b_total < 1) b_total = b;
     if (!gx_unit || !gy_unit || !dX || !dY || m < 1 || n < 1 || d < 1) return SMMD_EINVAL;
     if (variant != 0 && variant != 1) return SMMD_EINVAL;
     if (variant == 1 && gfeat && (!feat || dof < 1)) return SMMD_EINVAL;
@@ -487,9 +500,9 @@ smmd_status smmd_smmd_loss_bwd(const float *jac, int n_cols, int b, int64_t per_
     mp.dX = dX;
     mp.dY = dY;
     hipLaunchKernelGGL(scaled_loss_bwd_kernel, dim3((unsigned)blocks), dim3(256), 0,
-                       (hipStream_t)stream, jac, n_jac, b, feat, (int64_t)b * (dof > 0 ? dof : 0),
-                       dof, fwd_out, sc, variant, sqrt_scale, g_loss_grad, nullptr, gjac, gfeat,
-                       vec, mp);
+                       (hipStream_t)stream, jac, n_jac, b_total, feat,
+                       (int64_t)b * (dof > 0 ? dof : 0), dof, fwd_out, sc, variant, sqrt_scale,
+                       g_loss_grad, nullptr, gjac, gfeat, vec, mp);
     return last_launch_status();
 }
 

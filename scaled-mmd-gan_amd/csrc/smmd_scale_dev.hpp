@@ -30,6 +30,12 @@ struct ScaledLossArgs {
     float *out;
     float *per_sample_out;
     int nblocks;         // squared-norm blocks (rows * nchunk)
+    // the all-gather mode's fused loss (smmd_smmd_loss_fwd_gathered): J and nD
+    // are not reduced from the Jacobian here but summed, in rank order, from
+    // the gathered per-rank partials stats[r * stats_stride + {0, 1}]
+    // (ops.scaling_partials of every rank, carried by the feature all-gather)
+    const float *stats;
+    int stats_world, stats_stride;
 };
 
 // ---- per-(row, chunk) partial sum of squares of block `blk` (256 threads):
@@ -125,8 +131,18 @@ __device__ __forceinline__ void scaled_loss_final(const ScaledLossArgs &a, float
         nd = fs / ((double)b_total * dof);              // model.py:385
     }
     if (threadIdx.x == 0) {
-        const float J = (float)(jsum / (double)b_total); // model.py:384
-        const float nD = (float)nd;
+        float J = (float)(jsum / (double)b_total);       // model.py:384
+        float nD = (float)nd;
+        if (a.stats) {
+            // the gathered partials (each already / b_total), summed in rank
+            // order as collectives.StepExchange does: the same bits
+            J = a.stats[0];
+            nD = a.stats[1];
+            for (int r = 1; r < a.stats_world; ++r) {
+                J = J + a.stats[(size_t)r * a.stats_stride];
+                nD = nD + a.stats[(size_t)r * a.stats_stride + 1];
+            }
+        }
         const float q = (variant == 1) ? (J + nD) : J;  // model.py:387-390
         const float scale = 1.f / (sc * q + 1.f);
         const float f = sqrt_scale ? sqrtf(scale) : scale;   // smmd.py:22 / :41

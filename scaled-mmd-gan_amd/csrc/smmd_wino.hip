@@ -552,6 +552,9 @@ __global__ __launch_bounds__(WN_T, 1) void wino_conv_kernel(
 // accumulators through LDS and each finishes 8 of the 16 rows), so the two
 // kernels' outputs are bit-identical.
 constexpr int W8_T = 512;
+#ifndef W8_VPAIR
+#define W8_VPAIR 1      // the V stage in channel pairs (see store_vrow)
+#endif
 
 // The 8-wave kernel's transform of one channel where tile rows are whole lane
 // groups (no edge loads) and the rows outside the image were loaded as zeros
@@ -684,17 +687,51 @@ __device__ __forceinline__ void wino8_body(const float *__restrict__ x, const fl
 #pragma unroll
         for (int i = 0; i < 4; ++i) glds16(uoff[i], sb, dst + i * 1024);
     };
-    // V of this wave's channel: float index ((p h t) c4) with h = w >> 2, c4 = w & 3
+    // V of this wave's channel (h = w >> 2, c4 = w & 3).  W8_VPAIR (default):
+    // float index ((((p h) cp) t) c2) with cp = c4 >> 1, c2 = c4 & 1 -- a
+    // wave's ds_write_b32 then covers 16 banks of the 32 (2-way: no cost;
+    // the [t][c4] form's 4-way conflict doubled every V store) and a fragment
+    // is two conflict-free ds_read_b64 (the same 4 cycles as one b128);
+    // otherwise ((p h t) c4).  The MFMA operands are the same registers.
+#if W8_VPAIR
+    const int vlane = (((w >> 2) * 2 + ((w & 3) >> 1)) * 64 + lane) * 2 + (w & 1);
+#endif
     auto store_vrow = [&](float *Vf, int i, const float (&v)[4]) {
+#ifdef W8_NO_VSTORE       // timing-only diagnostic: the transform kept, its stores not issued
+#pragma unroll
+        for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(v[j]));
+        return;
+#endif
 #pragma unroll
         for (int j = 0; j < 4; ++j)
+#if W8_VPAIR
+            (Vf + vlane)[(i * 4 + j) * 512] = v[j];
+#else
             Vf[(((i * 4 + j) * 2 + (w >> 2)) * 64 + lane) * 4 + (w & 3)] = v[j];
+#endif
     };
     f32x16 acc[8];
 #pragma unroll
     for (int p = 0; p < 8; ++p) acc[p] = f32x16{};
 
     const int q = w & 3, th = q & 1, kh = q >> 1, hl = lane >> 5, l32 = lane & 31;
+    // a V fragment (point p, this lane's reduction half and tile)
+#if W8_VPAIR
+    // the channel pair's second half 64 f2v on, through an opaque (uniform)
+    // offset: two ds_read_b64 (4 cycles), not one merged ds_read2_b64 (8)
+    int vhi;
+    asm volatile("s_mov_b32 %0, 64" : "=s"(vhi));
+#endif
+    auto vfrag = [&](const float4 *V_, int p) -> float4 {
+#if W8_VPAIR
+        const f2v *V2 = reinterpret_cast<const f2v *>(V_) + (hl * 2 * 64 + th * 32 + l32);
+        const f2v lo = V2[p * 4 * 64];
+        const f2v hi = (V2 + vhi)[p * 4 * 64];
+        return float4{lo.x, lo.y, hi.x, hi.y};
+#else
+        return V_[(p * 2 + hl) * 64 + th * 32 + l32];
+#endif
+    };
     constexpr int P0 = 8 * PH;
     constexpr int SL = PH ? W8_SLOT1 : W8_SLOT;
     const float bias_k = (bias && tid < WN_KB) ? bias[kb * WN_KB + tid] : 0.f;
@@ -734,9 +771,8 @@ __device__ __forceinline__ void wino8_body(const float *__restrict__ x, const fl
         // under the next chunk's load issue
         const float4 *V_ = Vs + buf * (WN_STAGE / 4);
         const float4 *U_ = Us + buf * (WN_STAGE / 4);
-        float4 a0 = U_[(P0 * 2 + hl) * 64 + kh * 32 + l32], b0 = V_[(P0 * 2 + hl) * 64 + th * 32 + l32];
-        float4 a1 = U_[((P0 + 1) * 2 + hl) * 64 + kh * 32 + l32],
-               b1 = V_[((P0 + 1) * 2 + hl) * 64 + th * 32 + l32];
+        float4 a0 = U_[(P0 * 2 + hl) * 64 + kh * 32 + l32], b0 = vfrag(V_, P0);
+        float4 a1 = U_[((P0 + 1) * 2 + hl) * 64 + kh * 32 + l32], b1 = vfrag(V_, P0 + 1);
         __builtin_amdgcn_sched_barrier(0);
         if (more) {
 #ifndef W8_NO_DMA         // (W8_NO_*: timing-only diagnostic builds, wrong results)
@@ -766,9 +802,9 @@ __device__ __forceinline__ void wino8_body(const float *__restrict__ x, const fl
                         __builtin_amdgcn_mfma_f32_32x32x2f32(ca1[s4], cb1[s4], acc[2 * pp + 1], 0, 0, 0);
                 if (m == 0 && pp < 3) {
                     a0 = U_[((p + 2) * 2 + hl) * 64 + kh * 32 + l32];
-                    b0 = V_[((p + 2) * 2 + hl) * 64 + th * 32 + l32];
+                    b0 = vfrag(V_, p + 2);
                     a1 = U_[((p + 3) * 2 + hl) * 64 + kh * 32 + l32];
-                    b1 = V_[((p + 3) * 2 + hl) * 64 + th * 32 + l32];
+                    b1 = vfrag(V_, p + 3);
                 }
                 const int K = pp * 8 + m;
 #ifdef W8_NO_XFORM

@@ -29,7 +29,7 @@ SN_P1_READY = 1            # smmd_sn_power_iter_ex flag
 ADAM_SN_GDIRECT = 1        # smmd_adam_flat_sn2 flag
 OPT_MAX_FUSED = 96         # tensors smmd_adam_flat_sn takes in one call
 SN_MAX_FUSED = 16          # SN layers smmd_adam_flat_sn takes in one call
-ABI_VERSION = 16
+ABI_VERSION = 17
 
 KIND_RBF, KIND_RQ, KIND_DISTANCE, KIND_DOT = 0, 1, 2, 3
 SMMD_EUNSUPPORTED = 4       # smmd_status (include/smmd_hip.h)
@@ -109,6 +109,11 @@ _SIGS = {
                                 _I, _P, _P, _P, _P, _P]),
     'smmd_scaled_loss_bwd': (_I, [_P, _I, _I, _I, _I64, _P, _I, _P, _F, _I, _I, _P, _P, _P, _P,
                                   _P]),
+    'smmd_smmd_loss_fwd_gathered': (_I, [ctypes.POINTER(KernelDesc), _P, _I, _P, _I, _I, _I, _P,
+                                         _I, _I, _F, _I, _I, _P, _P, _P, _P, _P, _P, _SZ, _P, _SZ,
+                                         _P]),
+    'smmd_smmd_loss_bwd_ex': (_I, [_P, _I, _I, _I, _I64, _P, _I, _P, _F, _I, _I, _P, _P, _P, _I,
+                                   _P, _I, _I, _P, _P, _P, _P, _P]),
     'smmd_sn_workspace_bytes': (_SZ, [ctypes.POINTER(SnLayer), _I]),
     'smmd_sn_power_iter': (_I, [ctypes.POINTER(SnLayer), _I, _I, _F, _I, _P, _SZ, _P]),
     'smmd_sn_power_iter_ex': (_I, [ctypes.POINTER(SnLayer), _I, _I, _F, _I, _I, _P, _SZ, _P]),

@@ -103,9 +103,17 @@ class StepExchange:
         self.stats = None         # local partials [2] (J, nD), set ahead of gather
         self.stats_total = None   # global [2] after gather
         self.used = False
+        # the fused loss of this mode (mmd._mmd2_scaled_gathered): set by
+        # MMD_GAN._prepare_exchange when apply_scaling is SMMD's own
+        self.fuse = False
+        self.sc = None
+        self.variant = 0
+        self.result = None        # (mmd2, g_loss, out) of the fused launch
 
-    def gather(self, X, Y):
-        """[X; Y; stats] of every rank -> (X_all, Y_all) in rank order."""
+    def gather_packed(self, X, Y):
+        """The all-gather alone: (allp [world, (ml + nl) d (+ 2)], X_all,
+        Y_all), allp's tail columns being every rank's stats (the fused loss
+        sums them in its own launch, mmd._SMMDLossGathered)."""
         if self.used:
             raise RuntimeError('StepExchange.gather runs once per loss evaluation')
         self.used = True
@@ -117,6 +125,12 @@ class StepExchange:
         allp = gather_rows(packed, self.group).view(self.world, -1)
         Xa = allp[:, :ml * d].reshape(self.world * ml, d)
         Ya = allp[:, ml * d:(ml + nl) * d].reshape(self.world * nl, d)
+        return allp, Xa, Ya
+
+    def gather(self, X, Y):
+        """[X; Y; stats] of every rank -> (X_all, Y_all) in rank order."""
+        ml, nl, d = X.shape[0], Y.shape[0], X.shape[1]
+        allp, Xa, Ya = self.gather_packed(X, Y)
         if self.stats is not None:
             tot = allp[0, (ml + nl) * d:].clone()
             for r in range(1, self.world):      # fixed rank order

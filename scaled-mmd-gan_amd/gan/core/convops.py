@@ -180,13 +180,47 @@ def wino_applicable(x, cin, cout, k, stride, padding):
 # bumping versions; the SN bank's W_eff is a new tensor every refresh).  The
 # entry holds the weight only through a weak reference whose finalizer drops
 # the entry when the weight is freed, so a superseded W_eff or folded filter
-# takes its transform with it instead of pinning both until an eviction.  Off
-# during HIP-graph capture: a replay must re-transform what it convolves.
+# takes its transform with it instead of pinning both until an eviction.  Not
+# used during HIP-graph capture (a replay must re-transform what it convolves):
+# there the capture's own cache below serves the step's repeated transforms.
 # Shared by the 3x3 and the stride-2 kernels, capped at 1 GiB of transforms
 # (a 512 -> 1024 stride-2 filter transforms to 75 MB), oldest first.
 _WINO_CACHE = {}        # key -> (weakref to w, version, epoch, u)
 _WINO_CACHE_MAX_BYTES = 1 << 30
 _wino_cache_bytes = [0]
+
+
+# A step-graph capture's own filter cache (StepGraphs._capture arms it): inside
+# one captured step every weight keeps its values (the update comes last), so
+# a weight convolved several times is transformed once and the later launches
+# read the graph-pool buffer the first one wrote -- in every replay too.  It
+# holds the weights strongly (no id reuse) and lives for one capture only: a
+# buffer of another graph's pool must never be read.
+_CAPTURE_CACHE = [None]
+
+
+def arm_capture_cache(on):
+    _CAPTURE_CACHE[0] = {} if on else None
+
+
+def _filter_cache_get(key, w):
+    """(cached transform or None, whether the result may be stored)."""
+    if not torch.cuda.is_current_stream_capturing():
+        return _cache_get(key, w), True
+    cc = _CAPTURE_CACHE[0]
+    if cc is None:
+        return None, False
+    e = cc.get(key)
+    if e is not None and e[0] is w and e[1] == w._version:
+        return e[2], True
+    return None, True
+
+
+def _filter_cache_put(key, w, u):
+    if not torch.cuda.is_current_stream_capturing():
+        _cache_put(key, w, u)
+    elif _CAPTURE_CACHE[0] is not None:
+        _CAPTURE_CACHE[0][key] = (w, w._version, u)
 
 
 def _cache_get(key, w):
@@ -293,12 +327,10 @@ def _param_epoch(w):
 
 def _wino_filter(w, co, ci, mode):
     from . import _lib
-    capturing = torch.cuda.is_current_stream_capturing()
     key = (id(w), 'w3', mode)
-    if not capturing:
-        u = _cache_get(key, w)
-        if u is not None:
-            return u
+    u, store = _filter_cache_get(key, w)
+    if u is not None:
+        return u
     L = _lib.lib()
     u = torch.empty(L.smmd_wino3x3_filter_bytes(co, ci) // 4, dtype=w.dtype, device=w.device)
     lz = _lazy(w)
@@ -313,8 +345,8 @@ def _wino_filter(w, co, ci, mode):
             st = L.smmd_wino3x3_filter(_lib.ptr(w), co, ci, int(mode), _lib.ptr(u), u.numel() * 4,
                                        _lib.stream_handle(w.device))
     _lib.check(st, 'smmd_wino3x3_filter')
-    if not capturing:
-        _cache_put(key, w, u)
+    if store:
+        _filter_cache_put(key, w, u)
     return u
 
 
@@ -459,12 +491,10 @@ def _is_s2t(g, w, stride, padding):
 
 def _s2_filter(w, transposed):
     from . import _lib
-    capturing = torch.cuda.is_current_stream_capturing()
     key = (id(w), 's2', transposed)
-    if not capturing:
-        u = _cache_get(key, w)
-        if u is not None:
-            return u
+    u, store = _filter_cache_get(key, w)
+    if u is not None:
+        return u
     L = _lib.lib()
     a, b = w.shape[0], w.shape[1]
     u = torch.empty(L.smmd_wino4x4s2_filter_bytes(a, b) // 4, dtype=w.dtype, device=w.device)
@@ -480,8 +510,8 @@ def _s2_filter(w, transposed):
             fn = L.smmd_wino4x4s2t_filter if transposed else L.smmd_wino4x4s2_filter
             st = fn(_lib.ptr(w), a, b, _lib.ptr(u), u.numel() * 4, _lib.stream_handle(w.device))
     _lib.check(st, 'smmd_wino4x4s2_filter')
-    if not capturing:
-        _cache_put(key, w, u)
+    if store:
+        _filter_cache_put(key, w, u)
     return u
 
 
@@ -716,15 +746,13 @@ def _c1_fwd(x, w, b):
 def _c1_wt(w):
     """W^T [cin, cout] of a 1x1 weight, cached like the filter transforms (a
     critic step takes several input gradients of each shortcut)."""
-    capturing = torch.cuda.is_current_stream_capturing()
     key = (id(w), 'c1t')
-    if not capturing:
-        u = _cache_get(key, w)
-        if u is not None:
-            return u
+    u, store = _filter_cache_get(key, w)
+    if u is not None:
+        return u
     u = materialize(w).reshape(w.shape[0], w.shape[1]).t().contiguous()
-    if not capturing:
-        _cache_put(key, w, u)
+    if store:
+        _filter_cache_put(key, w, u)
     return u
 
 

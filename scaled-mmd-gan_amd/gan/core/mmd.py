@@ -310,6 +310,110 @@ class _SMMDLoss(torch.autograd.Function):
         return dX, dY, gjac, gfeat, None, None, None, None
 
 
+class _SMMDLossGathered(torch.autograd.Function):
+    """The all-gather mode's SMMD loss: the step exchange's one packed
+    all-gather, then ONE launch (smmd_smmd_loss_fwd_gathered) for the MMD^2
+    sweep over the gathered global rows and the scaled loss, whose J / nD the
+    kernel sums in rank order from the gathered per-rank partials; its
+    backward is one smmd_smmd_loss_bwd_ex launch over this rank's rows and
+    Jacobian (normaliser: the global batch).  Replaces, in that mode,
+    smmd_mmd2_fwd + the torch sum of the partials + smmd_scaled_loss_finalize
+    forward and the two separate backward passes."""
+
+    @staticmethod
+    def forward(ctx, X, Y, jac, feat, spec, biased, sc, variant, ex):
+        X = _features(X)
+        Y = _features(Y)
+        _lib.require_cuda(jac, feat)
+        jac = jac.contiguous()
+        feat_c = feat.contiguous() if feat is not None else None
+        dev = X.device
+        L = _lib.lib()
+        ml, nl, d = X.shape[0], Y.shape[0], X.shape[1]
+        allp, Xa, Ya = ex.gather_packed(X, Y)
+        allp = allp.contiguous()
+        world, rank = ex.world, ex.rank
+        m, n = Xa.shape[0], Ya.shape[0]
+        n_cols, b = jac.shape[0], jac.shape[1]
+        per = jac[0, 0].numel()
+        dof = feat_c.shape[1] if feat_c is not None else 0
+        sums = torch.empty(8, device=dev, dtype=torch.float32)
+        mm = torch.empty(1, device=dev, dtype=torch.float32)
+        gx = torch.empty((m, d), device=dev, dtype=torch.float32)
+        gy = torch.empty((n, d), device=dev, dtype=torch.float32)
+        out = torch.empty(8, device=dev, dtype=torch.float32)
+        ws = _lib.workspace('mmd2', L.smmd_mmd2_workspace_bytes(m, n, d), dev)
+        lws = _lib.workspace('scaled_loss', L.smmd_scaled_loss_workspace_bytes(1, 1), dev)
+        stats = allp[:, (ml + nl) * d:]
+        with _lib.timed('smmd_smmd_loss_fwd'):
+            st = L.smmd_smmd_loss_fwd_gathered(
+                spec.desc(), _lib.ptr(Xa), m, _lib.ptr(Ya), n, d, 1 if biased else 0,
+                _lib.ptr(stats), world, allp.shape[1], float(sc), variant, 0, _lib.ptr(sums),
+                _lib.ptr(mm), _lib.ptr(gx), _lib.ptr(gy), _lib.ptr(out), _lib.ptr(ws), ws.numel(),
+                _lib.ptr(lws), lws.numel(), _lib.stream_handle(dev))
+        _lib.check(st, 'smmd_smmd_loss_fwd_gathered')   # the Python gate mirrors use_tile
+        ex.stats_total = out[3:5]
+        gx_own = gx[rank * ml:(rank + 1) * ml]
+        gy_own = gy[rank * nl:(rank + 1) * nl]
+        ctx.save_for_backward(gx_own, gy_own, jac, feat_c, out)
+        ctx.cfg = (n_cols, b, world * b, per, dof, float(sc), variant, ml, nl, d)
+        ctx.mark_non_differentiable(sums, out)
+        ctx.set_materialize_grads(False)
+        return mm.view(()), out[0].view(()), sums, out
+
+    @staticmethod
+    def backward(ctx, g_mmd, g_loss, g_sums, g_out):
+        gx, gy, jac, feat, out = ctx.saved_tensors
+        n_cols, b, b_total, per, dof, sc, variant, m, n, d = ctx.cfg
+        dev = gx.device
+        go = (g_loss.reshape(1).contiguous().to(torch.float32) if g_loss is not None
+              else torch.zeros(1, device=dev, dtype=torch.float32))
+        gm = g_mmd.reshape(1).contiguous().to(torch.float32) if g_mmd is not None else None
+        dX, dY = torch.empty_like(gx), torch.empty_like(gy)
+        gjac = torch.empty_like(jac) if ctx.needs_input_grad[2] else None
+        gfeat = (torch.empty_like(feat) if (feat is not None and variant == 1
+                                            and ctx.needs_input_grad[3]) else None)
+        with _lib.timed('smmd_smmd_loss_bwd'):
+            st = _lib.lib().smmd_smmd_loss_bwd_ex(
+                _lib.ptr(jac), n_cols, b, b_total, per, _lib.ptr(feat), dof, _lib.ptr(out), sc,
+                variant, 0, _lib.ptr(go), _lib.ptr(gm), _lib.ptr(gx), m, _lib.ptr(gy), n, d,
+                _lib.ptr(gjac), _lib.ptr(gfeat), _lib.ptr(dX), _lib.ptr(dY),
+                _lib.stream_handle(dev))
+        _lib.check(st, 'smmd_smmd_loss_bwd_ex')
+        if feat is not None and gfeat is None and ctx.needs_input_grad[3]:
+            gfeat = torch.zeros_like(feat)
+        return dX, dY, gjac, gfeat, None, None, None, None, None
+
+
+# SMMD_GLOBAL_FUSED_LOSS=0: the all-gather mode's loss as separate launches
+GLOBAL_FUSED_LOSS = os.environ.get('SMMD_GLOBAL_FUSED_LOSS', '1') != '0'
+
+
+def _mmd2_scaled_gathered(K, biased, ex):
+    """mmd2 of K fused with the scaled loss in the all-gather mode (the step
+    exchange carries the Jacobian partials), or None when it does not apply:
+    a row-sharded global batch (> FULL_ROWS per side), a path the fused
+    launch does not take, an overridden apply_scaling."""
+    X, Y = K.X, K.Y
+    group = current_loss_group()
+    if not (GLOBAL_FUSED_LOSS and ex is not None and ex.fuse and not ex.used
+            and ex.result is None and ex.jac is not None and ex.stats is not None
+            and is_dp(group) and ex.group is group):
+        return None
+    if X.dim() == 1 or Y.dim() == 1 or X.shape[1] != Y.shape[1]:
+        return None
+    m, n, d = ex.world * X.shape[0], ex.world * Y.shape[0], X.shape[1]
+    if max(m, n) > FULL_ROWS or not fused_loss_path(m, n, d):
+        return None
+    feat = ex.feat if ex.variant == 1 else None
+    if ex.variant == 1 and feat is None:
+        return None
+    val, g, _, out = _SMMDLossGathered.apply(X, Y, ex.jac, feat, K.spec, bool(biased), ex.sc,
+                                             ex.variant, ex)
+    ex.result = (val, g, out)
+    return val
+
+
 class ScalePending:
     """The scaling regulariser's inputs known before ``set_loss`` runs (the
     Jacobian columns of the real batch, the critic output for nD): the first
@@ -547,6 +651,9 @@ def mmd2(K, biased=False):
             val = _mmd2_scaled(K, biased, p)
             if val is not None:
                 return val
+        val = _mmd2_scaled_gathered(K, biased, current_exchange())
+        if val is not None:
+            return val
         return mmd2_fused(K.X, K.Y, K.spec, biased, process_group=current_loss_group(),
                           exchange=current_exchange())
     K_XX, K_XY, K_YY, const_diagonal = K

@@ -235,15 +235,16 @@ class MMD_GAN:
         # mmd.mmd2 inside set_loss spans the global batch in the all-gather
         # mode, and one all-gather carries the features and the scale's partials
         grp = self._loss_group()
-        self._ex = self._prepare_exchange(grp) if grp is not None else None
+        self._ex = ex = self._prepare_exchange(grp) if grp is not None else None
         pend = self._prepare_scale() if grp is None else None
         try:
             with mmd.loss_group(grp, self._ex), mmd.pending_scale(pend):
                 self.set_loss(self.d_G, self.d_images)
         finally:
             self._ex = None
-        # the loss ran as ONE launch (smmd_smmd_loss_fwd)
-        self.fused_loss = pend is not None and pend.result is not None
+        # the loss ran as ONE launch (smmd_smmd_loss_fwd / _fwd_gathered)
+        self.fused_loss = ((pend is not None and pend.result is not None)
+                           or (ex is not None and ex.result is not None))
         return self.g_loss, self.d_loss, self.aux
 
     def _scaling_ahead(self):
@@ -281,6 +282,11 @@ class MMD_GAN:
             ex.jac = jac if need else jac.detach()
             ex.feat = self.d_images if need else self.d_images.detach()
             ex.stats = ops.scaling_partials(ex.jac, ex.feat, c.scaling_variant, grp)
+            # SMMD's own apply_scaling: set_loss's mmd2 and the scaled loss run
+            # as ONE launch after the gather (mmd._SMMDLossGathered)
+            ex.fuse = self._fused_scaling() == 'mul'
+            ex.sc = self.sc
+            ex.variant = {'grad': 0, 'value_and_grad': 1}[c.scaling_variant]
         return ex
 
     def set_loss(self, G, images):
@@ -359,6 +365,12 @@ class MMD_GAN:
                 and self.g_loss is pend.result[0]):
             # set_loss's mmd2 ran fused with this very scaling (one launch)
             _, self.g_loss, self.aux = pend.result
+            self.d_loss = -self.g_loss
+            return
+        if (ex is not None and ex.result is not None and fused == 'mul'
+                and self.g_loss is ex.result[0]):
+            # the all-gather mode: set_loss's mmd2 ran fused with this scaling
+            _, self.g_loss, self.aux = ex.result
             self.d_loss = -self.g_loss
             return
         if ex is not None and ex.jac is not None:
@@ -730,7 +742,9 @@ class StepGraphs:
     step.  Everything a replay must change is read from device memory: the
     images (copied into a static buffer), z (the graph-safe RNG), the Adam
     step size (``FlatAdam.lr_t_dev``, written before every replay); the
-    host-side folded-filter caches are off while graphs are in use, and the
+    host-side folded-filter caches across steps are off while graphs are in
+    use (within one captured step a weight's Winograd filter is transformed
+    once, convops.arm_capture_cache), and the
     host bookkeeping of a step (optimizer step counts, the SN bank's
     first-pass token) is replayed by ``run``.  A new scaling coefficient is
     recaptured automatically; anything else that changes a launch argument
@@ -783,8 +797,12 @@ class StepGraphs:
         counts = (m.d_optim.step_count, m.g_optim.step_count)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, pool=self.pool):
-            out = m.d_step(self.images) if critic else m.g_step(self.images)
+        convops.arm_capture_cache(True)       # the step's repeated filter transforms
+        try:
+            with torch.cuda.graph(g, pool=self.pool):
+                out = m.d_step(self.images) if critic else m.g_step(self.images)
+        finally:
+            convops.arm_capture_cache(False)
         self.pool = g.pool()
         # the capture ran the host side of one step without executing it
         m.sn_D._p1_token, m.sn_G._p1_token = tokens

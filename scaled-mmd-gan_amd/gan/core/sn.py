@@ -45,7 +45,9 @@ def _launch_refresh(bank, update_u, flags, Ws, ss):
     n = len(bank.entries)
     outs = []
     arr = (_lib.SnLayer * n)()
-    lazy = bank.lazy if (bank.lazy and not torch.cuda.is_current_stream_capturing()) else ()
+    # lazy in a captured step too: the filter transforms that stand in for
+    # P3's writes are captured kernels reading W, sigma and s at replay time
+    lazy = bank.lazy if (bank.lazy and os.environ.get('SMMD_SN_LAZY_GRAPH', '1') != '0') else ()
     for i, (e, W, s) in enumerate(zip(bank.entries, Ws, ss)):
         # each output channel's K values must be contiguous: true for the
         # default and the channels_last layouts (SN is invariant to the

@@ -119,8 +119,28 @@ class FakeLib:
         return self.smmd_scaled_loss_fwd(jac, n_cols, b, b, per, feat, dof, mm, sc, variant,
                                          sqrt_scale, out, per_sample, lws, lwsb, stream)
 
+    def smmd_smmd_loss_fwd_gathered(self, desc, X, m, Y, n, d, biased, stats, world, stride, sc,
+                                    variant, sqrt_scale, sums, mm, gx, gy, out, ws, wsb, lws,
+                                    lwsb, stream):
+        self.smmd_mmd2_fwd(desc, X, m, Y, n, d, biased, 0, m, 0, n, sums, mm, gx, gy, ws, wsb,
+                           stream)
+        st = _arr(stats, (world - 1) * stride + 2)
+        o = _arr(out, 8)
+        J, nD = np.float32(st[0]), np.float32(st[1])
+        for r in range(1, world):             # rank order, fp32 as the kernel
+            J = np.float32(J + st[r * stride])
+            nD = np.float32(nD + st[r * stride + 1])
+        o[3], o[4], o[5] = J, nD, _arr(mm, 1)[0]
+        return self.smmd_scaled_loss_finalize(out, sc, variant, sqrt_scale, stream)
+
     def smmd_smmd_loss_bwd(self, jac, n_cols, b, per, feat, dof, fwd, sc, variant, sqrt_scale, go,
                            gm, gx, m, gy, n, d, gjac, gfeat, dX, dY, stream):
+        return self.smmd_smmd_loss_bwd_ex(jac, n_cols, b, b, per, feat, dof, fwd, sc, variant,
+                                          sqrt_scale, go, gm, gx, m, gy, n, d, gjac, gfeat, dX, dY,
+                                          stream)
+
+    def smmd_smmd_loss_bwd_ex(self, jac, n_cols, b, b_total, per, feat, dof, fwd, sc, variant,
+                              sqrt_scale, go, gm, gx, m, gy, n, d, gjac, gfeat, dX, dY, stream):
         o = _arr(fwd, 8).astype(np.float64)
         f = np.sqrt(o[2]) if sqrt_scale else o[2]
         g = float(_arr(go, 1)[0])
@@ -128,7 +148,7 @@ class FakeLib:
         _arr(dX, m * d)[:] = _arr(gx, m * d) * dm
         _arr(dY, n * d)[:] = _arr(gy, n * d) * dm
         if _arr(gjac, 1) is not None:
-            self.smmd_scaled_loss_bwd(jac, n_cols, b, b, per, feat, dof, fwd, sc, variant,
+            self.smmd_scaled_loss_bwd(jac, n_cols, b, b_total, per, feat, dof, fwd, sc, variant,
                                       sqrt_scale, go, None, gjac, gfeat, stream)
         return 0
 

@@ -272,6 +272,69 @@ def test_step_exchange_one_collective(world, variant):
         np.testing.assert_allclose(gx, gx_ref, rtol=1e-4, atol=1e-7)
 
 
+def _worker_step_exchange_fused(rank, world, port, variant, q):
+    _init(rank, world, port)
+    from gan.core import mmd, ops
+    from gan.core.collectives import StepExchange
+    X, Y = _data()
+    n = X.shape[0] // world
+    rng = np.random.default_rng(3)
+    jac = rng.standard_normal((1, X.shape[0], 3, 2, 2)).astype(np.float32)
+    Xl = torch.tensor(X[rank * n:(rank + 1) * n], requires_grad=True)
+    Yl = torch.tensor(Y[rank * n:(rank + 1) * n], requires_grad=True)
+    jl = torch.tensor(jac[:, rank * n:(rank + 1) * n], requires_grad=True)
+    grp = dist.group.WORLD
+    cnt = _Count()
+    ex = StepExchange(grp)
+    feat = Xl[:, :1]
+    ex.jac, ex.feat = jl, feat
+    ex.stats = ops.scaling_partials(jl, feat, variant, grp)
+    ex.fuse, ex.sc = True, 10.0
+    ex.variant = {'grad': 0, 'value_and_grad': 1}[variant]
+    with mmd.loss_group(grp, ex):
+        val = mmd.mmd2(mmd._rbf_kernel(Xl, Yl))
+    assert ex.result is not None and ex.result[0] is val     # ONE fused launch
+    _, g, aux = ex.result
+    g.backward()
+    q.put((rank, float(g), float(aux[3]), Xl.grad.numpy().copy(), jl.grad.numpy().copy(),
+           dict(cnt.n)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world', WORLDS)
+@pytest.mark.parametrize('variant', ['grad', 'value_and_grad'])
+def test_step_exchange_fused_loss(world, variant):
+    """The all-gather mode's fused loss (mmd._SMMDLossGathered: the sweep
+    over the gathered rows and the scaled loss in one launch, J / nD summed
+    from the gathered partials in the launch, its backward with the global
+    batch as the Jacobian's normaliser): one all-gather, no all-reduce, and
+    the values and row gradients of one process on the concatenated batch."""
+    X, Y = _data()
+    spec = O.kernel_spec('rbf')
+    rng = np.random.default_rng(3)
+    jac = rng.standard_normal((1, X.shape[0], 3, 2, 2)).astype(np.float32).astype(np.float64)
+    J = np.mean(O.squared_norm_per_sample(jac[0]))
+    nD = np.mean(X[:, :1].astype(np.float64) ** 2) if variant == 'value_and_grad' else 0.0
+    scale = O.scale_factor(J + nD, 10.0)
+    mm = O.mmd2(spec, X, Y)
+    dX, _ = O.mmd2_grad(spec, X, Y)
+    res = _run(_worker_step_exchange_fused, variant, world=world)
+    n = X.shape[0] // world
+    cq = mm * (-10.0 * scale ** 2)
+    for rank, g, Jg, gx, gj, counts in res:
+        assert counts == {'all_gather_into_tensor': 1, 'all_reduce': 0}
+        assert Jg == pytest.approx(J, rel=1e-5)
+        assert g == pytest.approx(mm * scale, rel=1e-5)
+        np.testing.assert_allclose(gj, cq * 2.0 / X.shape[0] * jac[:, rank * n:(rank + 1) * n],
+                                   rtol=1e-4, atol=1e-8)
+        gx_ref = scale * dX[rank * n:(rank + 1) * n]
+        if variant == 'value_and_grad':      # d nD / d feat through X[:, :1]
+            gx_ref = gx_ref.copy()
+            gx_ref[:, :1] += cq * 2.0 / X.shape[0] * X[rank * n:(rank + 1) * n, :1]
+        np.testing.assert_allclose(gx, gx_ref, rtol=1e-4, atol=1e-7)
+
+
 def test_buckets_issue_in_order_when_completed_out_of_order():
     """A bucket whose tensors finish first still waits for its predecessors:
     ranks whose backward ran in different orders issue identical sequences."""

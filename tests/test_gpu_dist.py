@@ -87,7 +87,7 @@ def _worker(rank, world, port, q, mode='global', dp_gdirect='1'):
     images, z = _inputs(world)
     sl = slice(rank * N_PER_RANK, (rank + 1) * N_PER_RANK)
     res = _critic_update(model, images[sl].to(dev), z[sl].to(dev))
-    q.put((rank,) + res)
+    q.put((rank,) + res + (model.fused_loss,))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -110,7 +110,8 @@ def test_global_mode_two_ranks_equal_one_process(dev):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for _, d_loss, aux, grad, params in outs:
+    for _, d_loss, aux, grad, params, fused in outs:
+        assert fused        # the sweep + scaled loss as one launch (smmd_smmd_loss_fwd_gathered)
         # d_loss ~ -5e-5 is a difference of O(1e-2) kernel means: the summation
         # order of two ranks vs one process moves it by ~1e-4 relative
         np.testing.assert_allclose(d_loss, ref[0], rtol=1e-3)
@@ -194,7 +195,7 @@ def _rccl_worker(port, q, mode):
     assert not collectives._host_staged(torch.zeros(1, device=dev), dist.group.WORLD)
     images, z = _inputs(1)
     res = _critic_update(model, images.to(dev), z.to(dev))
-    q.put((mode, dict(seen)) + res)
+    q.put((mode, dict(seen)) + res + (model.fused_loss,))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -223,15 +224,16 @@ def test_rccl_world1_critic_update_equals_groupless(dev, mode):
     out = q.get(timeout=300)
     p.join(timeout=60)
     assert p.exitcode == 0
-    _, seen, d_loss, aux, grad, params = out
+    _, seen, d_loss, aux, grad, params, fused = out
+    assert fused            # global: the gathered fused launch; tower: the per-tower one
     assert seen['broadcast'] >= 2                  # the parameter broadcast at init
     assert seen['all_reduce'] >= 1 and seen['async'] >= 1   # bucketed, from the backward
     if mode == 'global':
         assert seen['all_gather_into_tensor'] == 1  # the step's one packed all-gather
     else:
         assert seen['all_gather_into_tensor'] == 0
-    # the global mode takes the unfused loss launches (the Jacobian's
-    # partials ride in the all-gather), so d_loss sums in another order
+    # the global mode's fused launch takes J from the gathered partials
+    # (summed over one rank): the loss of the group-less fused launch
     np.testing.assert_allclose(d_loss, ref[0], rtol=1e-4)
     np.testing.assert_allclose(aux[3], ref[1][3], rtol=1e-4)
     scale = np.abs(ref[2]).max()

@@ -511,6 +511,37 @@ def test_step_graphs_match_eager(dev):
     b.train_step(imgs[0])                      # back to eager
 
 
+def test_step_graphs_bit_identical_to_eager_all_library(dev):
+    """On the all-library step (SNResNet-64 at the ImageNet config's width: no
+    MIOpen convolution) the graph replays are the eager step bit for bit:
+    through every step kind (critic with and without the SN first pass
+    written, generator), parameters, Adam moments and u are torch.equal.
+    The capture's filter cache (one transform per weight and step) and the
+    lazy W_eff in the capture are covered by this."""
+    from gan.core.smmd import SMMD
+    a, images = _headline_model(dev, batch=8)
+    g = torch.Generator().manual_seed(3)
+    imgs = [torch.rand(8, 3, 64, 64, generator=g).to(dev) for _ in range(3)]
+    for i in range(7):                         # eager: every step kind once first
+        a.train_step(imgs[i % 3])
+    b = SMMD(a.config, device=dev)
+    b.load_state_dict(a.state_dict())
+    b.sample_z = a.sample_z
+    b.enable_graphs()
+    for i in range(13):
+        for m in (a, b):
+            m.train_step(imgs[i % 3])
+    torch.cuda.synchronize()
+    assert len(b._graphs.graphs) == 3
+    for name in ('d_optim', 'g_optim'):
+        for t in ('flat_param', 'm', 'v'):
+            ta, tb = getattr(getattr(a, name), t), getattr(getattr(b, name), t)
+            assert torch.equal(ta, tb), (name, t, float((ta - tb).abs().max()))
+    for ea, eb in zip(a.sn_D.entries, b.sn_D.entries):
+        assert torch.equal(ea.u, eb.u)
+    b.enable_graphs(False)
+
+
 @pytest.mark.parametrize('order', [1, 2])
 def test_linear_out_node_vs_float64(dev, order):
     """snops._LinOut (the critic's single-output linear layer with its own
