@@ -406,6 +406,7 @@ smmd_status smmd_scaled_loss_fwd(const float *jac, int n_cols, int b, int b_tota
     const int nchunk = (int)((per_sample + SQ_CHUNK - 1) / SQ_CHUNK);
     const int vec = (per_sample % 4 == 0) && ((uintptr_t)jac % 16 == 0);
     ScaledLossArgs a;
+    memset(&a, 0, sizeof(a));        // every field not set below (stats: none) is zero
     a.jac = jac;
     a.per_sample = per_sample;
     a.nchunk = nchunk;

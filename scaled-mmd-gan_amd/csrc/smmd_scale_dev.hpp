@@ -34,9 +34,11 @@ struct ScaledLossArgs {
     // are not reduced from the Jacobian here but summed, in rank order, from
     // the gathered per-rank partials stats[r * stats_stride + {0, 1}]
     // (ops.scaling_partials of every rank, carried by the feature all-gather)
-    const float *stats;
+    const float *stats;              // NULL: J / nD from the Jacobian partials
     int stats_world, stats_stride;
 };
+// (host code zero-fills a ScaledLossArgs before setting its fields: a field
+// added later must read as "off", never as stack garbage)
 
 // ---- per-(row, chunk) partial sum of squares of block `blk` (256 threads):
 // a thread's (up to) four float4 loads are issued before its fmas (one memory
