@@ -188,34 +188,52 @@ class GradBuckets:
         self._offs = offs
         self.armed = False
         self.left, self.works, self.next = [], [], 0
+        self.counted = set()
         self._hooks = [p.register_post_accumulate_grad_hook(self._hook(i))
                        for i, p in enumerate(opt.params)]
         self.launch_log = []      # bucket ids in issue order of the last step (tests)
         # tensors the bucket clip leaves alone (their owner clipped them: the
         # SN weights and scales under the tower-mode G-direct backward)
         self.clip_exclude = frozenset()
+        # tensors whose arrival only notify() reports (see notify)
+        self.notify_only = frozenset()
 
     def arm(self):
         """Call before the backward whose gradients this step exchanges."""
         self.armed = True
         self.left = [hi - lo for lo, hi in self.buckets]
+        self.counted = set()
         self.next = 0
         self.works = []
         self.launch_log = []
 
     def _hook(self, i):
         def fn(_p):
-            if not self.armed:
+            if i not in self.notify_only:
+                self._arrive(i)
+        return fn
+
+    def _arrive(self, i):
+        if self.armed:
+            b = self.bucket_of[i]
+            if i in self.counted:
+                # counted once per step: a tensor written by an SN group node
+                # (notify) still has its AccumulateGrad node run -- with no
+                # gradient, the group returns None -- and this hook fires again;
+                # counting both issued a bucket before its last tensor arrived
                 return
-            self.left[self.bucket_of[i]] -= 1
+            self.counted.add(i)
+            self.left[b] -= 1
             while self.next < len(self.buckets) and self.left[self.next] <= 0:
                 self._launch(self.next)
-        return fn
 
     def notify(self, i):
         """Tensor i's gradient is in place without autograd's accumulation
-        (the SN group backward writes it directly): count it as a hook would."""
-        self._hook(i)(self.opt.params[i])
+        (the SN group backward writes it directly): count it as a hook would.
+        Tensors in ``notify_only`` (the late-summed biases of a data-parallel
+        critic step, MMD_GAN.d_step) are counted by this call alone: their
+        AccumulateGrad node runs, with no gradient, before the group writes them."""
+        self._arrive(i)
 
     def _launch(self, b):
         lo, hi = self.buckets[b]

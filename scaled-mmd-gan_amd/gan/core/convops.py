@@ -1034,12 +1034,17 @@ def arm_late_wgrad_sums(on):
 # first + second by one out-of-place multi-tensor add (+ later ones in
 # place), the sums autograd forms in arrival order, bit for bit.
 BIAS_LATE_SUM = os.environ.get('SMMD_BIAS_LATE_SUM', '1') != '0'
-_lateb = {'armed': False, 'queue': [], 'queued': 0}
+_lateb = {'armed': False, 'queue': [], 'queued': 0, 'closed': set()}
 
 
 def arm_late_bias_sums(on):
     _lateb['armed'] = bool(on) and BIAS_LATE_SUM
     _lateb['queue'].clear()
+    _lateb['closed'].clear()
+
+
+def late_bias_armed():
+    return _lateb['armed']
 
 
 def _late_bias(p, g):
@@ -1047,50 +1052,72 @@ def _late_bias(p, g):
     if (g is None or p is None or not _lateb['armed'] or not p.is_leaf
             or torch.is_grad_enabled()):
         return g
+    if id(p) in _lateb['closed']:
+        # its gradient was already handed to its all-reduce bucket
+        raise RuntimeError('late bias sum: a gradient contribution of a bias (%s) arrived after '
+                           'its SN layer group flushed it (SMMD_BIAS_LATE_SUM=0 avoids the '
+                           'late sums)' % (tuple(p.shape),))
     _lateb['queue'].append((p, g))
     _lateb['queued'] += 1
     return None
 
 
-def flush_late_bias_sums():
+def flush_late_bias_sums(params=None):
     """p.grad = the sum of p's queued contributions in arrival order (round 1:
     one out-of-place _foreach_add of the first two of every parameter; round
     r > 1: one in-place _foreach_add_ of the r-th); a single contribution is
-    taken as it is, cloned when another parameter holds the same tensor."""
+    taken as it is, cloned when another parameter holds the same tensor.  A
+    parameter whose .grad already exists (the data-parallel step's views into
+    the flat gradient, zeroed before the backward) gets the sum added into it,
+    all of them by one more multi-tensor add: 0 + sum, the same values.
+    ``params``: only these parameters (a data-parallel SN group's biases,
+    whose buckets are then notified; a later contribution to one of them is
+    an error), else every queued one.  Returns the parameters it set."""
     q = _lateb['queue']
-    if not q:
-        return
+    if params is not None:
+        ids = {id(p) for p in params}
+        _lateb['closed'].update(ids)
+        take = [(p, g) for p, g in q if id(p) in ids]
+        q[:] = [(p, g) for p, g in q if id(p) not in ids]
+    else:
+        take = list(q)
+        q.clear()
+    if not take:
+        return []
     per = {}
-    for p, g in q:
+    for p, g in take:
         per.setdefault(id(p), (p, []))[1].append(g)
-    q.clear()
+    into_p, into_t = [], []
+
+    def assign(p, t):
+        if p.grad is None:
+            p.grad = t
+        else:                       # (an existing .grad: the flat view, or autograd's own)
+            into_p.append(p.grad)
+            into_t.append(t)
     with torch.no_grad():
         pairs = [(p, gs) for p, gs in per.values() if len(gs) >= 2]
         if pairs:
             sums = torch._foreach_add([gs[0] for _, gs in pairs], [gs[1] for _, gs in pairs])
-            for (p, _), t in zip(pairs, sums):
-                _set_bias_grad(p, t)
             r = 2
             while True:
-                more = [(p, gs[r]) for p, gs in pairs if len(gs) > r]
+                more = [(k, gs[r]) for k, (_, gs) in enumerate(pairs) if len(gs) > r]
                 if not more:
                     break
-                torch._foreach_add_([p.grad for p, _ in more], [g for _, g in more])
+                torch._foreach_add_([sums[k] for k, _ in more], [g for _, g in more])
                 r += 1
+            for (p, _), t in zip(pairs, sums):
+                assign(p, t)
         held = {}
         for p, gs in per.values():
             if len(gs) == 1:
                 held[id(gs[0])] = held.get(id(gs[0]), 0) + 1
         for p, gs in per.values():
             if len(gs) == 1:
-                _set_bias_grad(p, gs[0].clone() if held[id(gs[0])] > 1 else gs[0])
-
-
-def _set_bias_grad(p, t):
-    if p.grad is None:
-        p.grad = t
-    else:                           # (a contribution autograd accumulated itself)
-        p.grad.add_(t)
+                assign(p, gs[0].clone() if (held[id(gs[0])] > 1 and p.grad is None) else gs[0])
+        if into_p:
+            torch._foreach_add_(into_p, into_t)
+    return [p for p, _ in per.values()]
 
 
 def _shared_gy_key(ctx):

@@ -444,6 +444,18 @@ class MMD_GAN:
                   for lo, hi in bk.buckets]
 
         def direct(members, _bk=bk, _bank=bank, _index=index):
+            # the group's layers' biases: their queued contributions (late bias
+            # sums; every one is in by now -- a layer's bias gradients come
+            # from its own conv nodes or the downstream block input node, both
+            # ahead of its SN node) added into their flat-gradient views, and
+            # counted for their buckets like the weights
+            biases = [b for b in (getattr(_bank.entries[j].module, 'bias', None)
+                                  for j in members)
+                      if isinstance(b, torch.Tensor) and b.requires_grad and id(b) in _index]
+            if biases and convops.late_bias_armed():
+                convops.flush_late_bias_sums(biases)
+                for b in biases:
+                    _bk.notify(_index[id(b)])
             for j in members:
                 e = _bank.entries[j]
                 for p in (e.weight, e.scale):
@@ -499,7 +511,13 @@ class MMD_GAN:
         convops.arm_late_wgrad_sums(True)
         # the bias gradients' later contributions added after the backward
         # (one process, gathered gradients: no hook reads .grad during it)
-        convops.arm_late_bias_sums(self.d_optim.gather)
+        # (data parallel: flushed per SN group into the flat-gradient views,
+        # the buckets notified there -- MMD_GAN._group_sn)
+        late_dp = self.dp and self.sn_D.groups is not None and self.sn_D._direct is not None
+        convops.arm_late_bias_sums(self.d_optim.gather or late_dp)
+        if self.dp:
+            bk.notify_only = self._sn_bias_ids() if (late_dp and convops.late_bias_armed()) \
+                else frozenset()
         try:
             if ref:
                 d_loss.backward(inputs=self.d_vars)
@@ -518,6 +536,14 @@ class MMD_GAN:
         self._exchange(self.d_optim)
         self._dpgd = False
         return self._detach_step_state()
+
+    def _sn_bias_ids(self):
+        """Flat-buffer tensor indices of the critic's SN layers' biases (the
+        late-summed biases a data-parallel SN group flushes and notifies)."""
+        index = {id(p): i for i, p in enumerate(self.d_optim.params)}
+        return frozenset(index[id(b)] for b in (getattr(e.module, 'bias', None)
+                                                for e in self.sn_D.entries)
+                         if isinstance(b, torch.Tensor) and b.requires_grad and id(b) in index)
 
     def _sn_tensor_ids(self):
         """Flat-buffer tensor indices of the critic's SN weights and scales."""

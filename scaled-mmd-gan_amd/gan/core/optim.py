@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import struct
 import os
 
 import torch
@@ -35,6 +36,11 @@ _EPOCH = {}
 def param_epoch(t):
     """FlatAdam steps applied so far to the storage `t` lives in (0 if none)."""
     return _EPOCH.get(t.untyped_storage().data_ptr(), 0)
+
+
+def _f32(x):
+    """x rounded to float32 (as a ctypes c_float argument is), as a Python float."""
+    return struct.unpack('f', struct.pack('f', float(x)))[0]
 
 
 class FlatAdam:
@@ -233,7 +239,11 @@ class FlatAdam:
         double, as smmd_adam_flat computes it (model.py:405-412)."""
         t = self.step_count if step is None else step
         lr = self.lr if lr is None else lr
-        return lr * math.sqrt(1.0 - self.beta2 ** t) / (1.0 - self.beta1 ** t)
+        # lr and the betas as the float32 values the library receives (its
+        # adam_lr_t widens those to double): a graph replay's device lr_t is
+        # then the eager update's bit for bit
+        lr, b1, b2 = _f32(lr), _f32(self.beta1), _f32(self.beta2)
+        return lr * math.sqrt(1.0 - b2 ** t) / (1.0 - b1 ** t)
 
     def advance(self):
         """Host bookkeeping of one update (step count, parameter epoch); a

@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_dist.py tests/test_gpu_model.py -k "dist or rccl or graphs or bit_identical or two_ranks or tower" > gpurun_out/${TAG}_tests.txt 2>&1 || { echo "tests rc=$?"; tail -40 gpurun_out/${TAG}_tests.txt; exit 1; }
 tail -3 gpurun_out/${TAG}_tests.txt
-B="--steps 30 --warmup 6 --no-cpu-baseline --mmd-sweep 0 --ref-schedule-steps 0"
+B="--steps 30 --warmup 6 --no-cpu-baseline --mmd-sweep 0 --ref-schedule-steps 0 --instrument-cycles 0"
 for r in 1 2; do
   for v in 0 1; do
     timeout -k 10 400 python bench.py $B --graphs $v > gpurun_out/${TAG}_graphs${v}_$r.json 2> gpurun_out/${TAG}_graphs${v}_$r.err || { echo "bench graphs=$v rc=$?"; tail -20 gpurun_out/${TAG}_graphs${v}_$r.err; exit 1; }
