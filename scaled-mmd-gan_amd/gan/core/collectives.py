@@ -239,6 +239,11 @@ class GradBuckets:
         lo, hi = self.buckets[b]
         self.next = b + 1
         self.launch_log.append(b)
+        if getattr(self.opt, '_gathering', lambda: False)():
+            # gather mode (AccumulateGrad kept each gradient as its own tensor,
+            # no add into a zeroed view): the bucket's gradients copied into
+            # its flat range by one multi-tensor copy, then reduced
+            self.opt._gather_grads(lo, hi)
         if self.clip_norm > 0:
             i = lo
             while i < hi:                 # runs of tensors not excluded

@@ -621,7 +621,9 @@ class MMD_GAN:
             # one process: the generator's gradients gathered into the flat
             # buffer by one copy at the update (optim.FlatAdam.gather,
             # SMMD_GRAD_GATHER=0: accumulated into it parameter by parameter)
-            self.g_optim.gather = GRAD_GATHER and not self.dp
+            # (data parallel: each bucket gathers its range before its
+            # all-reduce, collectives.GradBuckets._launch)
+            self.g_optim.gather = GRAD_GATHER
             self.g_optim.zero_grad()
             fake = self.generator(self.sample_z(self.batch_size))
             g_loss, d_loss, aux = self.set_tower_loss(images, fake, need_critic_grad=ref)

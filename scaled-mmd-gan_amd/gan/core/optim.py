@@ -119,12 +119,15 @@ class FlatAdam:
                 if id(p) not in keep:
                     p.grad = None
 
-    def _gather_grads(self):
-        """Gather mode: every parameter's gradient into flat_grad (one
+    def _gather_grads(self, lo=0, hi=None):
+        """Gather mode: every parameter's gradient (of tensors lo .. hi - 1:
+        one all-reduce bucket, collectives.GradBuckets) into flat_grad (one
         _foreach_copy_; parameters without one get zeros) and the .grad views
         re-attached."""
         dst, src, empty = [], [], []
-        for i, p in enumerate(self.params):
+        hi = len(self.params) if hi is None else hi
+        for i in range(lo, hi):
+            p = self.params[i]
             if not p.numel():
                 continue
             view = self._view(self.flat_grad, p, self.offsets[i])
