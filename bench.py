@@ -55,11 +55,11 @@ _JSON_OUT = sys.stdout           # the result line's stream (main: the real fd 1
 # committed counter evidence of this workload, each file stamped with the
 # smmd_source_hash of the library build it was measured on (tools/stamp.py);
 # embedded only when that stamp equals the running library's
-PMC_TRAFFIC = os.path.join(ROOT, 'profiles', 'r14', 'pmc_traffic.json')
+PMC_TRAFFIC = os.path.join(ROOT, 'profiles', 'r15', 'pmc_traffic.json')
 # executed FLOPs per kernel class over whole 5D+1G cycles of this workload
 # (tools/gpu_step_pmc.sh -> tools/step_flops_pmc.py: rocprofv3 SQ_INSTS_VALU_*
 # and SQ_INSTS_VALU_MFMA_MOPS_F32 counters + a kernel trace)
-STEP_PMC = os.path.join(ROOT, 'profiles', 'r14', 'step_flops_pmc.json')
+STEP_PMC = os.path.join(ROOT, 'profiles', 'r15', 'step_flops_pmc.json')
 
 
 def load_stamped(path, stamp):

@@ -464,6 +464,15 @@ __device__ __forceinline__ void wgrad2_body(const float *__restrict__ x,
     // pairs the compiler regrouped cost ~9 v_mov per k-step besides)
     auto tslice = [&](int q, const float (&d)[12], const float (&gv)[4], f2v (&t)[4],
                       float (&a)[8], float (&b)[8]) {
+#ifdef WG2_NO_XFORM       // timing-only diagnostic (wrong results): the LDS reads kept
+        if (q == 0) {
+#pragma unroll
+            for (int i = 0; i < 12; ++i) asm volatile("" ::"v"(d[i]));
+#pragma unroll
+            for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(gv[i]));
+        }
+        return;
+#endif
         if (q == 1) {
             // rows of A' dY: ph 0 (g01, g01 + g23), ph 1 (g01 - g23, g23); each
             // row R gives (R.x, R.x + R.y, R.x - R.y, R.y)
