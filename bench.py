@@ -615,10 +615,13 @@ def main():
                     help='1: torch.backends.cudnn.benchmark (MIOpen Find: times every '
                          'applicable solver per conv problem during warmup); the find '
                          'results persist in MIOPEN_USER_DB_PATH when set')
-    ap.add_argument('--graphs', type=int, default=0,
+    ap.add_argument('--graphs', type=int, default=-1,
                     help='1: the timed steps replay HIP graphs of the captured step kinds '
-                         '(model.enable_graphs; one GPU). Measured: no gain at batch 64 '
-                         '(GPU-bound), 1.85x at batch 8 (host-bound)')
+                         '(model.enable_graphs; one GPU); 0: eager; -1 (default): auto -- '
+                         'on one GPU, two untimed 5D+1G cycles each way during the warmup, '
+                         'graphs kept only when >= 5 %% faster (host-bound configs: CIFAR-10 '
+                         'SNGAN 1.37x; the GPU-bound ImageNet step stays eager, graphs 1.3 %% '
+                         'slower there)')
     ap.add_argument('--cpu-steps', type=int, default=24,
                     help='timed CPU-baseline steps of the ImageNet config (after 3 warm-ups; '
                          'SURVEY 8d asks >= 20; 24 = 4 whole 5D+1G cycles)')
@@ -709,10 +712,41 @@ def main():
         model.d_step(images[0])
         model.g_step(images[1])
     model.schedule = 'lean'
-    if args.graphs:
+    graphs_probe = None
+    use_graphs = args.graphs
+    if use_graphs < 0:
+        use_graphs = 0
+        if world == 1 and not dp_forced:
+            # auto: time two 5 D + 1 G cycles eagerly and with graphs (all of
+            # it untimed warmup), keep graphs only when clearly faster
+            def cycle_ms():
+                model.step = 21
+                model.d_counter = model.g_counter = 0
+                torch.cuda.synchronize()
+                t = time.perf_counter()
+                run_steps(model, images, 12)
+                torch.cuda.synchronize()
+                return (time.perf_counter() - t) / 12 * 1e3
+            model.step = 21
+            run_steps(model, images, 6)
+            eager_ms = cycle_ms()
+            model.enable_graphs()
+            model.step = 21
+            run_steps(model, images, 6)               # captures every step kind
+            graph_ms = cycle_ms()
+            use_graphs = 1 if graph_ms < 0.95 * eager_ms else 0
+            if not use_graphs:
+                model.enable_graphs(False)
+            graphs_probe = {'eager_ms_per_step': round(eager_ms, 3),
+                            'graphs_ms_per_step': round(graph_ms, 3),
+                            'chosen': 'graphs' if use_graphs else 'eager'}
+            log('graphs probe: eager %.3f ms/step, graphs %.3f -> %s'
+                % (eager_ms, graph_ms, graphs_probe['chosen']))
+    elif use_graphs:
         model.enable_graphs()       # capture every step kind before the warmup
         model.step = 21
         run_steps(model, images, 6)
+    args.graphs = use_graphs
     sync(world)
     log('primed D and G steps of both schedules in %.1f s' % (time.perf_counter() - tw))
 
@@ -942,7 +976,7 @@ def main():
         'n_gpus': world,
         'steps': args.steps,
         'warmup': args.warmup,
-        'prime_steps': 4 + (6 if args.graphs else 0),
+        'prime_steps': 4 + (36 if graphs_probe else (6 if args.graphs else 0)),
         'd_steps': counts['D'],
         'g_steps': counts['G'],
         'ms_per_step': round(ms_step, 3),
@@ -960,6 +994,7 @@ def main():
                    'miopen_winograd': bool(args.miopen_winograd),
                    'miopen_find': bool(args.miopen_find),
                    'step_graphs': bool(args.graphs),
+                   'step_graphs_probe': graphs_probe,
                    'conv_mean_pool': ('folded 4x4 stride-2 conv' if architecture.FOLD_POOL
                                       else 'conv3x3 + mean pool'),
                    'miopen_db': os.environ.get('MIOPEN_USER_DB_PATH')},
