@@ -689,6 +689,84 @@ def test_smmd_loss_fused_without_jacobian_grad(dev):
     assert torch.equal(grads[0], grads[1])
 
 
+class _GatherEmulation:
+    """A StepExchange of rank ``rank`` whose all-gather is emulated: every
+    rank's packed [X; Y; stats] row built from the given per-rank tensors."""
+
+    def __init__(self, rank, rows):
+        self.world, self.rank, self.rows = len(rows), rank, rows
+        self.used = False
+
+    def gather_packed(self, X, Y):
+        self.used = True
+        allp = torch.stack(self.rows)
+        ml, nl, d = X.shape[0], Y.shape[0], X.shape[1]
+        Xa = allp[:, :ml * d].reshape(self.world * ml, d)
+        Ya = allp[:, ml * d:(ml + nl) * d].reshape(self.world * nl, d)
+        return allp, Xa, Ya
+
+
+@pytest.mark.parametrize('world,variant', [(2, 'grad'), (8, 'grad'), (4, 'value_and_grad')])
+def test_smmd_loss_gathered_vs_oracle(dev, world, variant):
+    """The all-gather mode's fused loss through the ABI (smmd_smmd_loss_fwd_gathered
+    + smmd_smmd_loss_bwd_ex, mmd._SMMDLossGathered) with the all-gather emulated:
+    every rank gets mmd2, J, scale and g_loss of the global batch (the float64
+    oracle on the concatenated batch), bit-identical across ranks, and the
+    gradients of its own rows and Jacobian (normaliser: the global batch)."""
+    from gan.core import mmd, ops
+    b = 16
+    B = world * b
+    rng = np.random.default_rng(7 + world)
+    X = rng.standard_normal((B, 1)).astype(np.float32)
+    Y = (rng.standard_normal((B, 1)) * 0.7 + 0.3).astype(np.float32)
+    jac = rng.standard_normal((1, B, 3, 8, 8)).astype(np.float32) * 0.05
+    v = {'grad': 0, 'value_and_grad': 1}[variant]
+    ranks, rows = [], []
+    for r in range(world):
+        sl = slice(r * b, (r + 1) * b)
+        Xt = torch.tensor(X[sl], device=dev, requires_grad=True)
+        Yt = torch.tensor(Y[sl], device=dev, requires_grad=True)
+        jt = torch.tensor(jac[:, sl], device=dev, requires_grad=True)
+        # this rank's (J, nD) shares over the global batch (ops.scaling_partials)
+        L = mmd._lib.lib()
+        out = torch.empty(8, device=dev)
+        ws = mmd._lib.workspace('scaled_loss', L.smmd_scaled_loss_workspace_bytes(b, 3 * 64), dev)
+        assert L.smmd_scaled_loss_fwd(mmd._lib.ptr(jt.detach()), 1, b, B, 3 * 64,
+                                      mmd._lib.ptr(Yt.detach()), 1, None, 0.0, v, 0,
+                                      mmd._lib.ptr(out), None, mmd._lib.ptr(ws), ws.numel(),
+                                      mmd._lib.stream_handle(dev)) == 0
+        rows.append(torch.cat([Xt.detach().reshape(-1), Yt.detach().reshape(-1), out[3:5]]))
+        ranks.append((Xt, Yt, jt))
+    spec = O.kernel_spec('rbf')
+    mm = O.mmd2(spec, X, Y)
+    J = np.mean(O.squared_norm_per_sample(jac[0]))
+    nD = np.mean(Y.astype(np.float64) ** 2)
+    sc_ = O.scale_factor(J, 10.0, nD, variant)
+    dX, dY = O.mmd2_grad(spec, X, Y)
+    coefq = mm * (-10.0 * sc_ ** 2)
+    outs = []
+    for r, (Xt, Yt, jt) in enumerate(ranks):
+        ex = _GatherEmulation(r, rows)
+        val, g, _, out = mmd._SMMDLossGathered.apply(Xt, Yt, jt, Yt if v else None,
+                                                     mmd.get_kernel_spec("rbf"), False, 10.0,
+                                                     v, ex)
+        outs.append(out.clone())
+        _close(val.item(), mm, 1e-5, 1e-4, 'mmd2')
+        _close(out[3].item(), J, 0, 1e-5, 'J')
+        _close(out[2].item(), sc_, 0, 1e-5, 'scale')
+        _close(g.item(), mm * sc_, 1e-6, 1e-4, 'g_loss')
+        g.backward()
+        sl = slice(r * b, (r + 1) * b)
+        gy_ref = sc_ * dY[sl]
+        if v:
+            gy_ref = gy_ref + coefq * 2.0 / B * Y[sl].astype(np.float64)
+        _grad_close(Xt.grad.cpu().numpy(), sc_ * dX[sl], 'dX')
+        _grad_close(Yt.grad.cpu().numpy(), gy_ref, 'dY')
+        _grad_close(jt.grad.cpu().numpy(), coefq * 2.0 / B * jac[:, sl].astype(np.float64),
+                    'd jac')
+    assert all(torch.equal(o, outs[0]) for o in outs)     # the same bits on every rank
+
+
 def test_scaled_loss_workspace_reuse(dev):
     """The squared-norm pass elects its finalizing block by a ticket at a fixed
     offset of the cached workspace; calls with fewer rows reuse the buffer
