@@ -368,16 +368,33 @@ def reset_timing():
 # workspaces: zero-filled at allocation, owned per (device, stream, tag)
 # ---------------------------------------------------------------------------
 _ws_cache = {}
+# Workspaces a HIP-graph capture was handed: a captured launch keeps their raw
+# address for every replay, so one superseded by a larger request must stay
+# allocated (freeing it returned it to its graph pool -- or, once the last
+# tensor of an earlier capture's pool was gone, to the device -- and the next
+# replay of the graph that recorded it wrote through a stale address)
+_ws_captured = set()
+_ws_retired = []
 
 
 def workspace(tag: str, nbytes: int, device: torch.device):
     key = (device.index, torch.cuda.current_stream(device).cuda_stream, tag)
     buf = _ws_cache.get(key)
+    capturing = torch.cuda.is_current_stream_capturing()
     if buf is None or buf.numel() < nbytes:
+        if buf is not None and key in _ws_captured:
+            _ws_retired.append(buf)
+        _ws_captured.discard(key)
         buf = torch.zeros(max(int(nbytes), 256), dtype=torch.uint8, device=device)
         _ws_cache[key] = buf
+    if capturing:
+        _ws_captured.add(key)
     return buf
 
 
 def clear_workspaces():
+    """Drop the cached workspaces (none that a live step graph recorded: call
+    it with no graphs alive)."""
     _ws_cache.clear()
+    _ws_captured.clear()
+    _ws_retired.clear()
