@@ -41,7 +41,8 @@ constexpr int WN_CC = 8;                  // input channels per chunk
 constexpr int WN_STAGE = 16 * WN_CC * 64; // floats per V (and per U) stage
 // + the block's 64 biases: the epilogue reads them from LDS, so its rows never
 // wait on a global load (a load there waits, in order, for every earlier store)
-constexpr size_t WN_LDS = 2 * 2 * WN_STAGE * sizeof(float) + WN_KB * sizeof(float);
+constexpr size_t WN_LDS = 2 * 2 * WN_STAGE * sizeof(float) + WN_KB * sizeof(float) +
+                          2 * 2 * 16 * sizeof(float);   // (+ the 8-wave kernel's V padding)
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f4v __attribute__((ext_vector_type(4)));
@@ -555,6 +556,15 @@ constexpr int W8_T = 512;
 #ifndef W8_VPAIR
 #define W8_VPAIR 1      // the V stage in channel pairs (see store_vrow)
 #endif
+#ifndef W8_VPAD
+#define W8_VPAD 1       // each point's V block padded by 8 bytes (see vfrag)
+#endif
+// floats per point of the 8-wave kernel's V stage, and per V buffer
+constexpr int W8_VP = (W8_VPAIR && W8_VPAD) ? 514 : 512;
+constexpr int W8_VST = 16 * W8_VP;
+static_assert(W8_VST % 4 == 0, "V buffers of whole float4");
+static_assert((2 * W8_VST + 2 * WN_STAGE) * sizeof(float) >= 8 * 8 * 2 * 64 * 16,
+              "the epilogue's accumulator exchange fits below the biases");
 
 // The 8-wave kernel's transform of one channel where tile rows are whole lane
 // groups (no edge loads) and the rows outside the image were loaded as zeros
@@ -618,9 +628,9 @@ __device__ __forceinline__ void wino8_body(const float *__restrict__ x, const fl
                                            const float *__restrict__ bias, float *__restrict__ y,
                                            const WnGeom &g) {
     extern __shared__ float4 wn_lds[];
-    float4 *const Vs = wn_lds;                         // [2][p][h][t64]  (float4 = c4)
-    float4 *const Us = wn_lds + 2 * (WN_STAGE / 4);    // [2][p][h][k64]
-    float *const Bs = reinterpret_cast<float *>(wn_lds + 4 * (WN_STAGE / 4));   // [k64]
+    float4 *const Vs = wn_lds;                         // [2][p][h][cp][t64][c2] (see store_vrow)
+    float4 *const Us = wn_lds + 2 * (W8_VST / 4);      // [2][p][h][k64]
+    float *const Bs = reinterpret_cast<float *>(Us + 2 * (WN_STAGE / 4));   // [k64]
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const W8Block blk = w8_block(g);
@@ -705,7 +715,7 @@ __device__ __forceinline__ void wino8_body(const float *__restrict__ x, const fl
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #if W8_VPAIR
-            (Vf + vlane)[(i * 4 + j) * 512] = v[j];
+            (Vf + vlane)[(i * 4 + j) * W8_VP] = v[j];
 #else
             Vf[(((i * 4 + j) * 2 + (w >> 2)) * 64 + lane) * 4 + (w & 3)] = v[j];
 #endif
@@ -725,8 +735,11 @@ __device__ __forceinline__ void wino8_body(const float *__restrict__ x, const fl
     auto vfrag = [&](const float4 *V_, int p) -> float4 {
 #if W8_VPAIR
         const f2v *V2 = reinterpret_cast<const f2v *>(V_) + (hl * 2 * 64 + th * 32 + l32);
-        const f2v lo = V2[p * 4 * 64];
-        const f2v hi = (V2 + vhi)[p * 4 * 64];
+        // (W8_VPAD: a point's block is W8_VP = 514 floats, 2056 B, so the
+        // reads of points p and p + 1 are no pair the compiler can merge into
+        // one ds_read2st64_b64, 8 cycles, against two ds_read_b64 of 2 each)
+        const f2v lo = V2[p * (W8_VP / 2)];
+        const f2v hi = (V2 + vhi)[p * (W8_VP / 2)];
         return float4{lo.x, lo.y, hi.x, hi.y};
 #else
         return V_[(p * 2 + hl) * 64 + th * 32 + l32];
@@ -769,7 +782,7 @@ __device__ __forceinline__ void wino8_body(const float *__restrict__ x, const fl
         const int buf = cc & 1, nbuf = buf ^ 1;
         // the first fragments' LDS reads go out first, so their latency runs
         // under the next chunk's load issue
-        const float4 *V_ = Vs + buf * (WN_STAGE / 4);
+        const float4 *V_ = Vs + buf * (W8_VST / 4);
         const float4 *U_ = Us + buf * (WN_STAGE / 4);
         float4 a0 = U_[(P0 * 2 + hl) * 64 + kh * 32 + l32], b0 = vfrag(V_, P0);
         float4 a1 = U_[((P0 + 1) * 2 + hl) * 64 + kh * 32 + l32], b1 = vfrag(V_, P0 + 1);
@@ -787,7 +800,7 @@ __device__ __forceinline__ void wino8_body(const float *__restrict__ x, const fl
         float tx[4], ty[4], tl[4], tr[4], v[4];
         f2v t[4];
         const float *xc = more ? xbase(cc + 1) + ((int64_t)tn * g.C + w) * HW : x;
-        float *Vn = reinterpret_cast<float *>(Vs + nbuf * (WN_STAGE / 4));
+        float *Vn = reinterpret_cast<float *>(Vs + nbuf * (W8_VST / 4));
 #pragma unroll
         for (int pp = 0; pp < 4; ++pp) {
             const int p = P0 + 2 * pp;
