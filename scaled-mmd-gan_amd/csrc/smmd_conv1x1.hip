@@ -33,6 +33,7 @@
 // Accumulation order: fixed (per chunk, MFMA t in order; slices in order), so
 // the results are deterministic; fp32 products and sums, as the reference.
 #include "smmd_common.hpp"
+#include "smmd_ldsdma.hpp"
 
 namespace smmd {
 
@@ -309,6 +310,291 @@ __global__ __launch_bounds__(C1_T) void c1_wgrad_kernel(const float *__restrict_
     }
 }
 
+// ---- LDS-DMA forms (C1_DMA) --------------------------------------------------
+// The register-staged kernels above keep one chunk in flight: at the deep
+// layers (16-32 chunks per block, 256-512 blocks, one wave per SIMD) each
+// chunk costs one global-load latency, and a build without MFMAs took 60-70 %
+// of their time (profiles/r14/conv1x1_variants.txt).  These forms move the
+// operands global -> LDS by global_load_lds_dwordx4 (1 KiB per wave
+// instruction, no registers, no LDS store instructions) with C1_STAGES - 1
+// chunks in flight.  Same tiles, same MFMA operands in the same order, so the
+// results are bit-identical to the register-staged kernels.
+//   [row][32] operands (the forward's A = W, both wgrad operands): 8 rows of
+//   128 B per piece, the 16-byte quad Q of row m at slot Q ^ ((m >> 1) & 7)
+//   (the source lane picks the quad, so the swizzle costs nothing): a lane's
+//   ds_read_b128 of row m (16 lanes per cycle, rows m0 .. m0 + 15) hit 16
+//   distinct 16-byte bank groups.
+//   [row][64] operands (X, and A^T for the input gradient): 4 rows of 256 B per
+//   piece, pieces 1056 B apart, so rows r and r + 16 (the two lane halves of
+//   one ds_read_b32) sit on opposite bank halves.
+#ifndef C1_DMA
+#define C1_DMA 1
+#endif
+#ifndef C1_STAGES
+#define C1_STAGES 2
+#endif
+#ifndef C1_G2_MAX
+#define C1_G2_MAX 256         // grids up to this many blocks run two wave groups per block
+#endif
+constexpr int C1_PIECE = 1024;
+constexpr int C1_PPAD = C1_PIECE + 32;
+constexpr int C1D_OPER = 8 * C1_PPAD;          // bytes of one operand of a stage
+constexpr int C1D_STAGE = 2 * C1D_OPER;
+
+__device__ __forceinline__ int c1_swz(int row) { return (row >> 1) & 7; }
+
+// this wave's pieces of its k newest chunks may stay in flight (4 per chunk)
+__device__ __forceinline__ void c1_wait_chunks(int k) {
+    if (k >= 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if (k == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (k == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// G wave groups of 4 (G = 2: 8 waves, two per SIMD): group g takes chunks
+// g, g + G, ... of the block's reduction (a step = G chunks, one per group,
+// each group's waves moving its own chunk), so one group's barrier waits,
+// LDS reads and DMA issue overlap the other's MFMAs; the groups' sums are
+// added at the end (group 0's + group 1's, a fixed order).  G = 1 is the
+// register-staged kernel's accumulation order, bit for bit.
+template <bool TA, int S, int G>
+__global__ __launch_bounds__(C1_T * G) void c1_gemm_dma_kernel(const float *__restrict__ A,
+                                                               const float *__restrict__ X,
+                                                               const float *__restrict__ bias,
+                                                               float *__restrict__ Y, int M, int R,
+                                                               int P, int64_t J, int cps) {
+    static_assert(S >= 2 && S <= 5, "c1_wait_chunks covers up to 3 steps in flight");
+    static_assert(G == 1 || G == 2, "one or two wave groups");
+    extern __shared__ float4 c1_dyn[];
+    const char *const lds = reinterpret_cast<const char *>(c1_dyn);
+    const uint32_t lds0 = lds_addr(c1_dyn);
+    constexpr int GST = G * C1D_STAGE;          // bytes of one pipeline stage
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int grp = w >> 2, wl = w & 3;
+    const int wu = __builtin_amdgcn_readfirstlane(wl);
+    const int gu = __builtin_amdgcn_readfirstlane(grp);
+    const int mb_n = M / 64;
+    const int64_t jb_n = J / 64;
+    const int64_t blk = xcd_order(blockIdx.x, (int)(jb_n * mb_n));
+    const int mb = (int)(blk % mb_n);
+    const int64_t jb = blk / mb_n;
+    const int m0 = mb * 64;
+    const int64_t j0 = jb * 64;
+    const int rbeg = blockIdx.y * cps * C1_RC;
+    const int nchunk = min(cps, R / C1_RC - (int)blockIdx.y * cps);
+    const int nstep = (nchunk + G - 1) / G;
+
+    // wave wl of a group moves pieces 2 wl and 2 wl + 1 of each operand of
+    // its group's chunk.  X piece i: rows 4 i + lane / 16 of the chunk,
+    // columns j0 + 4 (lane % 16) (the row part 4 i and the chunk go into the
+    // uniform base)
+    uint32_t vb;
+    {
+        const int64_t j = j0 + 4 * (lane & 15);
+        const int64_t n = j / P, p = j - n * P;
+        vb = (uint32_t)(((n * R + (lane >> 4)) * P + p) * 4);
+    }
+    uint32_t va[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        if constexpr (TA) {        // A^T [R][M]: rows 4 pi + lane / 16, m0 + 4 (lane % 16)
+            va[i] = (uint32_t)(((lane >> 4) * M + m0 + 4 * (lane & 15)) * 4);
+        } else {                   // A [M][R]: row 8 pi + lane / 8, swizzled quad
+            const int m = 8 * (2 * wu + i) + (lane >> 3);
+            const int q = (lane & 7) ^ c1_swz(m);
+            va[i] = (uint32_t)(((int64_t)(m0 + m) * R + 4 * q) * 4);
+        }
+    }
+    // step i into stage s: this group's chunk G i + g (a group past the last
+    // chunk reloads it, so every wave has the same pieces in flight)
+    auto issue = [&](int i, int s) {
+        const int r = rbeg + C1_RC * min(G * i + gu, nchunk - 1);
+        const uint32_t st = lds0 + (uint32_t)(s * GST + gu * C1D_STAGE);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int pi = 2 * wu + k;
+            if constexpr (TA)
+                glds16(va[k], A + (int64_t)(r + 4 * pi) * M, st + (uint32_t)(pi * C1_PPAD));
+            else
+                glds16(va[k], A + r, st + (uint32_t)(pi * C1_PIECE));
+            glds16(vb, X + (int64_t)(r + 4 * pi) * P, st + (uint32_t)(C1D_OPER + pi * C1_PPAD));
+        }
+    };
+
+    const int mh = wl >> 1, jh = wl & 1, h = lane >> 5, l32 = lane & 31;
+    const int am = mh * 32 + l32;
+    // byte offsets in a stage: MFMA t reduces over r = 16 h + t (as c1_gemm)
+    const int boff = grp * C1D_STAGE + C1D_OPER + 4 * h * C1_PPAD + (jh * 32 + l32) * 4;
+    const int aoff = grp * C1D_STAGE + (TA ? 4 * h * C1_PPAD + am * 4 : am * 128);
+    f32x16 acc = f32x16{};
+    Y += (int64_t)blockIdx.y * J * M;
+#pragma unroll
+    for (int s = 0; s < S - 1; ++s)
+        if (s < nstep) issue(s, s);
+    int sc = 0;                                 // stage of step i
+    for (int i = 0; i < nstep; ++i) {
+        c1_wait_chunks(min(S - 2, nstep - 1 - i));
+        __syncthreads();                        // step i landed; step i - 1 read by all
+        if (i + S - 1 < nstep) issue(i + S - 1, sc == 0 ? S - 1 : sc - 1);
+        if (G * i + gu < nchunk) {
+            const char *st = lds + sc * GST;
+            float av[16], bv[16];
+            if constexpr (TA) {
+#pragma unroll
+                for (int t = 0; t < 16; ++t)
+                    av[t] = *reinterpret_cast<const float *>(st + aoff + (t >> 2) * C1_PPAD +
+                                                             (t & 3) * 256);
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float4 v = *reinterpret_cast<const float4 *>(
+                        st + aoff + (((4 * h + q) ^ c1_swz(am)) * 16));
+                    av[4 * q] = v.x;
+                    av[4 * q + 1] = v.y;
+                    av[4 * q + 2] = v.z;
+                    av[4 * q + 3] = v.w;
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < 16; ++t)
+                bv[t] = *reinterpret_cast<const float *>(st + boff + (t >> 2) * C1_PPAD +
+                                                         (t & 3) * 256);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int t = 0; t < 16; ++t)
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[t], bv[t], acc, 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        sc = sc == S - 1 ? 0 : sc + 1;
+    }
+    if constexpr (G == 2) {
+        // group 1's sums through LDS (the stages are free after the barrier)
+        float *red = reinterpret_cast<float *>(c1_dyn) + wl * 16 * 64 + lane;
+        __syncthreads();
+        if (grp == 1) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) red[r * 64] = acc[r];
+        }
+        __syncthreads();
+        if (grp == 1) return;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = acc[r] + red[r * 64];
+    }
+    // epilogue: as c1_gemm
+    const int64_t j = j0 + jh * 32 + l32;
+    const int64_t n = j / P, p = j - n * (int64_t)P;
+    float *yc = Y + n * (int64_t)M * P + p;
+    const int mr = m0 + mh * 32 + 4 * h;
+    if (bias) {
+        float bb[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) bb[r] = bias[mr + (r & 3) + 8 * (r >> 2)];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) yc[(int64_t)(mr + (r & 3) + 8 * (r >> 2)) * P] = acc[r] + bb[r];
+    } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) yc[(int64_t)(mr + (r & 3) + 8 * (r >> 2)) * P] = acc[r];
+    }
+}
+
+// weight gradient: both operands [row][32 columns] (swizzled pieces); a
+// chunk's 32 columns lie in one image (P % 32 == 0) or span 32 / P whole
+// images (32 % P == 0), so a lane's source is a fixed offset from the
+// chunk's uniform base
+template <int S>
+__global__ __launch_bounds__(C1_T) void c1_wgrad_dma_kernel(const float *__restrict__ gy,
+                                                            const float *__restrict__ x,
+                                                            float *__restrict__ part, int K, int C,
+                                                            int P, int64_t J, int64_t cps,
+                                                            int accum) {
+    static_assert(S >= 2 && S <= 5, "c1_wait_chunks covers up to 3 chunks in flight");
+    extern __shared__ float4 c1_dyn[];
+    const char *const lds = reinterpret_cast<const char *>(c1_dyn);
+    const uint32_t lds0 = lds_addr(c1_dyn);
+    constexpr int WST = 2 * 8 * C1_PIECE;       // stage bytes: gy rows, then x rows
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wu = __builtin_amdgcn_readfirstlane(w);
+    const int cb_n = C / 64;
+    const int kb = blockIdx.x / cb_n, cb = blockIdx.x - kb * cb_n;
+    const int s = blockIdx.y;
+    const int64_t jbeg = (int64_t)s * cps;
+    const int64_t jend = min(J, jbeg + cps);
+    const int k0 = kb * 64, c0 = cb * 64;
+    const int nchunk = (int)((jend - jbeg) / C1_RC);
+    // lane part of piece pi (rows 8 pi + lane / 8, quad q swizzled): column
+    // 4 q of the chunk = image 4 q / P, pixel 4 q % P past the chunk's start
+    uint32_t vg[2], vx[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int row = 8 * (2 * wu + i) + (lane >> 3);
+        const int q = (lane & 7) ^ c1_swz(row);
+        const int img = P >= C1_RC ? 0 : (4 * q) / P;
+        const int pp = P >= C1_RC ? 4 * q : (4 * q) % P;
+        vg[i] = (uint32_t)((((int64_t)img * K + row) * P + pp) * 4);
+        vx[i] = (uint32_t)((((int64_t)img * C + row) * P + pp) * 4);
+    }
+    // the chunk's first column (n, p), advanced one chunk per issue
+    int64_t cn = jbeg / P;
+    int cp = (int)(jbeg - cn * P);
+    auto issue = [&](int sidx) {
+        const uint32_t st = lds0 + (uint32_t)(sidx * WST);
+        const float *bg = gy + (cn * K + k0) * (int64_t)P + cp;
+        const float *bx = x + (cn * C + c0) * (int64_t)P + cp;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int pi = 2 * wu + i;
+            glds16(vg[i], bg, st + (uint32_t)(pi * C1_PIECE));
+            glds16(vx[i], bx, st + (uint32_t)(8 * C1_PIECE + pi * C1_PIECE));
+        }
+        if (P >= C1_RC) {
+            cp += C1_RC;
+            if (cp >= P) {
+                cp = 0;
+                ++cn;
+            }
+        } else {
+            cn += C1_RC / P;
+        }
+    };
+    const int kh = w >> 1, ch = w & 1, h = lane >> 5, l32 = lane & 31;
+    const int ar = kh * 32 + l32, br = ch * 32 + l32;
+    f32x16 acc = f32x16{};
+#pragma unroll
+    for (int i = 0; i < S - 1; ++i)
+        if (i < nchunk) issue(i);
+    int sc = 0;
+    for (int c = 0; c < nchunk; ++c) {
+        c1_wait_chunks(min(S - 2, nchunk - 1 - c));
+        __syncthreads();
+        if (c + S - 1 < nchunk) issue(sc == 0 ? S - 1 : sc - 1);
+        const char *st = lds + sc * WST;
+        float4 a4[4], b4[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            a4[q] = *reinterpret_cast<const float4 *>(st + ar * 128 + (((4 * h + q) ^ c1_swz(ar)) * 16));
+            b4[q] = *reinterpret_cast<const float4 *>(st + 8 * C1_PIECE + br * 128 +
+                                                      (((4 * h + q) ^ c1_swz(br)) * 16));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[q].x, b4[q].x, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[q].y, b4[q].y, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[q].z, b4[q].z, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[q].w, b4[q].w, acc, 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        sc = sc == S - 1 ? 0 : sc + 1;
+    }
+    float *o = part + (int64_t)s * K * C;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int k = k0 + kh * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        float *d = o + (int64_t)k * C + c0 + ch * 32 + l32;
+        *d = accum ? *d + acc[r] : acc[r];
+    }
+}
+
 // out[i] = sum over slabs [g G, min(S, g G + G)) of n4 float4 each for group
 // g = blockIdx.y, in slab order (+ bias[(i / (rowlen / 4)) % nb] when bias):
 // the first level of a two-level fixed-order slab sum (G slabs per group;
@@ -435,9 +721,39 @@ static smmd_status c1_gemm_launch(const float *a, const float *x, const float *b
     const int Sused = (nch + cps - 1) / cps;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     float *part = Sused > 1 ? static_cast<float *>(ws) : y;
-    auto k = ta ? c1_gemm_kernel<true> : c1_gemm_kernel<false>;
-    k<<<dim3((unsigned)blocks, (unsigned)Sused), dim3(C1_T), 0, st>>>(
-        a, x, Sused > 1 ? nullptr : bias, part, m, r, p, J, cps);
+    const dim3 grid((unsigned)blocks, (unsigned)Sused);
+#if C1_DMA
+    // the DMA form's lane offsets are 32-bit byte offsets
+    if ((int64_t)n * r * p * 4 < (1ll << 31) && (int64_t)m * r * 4 < (1ll << 31)) {
+        // two wave groups when the grid leaves a CU one block (one wave per SIMD)
+        const bool g2 = blocks * Sused <= C1_G2_MAX && nch / Sused >= 2;
+        static bool attr = false;
+        constexpr int lds1 = C1_STAGES * C1D_STAGE, lds2 = 2 * C1_STAGES * C1D_STAGE;
+        if (!attr) {
+            const void *ks[4] = {reinterpret_cast<const void *>(c1_gemm_dma_kernel<true, C1_STAGES, 1>),
+                                 reinterpret_cast<const void *>(c1_gemm_dma_kernel<false, C1_STAGES, 1>),
+                                 reinterpret_cast<const void *>(c1_gemm_dma_kernel<true, C1_STAGES, 2>),
+                                 reinterpret_cast<const void *>(c1_gemm_dma_kernel<false, C1_STAGES, 2>)};
+            for (int i = 0; i < 4; ++i)
+                if (hipFuncSetAttribute(ks[i], hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        i < 2 ? lds1 : lds2) != hipSuccess)
+                    return SMMD_EHIP;
+            attr = true;
+        }
+        const float *b1 = Sused > 1 ? nullptr : bias;
+        if (g2) {
+            auto kd = ta ? c1_gemm_dma_kernel<true, C1_STAGES, 2> : c1_gemm_dma_kernel<false, C1_STAGES, 2>;
+            kd<<<grid, dim3(2 * C1_T), lds2, st>>>(a, x, b1, part, m, r, p, J, cps);
+        } else {
+            auto kd = ta ? c1_gemm_dma_kernel<true, C1_STAGES, 1> : c1_gemm_dma_kernel<false, C1_STAGES, 1>;
+            kd<<<grid, dim3(C1_T), lds1, st>>>(a, x, b1, part, m, r, p, J, cps);
+        }
+    } else
+#endif
+    {
+        auto k = ta ? c1_gemm_kernel<true> : c1_gemm_kernel<false>;
+        k<<<grid, dim3(C1_T), 0, st>>>(a, x, Sused > 1 ? nullptr : bias, part, m, r, p, J, cps);
+    }
     smmd_status e = last_launch_status();
     if (e != SMMD_OK || Sused == 1) return e;
     const int64_t total = J * m;
@@ -487,8 +803,26 @@ static smmd_status c1_wgrad_launch(const float *gy, const float *x, float *gw, i
     const int Sused = (int)((J + cps - 1) / cps);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     float *part = Sused > 1 ? static_cast<float *>(ws) : gw;
-    c1_wgrad_kernel<<<dim3((unsigned)tiles, (unsigned)Sused), dim3(C1_T), 0, st>>>(
-        gy, x, part, k, c, p, J, cps, Sused == 1 ? accum : 0);
+    const dim3 grid((unsigned)tiles, (unsigned)Sused);
+#if C1_DMA
+    // a chunk's 32 columns in one image or over whole images
+    if (p % C1_RC == 0 || C1_RC % p == 0) {
+        static bool attr = false;
+        constexpr int lds = C1_STAGES * 2 * 8 * C1_PIECE;
+        if (!attr) {
+            if (hipFuncSetAttribute(reinterpret_cast<const void *>(c1_wgrad_dma_kernel<C1_STAGES>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
+                return SMMD_EHIP;
+            attr = true;
+        }
+        c1_wgrad_dma_kernel<C1_STAGES><<<grid, dim3(C1_T), lds, st>>>(gy, x, part, k, c, p, J, cps,
+                                                                     Sused == 1 ? accum : 0);
+    } else
+#endif
+    {
+        c1_wgrad_kernel<<<grid, dim3(C1_T), 0, st>>>(gy, x, part, k, c, p, J, cps,
+                                                     Sused == 1 ? accum : 0);
+    }
     smmd_status e = last_launch_status();
     if (e != SMMD_OK || Sused == 1) return e;
     const int64_t total = (int64_t)k * c;

@@ -1,5 +1,5 @@
 """The residual shortcuts' 1x1 convolutions on the library (`smmd_conv1x1*`,
-csrc/smmd_conv1x1.hip, ABI 11): forward (+ bias), input gradient and weight
+csrc/smmd_conv1x1.hip, ABI 11; LDS-DMA forms since r15): forward (+ bias), input gradient and weight
 gradient against torch's float64 convolutions at the SNResNet-64 critic's and
 generator's shortcut shapes and smaller ones (one image per column tile, tiles
 across images, many weight-gradient slices), the convops dispatch (MIOpen not
@@ -14,7 +14,11 @@ DEV = 'cuda:0'
 
 # (N, C, K, H): x [N, C, H, H], W [K, C, 1, 1]
 SHAPES = [(64, 64, 128, 32), (64, 128, 256, 16), (64, 256, 512, 8), (64, 512, 1024, 4),
-          (64, 1024, 512, 4), (4, 64, 64, 4), (2, 128, 192, 8), (3, 64, 64, 16)]
+          (64, 1024, 512, 4), (4, 64, 64, 4), (2, 128, 192, 8), (3, 64, 64, 16),
+          # pixels per image dividing a 32-column chunk (the LDS-DMA weight
+          # gradient spans images), and neither dividing nor a multiple of it
+          # (the register-staged weight gradient)
+          (32, 512, 1024, 2), (64, 128, 256, 6)]
 
 
 def _ref(x, w, b, gy):
