@@ -500,20 +500,25 @@ __global__ __launch_bounds__(C1_T * G) void c1_gemm_dma_kernel(const float *__re
 // weight gradient: both operands [row][32 columns] (swizzled pieces); a
 // chunk's 32 columns lie in one image (P % 32 == 0) or span 32 / P whole
 // images (32 % P == 0), so a lane's source is a fixed offset from the
-// chunk's uniform base
-template <int S>
-__global__ __launch_bounds__(C1_T) void c1_wgrad_dma_kernel(const float *__restrict__ gy,
-                                                            const float *__restrict__ x,
-                                                            float *__restrict__ part, int K, int C,
-                                                            int P, int64_t J, int64_t cps,
-                                                            int accum) {
-    static_assert(S >= 2 && S <= 5, "c1_wait_chunks covers up to 3 chunks in flight");
+// chunk's uniform base.  G wave groups as c1_gemm_dma (G = 1: the
+// register-staged kernel's order, bit for bit).
+template <int S, int G>
+__global__ __launch_bounds__(C1_T * G) void c1_wgrad_dma_kernel(const float *__restrict__ gy,
+                                                                const float *__restrict__ x,
+                                                                float *__restrict__ part, int K,
+                                                                int C, int P, int64_t J,
+                                                                int64_t cps, int accum) {
+    static_assert(S >= 2 && S <= 5, "c1_wait_chunks covers up to 3 steps in flight");
+    static_assert(G == 1 || G == 2, "one or two wave groups");
     extern __shared__ float4 c1_dyn[];
     const char *const lds = reinterpret_cast<const char *>(c1_dyn);
     const uint32_t lds0 = lds_addr(c1_dyn);
-    constexpr int WST = 2 * 8 * C1_PIECE;       // stage bytes: gy rows, then x rows
+    constexpr int WST = 2 * 8 * C1_PIECE;       // chunk bytes: gy rows, then x rows
+    constexpr int GST = G * WST;                // bytes of one pipeline stage
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int wu = __builtin_amdgcn_readfirstlane(w);
+    const int grp = w >> 2, wl = w & 3;
+    const int wu = __builtin_amdgcn_readfirstlane(wl);
+    const int gu = __builtin_amdgcn_readfirstlane(grp);
     const int cb_n = C / 64;
     const int kb = blockIdx.x / cb_n, cb = blockIdx.x - kb * cb_n;
     const int s = blockIdx.y;
@@ -521,6 +526,7 @@ __global__ __launch_bounds__(C1_T) void c1_wgrad_dma_kernel(const float *__restr
     const int64_t jend = min(J, jbeg + cps);
     const int k0 = kb * 64, c0 = cb * 64;
     const int nchunk = (int)((jend - jbeg) / C1_RC);
+    const int nstep = (nchunk + G - 1) / G;
     // lane part of piece pi (rows 8 pi + lane / 8, quad q swizzled): column
     // 4 q of the chunk = image 4 q / P, pixel 4 q % P past the chunk's start
     uint32_t vg[2], vx[2];
@@ -533,58 +539,64 @@ __global__ __launch_bounds__(C1_T) void c1_wgrad_dma_kernel(const float *__restr
         vg[i] = (uint32_t)((((int64_t)img * K + row) * P + pp) * 4);
         vx[i] = (uint32_t)((((int64_t)img * C + row) * P + pp) * 4);
     }
-    // the chunk's first column (n, p), advanced one chunk per issue
-    int64_t cn = jbeg / P;
-    int cp = (int)(jbeg - cn * P);
-    auto issue = [&](int sidx) {
-        const uint32_t st = lds0 + (uint32_t)(sidx * WST);
-        const float *bg = gy + (cn * K + k0) * (int64_t)P + cp;
-        const float *bx = x + (cn * C + c0) * (int64_t)P + cp;
+    // step i into stage sidx: this group's chunk G i + g (past the last chunk:
+    // the last chunk again, so every wave has the same pieces in flight)
+    auto issue = [&](int i, int sidx) {
+        const uint32_t jc = (uint32_t)(jbeg + C1_RC * min(G * i + gu, nchunk - 1));
+        const uint32_t cn = jc / (uint32_t)P, cp = jc - cn * (uint32_t)P;
+        const uint32_t st = lds0 + (uint32_t)(sidx * GST + gu * WST);
+        const float *bg = gy + ((int64_t)cn * K + k0) * (int64_t)P + cp;
+        const float *bx = x + ((int64_t)cn * C + c0) * (int64_t)P + cp;
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int pi = 2 * wu + i;
-            glds16(vg[i], bg, st + (uint32_t)(pi * C1_PIECE));
-            glds16(vx[i], bx, st + (uint32_t)(8 * C1_PIECE + pi * C1_PIECE));
-        }
-        if (P >= C1_RC) {
-            cp += C1_RC;
-            if (cp >= P) {
-                cp = 0;
-                ++cn;
-            }
-        } else {
-            cn += C1_RC / P;
+        for (int k = 0; k < 2; ++k) {
+            const int pi = 2 * wu + k;
+            glds16(vg[k], bg, st + (uint32_t)(pi * C1_PIECE));
+            glds16(vx[k], bx, st + (uint32_t)(8 * C1_PIECE + pi * C1_PIECE));
         }
     };
-    const int kh = w >> 1, ch = w & 1, h = lane >> 5, l32 = lane & 31;
+    const int kh = wl >> 1, ch = wl & 1, h = lane >> 5, l32 = lane & 31;
     const int ar = kh * 32 + l32, br = ch * 32 + l32;
+    const int ao = grp * WST + ar * 128, bo = grp * WST + 8 * C1_PIECE + br * 128;
     f32x16 acc = f32x16{};
 #pragma unroll
     for (int i = 0; i < S - 1; ++i)
-        if (i < nchunk) issue(i);
+        if (i < nstep) issue(i, i);
     int sc = 0;
-    for (int c = 0; c < nchunk; ++c) {
-        c1_wait_chunks(min(S - 2, nchunk - 1 - c));
+    for (int i = 0; i < nstep; ++i) {
+        c1_wait_chunks(min(S - 2, nstep - 1 - i));
         __syncthreads();
-        if (c + S - 1 < nchunk) issue(sc == 0 ? S - 1 : sc - 1);
-        const char *st = lds + sc * WST;
-        float4 a4[4], b4[4];
+        if (i + S - 1 < nstep) issue(i + S - 1, sc == 0 ? S - 1 : sc - 1);
+        if (G * i + gu < nchunk) {
+            const char *st = lds + sc * GST;
+            float4 a4[4], b4[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            a4[q] = *reinterpret_cast<const float4 *>(st + ar * 128 + (((4 * h + q) ^ c1_swz(ar)) * 16));
-            b4[q] = *reinterpret_cast<const float4 *>(st + 8 * C1_PIECE + br * 128 +
-                                                      (((4 * h + q) ^ c1_swz(br)) * 16));
-        }
-        __builtin_amdgcn_sched_barrier(0);
+            for (int q = 0; q < 4; ++q) {
+                a4[q] = *reinterpret_cast<const float4 *>(st + ao + (((4 * h + q) ^ c1_swz(ar)) * 16));
+                b4[q] = *reinterpret_cast<const float4 *>(st + bo + (((4 * h + q) ^ c1_swz(br)) * 16));
+            }
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[q].x, b4[q].x, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[q].y, b4[q].y, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[q].z, b4[q].z, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[q].w, b4[q].w, acc, 0, 0, 0);
+            for (int q = 0; q < 4; ++q) {
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[q].x, b4[q].x, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[q].y, b4[q].y, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[q].z, b4[q].z, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[q].w, b4[q].w, acc, 0, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
         }
-        __builtin_amdgcn_sched_barrier(0);
         sc = sc == S - 1 ? 0 : sc + 1;
+    }
+    if constexpr (G == 2) {
+        float *red = reinterpret_cast<float *>(c1_dyn) + wl * 16 * 64 + lane;
+        __syncthreads();
+        if (grp == 1) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) red[r * 64] = acc[r];
+        }
+        __syncthreads();
+        if (grp == 1) return;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = acc[r] + red[r * 64];
     }
     float *o = part + (int64_t)s * K * C;
 #pragma unroll
@@ -646,8 +658,8 @@ int c1_groups(int S) { return S > 2 * C1_GROUP ? (S + C1_GROUP - 1) / C1_GROUP :
 #ifndef C1_MINCH_WGRAD
 #define C1_MINCH_WGRAD 8
 #endif
-int c1_slices(int tiles, int64_t nchunk, int min_chunks) {
-    int64_t S = (C1_TARGET + tiles - 1) / tiles;
+int c1_slices(int tiles, int64_t nchunk, int min_chunks, int target = C1_TARGET) {
+    int64_t S = (target + tiles - 1) / tiles;
     S = min(S, max((int64_t)1, nchunk / min_chunks));
     return (int)max((int64_t)1, S);
 }
@@ -780,9 +792,25 @@ extern "C" int smmd_conv1x1_wgrad_supported(int n, int c, int k, int p) {
            J % C1_RC == 0 && (int64_t)n * (c > k ? c : k) * p < (1ll << 40);
 }
 
+namespace {
+#ifndef C1_WG_G
+#define C1_WG_G 2             // wave groups of the LDS-DMA weight gradient
+#endif
+// the LDS-DMA weight gradient: a chunk's 32 columns in one image or over
+// whole images, 32-bit column indices
+bool c1_wgrad_dma(int n, int p) {
+    return C1_DMA && (p % C1_RC == 0 || C1_RC % p == 0) && (int64_t)n * p < (1ll << 31);
+}
+// column slices: ~C1_TARGET / G workgroups of G wave groups, >= 8 chunks per group
+int c1_wgrad_slices(int n, int c, int k, int p) {
+    const int g = c1_wgrad_dma(n, p) ? C1_WG_G : 1;
+    return c1_slices((k / 64) * (c / 64), (int64_t)n * p / C1_RC, C1_MINCH_WGRAD * g, C1_TARGET / g);
+}
+}  // namespace
+
 extern "C" size_t smmd_conv1x1_wgrad_workspace_bytes(int n, int c, int k, int p) {
     if (!smmd_conv1x1_wgrad_supported(n, c, k, p)) return 0;
-    const int S = c1_slices((k / 64) * (c / 64), (int64_t)n * p / C1_RC, C1_MINCH_WGRAD);
+    const int S = c1_wgrad_slices(n, c, k, p);
     return S > 1 ? (size_t)(S + c1_groups(S)) * k * c * sizeof(float) : 0;
 }
 
@@ -795,7 +823,7 @@ static smmd_status c1_wgrad_launch(const float *gy, const float *x, float *gw, i
     const int64_t J = (int64_t)n * p;
     const int tiles = (k / 64) * (c / 64);
     const int64_t nch = J / C1_RC;
-    const int S = c1_slices(tiles, nch, C1_MINCH_WGRAD);
+    const int S = c1_wgrad_slices(n, c, k, p);
     const size_t need = smmd_conv1x1_wgrad_workspace_bytes(n, c, k, p);
     if (need && (!ws || ws_bytes < need || !aligned16(ws))) return SMMD_EWORKSPACE;
     // columns per slice: whole chunks
@@ -805,18 +833,17 @@ static smmd_status c1_wgrad_launch(const float *gy, const float *x, float *gw, i
     float *part = Sused > 1 ? static_cast<float *>(ws) : gw;
     const dim3 grid((unsigned)tiles, (unsigned)Sused);
 #if C1_DMA
-    // a chunk's 32 columns in one image or over whole images
-    if (p % C1_RC == 0 || C1_RC % p == 0) {
+    if (c1_wgrad_dma(n, p)) {
+        constexpr int lds = C1_WG_G * C1_STAGES * 2 * 8 * C1_PIECE;
         static bool attr = false;
-        constexpr int lds = C1_STAGES * 2 * 8 * C1_PIECE;
         if (!attr) {
-            if (hipFuncSetAttribute(reinterpret_cast<const void *>(c1_wgrad_dma_kernel<C1_STAGES>),
+            if (hipFuncSetAttribute(reinterpret_cast<const void *>(c1_wgrad_dma_kernel<C1_STAGES, C1_WG_G>),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
                 return SMMD_EHIP;
             attr = true;
         }
-        c1_wgrad_dma_kernel<C1_STAGES><<<grid, dim3(C1_T), lds, st>>>(gy, x, part, k, c, p, J, cps,
-                                                                     Sused == 1 ? accum : 0);
+        c1_wgrad_dma_kernel<C1_STAGES, C1_WG_G><<<grid, dim3(C1_WG_G * C1_T), lds, st>>>(
+            gy, x, part, k, c, p, J, cps, Sused == 1 ? accum : 0);
     } else
 #endif
     {
