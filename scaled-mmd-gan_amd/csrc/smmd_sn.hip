@@ -33,6 +33,10 @@
 // under load) costs 25 us (profiles/r08/sn_p23_experiment.txt).
 #include "smmd_sn_tile.hpp"
 
+#ifndef SN_GSTAT_DIRECT
+#define SN_GSTAT_DIRECT 1   // smmd_sn_grad_stats' fold units without the LDS stage
+#endif
+
 #include <stdlib.h>
 
 namespace smmd {
@@ -758,6 +762,46 @@ __global__ __launch_bounds__(256) void sn_gstat_a_kernel(SnTable t) {
     if (!L.G) return;                            // this call skips the layer
     const int lt = unit - L.unit_begin;
     float ad = 0.f, ag = 0.f, au = 0.f;
+#if SN_GSTAT_DIRECT
+    if (L.fold) {
+        // each thread its own filter straight from global memory (G' as four
+        // float4, W as nine floats): no LDS stage and no barrier, the same
+        // arithmetic in the same order as the staged form (snf_adjoint)
+        const uint32_t nf = (uint32_t)L.N * (uint32_t)L.nfc;
+        const uint32_t q = (uint32_t)lt * SNF_T + threadIdx.x;
+        if (q < nf) {
+            const float4 *g4 = reinterpret_cast<const float4 *>(L.G) + (size_t)q * 4;
+            const float4 k0 = g4[0], k1 = g4[1], k2 = g4[2], k3 = g4[3];
+            const float *wq = L.W + (size_t)q * 9;
+            float wv[9], vk[9];
+#pragma unroll
+            for (int j = 0; j < 9; ++j) wv[j] = wq[j];
+            const uint32_t n = q / (uint32_t)L.nfc, c = q - n * (uint32_t)L.nfc;
+            const float un = L.ucur[n];
+#pragma unroll
+            for (int j = 0; j < 9; ++j) vk[j] = L.v[c * 9 + j];
+            const float k[16] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w,
+                                 k2.x, k2.y, k2.z, k2.w, k3.x, k3.y, k3.z, k3.w};
+            float gv = 0.f;
+#pragma unroll
+            for (int u = 0; u < 3; ++u)
+#pragma unroll
+                for (int v = 0; v < 3; ++v) {
+                    float acc = 0.f;
+#pragma unroll
+                    for (int a = 0; a < 2; ++a)
+#pragma unroll
+                        for (int b = 0; b < 2; ++b) acc += k[(u + a) * 4 + (v + b)];
+                    const float g = acc * 0.25f;
+                    const int j = u * 3 + v;
+                    ad = fmaf(g, wv[j], ad);
+                    ag = fmaf(g, g, ag);
+                    gv = fmaf(g, vk[j], gv);
+                }
+            au = un * gv;
+        }
+    } else
+#else
     if (L.fold) {
         __shared__ float s9[SNF_T * 9];
         __shared__ float s16[16 * SNF_S16];
@@ -788,7 +832,9 @@ __global__ __launch_bounds__(256) void sn_gstat_a_kernel(SnTable t) {
             }
             au = un * gv;
         }
-    } else {
+    } else
+#endif
+    {
         const int rt = lt / L.nct, ct = lt % L.nct;
         const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
         const int r0 = rt * SN_TR + w * SN_RPW;
